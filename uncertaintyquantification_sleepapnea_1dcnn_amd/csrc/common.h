@@ -1,0 +1,72 @@
+// Shared device helpers for the gfx950 (MI355X / CDNA4) kernels of apneauq.
+//
+// Written directly against CDNA4: 64-lane wavefronts, bf16 MFMA (v_mfma_f32_16x16x32_bf16),
+// 160 KiB LDS per CU.  No CUDA shims, no dual-platform paths.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace apneauq {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Explicit global-address-space views (keep loads as global_load_*, never flat_*).
+typedef __attribute__((address_space(1))) const bf16x8 gbf16x8;
+typedef __attribute__((address_space(1))) const f32x4 gf32x4;
+typedef __attribute__((address_space(1))) const float gfloat;
+typedef __attribute__((address_space(1))) const uint8_t guint8;
+
+constexpr int kWave = 64;
+
+// ---------------------------------------------------------------------------------------------
+// Counter-based dropout RNG -- bit-identical to ops/rng.py (see its docstring for the definition)
+// ---------------------------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__host__ __device__ __forceinline__ uint32_t stream_key(uint64_t seed, uint32_t layer, uint32_t pass) {
+  uint32_t k = mix32((uint32_t)(seed & 0xFFFFFFFFu) ^ 0x68BC21EBu);
+  k = mix32(k ^ (uint32_t)(seed >> 32));
+  k = mix32(k ^ (layer * 0x9E3779B9u));
+  k = mix32(k ^ pass);
+  return k;
+}
+
+__host__ __device__ __forceinline__ uint32_t sample_key(uint32_t skey, uint32_t sample) {
+  return mix32(skey ^ mix32(sample + 0x2545F491u));
+}
+
+// 16-bit uniforms of channels (c, c+1), c even, at time step t.
+__device__ __forceinline__ uint32_t dropout_bits2(uint32_t skey, uint32_t t, uint32_t c_even) {
+  return mix32(skey ^ ((t << 9) | (c_even >> 1)));
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+// Sum over the 16 lanes of a 16-lane group (lanes sharing lane>>4).
+__device__ __forceinline__ float group16_sum(float v) {
+  v += __shfl_xor(v, 1, kWave);
+  v += __shfl_xor(v, 2, kWave);
+  v += __shfl_xor(v, 4, kWave);
+  v += __shfl_xor(v, 8, kWave);
+  return v;
+}
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+}  // namespace apneauq

@@ -1,0 +1,353 @@
+// Fused whole-network inference of the Alarcón 1D-CNN on gfx950 (MI355X).
+//
+// Replaces the reference's hot loops
+//   * MC Dropout:    np.stack([model(x, training=True) for _ in range(T)])   (uq_techniques.py:22)
+//   * Deep Ensemble: np.stack([m.predict(x) for m in models])                (uq_techniques.py:29)
+// with ONE launch that runs all six Conv1D->ReLU->BN->Dropout blocks, GAP, Dense and sigmoid for
+// every (member, pass, window) sample.  Activations never leave LDS; weights stream from L2.
+//
+// Geometry (CDNA4-first):
+//   * a workgroup (4 waves, 256 threads) owns a tile of 2 samples;  each sample occupies a 64-row
+//     LDS slot: 60 valid time steps + 4 zero rows.  The zero rows double as the 'same' padding
+//     (halo) of the next slot, so the implicit-GEMM conv needs no bounds checks;
+//   * each block is an implicit GEMM  D^T[co][row] = W^T[co][k] * X^T[k][row],  k = tap*Cin + ci,
+//     on v_mfma_f32_16x16x32_bf16.  Weights are the A operand, pre-packed on the host in exact
+//     fragment order (one coalesced 1 KiB load per wave per fragment); activations are the B
+//     operand, read from LDS with ds_read_b128 (row stride 544 B => conflict-free lane groups);
+//   * the accumulator of a lane holds one time step x 4 consecutive channels, so the epilogue
+//     (bias + ReLU + BN affine + counter-based dropout + bf16 pack) writes 8 B per tile per lane,
+//     in place over the block input (the whole layer output lives in registers across the barrier);
+//   * block 6's epilogue feeds GAP + Dense(96->1) + sigmoid directly (fp32), never touching LDS.
+//   LDS per workgroup ~75 KiB -> 2 workgroups (8 waves) per CU.
+#include "common.h"
+
+namespace apneauq {
+namespace fused {
+
+constexpr int kL = 60;                         // valid time steps per window
+constexpr int kSR = 64;                        // LDS rows per sample slot
+constexpr int kSlots = 2;                      // samples per workgroup tile
+constexpr int kR = kSR * kSlots;               // GEMM rows per tile
+constexpr int kRT = kR / 16;                   // 16-row tiles per tile
+constexpr int kHalo = 4;                       // >= max (k-1)/2
+constexpr int kRows = kHalo + kR + kHalo;      // LDS rows incl. leading/trailing halo
+constexpr int kCin = 4;                        // input channels (SaO2, PR, THOR RES, ABDO RES)
+constexpr int kRS = 256 * 2 + 32;              // activation row stride in bytes (all layers)
+constexpr int kX0RS = kCin * 2;                // input row stride in bytes
+constexpr int kActBytes = kRows * kRS;
+constexpr int kX0Bytes = kRows * kX0RS;
+constexpr int kHeadBytes = 64;
+constexpr int kLdsBytes = kActBytes + kX0Bytes + kHeadBytes;
+constexpr int kThreads = 256;
+static_assert(kActBytes % 16 == 0 && kX0Bytes % 16 == 0, "LDS carve must stay 16-B aligned");
+
+// channel / kernel-size table of the default spec (cnn_baseline_train.py:59-86)
+constexpr int C[7] = {4, 128, 192, 224, 96, 256, 96};
+constexpr int KS[6] = {7, 5, 3, 7, 9, 9};
+
+__host__ __device__ constexpr int ksteps(int l) { return (C[l] * KS[l] + 31) / 32; }
+__host__ __device__ constexpr int wbytes(int l) { return ksteps(l) * (C[l + 1] / 16) * 1024; }
+__host__ __device__ constexpr int ebytes(int l) { return ((3 * C[l + 1] * 4) + 15) / 16 * 16; }
+__host__ __device__ constexpr int woff(int l) { return l == 0 ? 0 : woff(l - 1) + wbytes(l - 1); }
+__host__ __device__ constexpr int eoff(int l) { return l == 0 ? woff(6) : eoff(l - 1) + ebytes(l - 1); }
+constexpr int kDenseOff = eoff(6);
+constexpr int kBlobBytes = kDenseOff + ((C[6] + 1) * 4 + 15) / 16 * 16;
+
+extern __shared__ __attribute__((aligned(16))) char smem[];  // dynamic LDS, carved below
+
+struct Args {
+  const __bf16* x;         // (n_win, 60, 4) bf16, channels-last
+  const uint8_t* blob;     // (n_member, kBlobBytes) packed parameters
+  float* out;              // (n_member, n_pass, n_win)
+  long long blob_stride;   // bytes between members
+  int n_win, n_pass, n_member;
+  int tiles_per_member;
+  int total_items;
+  int chunk;               // items per workgroup (1)
+  unsigned window_offset;  // global index of window 0 (dropout sample id => sharding invariance)
+  unsigned pass_offset;
+  unsigned long long seed;
+  int dropout;             // apply dropout masks (MC Dropout)
+  int out_logits;          // 1: write logits instead of probabilities
+  unsigned thr[6];         // 16-bit drop thresholds per block
+  float dscale[6];         // 1/(1-rate) per block
+};
+
+// One Conv1D(relu) -> BN -> Dropout block as an LDS-resident implicit GEMM.
+//   WM x WN waves tile (rows x output channels);  CT/RT = 16-wide tiles per wave.
+#ifndef APNEAUQ_BLOCK_INLINE
+#define APNEAUQ_BLOCK_INLINE __forceinline__
+#endif
+
+// Per-block context passed by value to the (deliberately non-inlined) block functions: keeping
+// each block a separate function bounds register allocation to one block's live state.
+struct BlockCtx {
+  const guint8* blob;  // this member's packed parameters
+  unsigned skey0, skey1;  // dropout sample keys of the two slots (0 if no dropout)
+  unsigned thr;
+  float dsc;
+  int dropout;
+  int out_logits;
+};
+
+template <int LAYER, int WM, int WN, bool HEAD>
+__device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
+  char* act = smem;
+  const char* x0 = smem + kActBytes;
+  float* head = reinterpret_cast<float*>(smem + kActBytes + kX0Bytes);
+  const guint8* blob = X.blob;
+  constexpr int CIN = C[LAYER], COUT = C[LAYER + 1], K = KS[LAYER];
+  constexpr bool FIRST = (LAYER == 0);
+  constexpr int NSTEP = ksteps(LAYER);
+  constexpr int NCT = COUT / 16;
+  constexpr int CT = NCT / WN;
+  constexpr int RT = kRT / WM;
+  constexpr int PAD = (K - 1) / 2;
+  static_assert(NCT % WN == 0 && kRT % WM == 0 && WM * WN == kThreads / kWave, "wave tiling");
+  static_assert(FIRST || CIN % 32 == 0, "k-step must stay inside one tap");
+  static_assert(!HEAD || WM == kSlots, "head needs one sample slot per wave row");
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int m = lane & 15, h = lane >> 4;
+
+  const gbf16x8* wp = reinterpret_cast<const gbf16x8*>(blob + woff(LAYER)) + (wn * CT) * 64 + lane;
+  const int row0 = wm * RT * 16 + m;  // this lane's first output row (time row) in the tile
+
+  f32x4 acc[CT][RT];
+#pragma unroll
+  for (int c = 0; c < CT; ++c)
+#pragma unroll
+    for (int r = 0; r < RT; ++r) acc[c][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // B fragment (activations, LDS) of row tile r at k-step s
+  auto load_b = [&](int s, int r) -> bf16x8 {
+    if constexpr (FIRST) {
+      // k = tap*4 + ci: 8 consecutive k = two consecutive rows x 4 channels (16 B, 8-B aligned)
+      const char* base = x0 + (kHalo + row0 + r * 16 - PAD) * kX0RS + (32 * s + 8 * h) * 2;
+      const bf16x4 lo = *reinterpret_cast<const bf16x4*>(base);
+      const bf16x4 hi = *reinterpret_cast<const bf16x4*>(base + 8);
+      return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    } else {
+      constexpr int CB = CIN / 32;
+      const int tap = s / CB, cb = s - tap * CB;
+      return *reinterpret_cast<const bf16x8*>(act + (kHalo + row0 + r * 16 + tap - PAD) * kRS + (cb * 32 + 8 * h) * 2);
+    }
+  };
+  // A fragments (weights, global/L2) of k-step s
+  auto load_a = [&](int s, bf16x8 (&a)[CT]) {
+#pragma unroll
+    for (int c = 0; c < CT; ++c) a[c] = wp[(s * NCT + c) * 64];
+  };
+  auto step = [&](int s, const bf16x8 (&a)[CT]) {
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      const bf16x8 b = load_b(s, r);
+#pragma unroll
+      for (int c = 0; c < CT; ++c) acc[c][r] = mfma16(a[c], b, acc[c][r]);
+    }
+  };
+
+  // ---- K loop
+#ifndef APNEAUQ_A_DBUF
+#define APNEAUQ_A_DBUF 1
+#endif
+#if APNEAUQ_A_DBUF
+  bf16x8 a0[CT], a1[CT];
+  load_a(0, a0);
+#pragma unroll 1
+  for (int s = 0; s < NSTEP; s += 2) {
+    if (s + 1 < NSTEP) load_a(s + 1, a1);
+    step(s, a0);
+    if (s + 1 < NSTEP) {
+      if (s + 2 < NSTEP) load_a(s + 2, a0);
+      step(s + 1, a1);
+    }
+  }
+#else
+#pragma unroll 2
+  for (int s = 0; s < NSTEP; ++s) {
+    bf16x8 a0[CT];
+    load_a(s, a0);
+    step(s, a0);
+  }
+#endif
+
+  // ---- epilogue: bias + ReLU + BN(running) + dropout, then bf16 in place (or GAP head)
+  const unsigned thr = X.thr;
+  const float dsc = X.dsc;
+  const gfloat* epi = reinterpret_cast<const gfloat*>(blob + eoff(LAYER));
+
+  if constexpr (!HEAD) __syncthreads();  // every wave has finished reading this block's input
+
+  float gap = 0.f;  // HEAD: this lane's share of sum_t sum_co w[co] * y[t][co]
+#pragma unroll
+  for (int c = 0; c < CT; ++c) {
+    const int co0 = (wn * CT + c) * 16 + 4 * h;
+    const f32x4 bias = *reinterpret_cast<const gf32x4*>(epi + co0);
+    const f32x4 sc = *reinterpret_cast<const gf32x4*>(epi + COUT + co0);
+    const f32x4 sh = *reinterpret_cast<const gf32x4*>(epi + 2 * COUT + co0);
+    f32x4 dw;
+    if constexpr (HEAD) dw = *reinterpret_cast<const gf32x4*>(reinterpret_cast<const gfloat*>(blob + kDenseOff) + co0);
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      const int row = row0 + r * 16;
+      const int slot = row / kSR;
+      const int t = row - slot * kSR;
+      f32x4 v = acc[c][r];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i] + bias[i], 0.f) * sc[i] + sh[i];
+      if (X.dropout) {
+        const unsigned k = slot ? X.skey1 : X.skey0;
+        const unsigned b01 = dropout_bits2(k, t, co0);
+        const unsigned b23 = dropout_bits2(k, t, co0 + 2);
+        v[0] = (b01 & 0xFFFFu) >= thr ? v[0] * dsc : 0.f;
+        v[1] = (b01 >> 16) >= thr ? v[1] * dsc : 0.f;
+        v[2] = (b23 & 0xFFFFu) >= thr ? v[2] * dsc : 0.f;
+        v[3] = (b23 >> 16) >= thr ? v[3] * dsc : 0.f;
+      }
+      if (t >= kL) v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (HEAD) {
+        gap += v[0] * dw[0] + v[1] * dw[1] + v[2] * dw[2] + v[3] * dw[3];
+      } else {
+        bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+        *reinterpret_cast<bf16x4*>(act + (kHalo + row) * kRS + co0 * 2) = o;
+      }
+    }
+  }
+  if constexpr (HEAD) {
+    gap = wave_sum(gap);
+    if (lane == 0) head[wm * WN + wn] = gap;
+    __syncthreads();
+    if (threadIdx.x < kSlots) {
+      const int sl = threadIdx.x;
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < WN; ++j) s += head[sl * WN + j];
+      const float logit = s * (1.0f / kL) + reinterpret_cast<const gfloat*>(blob + kDenseOff)[C[6]];
+      head[8 + sl] = X.out_logits ? logit : 1.0f / (1.0f + __expf(-logit));
+    }
+  } else {
+    __syncthreads();  // block output visible before the next block reads it
+  }
+}
+
+__global__ __launch_bounds__(kThreads, 2) void fused_forward_kernel(Args A) {
+  char* act = smem;
+  char* x0 = smem + kActBytes;
+  float* head = reinterpret_cast<float*>(x0 + kX0Bytes);
+
+  // zero the halo rows once: leading / trailing rows of the activation and input buffers
+  for (int i = threadIdx.x; i < kHalo * kRS / 16; i += kThreads) {
+    reinterpret_cast<f32x4*>(act)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    reinterpret_cast<f32x4*>(act + (kHalo + kR) * kRS)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  if (threadIdx.x < kHalo * kX0RS / 16) {
+    reinterpret_cast<f32x4*>(x0)[threadIdx.x] = f32x4{0.f, 0.f, 0.f, 0.f};
+    reinterpret_cast<f32x4*>(x0 + (kHalo + kR) * kX0RS)[threadIdx.x] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  // XCD-aware item assignment (T1): blocks sharing an XCD get a contiguous item range, so a
+  // Deep-Ensemble member's weights stay in one XCD's L2.  Bijective for any grid size.
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q = nwg / 8, rem = nwg % 8, xcd = bid % 8;
+  const int wg = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + bid / 8;
+  const int samples = A.n_pass * A.n_win;
+  // One tile per workgroup.  (A persistent tile loop lets LICM hoist every block's address math
+  // out of the loop, which blows the 256-VGPR budget; one tile per launch slot keeps it at ~206.)
+  {
+    const int item = wg;
+    const int member = item / A.tiles_per_member;
+    const int tile = item - member * A.tiles_per_member;
+    const guint8* blob = (const guint8*)(A.blob) + (long long)member * A.blob_stride;
+    unsigned pass[kSlots], win[kSlots];
+    bool valid[kSlots];
+#pragma unroll
+    for (int sl = 0; sl < kSlots; ++sl) {
+      const int g = tile * kSlots + sl;
+      valid[sl] = g < samples;
+      const int gg = valid[sl] ? g : 0;
+      pass[sl] = gg / A.n_win;
+      win[sl] = gg - pass[sl] * A.n_win;
+    }
+    // stage the two input windows (480 B each) + 4 zero rows per slot into x0
+    if (threadIdx.x < kSlots * 32) {
+      const int sl = threadIdx.x >> 5, ch = threadIdx.x & 31;
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (ch < 30 && valid[sl])
+        v = reinterpret_cast<const f32x4*>(A.x + (long long)win[sl] * (kL * kCin))[ch];
+      reinterpret_cast<f32x4*>(x0 + (kHalo + sl * kSR) * kX0RS)[ch] = v;
+    }
+    __syncthreads();
+    BlockCtx X;
+    X.blob = blob;
+    X.dropout = A.dropout;
+    X.out_logits = A.out_logits;
+    X.skey0 = X.skey1 = 0u;
+#define APNEAUQ_CTX(L)                                                                                   \
+  X.thr = A.thr[L];                                                                                      \
+  X.dsc = A.dscale[L];                                                                                   \
+  if (A.dropout) {                                                                                       \
+    X.skey0 = sample_key(stream_key(A.seed, L, A.pass_offset + pass[0]), A.window_offset + win[0]);      \
+    X.skey1 = sample_key(stream_key(A.seed, L, A.pass_offset + pass[1]), A.window_offset + win[1]);      \
+  }
+    APNEAUQ_CTX(0) block<0, 1, 4, false>(X);
+    APNEAUQ_CTX(1) block<1, 1, 4, false>(X);
+    APNEAUQ_CTX(2) block<2, 2, 2, false>(X);
+    APNEAUQ_CTX(3) block<3, 2, 2, false>(X);
+    APNEAUQ_CTX(4) block<4, 1, 4, false>(X);
+    APNEAUQ_CTX(5) block<5, 2, 2, true>(X);
+#undef APNEAUQ_CTX
+    if (threadIdx.x < kSlots && valid[threadIdx.x]) {
+      const int sl = threadIdx.x;
+      A.out[((long long)member * A.n_pass + pass[sl]) * A.n_win + win[sl]] = head[8 + sl];
+    }
+  }
+}
+
+}  // namespace fused
+
+// ------------------------------------------------------------------------------------ host side
+int fused_blob_bytes() { return fused::kBlobBytes; }
+int fused_lds_bytes() { return fused::kLdsBytes; }
+void fused_layout(int* woffs, int* eoffs, int* dense_off) {
+  for (int l = 0; l < 6; ++l) {
+    woffs[l] = fused::woff(l);
+    eoffs[l] = fused::eoff(l);
+  }
+  *dense_off = fused::kDenseOff;
+}
+
+hipError_t launch_fused_forward(const void* x, const uint8_t* blob, long long blob_stride, float* out,
+                                int n_win, int n_pass, int n_member, unsigned window_offset,
+                                unsigned pass_offset, unsigned long long seed, int dropout,
+                                int out_logits, const unsigned* thr, const float* dscale, int grid,
+                                hipStream_t stream) {
+  fused::Args A;
+  A.x = reinterpret_cast<const __bf16*>(x);
+  A.blob = blob;
+  A.out = out;
+  A.blob_stride = blob_stride;
+  A.n_win = n_win;
+  A.n_pass = n_pass;
+  A.n_member = n_member;
+  A.tiles_per_member = (n_pass * n_win + fused::kSlots - 1) / fused::kSlots;
+  A.total_items = A.tiles_per_member * n_member;
+  (void)grid;
+  if (A.total_items < 1) return hipSuccess;
+  A.chunk = 1;
+  A.window_offset = window_offset;
+  A.pass_offset = pass_offset;
+  A.seed = seed;
+  A.dropout = dropout;
+  A.out_logits = out_logits;
+  for (int l = 0; l < 6; ++l) {  // thresholds come from ops/rng.py so host and device agree bit-exactly
+    A.thr[l] = thr ? thr[l] : 0u;
+    A.dscale[l] = dscale ? dscale[l] : 1.f;
+  }
+  hipLaunchKernelGGL(fused::fused_forward_kernel, dim3(A.total_items), dim3(fused::kThreads), fused::kLdsBytes, stream, A);
+  return hipGetLastError();
+}
+
+}  // namespace apneauq

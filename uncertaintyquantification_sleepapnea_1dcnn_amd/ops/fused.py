@@ -1,0 +1,160 @@
+"""Host side of the fused whole-network inference kernel (``csrc/fused_forward.hip``).
+
+``pack_blob`` turns one model's Keras-ordered parameters into the byte layout the kernel reads:
+per block the conv kernel transposed to ``W^T[co][k]`` (``k = tap*Cin + ci``, zero-padded to a
+multiple of 32) and re-ordered into v_mfma_f32_16x16x32_bf16 A-operand fragments (1 KiB per
+(k-step, 16-channel tile), lane ``l`` holding ``co = 16*tile + (l & 15)``,
+``k = 32*step + 8*(l >> 4) + j``), then the fp32 epilogue vectors ``[bias | bn_scale | bn_shift]``
+(inference BatchNorm folded to an affine), then the dense head.  The offsets are computed here
+and cross-checked against the kernel's own ``fused_layout()``.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..models.spec import DEFAULT_SPEC, ModelSpec
+from . import _ext, rng
+
+FUSED_CHANNELS = (4, 128, 192, 224, 96, 256, 96)
+FUSED_KSIZES = (7, 5, 3, 7, 9, 9)
+FUSED_LENGTH = 60
+
+
+def supports(spec: ModelSpec) -> bool:
+    """True if the fused kernel implements this architecture (the reference's no-pool CNN)."""
+    return (spec.input_length == FUSED_LENGTH and tuple(spec.channels()) == FUSED_CHANNELS
+            and tuple(b.kernel_size for b in spec.blocks) == FUSED_KSIZES and not spec.has_pool)
+
+
+def _ceil(a: int, b: int) -> int:
+    return (a + b - 1) // b * b
+
+
+def layout() -> Dict[str, object]:
+    ch, ks = FUSED_CHANNELS, FUSED_KSIZES
+    woff, eoff = [], []
+    off = 0
+    for l in range(6):
+        woff.append(off)
+        off += ((ch[l] * ks[l] + 31) // 32) * (ch[l + 1] // 16) * 1024
+    for l in range(6):
+        eoff.append(off)
+        off += _ceil(3 * ch[l + 1] * 4, 16)
+    dense = off
+    total = dense + _ceil((ch[6] + 1) * 4, 16)
+    return {"woff": woff, "eoff": eoff, "dense": dense, "bytes": total}
+
+
+def check_layout() -> None:
+    lay = layout()
+    v = list(_ext.ops().fused_layout())
+    want = lay["woff"] + lay["eoff"] + [lay["dense"], lay["bytes"]]
+    if v[:14] != want:
+        raise RuntimeError(f"fused blob layout mismatch host={want} kernel={v[:14]}")
+
+
+def pack_conv_fragments(kernel: torch.Tensor) -> torch.Tensor:
+    """Keras conv kernel (k, Cin, Cout) -> bf16 fragments (nstep, Cout/16, 64 lanes, 8)."""
+    k, cin, cout = kernel.shape
+    K = k * cin
+    nstep = (K + 31) // 32
+    wt = kernel.detach().float().reshape(K, cout).t()  # (cout, K), k = tap*cin + ci
+    wt = torch.nn.functional.pad(wt, (0, nstep * 32 - K))
+    fr = wt.reshape(cout // 16, 16, nstep, 4, 8).permute(2, 0, 3, 1, 4)  # (step, ct, h, m, j)
+    return fr.reshape(nstep, cout // 16, 64, 8).to(torch.bfloat16).contiguous()
+
+
+def unpack_conv_fragments(fr: torch.Tensor, k: int, cin: int, cout: int) -> torch.Tensor:
+    """Inverse of :func:`pack_conv_fragments` (returns fp32 (k, Cin, Cout))."""
+    nstep = fr.shape[0]
+    wt = fr.float().reshape(nstep, cout // 16, 4, 16, 8).permute(1, 3, 0, 2, 4).reshape(cout, nstep * 32)
+    return wt[:, : k * cin].t().reshape(k, cin, cout)
+
+
+def bn_affine(spec: ModelSpec, p, i: int):
+    gamma, beta = p[f"batchnorm_{i}/gamma"].float(), p[f"batchnorm_{i}/beta"].float()
+    mm, mv = p[f"batchnorm_{i}/moving_mean"].float(), p[f"batchnorm_{i}/moving_variance"].float()
+    scale = gamma * torch.rsqrt(mv + spec.bn_epsilon)
+    return scale, beta - mm * scale
+
+
+def pack_blob(spec: ModelSpec, p, bn_override: Optional[Sequence] = None) -> torch.Tensor:
+    """Pack one model into the fused kernel's byte blob (uint8, on the params' device).
+
+    ``bn_override``: optional list of 6 (scale, shift) pairs replacing the running-stat BN affine
+    (used by the batch-statistics MC-Dropout parity mode).
+    """
+    if not supports(spec):
+        raise ValueError("fused kernel supports only the reference (60, 4) no-pool architecture")
+    lay = layout()
+    dev = p["conv1d_1/kernel"].device
+    blob = torch.zeros(lay["bytes"], dtype=torch.uint8, device=dev)
+    for l in range(6):
+        i = l + 1
+        fr = pack_conv_fragments(p[f"conv1d_{i}/kernel"].to(dev))
+        b = fr.view(torch.uint8).reshape(-1)
+        blob[lay["woff"][l]: lay["woff"][l] + b.numel()] = b
+        if bn_override is not None:
+            scale, shift = bn_override[l]
+        else:
+            scale, shift = bn_affine(spec, p, i)
+        epi = torch.cat([p[f"conv1d_{i}/bias"].float().to(dev), scale.float().to(dev), shift.float().to(dev)])
+        e = epi.contiguous().view(torch.uint8)
+        blob[lay["eoff"][l]: lay["eoff"][l] + e.numel()] = e
+    head = torch.cat([p["output_layer/kernel"].float().reshape(-1), p["output_layer/bias"].float().reshape(-1)]).to(dev)
+    h = head.contiguous().view(torch.uint8)
+    blob[lay["dense"]: lay["dense"] + h.numel()] = h
+    return blob
+
+
+def dropout_tables(spec: ModelSpec):
+    thr = [rng.dropout_threshold(b.dropout) for b in spec.blocks]
+    dsc = [1.0 / (1.0 - b.dropout) if b.dropout < 1.0 else 0.0 for b in spec.blocks]
+    return thr, dsc
+
+
+def fused_forward(x_bf16: torch.Tensor, blobs: torch.Tensor, spec: ModelSpec = DEFAULT_SPEC, *, n_pass: int = 1,
+                  dropout: bool = False, seed: int = 0, window_offset: int = 0, pass_offset: int = 0,
+                  logits: bool = False) -> torch.Tensor:
+    """Run the fused kernel: returns (members, n_pass, N) fp32 probabilities (or logits)."""
+    o = _ext.ops()
+    if blobs.dim() == 1:
+        blobs = blobs.unsqueeze(0)
+    thr, dsc = dropout_tables(spec)
+    return o.fused_forward(x_bf16, blobs, int(n_pass), int(window_offset), int(pass_offset), int(seed) & ((1 << 63) - 1),
+                           bool(dropout), bool(logits), thr, dsc, 0)
+
+
+# ------------------------------------------------------------------------------------------------
+# CPU emulation of the kernel's arithmetic (bf16 operands, fp32 accumulate) straight from a blob.
+# Used by the CPU test tier to validate the packing and by the GPU tier as a tighter oracle.
+# ------------------------------------------------------------------------------------------------
+def emulate_blob_forward(blob: torch.Tensor, x: torch.Tensor, spec: ModelSpec = DEFAULT_SPEC, *, dropout: bool = False,
+                         seed: int = 0, pass_id: int = 0, sample_ids: Optional[torch.Tensor] = None,
+                         logits: bool = False) -> torch.Tensor:
+    from ..models.reference import conv1d_same
+
+    lay = layout()
+    blob = blob.cpu()
+    ch, ks = FUSED_CHANNELS, FUSED_KSIZES
+    n = x.shape[0]
+    if sample_ids is None:
+        sample_ids = torch.arange(n)
+    h = x.float().to(torch.bfloat16).float()
+    for l in range(6):
+        nstep = (ch[l] * ks[l] + 31) // 32
+        nbytes = nstep * (ch[l + 1] // 16) * 1024
+        fr = blob[lay["woff"][l]: lay["woff"][l] + nbytes].view(torch.bfloat16).reshape(nstep, ch[l + 1] // 16, 64, 8)
+        w = unpack_conv_fragments(fr, ks[l], ch[l], ch[l + 1])
+        epi = blob[lay["eoff"][l]: lay["eoff"][l] + 12 * ch[l + 1]].view(torch.float32).reshape(3, ch[l + 1])
+        y = conv1d_same(h, w, epi[0])
+        y = torch.relu(y) * epi[1] + epi[2]
+        if dropout:
+            y = rng.dropout_apply_torch(y, rng.stream_key(seed, l, pass_id), sample_ids, spec.blocks[l].dropout)
+        h = y if l == 5 else y.to(torch.bfloat16).float()
+    head = blob[lay["dense"]: lay["dense"] + 4 * (ch[6] + 1)].view(torch.float32)
+    logit = h.mean(dim=1) @ head[: ch[6]] + head[ch[6]]
+    return logit if logits else torch.sigmoid(logit)
