@@ -1,0 +1,62 @@
+"""GPU numerics of the UQ reduce / bootstrap / Adam HIP kernels vs fp32/fp64 host references."""
+import numpy as np
+import pytest
+import torch
+
+from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import _ext
+from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import uq as uq_ops
+from uncertaintyquantification_sleepapnea_1dcnn_amd.training.optim import Adam
+from uncertaintyquantification_sleepapnea_1dcnn_amd.uq import metrics as M
+
+pytestmark = pytest.mark.gpu
+
+
+def test_uq_reduce_matches_numpy():
+    _ext.require()
+    rs = np.random.RandomState(0)
+    p = np.clip(rs.rand(50, 3001), 0, 1).astype(np.float32)
+    p[:, 0] = 0.0
+    p[:, 1] = 1.0
+    m = uq_ops.metrics(torch.from_numpy(p).cuda()).cpu().numpy()
+    w = M.per_window(p)
+    np.testing.assert_allclose(m[uq_ops.MEAN], w["mean_pred"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(m[uq_ops.VAR], w["pred_variance"], rtol=1e-4, atol=1e-7)
+    np.testing.assert_allclose(m[uq_ops.ENT_NATS], w["total_pred_entropy"], rtol=1e-4, atol=2e-6)
+    np.testing.assert_allclose(m[uq_ops.EXP_ENT], w["expected_aleatoric_entropy"], rtol=1e-4, atol=2e-6)
+    np.testing.assert_allclose(m[uq_ops.MI], w["mutual_info"], rtol=1e-3, atol=5e-6)
+    np.testing.assert_allclose(m[uq_ops.ENT_BITS], M.binary_entropy_bits(w["mean_pred"]), rtol=1e-4, atol=2e-6)
+    np.testing.assert_array_equal(m[uq_ops.LABEL], (w["mean_pred"] > 0.5).astype(np.float32))
+
+
+@pytest.mark.parametrize("parity", [True, False])
+def test_bootstrap_kernel(parity):
+    _ext.require()
+    rs = np.random.RandomState(1)
+    p = rs.rand(7, 2000).astype(np.float32)
+    y = (rs.rand(2000) > 0.7).astype(np.int32)
+    w = M.per_window(p)
+    mt = uq_ops.metrics(torch.from_numpy(p).cuda())
+    if parity:
+        idx = M.parity_bootstrap_indices(2000, 20, 2025)
+        got = uq_ops.bootstrap(mt, torch.from_numpy(y).cuda(), 20, idx=torch.from_numpy(idx.astype(np.int32)).cuda())
+    else:
+        idx = uq_ops._hash_idx(2000, 20, 2025, "cpu").numpy()
+        got = uq_ops.bootstrap(mt, torch.from_numpy(y).cuda(), 20, seed=2025)
+    ref = M.bootstrap_from_windows(w, y, idx)
+    got = got.cpu().numpy()
+    for b in range(20):
+        np.testing.assert_allclose(got[b], [ref[b][k] for k in M.AGG_KEYS], rtol=2e-4, atol=1e-7)
+
+
+def test_adam_kernel_matches_eager():
+    _ext.require()
+    n = 851457
+    g = torch.Generator().manual_seed(0)
+    p0 = torch.randn(n, generator=g)
+    grads = [torch.randn(n, generator=g) for _ in range(3)]
+    a, b = Adam(1e-3), Adam(1e-3)
+    pa, pb = p0.clone(), p0.clone().cuda()
+    for gr in grads:
+        a.step(pa, gr)
+        b.step(pb, gr.cuda())
+    torch.testing.assert_close(pb.cpu(), pa, rtol=1e-6, atol=1e-6)

@@ -1,0 +1,55 @@
+// Multi-tensor Adam over the model's single flat fp32 parameter buffer (gfx950).
+//
+// Keras 2.12 Adam (the optimizer of cnn_baseline_train.py:100, lr 1e-3):
+//   m += (g - m) * (1 - b1);  v += (g^2 - v) * (1 - b2)
+//   p -= alpha * m / (sqrt(v) + eps),   alpha = lr * sqrt(1 - b2^t) / (1 - b1^t),  eps = 1e-7
+// One launch updates all 26 trainable tensors (851,457 values): 16-B vector loads/stores, grid
+// sized to the chip and grid-strided.  Optionally averages a data-parallel gradient (scale).
+#include "common.h"
+
+namespace apneauq {
+
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v, long long n,
+                                                    float b1, float b2, float alpha, float eps, float gscale) {
+  const long long n4 = n >> 2;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const float c1 = 1.f - b1, c2 = 1.f - b2;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    f32x4 pp = reinterpret_cast<f32x4*>(p)[i];
+    f32x4 gg = reinterpret_cast<const f32x4*>(g)[i] * gscale;
+    f32x4 mm = reinterpret_cast<f32x4*>(m)[i];
+    f32x4 vv = reinterpret_cast<f32x4*>(v)[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      mm[k] += (gg[k] - mm[k]) * c1;
+      vv[k] += (gg[k] * gg[k] - vv[k]) * c2;
+      pp[k] -= alpha * mm[k] / (sqrtf(vv[k]) + eps);
+    }
+    reinterpret_cast<f32x4*>(p)[i] = pp;
+    reinterpret_cast<f32x4*>(m)[i] = mm;
+    reinterpret_cast<f32x4*>(v)[i] = vv;
+  }
+  // scalar tail
+  const long long t = (n4 << 2) + blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (t < n && t < (n4 << 2) + 4) {
+    const float gg = g[t] * gscale;
+    float mm = m[t] + (gg - m[t]) * c1;
+    float vv = v[t] + (gg * gg - v[t]) * c2;
+    p[t] -= alpha * mm / (sqrtf(vv) + eps);
+    m[t] = mm;
+    v[t] = vv;
+  }
+}
+
+hipError_t launch_adam(float* p, const float* g, float* m, float* v, long long n, float b1, float b2, float alpha,
+                       float eps, float gscale, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  long long blocks = ((n >> 2) + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p, g, m, v, n, b1, b2, alpha, eps, gscale);
+  return hipGetLastError();
+}
+
+}  // namespace apneauq

@@ -20,6 +20,8 @@ void fused_layout(int* woffs, int* eoffs, int* dense_off);
 hipError_t launch_uq_reduce(const float* probs, int t_count, int n, float* out, hipStream_t stream);
 hipError_t launch_bootstrap(const float* metrics, const int* y, const int* idx, unsigned seed, int n, int n_boot,
                             double* out, hipStream_t stream);
+hipError_t launch_adam(float* p, const float* g, float* m, float* v, long long n, float b1, float b2, float alpha,
+                       float eps, float gscale, hipStream_t stream);
 }  // namespace apneauq
 
 namespace {
@@ -100,6 +102,19 @@ at::Tensor bootstrap(const at::Tensor& metrics, const at::Tensor& y, const c10::
   return out;
 }
 
+void adam_step(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v, double b1, double b2, double alpha,
+               double eps, double gscale) {
+  TORCH_CHECK(p.is_cuda() && g.is_cuda() && m.is_cuda() && v.is_cuda(), "adam_step: GPU tensors required");
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&p, &g, &m, &v})
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == p.numel() &&
+                    reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
+                "adam_step: contiguous, 16-B aligned fp32 tensors of equal size required");
+  const at::DeviceGuard guard(p.device());
+  check(apneauq::launch_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                             p.numel(), (float)b1, (float)b2, (float)alpha, (float)eps, (float)gscale, cur_stream()),
+        "adam_step");
+}
+
 std::vector<int64_t> fused_layout() {
   int w[6], e[6], d;
   apneauq::fused_layout(w, e, &d);
@@ -120,10 +135,13 @@ TORCH_LIBRARY(apneauq, m) {
   m.def("uq_reduce(Tensor probs) -> Tensor");
   m.def("bootstrap(Tensor metrics, Tensor y, Tensor? idx, int seed, int n_boot) -> Tensor");
   m.def("fused_layout() -> int[]", &fused_layout);
+  m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, float b1, float b2, float alpha, float eps, "
+        "float gscale) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
   m.impl("fused_forward", &fused_forward);
   m.impl("uq_reduce", &uq_reduce);
   m.impl("bootstrap", &bootstrap);
+  m.impl("adam_step", &adam_step);
 }

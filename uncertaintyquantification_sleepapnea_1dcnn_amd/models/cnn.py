@@ -1,0 +1,235 @@
+"""``AlarconCNN1D`` — the Keras-like model object of the framework.
+
+API parity with what the reference scripts call on their ``tf.keras.Model``
+(``al_1d_cnn_create_model`` at ``cnn_baseline_train.py:37``): ``model(x, training=...)``,
+``predict``, ``fit``, ``evaluate``, ``get_weights`` / ``set_weights`` (38 Keras-ordered arrays),
+``save`` / :func:`load_model`, ``summary``, ``count_params``.
+
+Execution backends (MI355X-first):
+
+* inference (``training=False`` / ``predict``) on the GPU runs the fused whole-network HIP
+  kernel (``ops/fused.py``); the packed weight blob is cached and invalidated on any update;
+* training steps run the layer-wise path (autograd over the fp32 reference ops today, HIP
+  conv kernels where available) with the Keras BatchNorm/Dropout/Adam semantics;
+* ``model(x, training=True)`` reproduces Keras exactly: dropout on, BatchNorm on the statistics of
+  the batch passed in, moving averages updated as a side effect (the reference's MC Dropout
+  quirk).
+On the CPU everything runs the fp32 reference.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..ops import _ext, fused, rng
+from . import reference as R
+from .params import ParamStore
+from .spec import ModelSpec
+
+
+def _default_device():
+    return torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
+
+
+class AlarconCNN1D:
+    def __init__(self, input_shape: Sequence[int] = (60, 4), spec: Optional[ModelSpec] = None, seed: int = 2025,
+                 device=None, name: str = "Alarcon_1D_CNN_Model", params=None, pool: bool = False):
+        self.spec = spec if spec is not None else ModelSpec.with_input(input_shape, pool=pool)
+        self.name = name
+        self.seed = int(seed)
+        self.device = torch.device(device) if device is not None else _default_device()
+        init = params if params is not None else R.init_params(self.spec, self.seed)
+        self.store = ParamStore(self.spec, init, self.device)
+        from ..training.optim import Adam
+
+        self.optimizer = Adam(1e-3)
+        self.loss = "binary_crossentropy"
+        self.metrics_names = ["loss", "accuracy", "auc"]
+        self.stop_training = False
+        self._blob = None
+        self._blob_version = -1
+        self._call_counter = 0
+        self._train_step_counter = 0
+
+    # ------------------------------------------------------------------ Keras-like surface
+    def compile(self, optimizer=None, loss="binary_crossentropy", metrics=None):
+        if optimizer is not None:
+            self.optimizer = optimizer
+        self.loss = loss
+        return self
+
+    @property
+    def input_shape(self) -> Tuple[Optional[int], int, int]:
+        return (None, self.spec.input_length, self.spec.input_channels)
+
+    def count_params(self) -> int:
+        return self.spec.num_params()[0]
+
+    def get_weights(self) -> List[np.ndarray]:
+        return self.store.get_weights()
+
+    def set_weights(self, arrays) -> None:
+        self.store.set_weights(arrays)
+
+    @property
+    def params(self):
+        return self.store.as_dict()
+
+    def snapshot(self):
+        return self.store.snapshot()
+
+    def restore(self, snap) -> None:
+        self.store.restore(snap)
+
+    def summary(self, print_fn=print) -> str:
+        ch, ln = self.spec.channels(), self.spec.lengths()
+        rows = [f'Model: "{self.name}"', "_" * 72, f"{'Layer (type)':<34}{'Output Shape':<22}{'Param #':>12}", "=" * 72]
+        for i, b in enumerate(self.spec.blocks, start=1):
+            rows.append(f"{f'conv1d_{i} (Conv1D)':<34}{str((None, ln[i - 1], b.filters)):<22}"
+                        f"{b.kernel_size * ch[i - 1] * b.filters + b.filters:>12,}")
+            rows.append(f"{f'batchnorm_{i} (BatchNormalization)':<34}{str((None, ln[i - 1], b.filters)):<22}{4 * b.filters:>12,}")
+            if b.pool:
+                rows.append(f"{f'maxpool_{i} (MaxPooling1D)':<34}{str((None, ln[i], b.filters)):<22}{0:>12}")
+            rows.append(f"{f'dropout_{i} (Dropout)':<34}{str((None, ln[i], b.filters)):<22}{0:>12}")
+        rows.append(f"{'global_avg_pooling_1d (GlobalAveragePooling1D)':<34}{str((None, ch[-1])):<22}{0:>12}")
+        rows.append(f"{'output_layer (Dense)':<34}{str((None, 1)):<22}{ch[-1] + 1:>12,}")
+        tot, tr = self.spec.num_params()
+        rows += ["=" * 72, f"Total params: {tot:,}", f"Trainable params: {tr:,}", f"Non-trainable params: {tot - tr:,}",
+                 "_" * 72]
+        text = "\n".join(rows)
+        if print_fn is not None:
+            print_fn(text)
+        return text
+
+    def to(self, device) -> "AlarconCNN1D":
+        self.device = torch.device(device)
+        self.store = self.store.to(self.device)
+        self._blob = None
+        return self
+
+    # ------------------------------------------------------------------ inference
+    def _as_input(self, x) -> torch.Tensor:
+        if isinstance(x, torch.Tensor):
+            t = x.to(self.device, torch.float32)
+        else:
+            t = torch.as_tensor(np.asarray(x), dtype=torch.float32, device=self.device)
+        if t.dim() != 3 or t.shape[1] != self.spec.input_length or t.shape[2] != self.spec.input_channels:
+            raise ValueError(f"expected input (N, {self.spec.input_length}, {self.spec.input_channels}), got {tuple(t.shape)}")
+        return t
+
+    def uses_fused(self) -> bool:
+        return self.device.type == "cuda" and fused.supports(self.spec)
+
+    def fused_blob(self) -> torch.Tensor:
+        """Packed parameters for the fused HIP kernel (cached per weight version)."""
+        if self._blob is None or self._blob_version != self.store.version:
+            self._blob = fused.pack_blob(self.spec, self.store.as_dict()).unsqueeze(0)
+            self._blob_version = self.store.version
+        return self._blob
+
+    def logits(self, x, training: bool = False, *, dropout: Optional[bool] = None,
+               bn_batch_stats: Optional[bool] = None, update_moving: Optional[bool] = None, seed: Optional[int] = None,
+               pass_id: Optional[int] = None, sample_ids=None) -> torch.Tensor:
+        x = self._as_input(x)
+        use_drop = training if dropout is None else dropout
+        use_batch = training if bn_batch_stats is None else bn_batch_stats
+        if not use_batch and self.uses_fused():
+            _ext.require()
+            sid = 0 if sample_ids is None else int(sample_ids)
+            out = fused.fused_forward(x.to(torch.bfloat16).contiguous(), self.fused_blob(), self.spec, n_pass=1,
+                                      dropout=use_drop, seed=self.seed if seed is None else seed,
+                                      pass_offset=0 if pass_id is None else pass_id, window_offset=sid, logits=True)
+            return out[0, 0].reshape(-1, 1)
+        upd = use_batch if update_moving is None else update_moving
+        with torch.no_grad():
+            out = R.forward(self.spec, self.store.as_dict(), x, dropout=use_drop, bn_batch_stats=use_batch,
+                            update_moving=upd, seed=self.seed if seed is None else seed,
+                            pass_id=0 if pass_id is None else pass_id, return_logits=True,
+                            sample_ids=sample_ids if isinstance(sample_ids, torch.Tensor) else None)
+        if upd and use_batch:
+            self.store.bump()
+        return out
+
+    def __call__(self, x, training: bool = False) -> torch.Tensor:
+        """Keras ``model(x, training=...)``: returns (N, 1) fp32 probabilities on the model device.
+
+        ``training=True`` draws a fresh dropout stream per call (pass id = call counter).
+        """
+        pass_id = None
+        if training:
+            pass_id = self._call_counter
+            self._call_counter += 1
+        return torch.sigmoid(self.logits(x, training=training, pass_id=pass_id))
+
+    def predict(self, x, batch_size: int = 32, verbose: int = 0) -> np.ndarray:
+        """Inference-mode probabilities (N, 1) as float32 NumPy (``model.predict``).
+
+        The fused kernel processes the whole array in one launch; ``batch_size`` only bounds the
+        CPU path's memory (results are independent of it).
+        """
+        x = self._as_input(x)
+        if self.uses_fused():
+            return torch.sigmoid(self.logits(x)).cpu().numpy()
+        outs = []
+        step = max(int(batch_size), 4096)
+        for s in range(0, x.shape[0], step):
+            outs.append(torch.sigmoid(self.logits(x[s: s + step])).cpu().numpy())
+        return np.concatenate(outs) if outs else np.zeros((0, 1), np.float32)
+
+    # ------------------------------------------------------------------ training
+    def train_step(self, x, y, return_probs: bool = False, grad_allreduce=None):
+        """One optimizer step on a batch (Keras training semantics); returns the summed BCE."""
+        from ..training import step as tstep
+
+        loss_sum, probs = tstep.train_step(self, self._as_input(x), torch.as_tensor(y, device=self.device).float(),
+                                           grad_allreduce=grad_allreduce)
+        self._train_step_counter += 1
+        self.store.bump()
+        if return_probs:
+            return loss_sum, probs
+        return float(loss_sum)
+
+    def fit(self, x, y, batch_size: int = 32, epochs: int = 1, verbose: int = 1, callbacks=None,
+            validation_split: float = 0.0, validation_data=None, shuffle: bool = True, **kw):
+        from ..training.trainer import fit as _fit
+
+        return _fit(self, x, y, batch_size=batch_size, epochs=epochs, verbose=verbose, callbacks=callbacks,
+                    validation_split=validation_split, validation_data=validation_data, shuffle=shuffle, **kw)
+
+    def evaluate(self, x, y, batch_size: int = 32, verbose: int = 0):
+        from ..training.trainer import evaluate_arrays
+
+        X = self._as_input(x)
+        Y = torch.as_tensor(np.asarray(y), dtype=torch.float32, device=self.device)
+        return list(evaluate_arrays(self, X, Y, max(batch_size, 1024)))
+
+    # ------------------------------------------------------------------ persistence
+    def save(self, path: str, include_optimizer: bool = False) -> str:
+        from ..utils.checkpoint import save_weights
+
+        opt = None
+        if include_optimizer and self.optimizer.m is not None:
+            opt = {"m": self.optimizer.m.cpu().numpy(), "v": self.optimizer.v.cpu().numpy(),
+                   "iterations": np.array(self.optimizer.iterations)}
+        return save_weights(path, self.spec, self.get_weights(), self.name, extra={"seed": self.seed}, opt_state=opt)
+
+
+def load_model(path: str, device=None) -> AlarconCNN1D:
+    """Load a checkpoint written by :meth:`AlarconCNN1D.save` (safe: no code is deserialised)."""
+    from ..utils.checkpoint import load_weights
+
+    spec, arrays, cfg, opt = load_weights(path)
+    m = AlarconCNN1D(spec=spec, seed=int(cfg.get("extra", {}).get("seed", 2025)), device=device,
+                     name=cfg.get("name", "Alarcon_1D_CNN_Model"), params=R.params_from_list(spec, arrays))
+    if opt:
+        m.optimizer.iterations = int(opt["iterations"])
+        m.optimizer.m = torch.from_numpy(opt["m"]).to(m.device)
+        m.optimizer.v = torch.from_numpy(opt["v"]).to(m.device)
+    return m
+
+
+def al_1d_cnn_create_model(input_shape: Sequence[int] = (60, 4), seed: int = 2025, device=None) -> AlarconCNN1D:
+    """Factory with the reference's name (``cnn_baseline_train.py:37``); returns a compiled model."""
+    return AlarconCNN1D(input_shape=input_shape, seed=seed, device=device).compile()

@@ -95,6 +95,7 @@ def forward(
     pass_id: int = 0,
     sample_ids: Optional[torch.Tensor] = None,
     return_logits: bool = False,
+    bn_stats_hook=None,
 ) -> torch.Tensor:
     """Forward pass; returns probabilities (N, 1) (or logits).
 
@@ -102,7 +103,8 @@ def forward(
     statistics.  ``dropout`` / ``bn_batch_stats`` override the two independently
     (``dropout=True, bn_batch_stats=False`` is standard MC Dropout, bn_mode="running").
     ``update_moving`` applies the Keras moving-average update in place (the side effect of
-    the reference MC Dropout loop).
+    the reference MC Dropout loop).  ``bn_stats_hook(h) -> (mean, var)`` replaces the
+    local batch statistics (data-parallel SyncBN: global moments via a differentiable all-reduce).
     """
     use_drop = training if dropout is None else dropout
     use_batch = training if bn_batch_stats is None else bn_batch_stats
@@ -115,8 +117,11 @@ def forward(
         gamma, beta = p[f"batchnorm_{i}/gamma"], p[f"batchnorm_{i}/beta"]
         mm, mv = p[f"batchnorm_{i}/moving_mean"], p[f"batchnorm_{i}/moving_variance"]
         if use_batch:
-            mean = h.mean(dim=(0, 1))
-            var = h.var(dim=(0, 1), unbiased=False)
+            if bn_stats_hook is not None:
+                mean, var = bn_stats_hook(h)
+            else:
+                mean = h.mean(dim=(0, 1))
+                var = h.var(dim=(0, 1), unbiased=False)
             if update_moving:
                 with torch.no_grad():
                     mm.mul_(spec.bn_momentum).add_(mean.detach() * (1 - spec.bn_momentum))

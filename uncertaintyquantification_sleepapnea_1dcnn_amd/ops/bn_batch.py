@@ -1,0 +1,60 @@
+"""MC Dropout with BatchNorm on batch statistics — exact reference semantics.
+
+The reference's ``mc_dropout_predict`` calls ``model(x_test, training=True)`` T times with the
+WHOLE test set as one batch (``uq_techniques.py:22``): dropout on, every BN layer normalises with
+the mean / biased variance of that pass's activations over all windows, and the moving averages
+are updated as a side effect (momentum 0.99, once per pass and layer).  Statistics are global over
+the test set, so execution is layer-synchronous: block l of every window must finish before block
+l+1 of any window can be normalised.
+
+``mc_dropout_batch_bn`` reproduces this.  With several GPUs the per-layer moments are combined
+with an all-reduce of (sum, sum of squares, count) per channel so that the result
+equals the single-device full-batch computation.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ..models import reference as R
+
+
+def _moments_hook(group=None):
+    import torch.distributed as dist
+
+    def hook(h: torch.Tensor):
+        s1 = h.sum(dim=(0, 1), dtype=torch.float64)
+        s2 = (h.double() * h.double()).sum(dim=(0, 1))
+        cnt = torch.tensor([h.shape[0] * h.shape[1]], dtype=torch.float64, device=h.device)
+        if dist.is_available() and dist.is_initialized():
+            buf = torch.cat([s1, s2, cnt])
+            dist.all_reduce(buf, group=group)
+            c = s1.numel()
+            s1, s2, cnt = buf[:c], buf[c: 2 * c], buf[2 * c:]
+        mean = s1 / cnt
+        var = (s2 / cnt - mean * mean).clamp_min(0)
+        return mean.float(), var.float()
+
+    return hook
+
+
+@torch.no_grad()
+def mc_dropout_batch_bn(model, x, n_pred: int, seed: Optional[int] = None, window_offset: int = 0,
+                        distributed: bool = False, update_moving: bool = True) -> torch.Tensor:
+    """(T, N, 1) probabilities; each pass = Keras ``model(x, training=True)`` on the full set."""
+    xt = model._as_input(x)
+    n = xt.shape[0]
+    sample_ids = torch.arange(window_offset, window_offset + n, device=xt.device)
+    hook = _moments_hook() if distributed else None
+    outs = []
+    base = model._call_counter
+    for t in range(n_pred):
+        logit = R.forward(model.spec, model.store.as_dict(), xt, dropout=True, bn_batch_stats=True,
+                          update_moving=update_moving, seed=model.seed if seed is None else seed,
+                          pass_id=base + t, sample_ids=sample_ids, return_logits=True, bn_stats_hook=hook)
+        outs.append(torch.sigmoid(logit))
+    model._call_counter = base + n_pred
+    if update_moving:
+        model.store.bump()
+    return torch.stack(outs)

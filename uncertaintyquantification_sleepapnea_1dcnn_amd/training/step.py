@@ -1,0 +1,60 @@
+"""One Keras-semantics optimizer step (forward in training mode, BCE-on-logits, backward, Adam).
+
+Backends:
+* ``"hip"``  — layer-wise HIP kernels (``ops/train_ops.py``) when the extension provides them;
+* ``"torch"``— autograd over the fp32 reference ops (CPU, and the fallback/oracle on GPU).
+
+Gradients land in ONE flat fp32 buffer (views of ``ParamStore.flat``), so the data-parallel
+all-reduce is a single bucket and Adam is a single launch.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from ..models import reference as R
+
+TRAIN_PASS_BASE = 1 << 30  # dropout pass ids used by training steps (disjoint from MC-Dropout passes)
+
+
+def _backend(model) -> str:
+    b = os.environ.get("APNEAUQ_TRAIN_BACKEND", "auto")
+    if b != "auto":
+        return b
+    if model.device.type == "cuda":
+        from ..ops import train_ops
+
+        if train_ops.supports(model.spec):
+            return "hip"
+    return "torch"
+
+
+def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None):
+    backend = _backend(model)
+    if backend == "hip":
+        from ..ops import train_ops
+
+        return train_ops.train_step(model, x, y, grad_allreduce=grad_allreduce)
+    store = model.store
+    flat = store.flat.detach().requires_grad_(True)
+    p = {}
+    for n in store.trainable:
+        off = store.offsets[n]
+        k = store.views[n].numel()
+        p[n] = flat[off: off + k].view(store.shapes[n])
+    for n in store.nontrainable:
+        p[n] = store.views[n]
+    sample_ids = torch.arange(x.shape[0], device=x.device)
+    logits = R.forward(model.spec, p, x, dropout=True, bn_batch_stats=True, update_moving=True, seed=model.seed,
+                       pass_id=TRAIN_PASS_BASE + model._train_step_counter, sample_ids=sample_ids,
+                       return_logits=True, bn_stats_hook=getattr(model, "bn_stats_hook", None))
+    lv = torch.nn.functional.binary_cross_entropy_with_logits(logits.reshape(-1), y.reshape(-1), reduction="none")
+    loss = lv.mean()
+    loss.backward()
+    grad = flat.grad
+    scale = 1.0
+    if grad_allreduce is not None:
+        scale = grad_allreduce(grad)
+    model.optimizer.step(store.flat, grad, grad_scale=scale)
+    return lv.detach().sum().double(), torch.sigmoid(logits.detach()).reshape(-1)
