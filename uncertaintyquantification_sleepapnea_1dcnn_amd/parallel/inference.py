@@ -61,9 +61,9 @@ def aggregate_sums(metrics: torch.Tensor, y: Optional[torch.Tensor]) -> torch.Te
     if y is not None:
         m0 = (y == 0)
         m1 = (y == 1)
-        out[2] = var[m0].sum()
+        out[2] = (var * m0).sum()
         out[3] = m0.sum()
-        out[4] = var[m1].sum()
+        out[4] = (var * m1).sum()
         out[5] = m1.sum()
     out[6] = metrics[uq_ops.ENT_NATS].double().sum()
     out[7] = metrics[uq_ops.EXP_ENT].double().sum()
