@@ -1,0 +1,87 @@
+"""GPU numerics of the layer-wise HIP training kernels vs fp32 autograd over the reference ops."""
+import numpy as np
+import pytest
+import torch
+
+from uncertaintyquantification_sleepapnea_1dcnn_amd.models import reference as R
+from uncertaintyquantification_sleepapnea_1dcnn_amd.models.cnn import AlarconCNN1D
+from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import _ext, train_ops
+from uncertaintyquantification_sleepapnea_1dcnn_amd.training.step import TRAIN_PASS_BASE
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch_grads(model, x, y):
+    store = model.store
+    flat = store.flat.detach().clone().requires_grad_(True)
+    stats = store.stats.detach().clone()
+    p = {}
+    for n in store.trainable:
+        off = store.offsets[n]
+        p[n] = flat[off: off + store.views[n].numel()].view(store.shapes[n])
+    off = 0
+    for n in store.nontrainable:
+        k = store.views[n].numel()
+        p[n] = stats[off: off + k].view(store.shapes[n])
+        off += k
+    logits = R.forward(model.spec, p, x, dropout=True, bn_batch_stats=True, update_moving=True, seed=model.seed,
+                       pass_id=TRAIN_PASS_BASE + model._train_step_counter, sample_ids=torch.arange(x.shape[0], device=x.device),
+                       return_logits=True)
+    lv = torch.nn.functional.binary_cross_entropy_with_logits(logits.reshape(-1), y, reduction="none")
+    lv.mean().backward()
+    return lv.sum().item(), flat.grad.detach(), stats, logits.detach().reshape(-1)
+
+
+def _rel(a, b):
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("n", [64, 37])
+def test_hip_train_step_matches_autograd(n):
+    _ext.require()
+    dev = torch.device("cuda")
+    m = AlarconCNN1D(seed=5, device=dev)
+    g = torch.Generator().manual_seed(n)
+    x = torch.randn(n, 60, 4, generator=g).to(dev)
+    y = (torch.rand(n, generator=g) > 0.5).float().to(dev)
+    m.optimizer.learning_rate = 0.0
+    ref_loss, ref_grad, ref_stats, ref_logits = _torch_grads(m, x, y)
+    loss, probs = train_ops.train_step(m, x, y)
+    ws = m._train_ws
+    assert abs(loss.item() - ref_loss) / ref_loss < 2e-2
+    torch.testing.assert_close(ws.logits[:n], ref_logits, atol=5e-2, rtol=5e-2)
+    st = m.store
+    for name in st.trainable:
+        off, k = st.offsets[name], st.views[name].numel()
+        e = _rel(ws.grad[off: off + k], ref_grad[off: off + k])
+        assert e < 0.08, (name, e)
+    torch.testing.assert_close(st.stats, ref_stats, atol=2e-3, rtol=2e-2)
+
+
+def test_batch_stats_mc_dropout_matches_reference():
+    _ext.require()
+    dev = torch.device("cuda")
+    m = AlarconCNN1D(seed=6, device=dev)
+    x = torch.randn(50, 60, 4, generator=torch.Generator().manual_seed(0)).to(dev)
+    snap = m.snapshot()
+    got = train_ops.forward_batch_stats(m, x, 3, pass_base=0, seed=m.seed, update_moving=True)
+    hip_stats = m.store.stats.clone()
+    m.restore(snap)
+    ref = []
+    for t in range(3):
+        ref.append(torch.sigmoid(R.forward(m.spec, m.store.as_dict(), x, dropout=True, bn_batch_stats=True,
+                                           update_moving=True, seed=m.seed, pass_id=t, return_logits=True)).reshape(-1))
+    ref = torch.stack(ref)
+    torch.testing.assert_close(got, ref, atol=3e-2, rtol=3e-2)
+    torch.testing.assert_close(hip_stats, m.store.stats, atol=2e-3, rtol=2e-2)
+
+
+def test_hip_training_reduces_loss():
+    _ext.require()
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.data.synthetic import synthetic_windows
+
+    x, y, _ = synthetic_windows(2048, seed=1)
+    m = AlarconCNN1D(seed=1, device="cuda")
+    h = m.fit(x, y.astype(np.float32), batch_size=256, epochs=3, validation_split=0.1, verbose=0)
+    assert h.history["loss"][-1] < h.history["loss"][0]
+    assert h.history["val_accuracy"][-1] > 0.8

@@ -7,6 +7,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <cstring>
 #include <vector>
 
 namespace apneauq {
@@ -22,6 +23,28 @@ hipError_t launch_bootstrap(const float* metrics, const int* y, const int* idx, 
                             double* out, hipStream_t stream);
 hipError_t launch_adam(float* p, const float* g, float* m, float* v, long long n, float b1, float b2, float alpha,
                        float eps, float gscale, hipStream_t stream);
+namespace train {
+struct Layer {
+  const void* wf; const void* wd; const float* bias; const float* gamma; const float* beta;
+  float* mmean; float* mvar; float* gw; float* gb; float* ggamma; float* gbeta;
+  void* R; void* dY; float* st; float* bst; unsigned thr; float dsc;
+};
+struct Args {
+  Layer L[6];
+  const void* x; const float* y; const float* dense_w; const float* dense_b; float* g_dense_w; float* g_dense_b;
+  float* logits; float* dlogit; float* loss_sum;
+  int B; int n_win; int groups; unsigned pass_base; unsigned window_offset; unsigned long long seed; int dropout;
+  float inv_count; float inv_batch; float eps; float momentum;
+};
+}  // namespace train
+int train_args_size();
+int train_layer_size();
+hipError_t train_launch_fwd(const train::Args& A, int l, hipStream_t st);
+hipError_t train_launch_head(const train::Args& A, int backward, hipStream_t st);
+hipError_t train_launch_dgrad(const train::Args& A, int l, hipStream_t st);
+hipError_t train_launch_wgrad(const train::Args& A, int l, hipStream_t st);
+hipError_t train_launch_finalize(const train::Args& A, int update_moving, int grads, hipStream_t st);
+hipError_t train_launch_pack(const float* w, int k, int cin, int cout, void* fwd, void* dgr, hipStream_t st);
 }  // namespace apneauq
 
 namespace {
@@ -115,6 +138,98 @@ void adam_step(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
         "adam_step");
 }
 
+// ctx: int64 CPU tensor of device pointers / scalars built once per workspace (ops/train_ops.py)
+constexpr int kCtxLayer = 17, kCtxLen = 6 * kCtxLayer + 20;
+
+float bits_to_float(int64_t v) {
+  uint32_t u = static_cast<uint32_t>(v);
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+apneauq::train::Args args_from_ctx(const at::Tensor& ctx, int64_t pass_base) {
+  TORCH_CHECK(apneauq::train_args_size() == (int)sizeof(apneauq::train::Args) &&
+                  apneauq::train_layer_size() == (int)sizeof(apneauq::train::Layer),
+              "train Args ABI mismatch between bindings and kernels");
+  TORCH_CHECK(ctx.device().is_cpu() && ctx.scalar_type() == at::kLong && ctx.numel() == kCtxLen,
+              "train ctx must be an int64 CPU tensor of length ", kCtxLen);
+  const int64_t* c = ctx.data_ptr<int64_t>();
+  apneauq::train::Args A;
+  for (int l = 0; l < 6; ++l) {
+    const int64_t* q = c + l * kCtxLayer;
+    auto& L = A.L[l];
+    L.wf = reinterpret_cast<const void*>(q[0]);
+    L.wd = reinterpret_cast<const void*>(q[1]);
+    L.bias = reinterpret_cast<const float*>(q[2]);
+    L.gamma = reinterpret_cast<const float*>(q[3]);
+    L.beta = reinterpret_cast<const float*>(q[4]);
+    L.mmean = reinterpret_cast<float*>(q[5]);
+    L.mvar = reinterpret_cast<float*>(q[6]);
+    L.gw = reinterpret_cast<float*>(q[7]);
+    L.gb = reinterpret_cast<float*>(q[8]);
+    L.ggamma = reinterpret_cast<float*>(q[9]);
+    L.gbeta = reinterpret_cast<float*>(q[10]);
+    L.R = reinterpret_cast<void*>(q[11]);
+    L.dY = reinterpret_cast<void*>(q[12]);
+    L.st = reinterpret_cast<float*>(q[13]);
+    L.bst = reinterpret_cast<float*>(q[14]);
+    L.thr = static_cast<unsigned>(q[15]);
+    L.dsc = bits_to_float(q[16]);
+  }
+  const int64_t* g = c + 6 * kCtxLayer;
+  A.x = reinterpret_cast<const void*>(g[0]);
+  A.y = reinterpret_cast<const float*>(g[1]);
+  A.dense_w = reinterpret_cast<const float*>(g[2]);
+  A.dense_b = reinterpret_cast<const float*>(g[3]);
+  A.g_dense_w = reinterpret_cast<float*>(g[4]);
+  A.g_dense_b = reinterpret_cast<float*>(g[5]);
+  A.logits = reinterpret_cast<float*>(g[6]);
+  A.dlogit = reinterpret_cast<float*>(g[7]);
+  A.loss_sum = reinterpret_cast<float*>(g[8]);
+  A.B = static_cast<int>(g[9]);
+  A.n_win = static_cast<int>(g[10]);
+  A.groups = static_cast<int>(g[11]);
+  A.pass_base = static_cast<unsigned>(pass_base >= 0 ? pass_base : g[12]);
+  A.window_offset = static_cast<unsigned>(g[13]);
+  A.seed = static_cast<unsigned long long>(g[14]);
+  A.dropout = static_cast<int>(g[15]);
+  A.inv_count = bits_to_float(g[16]);
+  A.inv_batch = bits_to_float(g[17]);
+  A.eps = bits_to_float(g[18]);
+  A.momentum = bits_to_float(g[19]);
+  return A;
+}
+
+// op: 0 fwd(layer) | 1 head(flag=backward) | 2 dgrad(layer) | 3 wgrad(layer) | 4 finalize(layer=update_moving, flag=grads)
+void train_call(const at::Tensor& ctx, int64_t op, int64_t layer, int64_t flag, int64_t pass_base, int64_t device) {
+  const at::DeviceGuard guard(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(device)));
+  auto A = args_from_ctx(ctx, pass_base);
+  TORCH_CHECK(A.B > 0 && A.n_win > 0 && A.groups > 0, "train_call: bad sizes");
+  hipStream_t s = cur_stream();
+  switch (op) {
+    case 0: TORCH_CHECK(layer >= 0 && layer < 6); check(apneauq::train_launch_fwd(A, (int)layer, s), "train fwd"); break;
+    case 1: check(apneauq::train_launch_head(A, (int)flag, s), "train head"); break;
+    case 2: TORCH_CHECK(layer >= 1 && layer < 6); check(apneauq::train_launch_dgrad(A, (int)layer, s), "train dgrad"); break;
+    case 3: TORCH_CHECK(layer >= 0 && layer < 6); check(apneauq::train_launch_wgrad(A, (int)layer, s), "train wgrad"); break;
+    case 4: check(apneauq::train_launch_finalize(A, (int)layer, (int)flag, s), "train finalize"); break;
+    default: TORCH_CHECK(false, "train_call: unknown op ", op);
+  }
+}
+
+void train_pack(const at::Tensor& w, int64_t k, int64_t cin, int64_t cout, at::Tensor& fwd, at::Tensor& dgr) {
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == k * cin * cout,
+              "train_pack: w must be a contiguous fp32 (k, cin, cout) GPU tensor");
+  const int64_t nf = ((cin * k + 31) / 32) * 32 * cout, nd = ((cout * k + 31) / 32) * 32 * cin;
+  TORCH_CHECK(fwd.scalar_type() == at::kBFloat16 && fwd.numel() == nf && dgr.scalar_type() == at::kBFloat16 &&
+                  dgr.numel() == nd && fwd.is_contiguous() && dgr.is_contiguous(),
+              "train_pack: fragment buffers have the wrong size/dtype");
+  const at::DeviceGuard guard(w.device());
+  check(apneauq::train_launch_pack(w.data_ptr<float>(), (int)k, (int)cin, (int)cout, fwd.data_ptr(), dgr.data_ptr(),
+                                   cur_stream()),
+        "train_pack");
+}
+
 std::vector<int64_t> fused_layout() {
   int w[6], e[6], d;
   apneauq::fused_layout(w, e, &d);
@@ -135,6 +250,8 @@ TORCH_LIBRARY(apneauq, m) {
   m.def("uq_reduce(Tensor probs) -> Tensor");
   m.def("bootstrap(Tensor metrics, Tensor y, Tensor? idx, int seed, int n_boot) -> Tensor");
   m.def("fused_layout() -> int[]", &fused_layout);
+  m.def("train_call(Tensor ctx, int op, int layer, int flag, int pass_base, int device) -> ()", &train_call);
+  m.def("train_pack(Tensor w, int k, int cin, int cout, Tensor(a!) fwd, Tensor(b!) dgr) -> ()");
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, float b1, float b2, float alpha, float eps, "
         "float gscale) -> ()");
 }
@@ -144,4 +261,5 @@ TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
   m.impl("uq_reduce", &uq_reduce);
   m.impl("bootstrap", &bootstrap);
   m.impl("adam_step", &adam_step);
+  m.impl("train_pack", &train_pack);
 }

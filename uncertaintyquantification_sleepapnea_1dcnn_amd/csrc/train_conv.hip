@@ -1,0 +1,842 @@
+// Layer-wise training kernels of the Alarcón 1D-CNN on gfx950 (MI355X): forward with batch-
+// statistics BatchNorm, head (GAP + Dense + BCE + its gradient), conv dgrad / wgrad, BN finalize.
+//
+// Replaces the TF/cuDNN work inside model.fit (cnn_baseline_train.py:210, train_deep_ensemble_cnns.py:158;
+// SURVEY K1-K8).  Keras semantics: ReLU inside the conv, BN on biased batch moments (eps 1e-3,
+// momentum 0.99), inverted dropout (counter-based masks, ops/rng.py), BCE on logits, batch mean.
+//
+// Data layout ("padded rows", PL): an activation buffer holds 4 leading zero rows, then every
+// sample as a 64-row slot (60 time steps + 4 zero rows), channels contiguous, bf16.  A workgroup
+// tile = 2 samples = rows [128*tile, 128*tile + 136) — one contiguous copy including the conv halo.
+//
+// Per block l the buffers are R_l = relu(conv(A_{l-1}) + b) (pre-BN, bf16) and dY_l = dL/dBN-output
+// (bf16).  BN apply + dropout of block l are never materialised: the consumer of A_l (the next
+// forward, the wgrad of block l+1) recomputes  A_l = mask * (R_l * s + t) / (1-p)  while staging
+// into LDS, and the consumers of dZ_l (dgrad / wgrad of block l) recompute
+//   dZ_l = [R_l > 0] * gamma * rstd * (dY_l - mean(dY_l) - xhat * mean(dY_l * xhat))
+// from the per-channel sums accumulated by the producer's epilogue (fp32 atomics).
+//
+// Forward and dgrad are implicit GEMMs on v_mfma_f32_16x16x32_bf16 with the weights as the A operand
+// (pre-packed fragments from global/L2) and the staged activations as the B operand (LDS,
+// ds_read_b128).  wgrad reduces over rows, so both operands are read with the CDNA4 transposing
+// LDS read ds_read_b64_tr_b16 from row-major tiles; each workgroup sums 16 row tiles in registers
+// and adds its output block to the fp32 gradient with global atomics.
+#include "common.h"
+
+namespace apneauq {
+namespace train {
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+
+constexpr int kL = 60, kSR = 64, kSlots = 2, kR = 128, kRT = 8, kHalo = 4, kRows = 136;
+constexpr int kRS = 256 * 2 + 32;  // LDS row stride (bytes) of staged activations
+constexpr int kThreads = 256;
+constexpr int C[7] = {4, 128, 192, 224, 96, 256, 96};
+constexpr int KS[6] = {7, 5, 3, 7, 9, 9};
+
+struct Layer {
+  const gbf16x8* wf;   // forward fragments  (ksteps, Cout/16, 64, 8)
+  const gbf16x8* wd;   // dgrad fragments    (ksteps', Cin/16, 64, 8)
+  const float* bias;
+  const float* gamma;
+  const float* beta;
+  float* mmean;
+  float* mvar;
+  float* gw;           // dW (k, Cin, Cout) fp32, in the flat gradient buffer
+  float* gb;
+  float* ggamma;
+  float* gbeta;
+  __bf16* R;           // PL (rows, C) post-ReLU, pre-BN
+  __bf16* dY;          // PL (rows, C) gradient wrt BN output (blocks 1..5)
+  float* st;           // [groups][2][C] forward sums (sum r, sum r^2)
+  float* bst;          // [2][C] backward sums (sum dY, sum dY * xhat)
+  unsigned thr;        // dropout threshold (16-bit units) and 1/(1-p)
+  float dsc;
+};
+
+struct Args {
+  Layer L[6];
+  const __bf16* x;     // PL (rows, 4)
+  const float* y;      // labels (B)
+  const float* dense_w;
+  const float* dense_b;
+  float* g_dense_w;
+  float* g_dense_b;
+  float* logits;       // (B)
+  float* dlogit;       // (B)
+  float* loss_sum;     // (1)
+  int B;               // samples in this launch (T*N for batch-BN MC Dropout)
+  int n_win;           // samples per stats group (B for training, N for MC Dropout)
+  int groups;          // number of stats groups
+  unsigned pass_base;  // dropout pass id of group 0
+  unsigned window_offset;
+  unsigned long long seed;
+  int dropout;
+  float inv_count;     // 1 / (samples per group * 60) — BN moment normaliser
+  float inv_batch;     // 1 / global batch size — BCE mean
+  float eps;
+  float momentum;
+};
+
+template <typename T>
+__device__ __forceinline__ T gld(const void* p) {
+  return *(const __attribute__((address_space(1))) T*)(p);
+}
+
+__device__ __forceinline__ int row_sample(int grow) { return (grow - kHalo) >> 6; }  // may be -1 / >= B
+__device__ __forceinline__ int row_time(int grow) { return (grow - kHalo) & 63; }
+
+// Per-channel BN affine of block l for stats group g, into LDS: s[c], t[c], mean[c], rstd[c].
+__device__ __forceinline__ void bn_affine_to_lds(const Args& A, int l, int g, float* s, float* t, float* mean,
+                                                 float* rstd) {
+  const int Cc = C[l + 1];
+  const Layer& Ly = A.L[l];
+  for (int c = threadIdx.x; c < Cc; c += kThreads) {
+    const float s1 = Ly.st[(g * 2 + 0) * Cc + c], s2 = Ly.st[(g * 2 + 1) * Cc + c];
+    const float mu = s1 * A.inv_count;
+    const float var = fmaxf(s2 * A.inv_count - mu * mu, 0.f);
+    const float rs = rsqrtf(var + A.eps);
+    const float sc = Ly.gamma[c] * rs;
+    s[c] = sc;
+    t[c] = Ly.beta[c] - mu * sc;
+    if (mean) mean[c] = mu;
+    if (rstd) rstd[c] = rs;
+  }
+}
+
+__device__ __forceinline__ unsigned layer_sample_key(const Args& A, int l, int sample) {
+  const unsigned g = (unsigned)(sample / A.n_win);
+  const unsigned w = (unsigned)(sample - (int)g * A.n_win);
+  return sample_key(stream_key(A.seed, l, A.pass_base + g), A.window_offset + w);
+}
+
+// Stage A_l (= dropout(BN(R_l))) rows [row0, row0 + nrows) x channels [c0, c0 + ncw*8) of global
+// PL buffer into LDS (row stride ldsrs bytes).  Pad rows and rows outside the batch become 0.
+template <int l>
+__device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, int row0, int nrows, int c0, int ncw,
+                                          const float* s, const float* t, int g0, int g1, int tile_sample0) {
+  constexpr int Cc = C[l + 1];
+  const Layer& Ly = A.L[l];
+  (void)tile_sample0;
+  for (int i = threadIdx.x; i < nrows * ncw; i += kThreads) {
+    const int r = i / ncw, cw = i - r * ncw;
+    const int grow = row0 + r;
+    const int n = row_sample(grow), tt = row_time(grow);
+    const int c = c0 + cw * 8;
+    bf16x8 o;
+    if (grow < kHalo || n >= A.B || tt >= kL) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (__bf16)0.f;
+    } else {
+      const bf16x8 v = gld<bf16x8>(Ly.R + (long long)grow * Cc + c);
+      const int g = n / A.n_win;
+      const float* sg = s + (g == g0 ? 0 : 256);
+      const float* tg = t + (g == g0 ? 0 : 256);
+      (void)g1;
+      unsigned key = 0;
+      if (A.dropout) key = layer_sample_key(A, l, n);
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        float a0 = (float)v[j] * sg[c + j] + tg[c + j];
+        float a1 = (float)v[j + 1] * sg[c + j + 1] + tg[c + j + 1];
+        if (A.dropout) {
+          const unsigned h = dropout_bits2(key, tt, c + j);
+          a0 = (h & 0xFFFFu) >= Ly.thr ? a0 * Ly.dsc : 0.f;
+          a1 = (h >> 16) >= Ly.thr ? a1 * Ly.dsc : 0.f;
+        }
+        o[j] = (__bf16)a0;
+        o[j + 1] = (__bf16)a1;
+      }
+    }
+    *reinterpret_cast<bf16x8*>(lds + r * ldsrs + cw * 16) = o;
+  }
+}
+
+// dZ_l rows into LDS (rows [row0, row0+nrows), channels [c0, c0+ncw*8)).
+//   l == 5: dY_6 = dlogit[n] * w[c] / 60 * mask6 * dsc6 (recomputed; never stored)
+template <int l>
+__device__ __forceinline__ void stage_dz(const Args& A, char* lds, int ldsrs, int row0, int nrows, int c0, int ncw,
+                                         const float* gam_rstd, const float* mean, const float* rstd, const float* mdy,
+                                         const float* mdyx, float* colsum = nullptr) {
+  constexpr int Cc = C[l + 1];
+  const Layer& Ly = A.L[l];
+  for (int i = threadIdx.x; i < nrows * ncw; i += kThreads) {
+    const int r = i / ncw, cw = i - r * ncw;
+    const int grow = row0 + r;
+    const int n = row_sample(grow), tt = row_time(grow);
+    const int c = c0 + cw * 8;
+    bf16x8 o;
+    if (grow < kHalo || n >= A.B || tt >= kL) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (__bf16)0.f;
+    } else {
+      const bf16x8 rv = gld<bf16x8>(Ly.R + (long long)grow * Cc + c);
+      float dy[8];
+      if constexpr (l == 5) {
+        const float dl = A.dlogit[n] * (1.0f / kL);
+        const unsigned key = A.dropout ? layer_sample_key(A, 5, n) : 0u;
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+          float d0 = dl * A.dense_w[c + j], d1 = dl * A.dense_w[c + j + 1];
+          if (A.dropout) {
+            const unsigned h = dropout_bits2(key, tt, c + j);
+            d0 = (h & 0xFFFFu) >= Ly.thr ? d0 * Ly.dsc : 0.f;
+            d1 = (h >> 16) >= Ly.thr ? d1 * Ly.dsc : 0.f;
+          }
+          dy[j] = d0;
+          dy[j + 1] = d1;
+        }
+      } else {
+        const bf16x8 dv = gld<bf16x8>(Ly.dY + (long long)grow * Cc + c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dy[j] = (float)dv[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float rr = (float)rv[j];
+        const float xh = (rr - mean[c + j]) * rstd[c + j];
+        const float dz = gam_rstd[c + j] * (dy[j] - mdy[c + j] - xh * mdyx[c + j]);
+        o[j] = (__bf16)(rr > 0.f ? dz : 0.f);
+      }
+      if (colsum) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) atomicAdd(colsum + (c - c0) + j, (float)o[j]);
+      }
+    }
+    *reinterpret_cast<bf16x8*>(lds + r * ldsrs + cw * 16) = o;
+  }
+}
+
+// Implicit-GEMM conv tile: D^T[co][row] over the 128-row tile, weights = packed A fragments.
+template <int CIN, int COUT, int K, int WM, int WN, bool FIRST>
+struct Conv {
+  static constexpr int NSTEP = (CIN * K + 31) / 32;
+  static constexpr int NCT = COUT / 16;
+  static constexpr int CT = NCT / WN;
+  static constexpr int RT = kRT / WM;
+  static constexpr int PAD = (K - 1) / 2;
+  static_assert(NCT % WN == 0 && kRT % WM == 0 && WM * WN == 4, "wave tiling");
+
+  __device__ __forceinline__ static void run(const gbf16x8* wfrag, const char* lds, int ldsrs, f32x4 (&acc)[CT][RT]) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int m = lane & 15, h = lane >> 4;
+    const gbf16x8* wp = wfrag + (wn * CT) * 64 + lane;
+    const int row0 = wm * RT * 16 + m;
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+#pragma unroll
+      for (int r = 0; r < RT; ++r) acc[c][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto load_b = [&](int s, int r) -> bf16x8 {
+      if constexpr (FIRST) {
+        const char* base = lds + (kHalo + row0 + r * 16 - PAD) * ldsrs + (32 * s + 8 * h) * 2;
+        const bf16x4 lo = *reinterpret_cast<const bf16x4*>(base);
+        const bf16x4 hi = *reinterpret_cast<const bf16x4*>(base + 8);
+        return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      } else {
+        constexpr int CB = CIN / 32;
+        const int tap = s / CB, cb = s - tap * CB;
+        return *reinterpret_cast<const bf16x8*>(lds + (kHalo + row0 + r * 16 + tap - PAD) * ldsrs + (cb * 32 + 8 * h) * 2);
+      }
+    };
+    auto load_a = [&](int s, bf16x8 (&a)[CT]) {
+#pragma unroll
+      for (int c = 0; c < CT; ++c) a[c] = wp[(s * NCT + c) * 64];
+    };
+    auto step = [&](int s, const bf16x8 (&a)[CT]) {
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        const bf16x8 b = load_b(s, r);
+#pragma unroll
+        for (int c = 0; c < CT; ++c) acc[c][r] = mfma16(a[c], b, acc[c][r]);
+      }
+    };
+    bf16x8 a0[CT], a1[CT];
+    load_a(0, a0);
+#pragma unroll 1
+    for (int s = 0; s < NSTEP; s += 2) {
+      if (s + 1 < NSTEP) load_a(s + 1, a1);
+      step(s, a0);
+      if (s + 1 < NSTEP) {
+        if (s + 2 < NSTEP) load_a(s + 2, a0);
+        step(s + 1, a1);
+      }
+    }
+  }
+};
+
+// wave tilings (WM, WN) per output-channel count
+template <int COUT> struct Tiling;
+template <> struct Tiling<128> { static constexpr int WM = 1, WN = 4; };
+template <> struct Tiling<192> { static constexpr int WM = 1, WN = 4; };
+template <> struct Tiling<224> { static constexpr int WM = 2, WN = 2; };
+template <> struct Tiling<96> { static constexpr int WM = 2, WN = 2; };
+template <> struct Tiling<256> { static constexpr int WM = 1, WN = 4; };
+
+extern __shared__ __attribute__((aligned(16))) char smem[];
+
+// Reduce per-lane partial sums over the 16 rows of a lane group and add them to a global
+// per-channel accumulator (fp32 atomics; one per channel per wave row-group).
+__device__ __forceinline__ void atomic_channel_sums(float* dst, int co0, const f32x4& a, bool leader) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float v = group16_sum(a[i]);
+    if (leader) atomicAdd(dst + co0 + i, v);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Forward of block l:  R_l = relu(conv(A_{l-1}) + b), fwd sums of R_l per stats group.
+// ------------------------------------------------------------------------------------------------
+template <int l>
+__global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
+  constexpr int CIN = C[l], COUT = C[l + 1];
+  using T = Tiling<COUT>;
+  using CV = Conv<CIN, COUT, KS[l], T::WM, T::WN, l == 0>;
+  char* act = smem;                                  // staged input, then staged output
+  float* prm = reinterpret_cast<float*>(smem + kRows * kRS);  // [s 512 | t 512]
+  const int tile = blockIdx.x;
+  const int row0 = kR * tile;                        // first staged row (global PL index)
+  const int smp0 = 2 * tile;
+  const int g0 = min(smp0, A.B - 1) / A.n_win, g1 = min(smp0 + 1, A.B - 1) / A.n_win;
+  constexpr int IN_RS = (l == 0) ? 8 : kRS;
+  if constexpr (l == 0) {
+    for (int i = threadIdx.x; i < kRows * 8 / 16; i += kThreads)
+      reinterpret_cast<f32x4*>(act)[i] = gld<f32x4>(A.x + (long long)row0 * 4 + i * 8);
+  } else {
+    bn_affine_to_lds(A, l - 1, g0, prm, prm + 512, nullptr, nullptr);
+    if (g1 != g0) bn_affine_to_lds(A, l - 1, g1, prm + 256, prm + 768, nullptr, nullptr);
+    __syncthreads();
+    stage_act<l - 1>(A, act, kRS, row0, kRows, 0, CIN / 8, prm, prm + 512, g0, g1, smp0);
+  }
+  __syncthreads();
+  f32x4 acc[CV::CT][CV::RT];
+  CV::run(A.L[l].wf, act, IN_RS, acc);
+  __syncthreads();  // all waves done reading the staged input; reuse it for the output tile
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / T::WN, wn = wave % T::WN;
+  const int m = lane & 15, h = lane >> 4;
+  const Layer& Ly = A.L[l];
+#pragma unroll
+  for (int c = 0; c < CV::CT; ++c) {
+    const int co0 = (wn * CV::CT + c) * 16 + 4 * h;
+    const f32x4 bias = gld<f32x4>(Ly.bias + co0);
+    f32x4 s1[kSlots] = {}, s2[kSlots] = {};
+#pragma unroll
+    for (int r = 0; r < CV::RT; ++r) {
+      const int row = wm * CV::RT * 16 + r * 16 + m;  // 0..127 within the tile
+      const int slot = row >> 6, tt = row & 63;
+      const bool valid = tt < kL && (smp0 + slot) < A.B;
+      f32x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = valid ? fmaxf(acc[c][r][i] + bias[i], 0.f) : 0.f;
+      bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+      *reinterpret_cast<bf16x4*>(act + row * kRS + co0 * 2) = o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float q = (float)o[i];  // moments of the values the consumers will normalise
+        if (slot == 0) { s1[0][i] += q; s2[0][i] += q * q; }
+        else { s1[1][i] += q; s2[1][i] += q * q; }
+      }
+    }
+    if (g0 == g1) {
+      s1[0] += s1[1];
+      s2[0] += s2[1];
+      atomic_channel_sums(Ly.st + (g0 * 2 + 0) * COUT, co0, s1[0], m == 0);
+      atomic_channel_sums(Ly.st + (g0 * 2 + 1) * COUT, co0, s2[0], m == 0);
+    } else {
+      atomic_channel_sums(Ly.st + (g0 * 2 + 0) * COUT, co0, s1[0], m == 0);
+      atomic_channel_sums(Ly.st + (g0 * 2 + 1) * COUT, co0, s2[0], m == 0);
+      atomic_channel_sums(Ly.st + (g1 * 2 + 0) * COUT, co0, s1[1], m == 0);
+      atomic_channel_sums(Ly.st + (g1 * 2 + 1) * COUT, co0, s2[1], m == 0);
+    }
+  }
+  __syncthreads();
+  // coalesced copy-out of the 128 tile rows (16 B per thread-iteration)
+  constexpr int CW = COUT / 8;
+  for (int i = threadIdx.x; i < kR * CW; i += kThreads) {
+    const int r = i / CW, cw = i - r * CW;
+    *reinterpret_cast<bf16x8*>(Ly.R + (long long)(row0 + kHalo + r) * COUT + cw * 8) =
+        *reinterpret_cast<const bf16x8*>(act + r * kRS + cw * 16);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Head: A_6 = dropout(BN(R_6)) -> GAP -> Dense(96->1) -> logit, BCE, dlogit = (sigmoid - y)/B,
+// dense gradients, and the backward sums of dY_6 (sum dY, sum dY * xhat) — one sample per wave,
+// each lane owning channels (lane, lane + 64).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void head_kernel(Args A, int backward) {
+  constexpr int Cc = C[6];
+  float* dw = reinterpret_cast<float*>(smem);  // [dW 128 | dsum 128 | dxsum 128]
+  float* bsum0 = dw + 128;
+  float* bsum1 = dw + 256;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = blockIdx.x * 4 + wave;
+  for (int c = threadIdx.x; c < 384; c += kThreads) dw[c] = 0.f;
+  __syncthreads();
+  const Layer& Ly = A.L[5];
+  if (n < A.B) {
+    const int g = n / A.n_win;
+    float sc[2] = {0.f, 0.f}, sh[2] = {0.f, 0.f}, mu[2] = {0.f, 0.f}, rs[2] = {0.f, 0.f}, w[2] = {0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int c = lane + 64 * q;
+      if (c < Cc) {
+        const float m1 = Ly.st[(g * 2) * Cc + c] * A.inv_count;
+        const float var = fmaxf(Ly.st[(g * 2 + 1) * Cc + c] * A.inv_count - m1 * m1, 0.f);
+        rs[q] = rsqrtf(var + A.eps);
+        mu[q] = m1;
+        sc[q] = Ly.gamma[c] * rs[q];
+        sh[q] = Ly.beta[c] - m1 * sc[q];
+        w[q] = A.dense_w[c];
+      }
+    }
+    const unsigned key = A.dropout ? layer_sample_key(A, 5, n) : 0u;
+    const __bf16* base = Ly.R + (long long)(kHalo + n * kSR) * Cc;
+    auto keep = [&](int tt, int c) -> bool {
+      const unsigned hh = dropout_bits2(key, tt, c & ~1);
+      return ((c & 1) ? (hh >> 16) : (hh & 0xFFFFu)) >= Ly.thr;
+    };
+    float gap[2] = {0.f, 0.f};
+    for (int tt = 0; tt < kL; ++tt) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int c = lane + 64 * q;
+        if (c < Cc) {
+          float a = (float)base[tt * Cc + c] * sc[q] + sh[q];
+          if (A.dropout) a = keep(tt, c) ? a * Ly.dsc : 0.f;
+          gap[q] += a;
+        }
+      }
+    }
+    gap[0] *= (1.0f / kL);
+    gap[1] *= (1.0f / kL);
+    const float z = wave_sum(gap[0] * w[0] + gap[1] * w[1]) + A.dense_b[0];
+    if (lane == 0) A.logits[n] = z;
+    if (backward) {
+      const float p = 1.0f / (1.0f + __expf(-z));
+      const float yv = A.y[n];
+      const float dl = (p - yv) * A.inv_batch;
+      if (lane == 0) {
+        const float loss = fmaxf(z, 0.f) - z * yv + log1pf(__expf(-fabsf(z)));  // BCE on logits
+        atomicAdd(A.loss_sum, loss);
+        A.dlogit[n] = dl;
+        atomicAdd(A.g_dense_b, dl);
+      }
+      float b0[2] = {0.f, 0.f}, b1[2] = {0.f, 0.f};
+      for (int tt = 0; tt < kL; ++tt) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int c = lane + 64 * q;
+          if (c < Cc) {
+            float dy = dl * w[q] * (1.0f / kL);
+            if (A.dropout) dy = keep(tt, c) ? dy * Ly.dsc : 0.f;
+            const float xh = ((float)base[tt * Cc + c] - mu[q]) * rs[q];
+            b0[q] += dy;
+            b1[q] += dy * xh;
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int c = lane + 64 * q;
+        if (c < Cc) {
+          atomicAdd(&dw[c], dl * gap[q]);
+          atomicAdd(&bsum0[c], b0[q]);
+          atomicAdd(&bsum1[c], b1[q]);
+        }
+      }
+    }
+  }
+  if (backward) {
+    __syncthreads();
+    for (int c = threadIdx.x; c < Cc; c += kThreads) {
+      atomicAdd(A.g_dense_w + c, dw[c]);
+      atomicAdd(Ly.bst + c, bsum0[c]);
+      atomicAdd(Ly.bst + Cc + c, bsum1[c]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// dgrad of block l (l >= 1): dA_{l-1} = conv^T(dZ_l, W_l);  epilogue -> dY_{l-1} = dA * mask_{l-1}
+// plus the backward sums of block l-1.
+// ------------------------------------------------------------------------------------------------
+template <int l>
+__global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
+  constexpr int CIN = C[l + 1], COUT = C[l];  // conv^T: input = dZ_l channels, output = block l-1 channels
+  using T = Tiling<COUT>;
+  using CV = Conv<CIN, COUT, KS[l], T::WM, T::WN, false>;
+  char* act = smem;
+  float* prm = reinterpret_cast<float*>(smem + kRows * kRS);
+  float* gr = prm;           // gamma*rstd of block l
+  float* mean = prm + 256;
+  float* rstd = prm + 512;
+  float* mdy = prm + 768;
+  float* mdyx = prm + 1024;
+  float* s_prev = prm + 1280;     // block l-1 affine (unused here) and its mean / rstd for xhat
+  float* t_prev = prm + 1536;
+  float* mean_prev = prm + 1792;
+  float* rstd_prev = prm + 2048;
+  const int tile = blockIdx.x;
+  const int row0 = kR * tile;
+  const int smp0 = 2 * tile;
+  {
+    const Layer& Ly = A.L[l];
+    bn_affine_to_lds(A, l, 0, gr, mdy, mean, rstd);  // mdy temporarily holds the shift (unused)
+    __syncthreads();
+    for (int c = threadIdx.x; c < CIN; c += kThreads) {
+      gr[c] = Ly.gamma[c] * rstd[c];
+      mdy[c] = Ly.bst[c] * A.inv_count;
+      mdyx[c] = Ly.bst[CIN + c] * A.inv_count;
+    }
+    bn_affine_to_lds(A, l - 1, 0, s_prev, t_prev, mean_prev, rstd_prev);
+  }
+  __syncthreads();
+  stage_dz<l>(A, act, kRS, row0, kRows, 0, CIN / 8, gr, mean, rstd, mdy, mdyx);
+  __syncthreads();
+  f32x4 acc[CV::CT][CV::RT];
+  CV::run(A.L[l].wd, act, kRS, acc);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / T::WN, wn = wave % T::WN;
+  const int m = lane & 15, h = lane >> 4;
+  const Layer& Lp = A.L[l - 1];
+  unsigned key[kSlots] = {0u, 0u};
+  if (A.dropout) {
+    key[0] = layer_sample_key(A, l - 1, min(smp0, A.B - 1));
+    key[1] = layer_sample_key(A, l - 1, min(smp0 + 1, A.B - 1));
+  }
+#pragma unroll
+  for (int c = 0; c < CV::CT; ++c) {
+    const int co0 = (wn * CV::CT + c) * 16 + 4 * h;
+    f32x4 b0 = {}, b1 = {};
+#pragma unroll
+    for (int r = 0; r < CV::RT; ++r) {
+      const int row = wm * CV::RT * 16 + r * 16 + m;
+      const int slot = row >> 6, tt = row & 63;
+      const bool valid = tt < kL && (smp0 + slot) < A.B;
+      f32x4 v = acc[c][r];
+      if (A.dropout) {
+        const unsigned k = slot ? key[1] : key[0];
+        const unsigned h01 = dropout_bits2(k, tt, co0), h23 = dropout_bits2(k, tt, co0 + 2);
+        v[0] = (h01 & 0xFFFFu) >= Lp.thr ? v[0] * Lp.dsc : 0.f;
+        v[1] = (h01 >> 16) >= Lp.thr ? v[1] * Lp.dsc : 0.f;
+        v[2] = (h23 & 0xFFFFu) >= Lp.thr ? v[2] * Lp.dsc : 0.f;
+        v[3] = (h23 >> 16) >= Lp.thr ? v[3] * Lp.dsc : 0.f;
+      }
+      if (!valid) v = f32x4{0.f, 0.f, 0.f, 0.f};
+      bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+      *reinterpret_cast<bf16x4*>(act + row * kRS + co0 * 2) = o;
+      if (valid) {
+        const bf16x4 rr = gld<bf16x4>(Lp.R + (long long)(row0 + kHalo + row) * COUT + co0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float q = (float)o[i];
+          const float xh = ((float)rr[i] - mean_prev[co0 + i]) * rstd_prev[co0 + i];
+          b0[i] += q;
+          b1[i] += q * xh;
+        }
+      }
+    }
+    atomic_channel_sums(Lp.bst, co0, b0, m == 0);
+    atomic_channel_sums(Lp.bst + COUT, co0, b1, m == 0);
+  }
+  __syncthreads();
+  constexpr int CW = COUT / 8;
+  for (int i = threadIdx.x; i < kR * CW; i += kThreads) {
+    const int r = i / CW, cw = i - r * CW;
+    *reinterpret_cast<bf16x8*>(Lp.dY + (long long)(row0 + kHalo + r) * COUT + cw * 8) =
+        *reinterpret_cast<const bf16x8*>(act + r * kRS + cw * 16);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// wgrad of block l: dW_l[tap][ci][co] = sum_rows A_{l-1}[row + tap - pad][ci] * dZ_l[row][co],
+// db_l = sum_rows dZ_l.  MFMA: D[co][ci] (16x16 tiles), A-op = dZ^T, B-op = A^shift; both read
+// with ds_read_b64_tr_b16 from row-major LDS tiles.  Block 1 stages an im2col (kk = tap*4+ci).
+// ------------------------------------------------------------------------------------------------
+template <int l> struct WgCfg;
+//                               CI_BLK CO_BLK WCO WCI
+template <> struct WgCfg<0> { static constexpr int CIB = 32, COB = 128, WCO = 4, WCI = 1; };  // im2col kk=32
+template <> struct WgCfg<1> { static constexpr int CIB = 32, COB = 192, WCO = 2, WCI = 2; };
+template <> struct WgCfg<2> { static constexpr int CIB = 32, COB = 224, WCO = 2, WCI = 2; };
+template <> struct WgCfg<3> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2; };
+template <> struct WgCfg<4> { static constexpr int CIB = 16, COB = 128, WCO = 4, WCI = 1; };
+template <> struct WgCfg<5> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2; };
+
+constexpr int kWgRowTiles = 16;  // 128-row tiles summed in registers per workgroup
+
+__device__ __forceinline__ bf16x8 tr_frag(const char* lds, int ldsrs, int row_base, int col0) {
+  // fragment for a 16x16x32 operand whose K index is the LDS row: lane (m, h) gets rows
+  // row_base + 8h + [0..8) of column col0 + m.  Group h reads 4 rows x 16 cols per instruction.
+  const int lane = threadIdx.x & 63;
+  const int h = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const char* a0 = lds + (row_base + 8 * h + q) * ldsrs + (col0 + 4 * p) * 2;
+  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)a0);
+  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)(a0 + 4 * ldsrs));
+  bf16x8 r;
+  const __bf16* pl = reinterpret_cast<const __bf16*>(&lo);
+  const __bf16* ph = reinterpret_cast<const __bf16*>(&hi);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r[j] = pl[j];
+    r[4 + j] = ph[j];
+  }
+  return r;
+}
+
+template <int l>
+__global__ __launch_bounds__(kThreads, 2) void wgrad_kernel(Args A) {
+  using W = WgCfg<l>;
+  constexpr int CIN = C[l], COUT = C[l + 1], K = KS[l], PAD = (K - 1) / 2;
+  constexpr bool FIRST = (l == 0);
+  constexpr int NTAP = FIRST ? 1 : K;           // block 1: taps folded into the im2col columns
+  constexpr int NCO = W::COB / 16 / W::WCO;     // co tiles per wave
+  constexpr int NCI = W::CIB / 16 / W::WCI;     // ci tiles per wave
+  constexpr int DZRS = W::COB * 2 + 16;         // LDS row strides (bytes)
+  constexpr int ARS = W::CIB * 2 + 16;
+  static_assert(W::WCO * W::WCI == 4, "4 waves");
+  char* dz_lds = smem;                                   // 128 rows x COB
+  char* a_lds = smem + kR * DZRS;                        // 136 rows x CIB (or 128 x 32 im2col)
+  float* prm = reinterpret_cast<float*>(a_lds + kRows * ARS);
+  float* gr = prm;
+  float* mean = prm + 256;
+  float* rstd = prm + 512;
+  float* mdy = prm + 768;
+  float* mdyx = prm + 1024;
+  float* sp = prm + 1280;   // block l-1 affine (scale | shift) for staging A_{l-1}
+  float* tp = prm + 1536;
+  float* colsum = prm + 2048;  // bias-gradient column sums (ci-block 0 only)
+  const int nci_blk = FIRST ? 1 : CIN / W::CIB;
+  const int nco_blk = COUT / W::COB;
+  const int blk = blockIdx.x % (nci_blk * nco_blk);
+  const int rg = blockIdx.x / (nci_blk * nco_blk);
+  const int ci0 = (blk % nci_blk) * W::CIB, co0 = (blk / nci_blk) * W::COB;
+  const bool do_bias = (ci0 == 0);
+  {
+    const Layer& Ly = A.L[l];
+    bn_affine_to_lds(A, l, 0, gr, mdy, mean, rstd);
+    for (int c = threadIdx.x; c < 256; c += kThreads) colsum[c] = 0.f;
+    __syncthreads();
+    for (int c = threadIdx.x; c < COUT; c += kThreads) {
+      gr[c] = Ly.gamma[c] * rstd[c];
+      mdy[c] = Ly.bst[c] * A.inv_count;
+      mdyx[c] = Ly.bst[COUT + c] * A.inv_count;
+    }
+    if constexpr (!FIRST) bn_affine_to_lds(A, l - 1, 0, sp, tp, nullptr, nullptr);
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wco = wave % W::WCO, wci = wave / W::WCO;
+  // D[ci][co] tiles: A-op = A_shift^T (rows of D = ci), B-op = dZ (cols of D = co); K = tile rows
+  f32x4 acc[NTAP][NCI][NCO];
+#pragma unroll
+  for (int k = 0; k < NTAP; ++k)
+#pragma unroll
+    for (int b = 0; b < NCI; ++b)
+#pragma unroll
+      for (int a = 0; a < NCO; ++a) acc[k][b][a] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int ntiles = (A.B + 1) / 2;
+  for (int it = 0; it < kWgRowTiles; ++it) {
+    const int tile = rg * kWgRowTiles + it;
+    if (tile >= ntiles) break;
+    const int row0 = kR * tile;
+    __syncthreads();
+    stage_dz<l>(A, dz_lds, DZRS, row0 + kHalo, kR, co0, W::COB / 8, gr, mean, rstd, mdy, mdyx,
+                do_bias ? colsum : nullptr);
+    if constexpr (FIRST) {
+      // im2col of the raw input: col kk = tap*4 + ci (kk < 28), rows = tile rows
+      for (int i = threadIdx.x; i < kR * 32; i += kThreads) {
+        const int r = i >> 5, kk = i & 31;
+        const int tap = kk >> 2, ci = kk & 3;
+        __bf16 v = (__bf16)0.f;
+        if (tap < K) v = A.x[(long long)(row0 + kHalo + r + tap - PAD) * 4 + ci];
+        *reinterpret_cast<__bf16*>(a_lds + r * ARS + kk * 2) = v;
+      }
+    } else {
+      stage_act<l - 1>(A, a_lds, ARS, row0, kRows, ci0, W::CIB / 8, sp, tp, 0, 0, 2 * tile);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < kR / 32; ++ks) {
+      bf16x8 fb[NCO];
+#pragma unroll
+      for (int a = 0; a < NCO; ++a) fb[a] = tr_frag(dz_lds, DZRS, ks * 32, (wco * NCO + a) * 16);
+#pragma unroll
+      for (int k = 0; k < NTAP; ++k) {
+#pragma unroll
+        for (int b = 0; b < NCI; ++b) {
+          const int arow = FIRST ? ks * 32 : kHalo + ks * 32 + k - PAD;
+          const bf16x8 fa = tr_frag(a_lds, ARS, arow, (wci * NCI + b) * 16);
+#pragma unroll
+          for (int a = 0; a < NCO; ++a) acc[k][b][a] = mfma16(fa, fb[a], acc[k][b][a]);
+        }
+      }
+    }
+  }
+  // lane (m, h) holds D[ci = 4h + i][co = m] of each tile: 16 consecutive co per row -> 64-B runs
+  const int m = lane & 15, h = lane >> 4;
+  const Layer& Ly = A.L[l];
+#pragma unroll
+  for (int k = 0; k < NTAP; ++k)
+#pragma unroll
+    for (int b = 0; b < NCI; ++b)
+#pragma unroll
+      for (int a = 0; a < NCO; ++a) {
+        const int co = co0 + (wco * NCO + a) * 16 + m;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int rowi = (wci * NCI + b) * 16 + 4 * h + i;  // ci (or kk for block 1)
+          if constexpr (FIRST) {
+            const int tap = rowi >> 2, ci = rowi & 3;
+            if (tap < K) atomicAdd(Ly.gw + (tap * CIN + ci) * COUT + co, acc[k][b][a][i]);
+          } else {
+            atomicAdd(Ly.gw + (k * CIN + ci0 + rowi) * COUT + co, acc[k][b][a][i]);
+          }
+        }
+      }
+  if (do_bias) {
+    __syncthreads();
+    for (int c = threadIdx.x; c < W::COB; c += kThreads) atomicAdd(Ly.gb + co0 + c, colsum[c]);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// BN finalize: moving averages (Keras momentum update on batch moments) and dgamma / dbeta.
+// ------------------------------------------------------------------------------------------------
+__global__ void bn_finalize_kernel(Args A, int update_moving, int grads) {
+  const int l = blockIdx.x;
+  const Layer& Ly = A.L[l];
+  const int Cc = (l == 0) ? C[1] : (l == 1) ? C[2] : (l == 2) ? C[3] : (l == 3) ? C[4] : (l == 4) ? C[5] : C[6];
+  for (int c = threadIdx.x; c < Cc; c += blockDim.x) {
+    if (update_moving) {
+      for (int g = 0; g < A.groups; ++g) {  // one Keras call (= one moving update) per group
+        const float mu = Ly.st[(g * 2) * Cc + c] * A.inv_count;
+        const float var = fmaxf(Ly.st[(g * 2 + 1) * Cc + c] * A.inv_count - mu * mu, 0.f);
+        Ly.mmean[c] = Ly.mmean[c] * A.momentum + mu * (1.f - A.momentum);
+        Ly.mvar[c] = Ly.mvar[c] * A.momentum + var * (1.f - A.momentum);
+      }
+    }
+    if (grads) {
+      Ly.gbeta[c] = Ly.bst[c];
+      Ly.ggamma[c] = Ly.bst[Cc + c];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Pack fp32 master kernels into bf16 MFMA A-operand fragments (forward and dgrad orientation).
+//   forward: frag[s][ct][lane][j] = W[tap][ci][co],  co = 16ct + (lane&15), kk = 32s + 8(lane>>4) + j,
+//            kk = tap*Cin + ci   (zero for kk >= k*Cin)
+//   dgrad:   W'[tap'][co][ci] = W[k-1-tap'][ci][co]: same formula with (Cin, Cout) swapped.
+// ------------------------------------------------------------------------------------------------
+__global__ void pack_kernel(const float* __restrict__ w, int k, int cin, int cout, __bf16* __restrict__ fwd,
+                            __bf16* __restrict__ dgr) {
+  const long long nf = (long long)((cin * k + 31) / 32) * 32 * cout;
+  const long long nd = (long long)((cout * k + 31) / 32) * 32 * cin;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < nf + nd; e += (long long)gridDim.x * blockDim.x) {
+    const bool is_f = e < nf;
+    const long long i = is_f ? e : e - nf;
+    const int ci_ = is_f ? cin : cout, co_ = is_f ? cout : cin;
+    const int j = (int)(i & 7), lane = (int)((i >> 3) & 63);
+    const long long fr = i >> 9;
+    const int nct = co_ / 16;
+    const int ct = (int)(fr % nct), s = (int)(fr / nct);
+    const int co = 16 * ct + (lane & 15);
+    const int kk = 32 * s + 8 * (lane >> 4) + j;
+    float v = 0.f;
+    if (kk < ci_ * k) {
+      const int tap = kk / ci_, ci = kk - tap * ci_;
+      v = is_f ? w[((long long)tap * cin + ci) * cout + co] : w[((long long)(k - 1 - tap) * cin + co) * cout + ci];
+    }
+    (is_f ? fwd : dgr)[i] = (__bf16)v;
+  }
+}
+
+}  // namespace train
+
+// ------------------------------------------------------------------------------------------------ host
+using train::Args;
+
+constexpr int lds_fwd() { return train::kRows * train::kRS + 1024 * 4; }
+constexpr int lds_dgrad() { return train::kRows * train::kRS + 2304 * 4; }
+template <int l>
+constexpr int lds_wgrad() {
+  return train::kR * (train::WgCfg<l>::COB * 2 + 16) + train::kRows * (train::WgCfg<l>::CIB * 2 + 16) + 2304 * 4;
+}
+
+int train_args_size() { return (int)sizeof(Args); }
+int train_layer_size() { return (int)sizeof(train::Layer); }
+
+hipError_t train_launch_fwd(const Args& A, int l, hipStream_t st) {
+  const int tiles = (A.B + 1) / 2;
+  switch (l) {
+    case 0: hipLaunchKernelGGL(train::fwd_kernel<0>, dim3(tiles), dim3(256), lds_fwd(), st, A); break;
+    case 1: hipLaunchKernelGGL(train::fwd_kernel<1>, dim3(tiles), dim3(256), lds_fwd(), st, A); break;
+    case 2: hipLaunchKernelGGL(train::fwd_kernel<2>, dim3(tiles), dim3(256), lds_fwd(), st, A); break;
+    case 3: hipLaunchKernelGGL(train::fwd_kernel<3>, dim3(tiles), dim3(256), lds_fwd(), st, A); break;
+    case 4: hipLaunchKernelGGL(train::fwd_kernel<4>, dim3(tiles), dim3(256), lds_fwd(), st, A); break;
+    case 5: hipLaunchKernelGGL(train::fwd_kernel<5>, dim3(tiles), dim3(256), lds_fwd(), st, A); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t train_launch_head(const Args& A, int backward, hipStream_t st) {
+  hipLaunchKernelGGL(train::head_kernel, dim3((A.B + 3) / 4), dim3(256), 384 * 4, st, A, backward);
+  return hipGetLastError();
+}
+
+hipError_t train_launch_dgrad(const Args& A, int l, hipStream_t st) {
+  const int tiles = (A.B + 1) / 2;
+  switch (l) {
+    case 1: hipLaunchKernelGGL(train::dgrad_kernel<1>, dim3(tiles), dim3(256), lds_dgrad(), st, A); break;
+    case 2: hipLaunchKernelGGL(train::dgrad_kernel<2>, dim3(tiles), dim3(256), lds_dgrad(), st, A); break;
+    case 3: hipLaunchKernelGGL(train::dgrad_kernel<3>, dim3(tiles), dim3(256), lds_dgrad(), st, A); break;
+    case 4: hipLaunchKernelGGL(train::dgrad_kernel<4>, dim3(tiles), dim3(256), lds_dgrad(), st, A); break;
+    case 5: hipLaunchKernelGGL(train::dgrad_kernel<5>, dim3(tiles), dim3(256), lds_dgrad(), st, A); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+template <int l>
+static void wg_launch(const Args& A, hipStream_t st) {
+  using W = train::WgCfg<l>;
+  const int nci = (l == 0) ? 1 : train::C[l] / W::CIB;
+  const int nco = train::C[l + 1] / W::COB;
+  const int tiles = (A.B + 1) / 2;
+  const int rgs = (tiles + train::kWgRowTiles - 1) / train::kWgRowTiles;
+  hipLaunchKernelGGL(train::wgrad_kernel<l>, dim3(nci * nco * rgs), dim3(256), lds_wgrad<l>(), st, A);
+}
+
+hipError_t train_launch_wgrad(const Args& A, int l, hipStream_t st) {
+  switch (l) {
+    case 0: wg_launch<0>(A, st); break;
+    case 1: wg_launch<1>(A, st); break;
+    case 2: wg_launch<2>(A, st); break;
+    case 3: wg_launch<3>(A, st); break;
+    case 4: wg_launch<4>(A, st); break;
+    case 5: wg_launch<5>(A, st); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t train_launch_finalize(const Args& A, int update_moving, int grads, hipStream_t st) {
+  hipLaunchKernelGGL(train::bn_finalize_kernel, dim3(6), dim3(256), 0, st, A, update_moving, grads);
+  return hipGetLastError();
+}
+
+hipError_t train_launch_pack(const float* w, int k, int cin, int cout, void* fwd, void* dgr, hipStream_t st) {
+  const long long n = (long long)((cin * k + 31) / 32) * 32 * cout + (long long)((cout * k + 31) / 32) * 32 * cin;
+  long long blocks = (n + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(train::pack_kernel, dim3((unsigned)blocks), dim3(256), 0, st, w, k, cin, cout,
+                     reinterpret_cast<__bf16*>(fwd), reinterpret_cast<__bf16*>(dgr));
+  return hipGetLastError();
+}
+
+}  // namespace apneauq

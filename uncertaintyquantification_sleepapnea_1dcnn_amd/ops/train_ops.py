@@ -1,11 +1,229 @@
-"""Layer-wise HIP training kernels (conv fwd/dgrad/wgrad with fused BN/dropout).  Placeholder
-until the kernels land: ``supports`` returns False so training uses the autograd path."""
+"""Host orchestration of the layer-wise HIP training kernels (``csrc/train_conv.hip``).
+
+One optimizer step (Keras semantics) is ~22 launches on one stream:
+
+  pack (bf16 MFMA fragments of all 6 kernels, forward + dgrad orientation)
+  fwd 1..6          R_l = relu(conv(dropout(BN(R_{l-1}))) + b), per-channel moments (atomics)
+  head              GAP + Dense + BCE + dlogit + dense grads + backward moments of block 6
+  dgrad 6..2        dY_{l-1} and the backward moments of block l-1
+  wgrad 6..1        dW_l, db_l (row-reduced in registers, fp32 atomics)
+  finalize          moving-average update + dgamma / dbeta
+  Adam              one multi-tensor launch over the flat buffer
+
+With data parallelism (``sync``) the per-layer moments and the backward moments are all-reduced
+between the launches (SyncBN: exactly the full-batch statistics of the reference's single-device
+Keras BN) and the flat gradient once at the end (one bucket, C1).
+
+The same forward kernels with ``groups = T`` implement MC Dropout with BatchNorm on per-pass
+batch statistics over the whole test set (the reference's ``model(x, training=True)``, Q1).
+"""
 from __future__ import annotations
 
+import struct
+from typing import Callable, List, Optional
 
-def supports(spec) -> bool:
-    return False
+import numpy as np
+import torch
+
+from ..models.spec import ModelSpec
+from . import _ext, fused, rng
+
+SR, HALO, ROWS_PER_TILE = 64, 4, 128
+TRAIN_PASS_BASE = 1 << 30
 
 
-def train_step(model, x, y, grad_allreduce=None):  # pragma: no cover
-    raise NotImplementedError
+def supports(spec: ModelSpec) -> bool:
+    return fused.supports(spec) and _ext.available()
+
+
+def _fbits(x: float) -> int:
+    return struct.unpack("<I", struct.pack("<f", float(x)))[0]
+
+
+def padded_rows(n_samples: int) -> int:
+    return ROWS_PER_TILE * ((n_samples + 1) // 2) + 2 * HALO
+
+
+def to_padded(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """(N, 60, C) -> padded-row layout (rows, C) bf16 with zero pad rows."""
+    n, L, c = x.shape
+    if out is None:
+        out = torch.zeros(padded_rows(n), c, dtype=torch.bfloat16, device=x.device)
+    out[HALO: HALO + SR * n].view(n, SR, c)[:, :L].copy_(x)
+    return out
+
+
+class TrainWorkspace:
+    """Device buffers + pointer context for one model and one (max) batch size."""
+
+    def __init__(self, model, batch: int, groups: int = 1, n_win: Optional[int] = None, with_backward: bool = True):
+        spec = model.spec
+        store = model.store
+        dev = store.device
+        self.model = model
+        self.B = int(batch)
+        self.groups = int(groups)
+        self.n_win = int(n_win if n_win is not None else batch)
+        rows = padded_rows(self.B)
+        ch = spec.channels()
+        ks = [b.kernel_size for b in spec.blocks]
+        bf = torch.bfloat16
+        self.x = torch.zeros(rows, ch[0], dtype=bf, device=dev)
+        self.R = [torch.zeros(rows, ch[l + 1], dtype=bf, device=dev) for l in range(6)]
+        self.dY = [torch.zeros(rows, ch[l + 1], dtype=bf, device=dev) if (with_backward and l < 5)
+                   else torch.zeros(16, dtype=bf, device=dev) for l in range(6)]
+        self.st_all = torch.zeros(sum(self.groups * 2 * ch[l + 1] for l in range(6)), device=dev)
+        self.bst_all = torch.zeros(sum(2 * ch[l + 1] for l in range(6)), device=dev)
+        self.st, self.bst = [], []
+        o1 = o2 = 0
+        for l in range(6):
+            n1, n2 = self.groups * 2 * ch[l + 1], 2 * ch[l + 1]
+            self.st.append(self.st_all[o1: o1 + n1])
+            self.bst.append(self.bst_all[o2: o2 + n2])
+            o1 += n1
+            o2 += n2
+        self.wf, self.wd = [], []
+        for l in range(6):
+            nf = ((ch[l] * ks[l] + 31) // 32) * 32 * ch[l + 1]
+            nd = ((ch[l + 1] * ks[l] + 31) // 32) * 32 * ch[l]
+            self.wf.append(torch.zeros(nf, dtype=bf, device=dev))
+            self.wd.append(torch.zeros(nd, dtype=bf, device=dev))
+        self.y = torch.zeros(self.B, device=dev)
+        self.logits = torch.zeros(self.B, device=dev)
+        self.dlogit = torch.zeros(self.B, device=dev)
+        self.loss = torch.zeros(1, device=dev)
+        self.grad = torch.zeros_like(store.flat)
+        self.gviews = {}
+        for n in store.trainable:
+            off = store.offsets[n]
+            self.gviews[n] = self.grad[off: off + store.views[n].numel()].view(store.shapes[n])
+        self.ks = ks
+        self.ch = ch
+        self._ctx_key = None
+        self.ctx = None
+
+    def build_ctx(self, n: int, n_win: int, groups: int, window_offset: int, seed: int, dropout: bool,
+                  inv_count: float, inv_batch: float):
+        key = (n, n_win, groups, window_offset, seed, dropout, inv_count, inv_batch)
+        if key == self._ctx_key:
+            return self.ctx
+        spec, v, g = self.model.spec, self.model.store.views, self.gviews
+        vals: List[int] = []
+        for l in range(6):
+            i = l + 1
+            p = spec.blocks[l].dropout
+            vals += [self.wf[l].data_ptr(), self.wd[l].data_ptr(), v[f"conv1d_{i}/bias"].data_ptr(),
+                     v[f"batchnorm_{i}/gamma"].data_ptr(), v[f"batchnorm_{i}/beta"].data_ptr(),
+                     v[f"batchnorm_{i}/moving_mean"].data_ptr(), v[f"batchnorm_{i}/moving_variance"].data_ptr(),
+                     g[f"conv1d_{i}/kernel"].data_ptr(), g[f"conv1d_{i}/bias"].data_ptr(),
+                     g[f"batchnorm_{i}/gamma"].data_ptr(), g[f"batchnorm_{i}/beta"].data_ptr(),
+                     self.R[l].data_ptr(), self.dY[l].data_ptr(), self.st[l].data_ptr(), self.bst[l].data_ptr(),
+                     rng.dropout_threshold(p), _fbits(1.0 / (1.0 - p) if p < 1 else 0.0)]
+        vals += [self.x.data_ptr(), self.y.data_ptr(), v["output_layer/kernel"].data_ptr(),
+                 v["output_layer/bias"].data_ptr(), g["output_layer/kernel"].data_ptr(),
+                 g["output_layer/bias"].data_ptr(), self.logits.data_ptr(), self.dlogit.data_ptr(),
+                 self.loss.data_ptr(), n, n_win, groups, TRAIN_PASS_BASE, window_offset,
+                 int(seed) & ((1 << 63) - 1), int(bool(dropout)), _fbits(inv_count), _fbits(inv_batch),
+                 _fbits(spec.bn_epsilon), _fbits(spec.bn_momentum)]
+        self.ctx = torch.tensor(vals, dtype=torch.int64)
+        self._ctx_key = key
+        return self.ctx
+
+    def pack(self) -> None:
+        o = _ext.ops()
+        v = self.model.store.views
+        for l in range(6):
+            o.train_pack(v[f"conv1d_{l + 1}/kernel"], self.ks[l], self.ch[l], self.ch[l + 1], self.wf[l], self.wd[l])
+
+
+def _call(ctx, op, layer=0, flag=0, pass_base=-1, device=0):
+    _ext.ops().train_call(ctx, op, layer, flag, pass_base, device)
+
+
+def _get_ws(model, batch: int) -> TrainWorkspace:
+    ws = getattr(model, "_train_ws", None)
+    if ws is None or ws.B < batch or ws.groups != 1:
+        ws = TrainWorkspace(model, batch)
+        model._train_ws = ws
+    return ws
+
+
+def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, sync: Optional[Callable] = None,
+               global_batch: Optional[int] = None, window_offset: int = 0):
+    """One Keras-semantics optimizer step with the HIP kernels; returns (loss_sum, probs)."""
+    n = x.shape[0]
+    ws = _get_ws(model, n)
+    gb = global_batch or n
+    sync = sync or getattr(model, "bn_sync", None)
+    if sync is not None and global_batch is None:
+        gb = getattr(model, "dp_global_batch", lambda b: b)(n)
+        window_offset = getattr(model, "dp_window_offset", lambda b: 0)(n)
+    ctx = ws.build_ctx(n, n, 1, window_offset, model.seed, True, 1.0 / (gb * 60), 1.0 / gb)
+    dev = x.device.index or 0
+    # inputs in padded-row layout (pad rows stay zero)
+    ws.x[HALO: HALO + SR * n].view(n, SR, ws.ch[0])[:, :60].copy_(x)
+    if n < ws.B:  # a partial last batch: clear rows of samples beyond n (stale data from a larger batch)
+        ws.x[HALO + SR * n:].zero_()
+    ws.y[:n].copy_(y.reshape(-1))
+    ws.st_all.zero_()
+    ws.bst_all.zero_()
+    ws.grad.zero_()
+    ws.loss.zero_()
+    ws.pack()
+    pb = TRAIN_PASS_BASE + model._train_step_counter
+    for l in range(6):
+        _call(ctx, 0, l, 0, pb, dev)
+        if sync is not None:
+            sync(ws.st[l])
+    _call(ctx, 1, 0, 1, pb, dev)
+    if sync is not None:
+        sync(ws.bst[5])
+    for l in range(5, 0, -1):
+        _call(ctx, 2, l, 0, pb, dev)
+        if sync is not None:
+            sync(ws.bst[l - 1])
+        _call(ctx, 3, l, 0, pb, dev)
+    _call(ctx, 3, 0, 0, pb, dev)
+    _call(ctx, 4, 1, 1, pb, dev)
+    scale = 1.0
+    if grad_allreduce is not None:
+        scale = grad_allreduce(ws.grad)
+    model.optimizer.step(model.store.flat, ws.grad, grad_scale=scale)
+    return ws.loss.double().sum(), torch.sigmoid(ws.logits[:n])
+
+
+@torch.no_grad()
+def forward_batch_stats(model, x: torch.Tensor, n_pass: int, pass_base: int, seed: int, update_moving: bool = True,
+                        sync: Optional[Callable] = None, window_offset: int = 0, global_n: Optional[int] = None,
+                        max_samples: int = 1 << 20) -> torch.Tensor:
+    """MC Dropout with BN on per-pass batch statistics (reference semantics): (T, N) probabilities.
+
+    Passes are processed in chunks (statistics are per pass, so chunking is exact).
+    """
+    n = x.shape[0]
+    gn = global_n or n
+    chunk = max(1, min(n_pass, max_samples // max(n, 1)))
+    outs = []
+    dev = x.device.index or 0
+    ws = getattr(model, "_mcd_ws", None)
+    if ws is None or ws.B != chunk * n or ws.groups != chunk:
+        ws = TrainWorkspace(model, chunk * n, groups=chunk, n_win=n, with_backward=False)
+        model._mcd_ws = ws
+    xb = x.to(torch.bfloat16)
+    for t0 in range(0, n_pass, chunk):
+        tc = min(chunk, n_pass - t0)
+        bs = tc * n
+        ctx = ws.build_ctx(bs, n, tc, window_offset, seed, True, 1.0 / (gn * 60), 1.0)
+        ws.x[HALO: HALO + SR * bs].view(tc, n, SR, ws.ch[0])[:, :, :60].copy_(xb.unsqueeze(0).expand(tc, n, 60, ws.ch[0]))
+        ws.st_all.zero_()
+        ws.pack()
+        for l in range(6):
+            _call(ctx, 0, l, 0, pass_base + t0, dev)
+            if sync is not None:
+                sync(ws.st[l])
+        _call(ctx, 1, 0, 0, pass_base + t0, dev)
+        if update_moving:
+            _call(ctx, 4, 1, 0, pass_base + t0, dev)
+        outs.append(torch.sigmoid(ws.logits[:bs].view(tc, n)).clone())
+    model.store.bump()
+    return torch.cat(outs, 0)
