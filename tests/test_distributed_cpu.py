@@ -1,0 +1,105 @@
+"""Multi-process (gloo, world_size 2, CPU) tests of the distributed paths: data-parallel step ==
+single-device step (SyncBN + gradient bucket), MC-Dropout sharding invariance, DE all_to_all,
+ensemble-parallel training with member-granularity resume."""
+import os
+
+import numpy as np
+import torch
+
+from .dist_utils import run_ranks
+
+
+def _data(n=24, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, 60, 4, generator=g)
+    y = (torch.rand(n, generator=g) > 0.5).float()
+    return x, y
+
+
+def _dp_step(rank, world):
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.models.cnn import AlarconCNN1D
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel.data_parallel import DPContext, split_batch
+
+    x, y = _data()
+    m = AlarconCNN1D(seed=3, device="cpu")
+    m.dp = DPContext(None, world, rank)
+    idx, off = split_batch(torch.arange(x.shape[0]), m.dp)
+    m.train_step(x[idx], y[idx], dp_step=(x.shape[0], off))
+    return m.store.flat.clone(), m.store.stats.clone()
+
+
+def test_data_parallel_step_equals_single_device():
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.models.cnn import AlarconCNN1D
+
+    res = run_ranks(_dp_step, 2)
+    x, y = _data()
+    m = AlarconCNN1D(seed=3, device="cpu")
+    m.train_step(x, y)
+    for flat, stats in res:
+        torch.testing.assert_close(flat, m.store.flat, atol=2e-6, rtol=1e-5)
+        torch.testing.assert_close(stats, m.store.stats, atol=2e-6, rtol=1e-5)
+
+
+def _mcd_shard(rank, world):
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.models.cnn import AlarconCNN1D
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel import dist as pdist
+
+    x, _ = _data(21, 1)
+    m = AlarconCNN1D(seed=4, device="cpu")
+    s, e = pdist.shard_range(x.shape[0], rank, world)
+    out = []
+    for t in range(3):
+        out.append(torch.sigmoid(m.logits(x[s:e], dropout=True, bn_batch_stats=False, pass_id=t,
+                                          sample_ids=torch.arange(s, e))).reshape(-1))
+    return s, torch.stack(out)
+
+
+def test_mc_dropout_sharding_invariance():
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.models.cnn import AlarconCNN1D
+
+    res = run_ranks(_mcd_shard, 2)
+    x, _ = _data(21, 1)
+    m = AlarconCNN1D(seed=4, device="cpu")
+    full = torch.stack([torch.sigmoid(m.logits(x, dropout=True, bn_batch_stats=False, pass_id=t)).reshape(-1)
+                        for t in range(3)])
+    got = torch.cat([r[1] for r in sorted(res, key=lambda r: r[0])], dim=1)
+    torch.testing.assert_close(got, full, atol=1e-6, rtol=1e-6)
+
+
+def _de_a2a(rank, world):
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel import inference as pinf
+
+    n_glob, M = 10, 4
+    probs_all = torch.arange(M * n_glob, dtype=torch.float32).reshape(M, n_glob) / 100.0
+    mloc = M // world
+    local = probs_all[rank * mloc:(rank + 1) * mloc]
+    got = pinf.all_to_all_members(local, world)
+    return got
+
+
+def test_de_member_parallel_all_to_all():
+    res = run_ranks(_de_a2a, 2)
+    M, n_glob = 4, 10
+    probs_all = torch.arange(M * n_glob, dtype=torch.float32).reshape(M, n_glob) / 100.0
+    for r, got in enumerate(res):
+        torch.testing.assert_close(got, probs_all[:, r * 5:(r + 1) * 5])
+
+
+def _ens_train(rank, world, save_dir):
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.data.synthetic import synthetic_windows
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel.ensemble import train_ensemble
+
+    x, y, _ = synthetic_windows(96, seed=2)
+    return train_ensemble(x, y.astype(np.float32), num_models=3, seed_base=7, save_dir=save_dir, epochs=1,
+                          batch_size=32, verbose=0, device="cpu")
+
+
+def test_ensemble_parallel_training_and_resume(tmp_path):
+    d = str(tmp_path / "ens")
+    paths = run_ranks(_ens_train, 2, (d,))[0]
+    assert all(os.path.exists(p) for p in paths) and len(paths) == 3
+    mt = {p: os.path.getmtime(p) for p in paths}
+    os.remove(paths[1])  # simulate a member lost to a failure: resume retrains only that one
+    run_ranks(_ens_train, 2, (d,))
+    assert os.path.exists(paths[1])
+    assert os.path.getmtime(paths[0]) == mt[paths[0]] and os.path.getmtime(paths[2]) == mt[paths[2]]

@@ -48,6 +48,7 @@ class AlarconCNN1D:
         self.loss = "binary_crossentropy"
         self.metrics_names = ["loss", "accuracy", "auc"]
         self.stop_training = False
+        self.dp = None  # parallel.data_parallel.DPContext when training data-parallel
         self._blob = None
         self._blob_version = -1
         self._call_counter = 0
@@ -179,12 +180,12 @@ class AlarconCNN1D:
         return np.concatenate(outs) if outs else np.zeros((0, 1), np.float32)
 
     # ------------------------------------------------------------------ training
-    def train_step(self, x, y, return_probs: bool = False, grad_allreduce=None):
+    def train_step(self, x, y, return_probs: bool = False, grad_allreduce=None, dp_step=None):
         """One optimizer step on a batch (Keras training semantics); returns the summed BCE."""
         from ..training import step as tstep
 
         loss_sum, probs = tstep.train_step(self, self._as_input(x), torch.as_tensor(y, device=self.device).float(),
-                                           grad_allreduce=grad_allreduce)
+                                           grad_allreduce=grad_allreduce, dp_step=dp_step)
         self._train_step_counter += 1
         self.store.bump()
         if return_probs:

@@ -31,6 +31,19 @@ def mcd_probs_local(blob: torch.Tensor, x_local_bf16: torch.Tensor, n_pass: int,
                                window_offset=window_offset)[0]
 
 
+def all_to_all_members(p_local: torch.Tensor, world: int, group=None) -> torch.Tensor:
+    """(M/G, N_global) member probabilities of this rank's members over ALL windows ->
+    (M, N_global/G) probabilities of ALL members over this rank's window shard (one RCCL all_to_all)."""
+    if world == 1:
+        return p_local
+    mloc, ng = p_local.shape
+    n = ng // world
+    send = p_local.reshape(mloc, world, n).transpose(0, 1).contiguous()  # (G dest, M/G, n)
+    recv = torch.empty_like(send)  # (G src, M/G, n)
+    dist.all_to_all_single(recv, send, group=group)
+    return recv.reshape(world * mloc, n)
+
+
 def de_probs_member_parallel(blobs_local: torch.Tensor, x_global_bf16: torch.Tensor, world: int,
                              spec: ModelSpec = DEFAULT_SPEC, group=None) -> torch.Tensor:
     """(M, N_global/G) ensemble probabilities of this rank's window shard.
@@ -39,14 +52,7 @@ def de_probs_member_parallel(blobs_local: torch.Tensor, x_global_bf16: torch.Ten
     resident on every rank, N_global divisible by G.
     """
     p = fused.fused_forward(x_global_bf16, blobs_local, spec)[:, 0]  # (M/G, N_global)
-    if world == 1:
-        return p
-    mloc, ng = p.shape
-    n = ng // world
-    send = p.reshape(mloc, world, n).transpose(0, 1).contiguous()  # (G dest, M/G, n)
-    recv = torch.empty_like(send)  # (G src, M/G, n)
-    dist.all_to_all_single(recv, send, group=group)
-    return recv.reshape(world * mloc, n)
+    return all_to_all_members(p, world, group)
 
 
 def aggregate_sums(metrics: torch.Tensor, y: Optional[torch.Tensor]) -> torch.Tensor:

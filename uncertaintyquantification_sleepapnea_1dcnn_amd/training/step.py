@@ -30,31 +30,44 @@ def _backend(model) -> str:
     return "torch"
 
 
-def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None):
+def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, dp_step=None):
+    """``dp_step = (global_batch, offset)`` when the model trains data-parallel (``model.dp``)."""
     backend = _backend(model)
+    dp = getattr(model, "dp", None)
+    if dp is not None and dp.size == 1:
+        dp = None
+    gn, off = dp_step if (dp is not None and dp_step is not None) else (x.shape[0], 0)
     if backend == "hip":
         from ..ops import train_ops
 
+        if dp is not None:
+            def _gar(g):
+                dp.all_reduce_(g)
+                return 1.0  # kernels already scale by 1/global batch
+
+            return train_ops.train_step(model, x, y, grad_allreduce=_gar, sync=dp.all_reduce_, global_batch=gn,
+                                        window_offset=off)
         return train_ops.train_step(model, x, y, grad_allreduce=grad_allreduce)
     store = model.store
     flat = store.flat.detach().requires_grad_(True)
     p = {}
     for n in store.trainable:
-        off = store.offsets[n]
-        k = store.views[n].numel()
-        p[n] = flat[off: off + k].view(store.shapes[n])
+        o = store.offsets[n]
+        p[n] = flat[o: o + store.views[n].numel()].view(store.shapes[n])
     for n in store.nontrainable:
         p[n] = store.views[n]
-    sample_ids = torch.arange(x.shape[0], device=x.device)
+    sample_ids = off + torch.arange(x.shape[0], device=x.device)
     logits = R.forward(model.spec, p, x, dropout=True, bn_batch_stats=True, update_moving=True, seed=model.seed,
                        pass_id=TRAIN_PASS_BASE + model._train_step_counter, sample_ids=sample_ids,
-                       return_logits=True, bn_stats_hook=getattr(model, "bn_stats_hook", None))
+                       return_logits=True, bn_stats_hook=dp.moments_hook() if dp is not None else None)
     lv = torch.nn.functional.binary_cross_entropy_with_logits(logits.reshape(-1), y.reshape(-1), reduction="none")
-    loss = lv.mean()
+    loss = lv.sum() / gn  # mean over the (global) batch
     loss.backward()
     grad = flat.grad
     scale = 1.0
-    if grad_allreduce is not None:
+    if dp is not None:
+        dp.all_reduce_(grad)
+    elif grad_allreduce is not None:
         scale = grad_allreduce(grad)
     model.optimizer.step(store.flat, grad, grad_scale=scale)
     return lv.detach().sum().double(), torch.sigmoid(logits.detach()).reshape(-1)

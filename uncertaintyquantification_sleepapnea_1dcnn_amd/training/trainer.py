@@ -23,7 +23,22 @@ import numpy as np
 import torch
 
 from .callbacks import Callback, History
+from ..parallel.data_parallel import split_batch
 from .metrics import AUC, BinaryAccuracy, MeanMetric
+
+
+def _sync_metrics(dp, loss_acc: torch.Tensor, acc_m, auc_m) -> None:
+    """Sum the epoch's per-rank metric state over the data-parallel group."""
+    dev = loss_acc.device
+    buf = torch.tensor([acc_m.total, acc_m.count], dtype=torch.float64, device=dev)
+    hist = torch.tensor(np.concatenate([auc_m.pos_hist, auc_m.neg_hist]), dtype=torch.float64, device=dev)
+    dp.all_reduce_(loss_acc)
+    dp.all_reduce_(buf)
+    dp.all_reduce_(hist)
+    acc_m.total, acc_m.count = float(buf[0]), float(buf[1])
+    k = auc_m.pos_hist.size
+    h = hist.cpu().numpy()
+    auc_m.pos_hist, auc_m.neg_hist = h[:k].copy(), h[k:].copy()
 
 
 def _to_device(a, device, dtype=torch.float32) -> torch.Tensor:
@@ -82,14 +97,23 @@ def fit(model, x, y, batch_size: int = 32, epochs: int = 1, verbose: int = 1, ca
         perm = torch.randperm(n, generator=gen).to(dev) if shuffle else torch.arange(n, device=dev)
         loss_m, acc_m, auc_m = MeanMetric(), BinaryAccuracy(), AUC()
         loss_acc = torch.zeros((), dtype=torch.float64, device=dev)
+        dp = getattr(model, "dp", None)
+        n_seen = 0
         for s in range(steps):
-            idx = perm[s * batch_size: (s + 1) * batch_size]
+            gidx = perm[s * batch_size: (s + 1) * batch_size]
+            if dp is not None and dp.size > 1 and gidx.numel() < dp.size:
+                continue  # a tail batch smaller than the DP group is dropped on every rank
+            idx, off = split_batch(gidx, dp)
             xb, yb = Xt.index_select(0, idx), Yt.index_select(0, idx)
-            loss_sum, p = model.train_step(xb, yb, return_probs=True, grad_allreduce=grad_allreduce)
+            loss_sum, p = model.train_step(xb, yb, return_probs=True, grad_allreduce=grad_allreduce,
+                                           dp_step=(int(gidx.numel()), off))
             loss_acc += loss_sum
+            n_seen += int(gidx.numel())
             acc_m.update_state(yb, p)
             auc_m.update_state(yb, p)
-        loss_m.update(loss_acc.item(), n)
+        if dp is not None and dp.size > 1:
+            _sync_metrics(dp, loss_acc, acc_m, auc_m)
+        loss_m.update(loss_acc.item(), n_seen)
         logs = {"loss": loss_m.result(), "accuracy": acc_m.result(), "auc": auc_m.result()}
         if Xv is not None and Xv.shape[0] > 0:
             vl, va, vauc = evaluate_arrays(model, Xv, Yv, batch_size)
