@@ -1,0 +1,84 @@
+"""CPU tier: architecture spec, Keras-default init, 38-array checkpoint layout, counter-based
+dropout masks (NumPy == torch, rate), fused-blob packing (bf16 emulation == fp32 reference)."""
+import numpy as np
+import pytest
+import torch
+
+from uncertaintyquantification_sleepapnea_1dcnn_amd.models import reference as R
+from uncertaintyquantification_sleepapnea_1dcnn_amd.models.cnn import AlarconCNN1D, load_model
+from uncertaintyquantification_sleepapnea_1dcnn_amd.models.spec import DEFAULT_SPEC, ModelSpec
+from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import fused, rng
+
+
+def test_spec_counts():
+    assert DEFAULT_SPEC.num_params() == (853441, 851457)
+    assert DEFAULT_SPEC.forward_macs() == 50903136
+    assert len(DEFAULT_SPEC.weight_names()) == 38
+    assert DEFAULT_SPEC.weight_shapes()[0] == (7, 4, 128)
+    assert DEFAULT_SPEC.weight_shapes()[-2:] == [(96, 1), (1,)]
+    s = ModelSpec.from_dict(DEFAULT_SPEC.to_dict())
+    assert s == DEFAULT_SPEC
+
+
+def test_keras_init():
+    p = R.init_params(DEFAULT_SPEC, 0)
+    k = p["conv1d_2/kernel"]
+    lim = np.sqrt(6.0 / (5 * 128 + 5 * 192))
+    assert float(k.abs().max()) <= lim + 1e-6 and float(k.abs().max()) > 0.9 * lim
+    assert torch.all(p["batchnorm_3/moving_variance"] == 1) and torch.all(p["conv1d_3/bias"] == 0)
+
+
+def test_checkpoint_roundtrip(tmp_path):
+    m = AlarconCNN1D(seed=1, device="cpu")
+    w = m.get_weights()
+    assert len(w) == 38 and [a.shape for a in w] == [tuple(s) for s in DEFAULT_SPEC.weight_shapes()]
+    w[5] = w[5] + 0.5  # moving variance of BN1
+    m.set_weights(w)
+    path = m.save(str(tmp_path / "AlCNN_smote_seed21.keras"))
+    m2 = load_model(path, device="cpu")
+    for a, b in zip(m.get_weights(), m2.get_weights()):
+        np.testing.assert_array_equal(a, b)
+    with np.load(path, allow_pickle=False) as z:
+        assert "conv1d_1/kernel" in z.files and "output_layer/bias" in z.files
+
+
+def test_dropout_masks_numpy_equals_torch_and_rate():
+    key = rng.stream_key(2025, 3, 17)
+    samples = np.arange(100, 140)
+    a = rng.keep_mask_np(key, samples, 60, 96, 0.2)
+    b = rng.keep_mask_torch(key, torch.from_numpy(samples), 60, 96, 0.2).numpy()
+    np.testing.assert_array_equal(a, b)
+    assert abs(a.mean() - 0.8) < 0.01
+    c = rng.keep_mask_np(rng.stream_key(2025, 3, 18), samples, 60, 96, 0.2)
+    assert (a != c).mean() > 0.2  # different pass -> different mask
+
+
+def test_reference_forward_modes():
+    m = AlarconCNN1D(seed=2, device="cpu")
+    x = torch.randn(5, 60, 4)
+    p1 = m(x)
+    p2 = m(x)
+    torch.testing.assert_close(p1, p2)  # inference is deterministic
+    t1 = m(x, training=True)
+    t2 = m(x, training=True)
+    assert (t1 - t2).abs().max() > 0  # fresh dropout stream per call
+    assert p1.shape == (5, 1) and torch.all((p1 > 0) & (p1 < 1))
+
+
+def test_fused_packing_roundtrip_and_emulation():
+    p = R.init_params(DEFAULT_SPEC, 3)
+    for i in range(1, 7):
+        c = DEFAULT_SPEC.blocks[i - 1].filters
+        p[f"batchnorm_{i}/moving_mean"] = torch.rand(c) * 0.3
+        p[f"batchnorm_{i}/moving_variance"] = torch.rand(c) + 0.5
+    for i, b in enumerate(DEFAULT_SPEC.blocks, start=1):
+        w = p[f"conv1d_{i}/kernel"]
+        fr = fused.pack_conv_fragments(w)
+        back = fused.unpack_conv_fragments(fr, *w.shape)
+        torch.testing.assert_close(back, w.to(torch.bfloat16).float())
+    blob = fused.pack_blob(DEFAULT_SPEC, p)
+    assert blob.numel() == fused.layout()["bytes"]
+    x = torch.randn(7, 60, 4)
+    ref = R.forward(DEFAULT_SPEC, p, x, dropout=False, bn_batch_stats=False, return_logits=True).reshape(-1)
+    emu = fused.emulate_blob_forward(blob, x, logits=True)
+    assert (ref - emu).abs().max() < 0.05

@@ -1,0 +1,109 @@
+"""Keras-semantics tests (SURVEY §4 test 3): tail validation split, EarlyStopping restore rule,
+BN momentum/epsilon, Adam epsilon, AUC thresholds, loss reduction on a learnable task."""
+import numpy as np
+import pytest
+import torch
+from sklearn.metrics import roc_auc_score
+
+from uncertaintyquantification_sleepapnea_1dcnn_amd.data.synthetic import synthetic_windows
+from uncertaintyquantification_sleepapnea_1dcnn_amd.models.cnn import AlarconCNN1D
+from uncertaintyquantification_sleepapnea_1dcnn_amd.training.callbacks import EarlyStopping
+from uncertaintyquantification_sleepapnea_1dcnn_amd.training.metrics import AUC, keras_thresholds
+from uncertaintyquantification_sleepapnea_1dcnn_amd.training.optim import Adam
+
+
+class _Dummy:
+    def __init__(self):
+        self.w = 0
+        self.stop_training = False
+        self.restored = None
+
+    def snapshot(self):
+        return self.w
+
+    def restore(self, s):
+        self.restored = s
+
+
+def test_early_stopping_keras_rule():
+    es = EarlyStopping(patience=2, restore_best_weights=True)
+    m = _Dummy()
+    es.set_model(m)
+    es.on_train_begin()
+    for epoch, vl in enumerate([1.0, 0.8, 0.9, 0.95, 0.7]):
+        m.w = epoch
+        es.on_epoch_end(epoch, {"val_loss": vl})
+        if m.stop_training:
+            break
+    assert m.stop_training and es.stopped_epoch == 3 and m.restored == 1  # best epoch 1 restored at the stop
+    # no restore when training ends naturally
+    es2 = EarlyStopping(patience=5, restore_best_weights=True)
+    m2 = _Dummy()
+    es2.set_model(m2)
+    es2.on_train_begin()
+    for epoch, vl in enumerate([1.0, 0.8, 0.9]):
+        es2.on_epoch_end(epoch, {"val_loss": vl})
+    assert not m2.stop_training and m2.restored is None
+
+
+def test_adam_keras_formula():
+    p = torch.tensor([1.0, -2.0])
+    g = torch.tensor([0.5, 0.25])
+    opt = Adam(1e-3)
+    opt.step(p, g)
+    # first step: m = 0.1 g, v = 0.001 g^2, alpha = lr*sqrt(1-0.999)/(1-0.9)
+    alpha = 1e-3 * np.sqrt(1 - 0.999) / (1 - 0.9)
+    m, v = 0.1 * g, 0.001 * g * g
+    exp = torch.tensor([1.0, -2.0]) - alpha * m / (v.sqrt() + 1e-7)
+    torch.testing.assert_close(p, exp)
+
+
+def test_auc_matches_threshold_rule():
+    rs = np.random.RandomState(0)
+    y = (rs.rand(2000) > 0.5).astype(np.float32)
+    p = np.clip(y * 0.3 + rs.rand(2000) * 0.7, 0, 1).astype(np.float32)
+    a = AUC()
+    a.update_state(torch.from_numpy(y[:700]), torch.from_numpy(p[:700]))
+    a.update_state(torch.from_numpy(y[700:]), torch.from_numpy(p[700:]))
+    thr = keras_thresholds()
+    tp = np.array([((p > t) & (y == 1)).sum() for t in thr])
+    fp = np.array([((p > t) & (y == 0)).sum() for t in thr])
+    tpr, fpr = tp / (y == 1).sum(), fp / (y == 0).sum()
+    ref = np.sum((fpr[:-1] - fpr[1:]) * (tpr[:-1] + tpr[1:]) / 2)
+    assert a.result() == pytest.approx(ref, abs=1e-9)
+    assert a.result() == pytest.approx(roc_auc_score(y, p), abs=5e-3)
+
+
+def test_bn_moving_update_and_tail_validation_split():
+    m = AlarconCNN1D(seed=0, device="cpu")
+    x, y, _ = synthetic_windows(100, seed=0)
+    before = m.store.views["batchnorm_1/moving_mean"].clone()
+    m(torch.from_numpy(x), training=True)
+    after = m.store.views["batchnorm_1/moving_mean"]
+    h = torch.relu(torch.nn.functional.conv1d(torch.nn.functional.pad(torch.from_numpy(x).transpose(1, 2), (3, 3)),
+                                              m.store.views["conv1d_1/kernel"].permute(2, 1, 0),
+                                              m.store.views["conv1d_1/bias"]))
+    torch.testing.assert_close(after, before * 0.99 + h.mean((0, 2)) * 0.01, atol=1e-6, rtol=1e-5)
+    # tail split: the validation set is the LAST 10 % of the arrays (not shuffled)
+    seen = {}
+
+    def spy(model, X, Y, bs=1024):
+        seen["val"] = X.clone()
+        return 0.5, 0.5, 0.5
+
+    import uncertaintyquantification_sleepapnea_1dcnn_amd.training.trainer as T
+
+    orig = T.evaluate_arrays
+    T.evaluate_arrays = spy
+    try:
+        m.fit(x, y.astype(np.float32), batch_size=32, epochs=1, validation_split=0.1, verbose=0)
+    finally:
+        T.evaluate_arrays = orig
+    torch.testing.assert_close(seen["val"], torch.from_numpy(x[90:]))
+
+
+def test_training_learns_cpu():
+    x, y, _ = synthetic_windows(512, seed=3)
+    m = AlarconCNN1D(seed=3, device="cpu")
+    h = m.fit(x, y.astype(np.float32), batch_size=64, epochs=2, validation_split=0.1, verbose=0)
+    assert h.history["loss"][1] < h.history["loss"][0]
