@@ -149,30 +149,21 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
     }
   };
 
-  // ---- K loop
-#ifndef APNEAUQ_A_DBUF
-#define APNEAUQ_A_DBUF 1
-#endif
-#if APNEAUQ_A_DBUF
+  // ---- K loop.  Weight fragments of step s+1 are in flight under step s's MFMAs.  Every load is
+  // unconditional (the prefetch index is clamped) so hipcc's vmcnt bookkeeping stays exact: with a
+  // conditional prefetch it must assume the short path and waits vmcnt(0) on the prefetch itself.
   bf16x8 a0[CT], a1[CT];
   load_a(0, a0);
 #pragma unroll 1
-  for (int s = 0; s < NSTEP; s += 2) {
-    if (s + 1 < NSTEP) load_a(s + 1, a1);
+  for (int s = 0; s + 1 < NSTEP; s += 2) {
+    load_a(s + 1, a1);
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this step's MFMAs
     step(s, a0);
-    if (s + 1 < NSTEP) {
-      if (s + 2 < NSTEP) load_a(s + 2, a0);
-      step(s + 1, a1);
-    }
+    load_a(s + 2 < NSTEP ? s + 2 : s + 1, a0);
+    __builtin_amdgcn_sched_barrier(0);
+    step(s + 1, a1);
   }
-#else
-#pragma unroll 2
-  for (int s = 0; s < NSTEP; ++s) {
-    bf16x8 a0[CT];
-    load_a(s, a0);
-    step(s, a0);
-  }
-#endif
+  if constexpr (NSTEP & 1) step(NSTEP - 1, a0);
 
   // ---- epilogue: bias + ReLU + BN(running) + dropout, then bf16 in place (or GAP head)
   const unsigned thr = X.thr;

@@ -251,17 +251,19 @@ struct Conv {
         for (int c = 0; c < CT; ++c) acc[c][r] = mfma16(a[c], b, acc[c][r]);
       }
     };
+    // unconditional (clamped) prefetch keeps hipcc's vmcnt accounting exact (see fused_forward.hip)
     bf16x8 a0[CT], a1[CT];
     load_a(0, a0);
 #pragma unroll 1
-    for (int s = 0; s < NSTEP; s += 2) {
-      if (s + 1 < NSTEP) load_a(s + 1, a1);
+    for (int s = 0; s + 1 < NSTEP; s += 2) {
+      load_a(s + 1, a1);
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this step's MFMAs
       step(s, a0);
-      if (s + 1 < NSTEP) {
-        if (s + 2 < NSTEP) load_a(s + 2, a0);
-        step(s + 1, a1);
-      }
+      load_a(s + 2 < NSTEP ? s + 2 : s + 1, a0);
+      __builtin_amdgcn_sched_barrier(0);
+      step(s + 1, a1);
     }
+    if constexpr (NSTEP & 1) step(NSTEP - 1, a0);
   }
 };
 
