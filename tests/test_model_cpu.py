@@ -82,3 +82,20 @@ def test_fused_packing_roundtrip_and_emulation():
     ref = R.forward(DEFAULT_SPEC, p, x, dropout=False, bn_batch_stats=False, return_logits=True).reshape(-1)
     emu = fused.emulate_blob_forward(blob, x, logits=True)
     assert (ref - emu).abs().max() < 0.05
+
+
+def test_eager_comparator_matches_reference_forward():
+    """bench/comparator.py's torch.nn model computes the same function as models/reference.py."""
+    from bench.comparator import EagerCNN
+
+    p = R.synthetic_params(DEFAULT_SPEC, 3)
+    m = EagerCNN().load_keras(p).eval()
+    x = torch.randn(16, 60, 4)
+    with torch.no_grad():
+        np.testing.assert_allclose(m(x).numpy(), R.forward(DEFAULT_SPEC, p, x).numpy(), rtol=1e-4, atol=1e-5)
+        m.train()
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.Dropout):
+                mod.p = 0.0
+        ref = R.forward(DEFAULT_SPEC, p, x, training=True, dropout=False)
+        np.testing.assert_allclose(m(x).numpy(), ref.numpy(), rtol=1e-4, atol=1e-5)

@@ -73,6 +73,42 @@ struct Args {
   float dscale[6];         // 1/(1-rate) per block
 };
 
+// Ablation hooks for tools/probes/fused_ablation.hip (always 0 in the library build):
+//   1 = epilogue without bias/ReLU/BN/dropout math   2 = no epilogue LDS stores
+//   4 = K loop without B (LDS) reads                  8 = K loop without A (global) loads
+//  16 = no block-level barriers                      32 = multiply-free stand-in for the dropout hash
+//  (timing only; results are garbage for every nonzero value)
+#ifndef APNEAUQ_ABL
+#define APNEAUQ_ABL 0
+#endif
+#define APNEAUQ_SYNC() \
+  do {                 \
+    if constexpr (!(APNEAUQ_ABL & 16)) __syncthreads(); \
+  } while (0)
+
+// Weight-prefetch depth per block (steps in flight ahead of the MFMAs; see the K loop).  Measured
+// on MI355X (tools/probes/fused_ablation.hip, same box, 3 interleaved reps): depth 1 everywhere
+// 64.1-64.3 ms for MCD T=50 x 16384 windows; depths (1,2,2,3,3,3) 65.4-66.5 ms.  The weight
+// stream is bound by vector-memory issue (~2.6 MB of fragments per 2-sample tile), not latency.
+#ifndef APNEAUQ_PD0
+#define APNEAUQ_PD0 1
+#endif
+#ifndef APNEAUQ_PD1
+#define APNEAUQ_PD1 1
+#endif
+#ifndef APNEAUQ_PD2
+#define APNEAUQ_PD2 1
+#endif
+#ifndef APNEAUQ_PD3
+#define APNEAUQ_PD3 1
+#endif
+#ifndef APNEAUQ_PD4
+#define APNEAUQ_PD4 1
+#endif
+#ifndef APNEAUQ_PD5
+#define APNEAUQ_PD5 1
+#endif
+
 // One Conv1D(relu) -> BN -> Dropout block as an LDS-resident implicit GEMM.
 //   WM x WN waves tile (rows x output channels);  CT/RT = 16-wide tiles per wave.
 #ifndef APNEAUQ_BLOCK_INLINE
@@ -90,7 +126,7 @@ struct BlockCtx {
   int out_logits;
 };
 
-template <int LAYER, int WM, int WN, bool HEAD>
+template <int LAYER, int WM, int WN, int PD, bool HEAD, bool DROP>
 __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
   char* act = smem;
   const char* x0 = smem + kActBytes;
@@ -123,7 +159,10 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
 
   // B fragment (activations, LDS) of row tile r at k-step s
   auto load_b = [&](int s, int r) -> bf16x8 {
-    if constexpr (FIRST) {
+    if constexpr ((APNEAUQ_ABL & 4) != 0) {
+      const __bf16 v = (__bf16)(float)(lane + s + r);
+      return bf16x8{v, v, v, v, v, v, v, v};
+    } else if constexpr (FIRST) {
       // k = tap*4 + ci: 8 consecutive k = two consecutive rows x 4 channels (16 B, 8-B aligned)
       const char* base = x0 + (kHalo + row0 + r * 16 - PAD) * kX0RS + (32 * s + 8 * h) * 2;
       const bf16x4 lo = *reinterpret_cast<const bf16x4*>(base);
@@ -138,7 +177,14 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
   // A fragments (weights, global/L2) of k-step s
   auto load_a = [&](int s, bf16x8 (&a)[CT]) {
 #pragma unroll
-    for (int c = 0; c < CT; ++c) a[c] = wp[(s * NCT + c) * 64];
+    for (int c = 0; c < CT; ++c) {
+      if constexpr ((APNEAUQ_ABL & 8) != 0) {
+        const __bf16 v = (__bf16)(float)(lane + s + c);
+        a[c] = bf16x8{v, v, v, v, v, v, v, v};
+      } else {
+        a[c] = wp[(s * NCT + c) * 64];
+      }
+    }
   };
   auto step = [&](int s, const bf16x8 (&a)[CT]) {
 #pragma unroll
@@ -149,61 +195,90 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
     }
   };
 
-  // ---- K loop.  Weight fragments of step s+1 are in flight under step s's MFMAs.  Every load is
-  // unconditional (the prefetch index is clamped) so hipcc's vmcnt bookkeeping stays exact: with a
-  // conditional prefetch it must assume the short path and waits vmcnt(0) on the prefetch itself.
-  bf16x8 a0[CT], a1[CT];
-  load_a(0, a0);
+  // ---- K loop.  A ring of PD+1 weight-fragment stages: the fragments of step s+PD are in flight
+  // under step s's MFMAs.  Every load is unconditional (indices are clamped)
+  // so hipcc's vmcnt bookkeeping stays exact; sched_barrier keeps each prefetch ahead of the MFMAs.
+  constexpr int NS = PD + 1;
+  bf16x8 a[NS][CT];
+#pragma unroll
+  for (int j = 0; j < PD; ++j) load_a(j < NSTEP ? j : NSTEP - 1, a[j]);
+  constexpr int NFULL = NSTEP / NS * NS;
 #pragma unroll 1
-  for (int s = 0; s + 1 < NSTEP; s += 2) {
-    load_a(s + 1, a1);
-    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this step's MFMAs
-    step(s, a0);
-    load_a(s + 2 < NSTEP ? s + 2 : s + 1, a0);
-    __builtin_amdgcn_sched_barrier(0);
-    step(s + 1, a1);
+  for (int s0 = 0; s0 < NFULL; s0 += NS) {
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const int s = s0 + j;
+      load_a(s + PD < NSTEP ? s + PD : NSTEP - 1, a[(j + PD) % NS]);
+      __builtin_amdgcn_sched_barrier(0);
+      step(s, a[j]);
+    }
   }
-  if constexpr (NSTEP & 1) step(NSTEP - 1, a0);
+#pragma unroll
+  for (int j = 0; j < NSTEP - NFULL; ++j) step(NFULL + j, a[j]);
 
-  // ---- epilogue: bias + ReLU + BN(running) + dropout, then bf16 in place (or GAP head)
-  const unsigned thr = X.thr;
-  const float dsc = X.dsc;
+  // ---- epilogue: bias + ReLU + BN(running) + dropout, then bf16 in place (or GAP head).
+  // Dropout's 1/(1-rate) is folded into the BN affine once per column tile.  Rows t >= 60 of a
+  // slot are the next block's zero halo: they are simply never written (zeroed at kernel start).
+  // row0 = wm*RT*16 + m with RT*16 a multiple of 64, so t = (16r mod 64) + m is compile-time up to m.
   const gfloat* epi = reinterpret_cast<const gfloat*>(blob + eoff(LAYER));
+  const bool tail_lane = m >= kL - 48;  // lanes whose row in a 48..63 row tile is a halo row
 
-  if constexpr (!HEAD) __syncthreads();  // every wave has finished reading this block's input
+  if constexpr (!HEAD) APNEAUQ_SYNC();  // every wave has finished reading this block's input
 
   float gap = 0.f;  // HEAD: this lane's share of sum_t sum_co w[co] * y[t][co]
 #pragma unroll
   for (int c = 0; c < CT; ++c) {
     const int co0 = (wn * CT + c) * 16 + 4 * h;
     const f32x4 bias = *reinterpret_cast<const gf32x4*>(epi + co0);
-    const f32x4 sc = *reinterpret_cast<const gf32x4*>(epi + COUT + co0);
-    const f32x4 sh = *reinterpret_cast<const gf32x4*>(epi + 2 * COUT + co0);
+    f32x4 sc = *reinterpret_cast<const gf32x4*>(epi + COUT + co0);
+    f32x4 sh = *reinterpret_cast<const gf32x4*>(epi + 2 * COUT + co0);
+    if constexpr (DROP) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        sc[i] *= X.dsc;
+        sh[i] *= X.dsc;
+      }
+    }
     f32x4 dw;
     if constexpr (HEAD) dw = *reinterpret_cast<const gf32x4*>(reinterpret_cast<const gfloat*>(blob + kDenseOff) + co0);
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
       const int row = row0 + r * 16;
-      const int slot = row / kSR;
-      const int t = row - slot * kSR;
+      constexpr int kTail = 48;  // (16 r) mod 64 of the row tile that holds t = 48..63
+      const bool tail_tile = ((r * 16) % kSR) == kTail;
+      const int slot = (wm * RT * 16 + r * 16) / kSR;
+      const int t = (r * 16) % kSR + m;
       f32x4 v = acc[c][r];
+      if constexpr ((APNEAUQ_ABL & 1) == 0) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i] + bias[i], 0.f) * sc[i] + sh[i];
-      if (X.dropout) {
-        const unsigned k = slot ? X.skey1 : X.skey0;
-        const unsigned b01 = dropout_bits2(k, t, co0);
-        const unsigned b23 = dropout_bits2(k, t, co0 + 2);
-        v[0] = (b01 & 0xFFFFu) >= thr ? v[0] * dsc : 0.f;
-        v[1] = (b01 >> 16) >= thr ? v[1] * dsc : 0.f;
-        v[2] = (b23 & 0xFFFFu) >= thr ? v[2] * dsc : 0.f;
-        v[3] = (b23 >> 16) >= thr ? v[3] * dsc : 0.f;
+        for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i] + bias[i], 0.f) * sc[i] + sh[i];
+        if constexpr (DROP) {
+          const unsigned k = slot ? X.skey1 : X.skey0;
+#if (APNEAUQ_ABL & 32)
+          auto cheap = [](unsigned x) { x ^= x >> 13; x ^= x << 7; x ^= x >> 17; return x; };
+          const unsigned b01 = cheap(k ^ ((t << 9) | (co0 >> 1)));
+          const unsigned b23 = cheap(k ^ ((t << 9) | ((co0 + 2) >> 1)));
+#else
+          const unsigned b01 = dropout_bits2(k, t, co0);
+          const unsigned b23 = dropout_bits2(k, t, co0 + 2);
+#endif
+          v[0] = (b01 & 0xFFFFu) >= X.thr ? v[0] : 0.f;
+          v[1] = (b01 >> 16) >= X.thr ? v[1] : 0.f;
+          v[2] = (b23 & 0xFFFFu) >= X.thr ? v[2] : 0.f;
+          v[3] = (b23 >> 16) >= X.thr ? v[3] : 0.f;
+        }
       }
-      if (t >= kL) v = f32x4{0.f, 0.f, 0.f, 0.f};
       if constexpr (HEAD) {
-        gap += v[0] * dw[0] + v[1] * dw[1] + v[2] * dw[2] + v[3] * dw[3];
+        const float g = v[0] * dw[0] + v[1] * dw[1] + v[2] * dw[2] + v[3] * dw[3];
+        gap += (tail_tile && tail_lane) ? 0.f : g;
       } else {
         bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
-        *reinterpret_cast<bf16x4*>(act + (kHalo + row) * kRS + co0 * 2) = o;
+        bf16x4* dst = reinterpret_cast<bf16x4*>(act + (kHalo + row) * kRS + co0 * 2);
+        if constexpr ((APNEAUQ_ABL & 2) != 0) {
+          if (v[0] == 123.f) *dst = o;
+        } else if (!(tail_tile && tail_lane)) {
+          *dst = o;
+        }
       }
     }
   }
@@ -220,19 +295,23 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
       head[8 + sl] = X.out_logits ? logit : 1.0f / (1.0f + __expf(-logit));
     }
   } else {
-    __syncthreads();  // block output visible before the next block reads it
+    APNEAUQ_SYNC();  // block output visible before the next block reads it
   }
 }
 
+template <bool DROP>
 __global__ __launch_bounds__(kThreads, 2) void fused_forward_kernel(Args A) {
   char* act = smem;
   char* x0 = smem + kActBytes;
   float* head = reinterpret_cast<float*>(x0 + kX0Bytes);
 
-  // zero the halo rows once: leading / trailing rows of the activation and input buffers
+  // zero the halo rows once: leading / trailing rows of the activation and input buffers and the
+  // rows t = 60..63 of every slot (the epilogues never write them)
   for (int i = threadIdx.x; i < kHalo * kRS / 16; i += kThreads) {
     reinterpret_cast<f32x4*>(act)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    reinterpret_cast<f32x4*>(act + (kHalo + kR) * kRS)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int sl = 0; sl < kSlots; ++sl)
+      reinterpret_cast<f32x4*>(act + (kHalo + sl * kSR + kL) * kRS)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   if (threadIdx.x < kHalo * kX0RS / 16) {
     reinterpret_cast<f32x4*>(x0)[threadIdx.x] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -273,22 +352,21 @@ __global__ __launch_bounds__(kThreads, 2) void fused_forward_kernel(Args A) {
     __syncthreads();
     BlockCtx X;
     X.blob = blob;
-    X.dropout = A.dropout;
     X.out_logits = A.out_logits;
     X.skey0 = X.skey1 = 0u;
 #define APNEAUQ_CTX(L)                                                                                   \
   X.thr = A.thr[L];                                                                                      \
   X.dsc = A.dscale[L];                                                                                   \
-  if (A.dropout) {                                                                                       \
+  if (DROP) {                                                                                            \
     X.skey0 = sample_key(stream_key(A.seed, L, A.pass_offset + pass[0]), A.window_offset + win[0]);      \
     X.skey1 = sample_key(stream_key(A.seed, L, A.pass_offset + pass[1]), A.window_offset + win[1]);      \
   }
-    APNEAUQ_CTX(0) block<0, 1, 4, false>(X);
-    APNEAUQ_CTX(1) block<1, 1, 4, false>(X);
-    APNEAUQ_CTX(2) block<2, 2, 2, false>(X);
-    APNEAUQ_CTX(3) block<3, 2, 2, false>(X);
-    APNEAUQ_CTX(4) block<4, 1, 4, false>(X);
-    APNEAUQ_CTX(5) block<5, 2, 2, true>(X);
+    APNEAUQ_CTX(0) block<0, 1, 4, APNEAUQ_PD0, false, DROP>(X);
+    APNEAUQ_CTX(1) block<1, 1, 4, APNEAUQ_PD1, false, DROP>(X);
+    APNEAUQ_CTX(2) block<2, 2, 2, APNEAUQ_PD2, false, DROP>(X);
+    APNEAUQ_CTX(3) block<3, 2, 2, APNEAUQ_PD3, false, DROP>(X);
+    APNEAUQ_CTX(4) block<4, 1, 4, APNEAUQ_PD4, false, DROP>(X);
+    APNEAUQ_CTX(5) block<5, 2, 2, APNEAUQ_PD5, true, DROP>(X);
 #undef APNEAUQ_CTX
     if (threadIdx.x < kSlots && valid[threadIdx.x]) {
       const int sl = threadIdx.x;
@@ -337,7 +415,10 @@ hipError_t launch_fused_forward(const void* x, const uint8_t* blob, long long bl
     A.thr[l] = thr ? thr[l] : 0u;
     A.dscale[l] = dscale ? dscale[l] : 1.f;
   }
-  hipLaunchKernelGGL(fused::fused_forward_kernel, dim3(A.total_items), dim3(fused::kThreads), fused::kLdsBytes, stream, A);
+  if (dropout)
+    hipLaunchKernelGGL(fused::fused_forward_kernel<true>, dim3(A.total_items), dim3(fused::kThreads), fused::kLdsBytes, stream, A);
+  else
+    hipLaunchKernelGGL(fused::fused_forward_kernel<false>, dim3(A.total_items), dim3(fused::kThreads), fused::kLdsBytes, stream, A);
   return hipGetLastError();
 }
 

@@ -55,6 +55,19 @@ def init_params(spec: ModelSpec, seed: int = 2025) -> Params:
     return p
 
 
+def synthetic_params(spec: ModelSpec, seed: int = 2025) -> Params:
+    """Random-init weights with non-trivial BN statistics (benchmarks: nothing folds to identity)."""
+    p = init_params(spec, seed)
+    g = torch.Generator().manual_seed(int(seed) + 7919)
+    for i, b in enumerate(spec.blocks, start=1):
+        c = b.filters
+        p[f"batchnorm_{i}/moving_mean"] = torch.rand(c, generator=g) * 0.5
+        p[f"batchnorm_{i}/moving_variance"] = torch.rand(c, generator=g) + 0.5
+        p[f"batchnorm_{i}/gamma"] = torch.rand(c, generator=g) + 0.5
+        p[f"batchnorm_{i}/beta"] = torch.randn(c, generator=g) * 0.1
+    return p
+
+
 def params_to_list(spec: ModelSpec, p: Params) -> List[np.ndarray]:
     return [p[n].detach().cpu().numpy().astype(np.float32) for n in spec.weight_names()]
 
