@@ -78,3 +78,19 @@ def test_fused_multi_member():
     for m, p in enumerate(ps):
         ref = R.forward(S, p, x, dropout=False, bn_batch_stats=False).reshape(-1)
         assert torch.allclose(out[m], ref, atol=1e-2), (m, (out[m] - ref).abs().max())
+
+
+def test_fused_bitwise_deterministic_and_pass_offset():
+    """Same seed => bitwise-identical MC-Dropout outputs across runs; a pass-sharded run
+    (pass_offset) reproduces the corresponding rows of the full run (SURVEY §5 determinism)."""
+    _ext.require()
+    p = _params(6)
+    x = torch.randn(300, 60, 4, generator=torch.Generator().manual_seed(4)).to(torch.bfloat16).cuda()
+    blob = F.pack_blob(S, p).cuda()
+    a = F.fused_forward(x, blob, S, n_pass=8, dropout=True, seed=5)[0]
+    b = F.fused_forward(x, blob, S, n_pass=8, dropout=True, seed=5)[0]
+    assert torch.equal(a, b)
+    tail = F.fused_forward(x, blob, S, n_pass=3, dropout=True, seed=5, pass_offset=5)[0]
+    assert torch.equal(tail, a[5:])
+    c = F.fused_forward(x, blob, S, n_pass=8, dropout=True, seed=6)[0]
+    assert not torch.equal(a, c)

@@ -6,6 +6,17 @@ torch.library bindings (``bindings.cpp``) by the host C++ compiler; the result i
 JIT cache: the ``.so`` sits in the source tree so it travels with the repository snapshot.
 
 Usage: ``python -m uncertaintyquantification_sleepapnea_1dcnn_amd.csrc.build [--force] [-j N]``
+
+Debug variants (SURVEY §5 "Race detection / sanitizers"):
+
+* ``APNEAUQ_DEBUG=1``: kernels are built with ``-DAPNEAUQ_DEBUG`` — device ``assert``s on every
+  launch-geometry / index invariant the kernels rely on (grid vs. item count, member / window /
+  row bounds) — and the host side with ``-g -fno-omit-frame-pointer``.  Run with
+  ``AMD_SERIALIZE_KERNEL=3`` to attribute a failing assert to its launch.
+* ``APNEAUQ_HOST_SANITIZE=address,undefined``: ``-fsanitize=`` on the host objects only (GPU
+  sanitizers are unavailable on the pool); load with ``LD_PRELOAD=$(gcc -print-file-name=libasan.so)``.
+
+Both flags are part of the build stamp, so switching variants rebuilds.
 """
 from __future__ import annotations
 
@@ -25,6 +36,8 @@ SO_PATH = os.path.join(PKG, SO_NAME)
 BUILD_DIR = os.path.join(HERE, "build")
 ARCH = os.environ.get("APNEAUQ_OFFLOAD_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+DEBUG = os.environ.get("APNEAUQ_DEBUG", "0") not in ("", "0")
+HOST_SAN = os.environ.get("APNEAUQ_HOST_SANITIZE", "")
 
 
 def _torch_paths():
@@ -51,21 +64,25 @@ def commands():
     hip, cpp, _ = sources()
     common = [f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1", "-fPIC", "-O3",
               "-std=c++17", f"-I{HERE}", f"-I{ROCM}/include"]
+    if DEBUG:
+        common += ["-DAPNEAUQ_DEBUG=1", "-g", "-fno-omit-frame-pointer"]
+    host_san = [f"-fsanitize={HOST_SAN}"] if HOST_SAN else []
     cmds = []
     objs = []
     for src in hip:
         obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
+        san = (["-Xarch_host"] + host_san) if host_san else []
         cmds.append([_hipcc(), f"--offload-arch={ARCH}", "-c", src, "-o", obj, "-ffp-contract=fast",
-                     "-munsafe-fp-atomics"] + common)
+                     "-munsafe-fp-atomics"] + san + common)
         objs.append(obj)
     py_inc = sysconfig.get_paths()["include"]
     for src in cpp:
         obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
-        cmds.append(["g++", "-c", src, "-o", obj, f"-I{py_inc}"] + [f"-I{i}" for i in incs] + common)
+        cmds.append(["g++", "-c", src, "-o", obj, f"-I{py_inc}"] + [f"-I{i}" for i in incs] + host_san + common)
         objs.append(obj)
     link = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-o", SO_PATH + ".tmp"] + objs + [
         f"-L{libdir}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", f"-Wl,-rpath,{libdir}",
-        f"-L{ROCM}/lib", "-lamdhip64"]
+        f"-L{ROCM}/lib", "-lamdhip64"] + host_san
     return cmds, link
 
 
@@ -77,6 +94,7 @@ def _stamp():
         with open(f, "rb") as fh:
             h.update(fh.read())
     h.update(ARCH.encode())
+    h.update(f"debug={DEBUG};san={HOST_SAN}".encode())
     return h.hexdigest()
 
 

@@ -7,6 +7,15 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Bounds-checked debug builds (APNEAUQ_DEBUG=1, see build.py): device asserts on the launch
+// geometry and index invariants every kernel relies on.  Compiled out otherwise.
+#ifdef APNEAUQ_DEBUG
+#include <cassert>
+#define APNEAUQ_DASSERT(x) assert(x)
+#else
+#define APNEAUQ_DASSERT(x) ((void)0)
+#endif
+
 namespace apneauq {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));

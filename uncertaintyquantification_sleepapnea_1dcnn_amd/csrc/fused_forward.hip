@@ -318,6 +318,13 @@ __global__ __launch_bounds__(kThreads, 2) void fused_forward_kernel(Args A) {
     reinterpret_cast<f32x4*>(x0 + (kHalo + kR) * kX0RS)[threadIdx.x] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
+#ifdef APNEAUQ_STAGGER_US
+  // probe: delay the second co-resident workgroup of every CU by ~half a tile
+  if (blockIdx.x >= 256 && blockIdx.x < 512) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < 100ull * APNEAUQ_STAGGER_US) __builtin_amdgcn_s_sleep(8);
+  }
+#endif
   // XCD-aware item assignment (T1): blocks sharing an XCD get a contiguous item range, so a
   // Deep-Ensemble member's weights stay in one XCD's L2.  Bijective for any grid size.
   const int nwg = gridDim.x, bid = blockIdx.x;
@@ -328,7 +335,9 @@ __global__ __launch_bounds__(kThreads, 2) void fused_forward_kernel(Args A) {
   // out of the loop, which blows the 256-VGPR budget; one tile per launch slot keeps it at ~206.)
   {
     const int item = wg;
+    APNEAUQ_DASSERT(item < A.total_items && (int)gridDim.x == A.total_items && blockDim.x == kThreads);
     const int member = item / A.tiles_per_member;
+    APNEAUQ_DASSERT(member < A.n_member);
     const int tile = item - member * A.tiles_per_member;
     const guint8* blob = (const guint8*)(A.blob) + (long long)member * A.blob_stride;
     unsigned pass[kSlots], win[kSlots];
@@ -340,6 +349,7 @@ __global__ __launch_bounds__(kThreads, 2) void fused_forward_kernel(Args A) {
       const int gg = valid[sl] ? g : 0;
       pass[sl] = gg / A.n_win;
       win[sl] = gg - pass[sl] * A.n_win;
+      APNEAUQ_DASSERT((int)pass[sl] < A.n_pass && (int)win[sl] < A.n_win);
     }
     // stage the two input windows (480 B each) + 4 zero rows per slot into x0
     if (threadIdx.x < kSlots * 32) {

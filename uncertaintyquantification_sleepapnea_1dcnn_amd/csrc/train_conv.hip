@@ -298,6 +298,7 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
   char* act = smem;                                  // staged input, then staged output
   float* prm = reinterpret_cast<float*>(smem + kRows * kRS);  // [s 512 | t 512]
   const int tile = blockIdx.x;
+  APNEAUQ_DASSERT(2 * tile < A.B + 1 && blockDim.x == kThreads);
   const int row0 = kR * tile;                        // first staged row (global PL index)
   const int smp0 = 2 * tile;
   const int g0 = min(smp0, A.B - 1) / A.n_win, g1 = min(smp0 + 1, A.B - 1) / A.n_win;
@@ -482,6 +483,7 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
   float* mean_prev = prm + 1792;
   float* rstd_prev = prm + 2048;
   const int tile = blockIdx.x;
+  APNEAUQ_DASSERT(2 * tile < A.B + 1 && blockDim.x == kThreads);
   const int row0 = kR * tile;
   const int smp0 = 2 * tile;
   {

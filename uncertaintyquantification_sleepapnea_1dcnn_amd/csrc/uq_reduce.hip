@@ -65,6 +65,7 @@ __global__ __launch_bounds__(kBootThreads) void bootstrap_kernel(const float* __
                                                                  const int* __restrict__ idx, unsigned seed, int n,
                                                                  double* __restrict__ out) {
   const int b = blockIdx.x;
+  APNEAUQ_DASSERT(blockDim.x == kBootThreads && n > 0);
   const float* var = metrics + kVar * (long long)n;
   const float* ent = metrics + kEntNats * (long long)n;
   const float* eent = metrics + kExpEnt * (long long)n;

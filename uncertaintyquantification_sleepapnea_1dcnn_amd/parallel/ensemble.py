@@ -8,7 +8,10 @@ Training replaces the reference's sequential member loop (``train_deep_ensemble_
   ``world/M`` ranks of its group (``parallel/data_parallel.py``: SyncBN + one gradient bucket);
 * **resume** at member granularity: a member whose checkpoint exists is skipped (the reference's
   skip-if-exists, ``:130-132``) — a killed job rerun retrains only the missing members; checkpoints
-  are written atomically (tmp + rename) so a crash never leaves a half-written member.
+  are written atomically (tmp + rename) so a crash never leaves a half-written member;
+* **resume** at epoch granularity inside a member (``epoch_backup``): a per-member
+  ``BackupAndRestore`` file holds weights + Adam state + epoch, so a member killed mid-training
+  continues from its last finished epoch (fault sites for tests: ``utils/faults.py``).
 
 Checkpoint names keep the reference's scheme ``{prefix}{name_offset + i}.keras``
 (``AlCNN_smote_seed{21+i}``); :func:`load_ensemble` takes the loaders' offsets (``i+5`` in
@@ -23,8 +26,9 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from ..utils.faults import maybe_fail
 from ..models.cnn import AlarconCNN1D, load_model
-from ..training.callbacks import EarlyStopping
+from ..training.callbacks import BackupAndRestore, EarlyStopping
 from . import dist as pdist
 from .data_parallel import DPContext
 
@@ -46,7 +50,8 @@ def plan(num_models: int, world: int) -> List[List[int]]:
 def train_ensemble(x_train, y_train, num_models: int = 5, seed_base: int = 2025, save_dir: str = "./models/ensemble_cnn_no_pool",
                    prefix: str = MODEL_PREFIX, name_offset: int = 21, epochs: int = 50, batch_size: int = 1024,
                    patience: int = 5, validation_split: float = 0.1, verbose: int = 2, resume: bool = True,
-                   device=None, input_shape: Optional[Sequence[int]] = None) -> List[str]:
+                   device=None, input_shape: Optional[Sequence[int]] = None, epoch_backup: bool = True,
+                   extra_callbacks: Optional[Sequence] = None) -> List[str]:
     info = pdist.init()
     world, rank = info.world, info.rank
     groups = plan(num_models, world)
@@ -75,8 +80,12 @@ def train_ensemble(x_train, y_train, num_models: int = 5, seed_base: int = 2025,
         if len(ranks) > 1:
             model.dp = DPContext(pgroups[m], len(ranks), ranks.index(rank))
         es = EarlyStopping(monitor="val_loss", patience=patience, restore_best_weights=True)
+        cbs = [es] + list(extra_callbacks or [])
+        if epoch_backup:  # a member killed mid-training resumes at its last finished epoch
+            cbs.append(BackupAndRestore(os.path.join(save_dir, ".backup_" + os.path.splitext(os.path.basename(path))[0])))
         hist = model.fit(x_train, y_train, epochs=epochs, batch_size=batch_size, validation_split=validation_split,
-                         callbacks=[es], verbose=verbose if ranks.index(rank) == 0 else 0)
+                         callbacks=cbs, verbose=verbose if ranks.index(rank) == 0 else 0)
+        maybe_fail("ensemble.before_save", member=m)
         if ranks.index(rank) == 0:
             model.save(path)
             if verbose:

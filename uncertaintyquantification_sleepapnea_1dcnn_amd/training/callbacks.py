@@ -100,3 +100,108 @@ class EarlyStopping(Callback):
     def on_train_end(self, logs=None):
         if self.stopped_epoch > 0 and self.verbose > 0:
             print(f"Epoch {self.stopped_epoch + 1}: early stopping")
+
+
+class JsonlLogger(Callback):
+    """Stream per-epoch logs (loss, accuracy, auc, val_*) as JSON lines (SURVEY §5 observability).
+
+    The reference persists nothing of its ``History`` (``train_deep_ensemble_cnns.py:171``)."""
+
+    def __init__(self, path: str, run: Optional[str] = None, all_ranks: bool = False):
+        from ..utils.logging import JsonlWriter
+
+        self.writer = JsonlWriter(path, all_ranks=all_ranks)
+        self.run = run
+        self._t0 = None
+
+    def on_train_begin(self, logs=None):
+        import time
+
+        self._t0 = time.time()
+        self.writer.write({"event": "train_begin", "run": self.run, "model": getattr(self.model, "name", None)})
+
+    def on_epoch_end(self, epoch, logs=None):
+        import time
+
+        self.writer.write({"event": "epoch", "run": self.run, "epoch": epoch, "elapsed_s": time.time() - self._t0, **(logs or {})})
+
+    def on_train_end(self, logs=None):
+        self.writer.write({"event": "train_end", "run": self.run})
+
+
+class BackupAndRestore(Callback):
+    """Epoch-granularity fault tolerance (Keras ``callbacks.BackupAndRestore`` semantics).
+
+    After every epoch the weights, the Adam state (m, v, iterations), the dropout step counter and
+    the epoch index are written atomically to ``backup_dir``.  When a training run starts and a
+    backup exists, it is restored and ``fit`` resumes at the next epoch (its shuffling generator is
+    fast-forwarded, so the resumed run sees the same batches as an uninterrupted one).  The backup
+    is deleted when training ends normally.  As in Keras, other callbacks' state (e.g.
+    EarlyStopping's patience counter) is not part of the backup.
+    """
+
+    FILE = "backup.npz"
+
+    def __init__(self, backup_dir: str, delete_checkpoint: bool = True):
+        self.backup_dir = backup_dir
+        self.delete_checkpoint = delete_checkpoint
+
+    @property
+    def path(self) -> str:
+        import os
+
+        return os.path.join(self.backup_dir, self.FILE)
+
+    def on_train_begin(self, logs=None):
+        import os
+
+        import numpy as np
+        import torch
+
+        from ..utils.checkpoint import load_weights
+
+        if not os.path.exists(self.path):
+            return
+        spec, arrays, cfg, opt = load_weights(self.path)
+        m = self.model
+        m.set_weights(arrays)
+        if opt:
+            m.optimizer.iterations = int(opt["iterations"])
+            m.optimizer.m = torch.from_numpy(np.array(opt["m"])).to(m.device)
+            m.optimizer.v = torch.from_numpy(np.array(opt["v"])).to(m.device)
+        extra = cfg.get("extra", {})
+        m._train_step_counter = int(extra.get("train_step_counter", 0))
+        m._resume_epoch = int(extra["epoch"]) + 1
+
+    def on_epoch_end(self, epoch, logs=None):
+        import os
+
+        import numpy as np
+
+        from ..utils.checkpoint import save_weights
+
+        m = self.model
+        dp = getattr(m, "dp", None)
+        if dp is not None and dp.rank != 0:
+            return  # one writer per data-parallel group; every rank restores from it
+        os.makedirs(self.backup_dir, exist_ok=True)
+        opt = None
+        if m.optimizer.m is not None:
+            opt = {"m": m.optimizer.m.cpu().numpy(), "v": m.optimizer.v.cpu().numpy(),
+                   "iterations": np.array(m.optimizer.iterations)}
+        save_weights(self.path, m.spec, m.get_weights(), m.name,
+                     extra={"seed": m.seed, "epoch": int(epoch), "train_step_counter": int(m._train_step_counter)},
+                     opt_state=opt)
+
+    def on_train_end(self, logs=None):
+        import os
+
+        dp = getattr(self.model, "dp", None)
+        if dp is not None and dp.rank != 0:
+            return
+        if self.delete_checkpoint and os.path.exists(self.path):
+            os.remove(self.path)
+            try:
+                os.rmdir(self.backup_dir)  # only if empty
+            except OSError:
+                pass

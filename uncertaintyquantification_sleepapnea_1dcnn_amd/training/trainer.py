@@ -22,6 +22,7 @@ from typing import List, Optional
 import numpy as np
 import torch
 
+from ..utils.faults import maybe_fail
 from .callbacks import Callback, History
 from ..parallel.data_parallel import split_batch
 from .metrics import AUC, BinaryAccuracy, MeanMetric
@@ -86,8 +87,14 @@ def fit(model, x, y, batch_size: int = 32, epochs: int = 1, verbose: int = 1, ca
     gen = torch.Generator(device="cpu")
     gen.manual_seed(int(model.seed if seed is None else seed))
     steps = (n + batch_size - 1) // batch_size
+    model._resume_epoch = 0
     for cb in cbs:
         cb.on_train_begin()
+    if model._resume_epoch > initial_epoch:  # BackupAndRestore found a backup
+        for _ in range(initial_epoch, model._resume_epoch):
+            if shuffle:
+                torch.randperm(n, generator=gen)  # keep the batch order of an uninterrupted run
+        initial_epoch = model._resume_epoch
     if verbose:
         print(f"Train on {n} samples" + (f", validate on {Xv.shape[0]} samples" if Xv is not None else ""))
     for epoch in range(initial_epoch, epochs):
@@ -124,6 +131,7 @@ def fit(model, x, y, batch_size: int = 32, epochs: int = 1, verbose: int = 1, ca
             print(f"Epoch {epoch + 1}/{epochs}\n{steps}/{steps} - {dt:.0f}s - {line}", flush=True)
         for cb in cbs:
             cb.on_epoch_end(epoch, logs)
+        maybe_fail("fit.epoch_end", epoch=epoch)
         if model.stop_training:
             break
     for cb in cbs:
