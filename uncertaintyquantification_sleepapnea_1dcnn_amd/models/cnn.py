@@ -121,7 +121,12 @@ class AlarconCNN1D:
         return t
 
     def uses_fused(self) -> bool:
-        return self.device.type == "cuda" and fused.supports(self.spec)
+        if self.device.type != "cuda":
+            return False
+        if not fused.supports(self.spec):
+            fused.warn_unsupported(self.spec, "inference")
+            return False
+        return True
 
     def fused_blob(self) -> torch.Tensor:
         """Packed parameters for the fused HIP kernel (cached per weight version)."""

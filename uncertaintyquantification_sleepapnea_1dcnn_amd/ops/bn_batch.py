@@ -41,10 +41,34 @@ def _moments_hook(group=None):
 
 @torch.no_grad()
 def mc_dropout_batch_bn(model, x, n_pred: int, seed: Optional[int] = None, window_offset: int = 0,
-                        distributed: bool = False, update_moving: bool = True) -> torch.Tensor:
-    """(T, N, 1) probabilities; each pass = Keras ``model(x, training=True)`` on the full set."""
+                        distributed: bool = False, update_moving: bool = True, global_n: Optional[int] = None,
+                        chunk_rows: Optional[int] = None) -> torch.Tensor:
+    """(T, N, 1) probabilities; each pass = Keras ``model(x, training=True)`` on the full set.
+
+    On a GPU with the HIP extension the passes run on the layer-wise training kernels
+    (``train_ops.forward_batch_stats``: BN moments accumulated in the conv epilogue, SyncBN by one
+    all-reduce of the per-layer (sum, sum of squares) buffer when ``distributed``); otherwise the
+    fp32 PyTorch reference path.  ``global_n`` = windows over all ranks; ``chunk_rows`` (ranks must
+    agree on it) bounds the windows x passes processed per launch.
+    """
     xt = model._as_input(x)
     n = xt.shape[0]
+    if xt.is_cuda:
+        from . import train_ops
+
+        if train_ops.supports(model.spec):
+            sync = None
+            if distributed:
+                import torch.distributed as dist
+
+                if dist.is_available() and dist.is_initialized():
+                    sync = dist.all_reduce
+            base = model._call_counter
+            out = train_ops.forward_batch_stats(model, xt, n_pred, pass_base=base, seed=model.seed if seed is None else seed,
+                                                update_moving=update_moving, sync=sync, window_offset=window_offset,
+                                                global_n=global_n, max_samples=chunk_rows or (1 << 20))
+            model._call_counter = base + n_pred
+            return out.unsqueeze(-1)
     sample_ids = torch.arange(window_offset, window_offset + n, device=xt.device)
     hook = _moments_hook() if distributed else None
     outs = []

@@ -29,6 +29,20 @@ def supports(spec: ModelSpec) -> bool:
             and tuple(b.kernel_size for b in spec.blocks) == FUSED_KSIZES and not spec.has_pool)
 
 
+_WARNED = set()
+
+
+def warn_unsupported(spec: ModelSpec, what: str) -> None:
+    """One warning per (architecture, path) that runs on the fp32 PyTorch path instead of HIP."""
+    key = (repr(spec), what)
+    if key not in _WARNED and torch.cuda.is_available():
+        _WARNED.add(key)
+        import warnings
+
+        warnings.warn(f"apneauq: no HIP {what} kernel for this architecture (input {spec.input_length}x"
+                      f"{spec.input_channels}, pool={spec.has_pool}); using the fp32 PyTorch path", stacklevel=3)
+
+
 def _ceil(a: int, b: int) -> int:
     return (a + b - 1) // b * b
 

@@ -33,7 +33,16 @@ TRAIN_PASS_BASE = 1 << 30
 
 
 def supports(spec: ModelSpec) -> bool:
-    return fused.supports(spec) and _ext.available()
+    """True if the HIP training kernels implement ``spec``.  On a GPU machine a missing extension
+    raises (no silent eager fallback) unless ``APNEAUQ_ALLOW_FALLBACK=1``."""
+    if not fused.supports(spec):
+        fused.warn_unsupported(spec, "training")
+        return False
+    if _ext.available():
+        return True
+    if not _ext.fallback_allowed():
+        _ext.require()
+    return False
 
 
 def _fbits(x: float) -> int:
@@ -202,7 +211,15 @@ def forward_batch_stats(model, x: torch.Tensor, n_pass: int, pass_base: int, see
     """
     n = x.shape[0]
     gn = global_n or n
-    chunk = max(1, min(n_pass, max_samples // max(n, 1)))
+    # the chunking must be identical on every rank when ``sync`` all-reduces per chunk: derive it
+    # from the largest shard (ceil(global_n / world)) rather than from this rank's n
+    ref_n = n
+    if sync is not None and global_n:
+        import torch.distributed as dist
+
+        w = dist.get_world_size() if dist.is_initialized() else 1
+        ref_n = -(-global_n // w)
+    chunk = max(1, min(n_pass, max_samples // max(ref_n, 1)))
     outs = []
     dev = x.device.index or 0
     ws = getattr(model, "_mcd_ws", None)

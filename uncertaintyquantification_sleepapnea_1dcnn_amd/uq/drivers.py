@@ -55,8 +55,20 @@ def per_window_table(probs, y, patient_ids=None) -> pd.DataFrame:
     })
 
 
+def _main_rank() -> bool:
+    from . import distributed as D
+
+    if not D.active():
+        return True
+    import torch.distributed as dist
+
+    return dist.get_rank() == 0
+
+
 def _finish(probs_np, y, patient_ids, label, save_detailed_csv, output_csv_dir, output_plot_dir, n_bootstrap, seed,
             raw_pred_path, make_plots) -> Optional[Dict]:
+    if not _main_rank():
+        return None  # under torchrun every rank holds the gathered samples; rank 0 writes the outputs
     if raw_pred_path:
         d = os.path.dirname(raw_pred_path)
         if d:

@@ -53,18 +53,23 @@ def _gpu_ok() -> bool:
 
 # ===================== Core Prediction Functions =====================
 def mc_dropout_predict(model, x_test_data, n_pred: int = 50, bn_mode: str = "batch", seed: Optional[int] = None,
-                       as_numpy: bool = True):
+                       as_numpy: bool = True, distributed: Optional[bool] = None):
     """MC Dropout predictions (n_pred, samples, 1) float32.
 
     ``bn_mode="batch"`` (default, reference parity): each pass is ``model(x, training=True)``.
     ``bn_mode="running"``: dropout on, BatchNorm on running statistics — all passes in one fused
-    kernel launch on the GPU.
+    kernel launch on the GPU.  Under ``torchrun`` (``distributed=None`` = auto) the windows are
+    sharded over the ranks and the result is all-gathered (``uq/distributed.py``).
     """
     torch = _torch()
     start_time = time.time()
     if bn_mode not in ("batch", "running"):
         raise ValueError("bn_mode must be 'batch' or 'running'")
-    if bn_mode == "running" and getattr(model, "uses_fused", lambda: False)():
+    from . import distributed as D
+
+    if (D.active() if distributed is None else distributed):
+        out = D.mc_dropout_predict_sharded(model, x_test_data, n_pred, bn_mode, seed)
+    elif bn_mode == "running" and getattr(model, "uses_fused", lambda: False)():
         from ..ops import fused
 
         x = model._as_input(x_test_data).to(torch.bfloat16).contiguous()
@@ -84,11 +89,18 @@ def mc_dropout_predict(model, x_test_data, n_pred: int = 50, bn_mode: str = "bat
     return out
 
 
-def deep_ensembles_predict(ensemble_models: List, x_test_data, as_numpy: bool = True):
-    """Deep-ensemble predictions (n_models, samples, 1) float32 (inference mode)."""
+def deep_ensembles_predict(ensemble_models: List, x_test_data, as_numpy: bool = True,
+                           distributed: Optional[bool] = None):
+    """Deep-ensemble predictions (n_models, samples, 1) float32 (inference mode); member-parallel
+    over the ranks under ``torchrun`` (``distributed=None`` = auto)."""
     torch = _torch()
     start_time = time.time()
-    if ensemble_models and all(getattr(m, "uses_fused", lambda: False)() for m in ensemble_models):
+    from . import distributed as D
+
+    if ensemble_models and (D.active() if distributed is None else distributed):
+        out = D.deep_ensembles_predict_sharded(ensemble_models, x_test_data)
+        out = out.cpu().numpy() if as_numpy else out
+    elif ensemble_models and all(getattr(m, "uses_fused", lambda: False)() for m in ensemble_models):
         from ..ops import fused
 
         m0 = ensemble_models[0]
