@@ -99,3 +99,20 @@ def test_cohort_descriptives(tmp_path):
     assert [r["ahi_categories"]["counts"][k] for k in cohort.AHI_CATEGORIES] == [1, 1, 1, 1]
     q = cohort.analyze_signal_quality(str(p), verbose=False)
     assert q["quoxim"]["counts"] == {3: 1, 4: 1, 5: 2}
+
+
+def test_pr_fallback_gates_resample_reshape(tmp_path):
+    rs = np.random.RandomState(3)
+    sig = {"SaO2": 90 + rs.rand(300) * 5, "H.R.": 60 + rs.rand(300) * 20, "THOR RES": rs.randn(3000)}
+    p = edf.write_edf(str(tmp_path / "b.edf"), sig, {"SaO2": 1.0, "H.R.": 1.0, "THOR RES": 10.0},
+                      phys_ranges={"SaO2": (0, 100), "H.R.": (0, 250), "THOR RES": (-5, 5)})
+    s, r = preprocess.get_edf_channels(p, ["SaO2", "PR", "THOR RES"])
+    assert set(s) == {"SaO2", "PR", "THOR RES"} and r["PR"] == 1.0  # PR read from H.R.
+    np.testing.assert_allclose(s["PR"], sig["H.R."], atol=250 / 65535)
+    assert preprocess.check_artifacts_and_missing_values({"a": np.r_[np.ones(95), np.full(5, np.nan)]})
+    assert not preprocess.check_artifacts_and_missing_values({"a": np.r_[np.ones(85), np.full(15, np.nan)]})
+    out = preprocess.resample_signals({"THOR RES": s["THOR RES"]}, {"THOR RES": 10.0}, 1)
+    assert out["THOR RES"].shape == (300,)
+    flat = np.arange(2 * 240, dtype=np.float64).reshape(2, 240)  # t-major: SaO2_t0, PR_t0, THOR_t0, ABDO_t0, ...
+    x3 = prepare.reshape_flat_to_3d(flat, 60, 4)
+    assert x3.shape == (2, 60, 4) and x3[0, 1, 0] == 4 and x3[1, 0, 3] == 243

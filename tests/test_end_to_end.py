@@ -49,6 +49,13 @@ def test_pipeline(tmp_path, monkeypatch):
                                              "--mcd_summary", "pm/patient_summary_metrics_MCD.csv",
                                              "--de_summary", "pd/patient_summary_metrics_DE.csv", "--output_dir", "figs"])
     assert len(figs) == 4 and all(os.path.exists(f) for f in figs)
+    import shutil
+
+    for i, src in enumerate(["ens/AlCNN_smote_seed5.keras", "ens/AlCNN_smote_seed6.keras"]):
+        shutil.copy(src, f"ens/glob{i}.keras")  # evaluate_de_global.py naming: {prefix}{i}.keras
+    g = C.evaluate_de_global(["--data_dir", "proc", "--model_prefix", "ens/glob", "--num_models", "2", "--n_bootstrap", "3",
+                              "--no_plots"])
+    assert len(g["unbalanced"]) == 25 and len(g["balanced"]) == 25
     C.convergence_sweep(["--method", "de", "--data_dir", "proc", "--model_dir", "ens", "--counts", "1,2",
                          "--output_csv", "conv.csv"])
     assert C.hyperparameter_plot_mcd_or_de_pass_convergence(["--input_csv", "conv.csv", "--method", "de",

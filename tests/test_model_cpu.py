@@ -99,3 +99,14 @@ def test_eager_comparator_matches_reference_forward():
                 mod.p = 0.0
         ref = R.forward(DEFAULT_SPEC, p, x, training=True, dropout=False)
         np.testing.assert_allclose(m(x).numpy(), ref.numpy(), rtol=1e-4, atol=1e-5)
+
+
+def test_evaluate_classification_model_keys():
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.evaluation.evaluate_classification import (
+        evaluate_classification_model)
+
+    m = AlarconCNN1D(seed=1, device="cpu")
+    x = torch.randn(64, 60, 4).numpy()
+    y = (np.arange(64) % 3 == 0).astype(int)
+    r = evaluate_classification_model(m, x, y, "t")
+    assert len(r) == 14 and {"roc_auc", "auc_pr", "overall_sensitivity", "overall_specificity", "cohen_kappa", "mcc"} <= set(r)

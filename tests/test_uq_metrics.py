@@ -1,6 +1,8 @@
 """UQ metric parity: framework API vs an independent re-statement of the reference algorithm
 (uq_techniques.py:40-206: full metric recomputation on every bootstrap resample, global-seeded
 legacy RNG).  Also covers the bootstrap gather reformulation and the CI keys."""
+import os
+
 import numpy as np
 import pytest
 from scipy.stats import entropy
@@ -107,3 +109,15 @@ def test_eager_device_formulas_match_numpy(data):
     ref = M.bootstrap_from_windows(w, y, idx)
     for i in range(5):
         np.testing.assert_allclose(b[i], [ref[i][k] for k in M.AGG_KEYS], rtol=1e-4, atol=1e-7)
+
+
+def test_plots_and_demo(tmp_path, data):
+    p, y = data
+    out = tmp_path / "plots"
+    U.evaluate_uq_methods(p[:, :, None], y, "lbl", n_bootstrap=4, random_state=0, output_plot_dir=str(out))
+    names = sorted(os.listdir(out))
+    assert any(n.startswith("hist_") for n in names) and any(n.startswith("bar_class_variance") for n in names)
+    U.plot_uncertainty_metric(p.var(0), "lbl", "variance", output_dir=str(out))
+    assert any(n.startswith("line_") for n in os.listdir(out))
+    res = U.demo(output_plot_dir=str(tmp_path / "demo"), n_samples=200)
+    assert res is not None and len(res) == 24
