@@ -35,7 +35,7 @@ int main(int argc, char** argv) {
   srand(7);
   for (int m = 0; m < n_member; ++m) {
     uint8_t* b = blob.data() + (size_t)m * blob_bytes;
-    // weights: small bf16; epilogue/dense: sane fp32 (bias 0, scale 1, shift 0)
+    // weights: small bf16; epilogue/dense: sane fp32 (bias 0.01, scale 1, shift 0)
     const int wend = apneauq::fused::woff(6);
     for (int i = 0; i < wend / 2; ++i) {
       const uint16_t v = to_bf16(((rand() & 1023) - 512) / 8192.f);
@@ -45,9 +45,11 @@ int main(int argc, char** argv) {
       float* e = reinterpret_cast<float*>(b + apneauq::fused::eoff(l));
       const int co = apneauq::fused::C[l + 1];
       for (int c = 0; c < co; ++c) {
-        e[c] = 0.01f;
-        e[co + c] = 1.f;
-        e[2 * co + c] = 0.f;
+        e[c] = 1.f;                  // s
+        e[co + c] = 0.01f;           // t' = b*s + t
+        e[2 * co + c] = 0.f;         // lo (s >= 0: t)
+        e[3 * co + c] = 1e30f;       // hi (+inf)
+        for (int q = 0; q < 4; ++q) e[(4 + q) * co + c] = e[q * co + c] * 1.25f;  // MC-Dropout rows
       }
     }
     float* d = reinterpret_cast<float*>(b + apneauq::fused::kDenseOff);
@@ -83,6 +85,25 @@ int main(int argc, char** argv) {
   CK(hipEventElapsedTime(&ms, e0, e1));
   ms /= iters;
   const double samples = (double)n_win * n_pass * n_member;
+#ifdef APNEAUQ_STAMPS
+  {
+    run();
+    CK(hipDeviceSynchronize());
+    using namespace apneauq::fused;
+    std::vector<unsigned long long> st((size_t)kStampWG * 4 * kStampN);
+    std::vector<unsigned> cu(kStampWG);
+    CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_stamps), st.size() * 8));
+    CK(hipMemcpyFromSymbol(cu.data(), HIP_SYMBOL(g_stamp_cu), cu.size() * 4));
+    char fn[256];
+    std::snprintf(fn, sizeof fn, "gpurun_out/stamps_%s.bin", mcd ? "mcd" : "de");
+    FILE* f = std::fopen(fn, "wb");
+    if (f) {
+      std::fwrite(cu.data(), 4, cu.size(), f);
+      std::fwrite(st.data(), 8, st.size(), f);
+      std::fclose(f);
+    }
+  }
+#endif
   std::printf("{\"abl\": %d, \"mode\": \"%s\", \"ms\": %.3f, \"samples_per_s\": %.0f}\n", APNEAUQ_ABL, mcd ? "mcd" : "de", ms,
               samples / (ms * 1e-3));
   return 0;

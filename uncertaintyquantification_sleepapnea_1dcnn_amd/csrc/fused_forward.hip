@@ -47,7 +47,8 @@ constexpr int KS[6] = {7, 5, 3, 7, 9, 9};
 
 __host__ __device__ constexpr int ksteps(int l) { return (C[l] * KS[l] + 31) / 32; }
 __host__ __device__ constexpr int wbytes(int l) { return ksteps(l) * (C[l + 1] / 16) * 1024; }
-__host__ __device__ constexpr int ebytes(int l) { return ((3 * C[l + 1] * 4) + 15) / 16 * 16; }
+constexpr int kEpiRows = 8;  // per-channel [s, t' = b*s + t, lo, hi], then the same x 1/(1-rate) (ops/fused.py)
+__host__ __device__ constexpr int ebytes(int l) { return ((kEpiRows * C[l + 1] * 4) + 15) / 16 * 16; }
 __host__ __device__ constexpr int woff(int l) { return l == 0 ? 0 : woff(l - 1) + wbytes(l - 1); }
 __host__ __device__ constexpr int eoff(int l) { return l == 0 ? woff(6) : eoff(l - 1) + ebytes(l - 1); }
 constexpr int kDenseOff = eoff(6);
@@ -85,6 +86,21 @@ struct Args {
   do {                 \
     if constexpr (!(APNEAUQ_ABL & 16)) __syncthreads(); \
   } while (0)
+
+// In-kernel phase stamps for tools/probes (never enabled in the library build): s_memtime at
+// every phase boundary of the first kStampWG workgroups, lane 0 of each wave.
+#ifdef APNEAUQ_STAMPS
+constexpr int kStampWG = 2048, kStampN = 32;
+__device__ unsigned long long g_stamps[kStampWG][4][kStampN];
+__device__ unsigned g_stamp_cu[kStampWG];
+#define APNEAUQ_STAMP(i)                                                              \
+  do {                                                                                \
+    if (blockIdx.x < kStampWG && (threadIdx.x & 63) == 0)                             \
+      g_stamps[blockIdx.x][threadIdx.x >> 6][(i)] = __builtin_amdgcn_s_memtime();     \
+  } while (0)
+#else
+#define APNEAUQ_STAMP(i) ((void)0)
+#endif
 
 // Weight-prefetch depth per block (steps in flight ahead of the MFMAs; see the K loop).  Measured
 // on MI355X (tools/probes/fused_ablation.hip, same box, 3 interleaved reps): depth 1 everywhere
@@ -157,6 +173,7 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
 #pragma unroll
     for (int r = 0; r < RT; ++r) acc[c][r] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  const char* bbase = act + (kHalo + row0 - PAD) * kRS + 16 * h;
   // B fragment (activations, LDS) of row tile r at k-step s
   auto load_b = [&](int s, int r) -> bf16x8 {
     if constexpr ((APNEAUQ_ABL & 4) != 0) {
@@ -169,9 +186,11 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
       const bf16x4 hi = *reinterpret_cast<const bf16x4*>(base + 8);
       return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     } else {
+      // lane base + uniform step offset + compile-time row-tile offset (a ds_read immediate)
       constexpr int CB = CIN / 32;
       const int tap = s / CB, cb = s - tap * CB;
-      return *reinterpret_cast<const bf16x8*>(act + (kHalo + row0 + r * 16 + tap - PAD) * kRS + (cb * 32 + 8 * h) * 2);
+      const int soff = __builtin_amdgcn_readfirstlane(tap * kRS + cb * 64);
+      return *reinterpret_cast<const bf16x8*>(bbase + soff + r * 16 * kRS);
     }
   };
   // A fragments (weights, global/L2) of k-step s
@@ -186,6 +205,8 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
       }
     }
   };
+  // (B fragments are read just in time: a DB-deep register ring over the (k-step, row-tile)
+  // sequence measured 0.5-1 % slower on MI355X — the co-resident wave already hides LDS latency.)
   auto step = [&](int s, const bf16x8 (&a)[CT]) {
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
@@ -198,10 +219,15 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
   // ---- K loop.  A ring of PD+1 weight-fragment stages: the fragments of step s+PD are in flight
   // under step s's MFMAs.  Every load is unconditional (indices are clamped)
   // so hipcc's vmcnt bookkeeping stays exact; sched_barrier keeps each prefetch ahead of the MFMAs.
+  APNEAUQ_STAMP(2 + 4 * LAYER);  // K loop start
+#ifdef APNEAUQ_PRIO_K
+  __builtin_amdgcn_s_setprio(APNEAUQ_PRIO_K);  // probe: wave priority during the MFMA phase
+#endif
   constexpr int NS = PD + 1;
   bf16x8 a[NS][CT];
 #pragma unroll
   for (int j = 0; j < PD; ++j) load_a(j < NSTEP ? j : NSTEP - 1, a[j]);
+
   constexpr int NFULL = NSTEP / NS * NS;
 #pragma unroll 1
   for (int s0 = 0; s0 < NFULL; s0 += NS) {
@@ -215,30 +241,30 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
   }
 #pragma unroll
   for (int j = 0; j < NSTEP - NFULL; ++j) step(NFULL + j, a[j]);
+  APNEAUQ_STAMP(3 + 4 * LAYER);  // K loop issued (MFMAs may still drain)
 
   // ---- epilogue: bias + ReLU + BN(running) + dropout, then bf16 in place (or GAP head).
-  // Dropout's 1/(1-rate) is folded into the BN affine once per column tile.  Rows t >= 60 of a
-  // slot are the next block's zero halo: they are simply never written (zeroed at kernel start).
+  // relu(acc + b) * s + t == clamp(fma(acc, s, b*s + t), lo, hi) (host-folded constants, one v_fma +
+  // one v_med3 per element); MC Dropout reads a second copy pre-scaled by 1/(1-rate).  Rows t >= 60
+  // of a slot are the next block's zero halo: they are simply never written (zeroed at kernel start).
   // row0 = wm*RT*16 + m with RT*16 a multiple of 64, so t = (16r mod 64) + m is compile-time up to m.
-  const gfloat* epi = reinterpret_cast<const gfloat*>(blob + eoff(LAYER));
+  const gfloat* epi = reinterpret_cast<const gfloat*>(blob + eoff(LAYER)) + (DROP ? 4 * COUT : 0);
   const bool tail_lane = m >= kL - 48;  // lanes whose row in a 48..63 row tile is a halo row
 
   if constexpr (!HEAD) APNEAUQ_SYNC();  // every wave has finished reading this block's input
+  APNEAUQ_STAMP(4 + 4 * LAYER);  // epilogue start (after the barrier)
+#ifdef APNEAUQ_PRIO_E
+  __builtin_amdgcn_s_setprio(APNEAUQ_PRIO_E);  // probe: wave priority during the VALU epilogue
+#endif
 
   float gap = 0.f;  // HEAD: this lane's share of sum_t sum_co w[co] * y[t][co]
 #pragma unroll
   for (int c = 0; c < CT; ++c) {
     const int co0 = (wn * CT + c) * 16 + 4 * h;
-    const f32x4 bias = *reinterpret_cast<const gf32x4*>(epi + co0);
-    f32x4 sc = *reinterpret_cast<const gf32x4*>(epi + COUT + co0);
-    f32x4 sh = *reinterpret_cast<const gf32x4*>(epi + 2 * COUT + co0);
-    if constexpr (DROP) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        sc[i] *= X.dsc;
-        sh[i] *= X.dsc;
-      }
-    }
+    const f32x4 sc = *reinterpret_cast<const gf32x4*>(epi + co0);
+    const f32x4 sh = *reinterpret_cast<const gf32x4*>(epi + COUT + co0);
+    const f32x4 lo = *reinterpret_cast<const gf32x4*>(epi + 2 * COUT + co0);
+    const f32x4 hi = *reinterpret_cast<const gf32x4*>(epi + 3 * COUT + co0);
     f32x4 dw;
     if constexpr (HEAD) dw = *reinterpret_cast<const gf32x4*>(reinterpret_cast<const gfloat*>(blob + kDenseOff) + co0);
 #pragma unroll
@@ -251,7 +277,7 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
       f32x4 v = acc[c][r];
       if constexpr ((APNEAUQ_ABL & 1) == 0) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i] + bias[i], 0.f) * sc[i] + sh[i];
+        for (int i = 0; i < 4; ++i) v[i] = __builtin_amdgcn_fmed3f(__builtin_fmaf(v[i], sc[i], sh[i]), lo[i], hi[i]);
         if constexpr (DROP) {
           const unsigned k = slot ? X.skey1 : X.skey0;
 #if (APNEAUQ_ABL & 32)
@@ -266,6 +292,9 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
           v[1] = (b01 >> 16) >= X.thr ? v[1] : 0.f;
           v[2] = (b23 & 0xFFFFu) >= X.thr ? v[2] : 0.f;
           v[3] = (b23 >> 16) >= X.thr ? v[3] : 0.f;
+          // keep the selects in fp32: otherwise LLVM folds cvt(select(x, 0)) into select(cvt(x), 0),
+          // converting every element separately and re-packing the pairs with v_perm
+          asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
         }
       }
       if constexpr (HEAD) {
@@ -295,6 +324,7 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
       head[8 + sl] = X.out_logits ? logit : 1.0f / (1.0f + __expf(-logit));
     }
   } else {
+    APNEAUQ_STAMP(5 + 4 * LAYER);  // epilogue done, before the barrier
     APNEAUQ_SYNC();  // block output visible before the next block reads it
   }
 }
@@ -334,6 +364,10 @@ __global__ __launch_bounds__(kThreads, 2) void fused_forward_kernel(Args A) {
   // One tile per workgroup.  (A persistent tile loop lets LICM hoist every block's address math
   // out of the loop, which blows the 256-VGPR budget; one tile per launch slot keeps it at ~206.)
   {
+    APNEAUQ_STAMP(0);
+#ifdef APNEAUQ_STAMPS
+    if (blockIdx.x < kStampWG && threadIdx.x == 0) g_stamp_cu[blockIdx.x] = __smid();
+#endif
     const int item = wg;
     APNEAUQ_DASSERT(item < A.total_items && (int)gridDim.x == A.total_items && blockDim.x == kThreads);
     const int member = item / A.tiles_per_member;
@@ -382,6 +416,7 @@ __global__ __launch_bounds__(kThreads, 2) void fused_forward_kernel(Args A) {
       const int sl = threadIdx.x;
       A.out[((long long)member * A.n_pass + pass[sl]) * A.n_win + win[sl]] = head[8 + sl];
     }
+    APNEAUQ_STAMP(1);
   }
 }
 

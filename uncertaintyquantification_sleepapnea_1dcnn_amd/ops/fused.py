@@ -43,6 +43,22 @@ def warn_unsupported(spec: ModelSpec, what: str) -> None:
                       f"{spec.input_channels}, pool={spec.has_pool}); using the fp32 PyTorch path", stacklevel=3)
 
 
+EPI_ROWS = 8  # per-channel epilogue constants [s, t', lo, hi] as-is, then pre-scaled by 1/(1-rate)
+
+
+def epilogue_constants(bias: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor) -> torch.Tensor:
+    """Fold bias + ReLU + BN affine into one fma + one clamp (``v_fma`` + ``v_med3``):
+
+    ``relu(acc + b) * s + t == clamp(acc * s + (b * s + t), lo, hi)`` with ``[lo, hi] = [t, +inf]``
+    for ``s >= 0`` and ``[-inf, t]`` for ``s < 0``.  Returns (4, C) fp32 rows [s, t', lo, hi]."""
+    s = scale.float()
+    t = shift.float()
+    inf = torch.full_like(t, float("inf"))
+    lo = torch.where(s >= 0, t, -inf)
+    hi = torch.where(s >= 0, inf, t)
+    return torch.stack([s, bias.float() * s + t, lo, hi])
+
+
 def _ceil(a: int, b: int) -> int:
     return (a + b - 1) // b * b
 
@@ -56,7 +72,7 @@ def layout() -> Dict[str, object]:
         off += ((ch[l] * ks[l] + 31) // 32) * (ch[l + 1] // 16) * 1024
     for l in range(6):
         eoff.append(off)
-        off += _ceil(3 * ch[l + 1] * 4, 16)
+        off += _ceil(EPI_ROWS * ch[l + 1] * 4, 16)
     dense = off
     total = dense + _ceil((ch[6] + 1) * 4, 16)
     return {"woff": woff, "eoff": eoff, "dense": dense, "bytes": total}
@@ -115,8 +131,10 @@ def pack_blob(spec: ModelSpec, p, bn_override: Optional[Sequence] = None) -> tor
             scale, shift = bn_override[l]
         else:
             scale, shift = bn_affine(spec, p, i)
-        epi = torch.cat([p[f"conv1d_{i}/bias"].float().to(dev), scale.float().to(dev), shift.float().to(dev)])
-        e = epi.contiguous().view(torch.uint8)
+        epi = epilogue_constants(p[f"conv1d_{i}/bias"].float().to(dev), scale.float().to(dev), shift.float().to(dev))
+        rate = spec.blocks[l].dropout
+        epi = torch.cat([epi, epi * (1.0 / (1.0 - rate) if rate < 1.0 else 0.0)])  # MC-Dropout rows
+        e = epi.contiguous().view(torch.uint8).reshape(-1)
         blob[lay["eoff"][l]: lay["eoff"][l] + e.numel()] = e
     head = torch.cat([p["output_layer/kernel"].float().reshape(-1), p["output_layer/bias"].float().reshape(-1)]).to(dev)
     h = head.contiguous().view(torch.uint8)
@@ -163,9 +181,9 @@ def emulate_blob_forward(blob: torch.Tensor, x: torch.Tensor, spec: ModelSpec = 
         nbytes = nstep * (ch[l + 1] // 16) * 1024
         fr = blob[lay["woff"][l]: lay["woff"][l] + nbytes].view(torch.bfloat16).reshape(nstep, ch[l + 1] // 16, 64, 8)
         w = unpack_conv_fragments(fr, ks[l], ch[l], ch[l + 1])
-        epi = blob[lay["eoff"][l]: lay["eoff"][l] + 12 * ch[l + 1]].view(torch.float32).reshape(3, ch[l + 1])
-        y = conv1d_same(h, w, epi[0])
-        y = torch.relu(y) * epi[1] + epi[2]
+        epi = blob[lay["eoff"][l]: lay["eoff"][l] + 4 * EPI_ROWS * ch[l + 1]].view(torch.float32).reshape(EPI_ROWS, ch[l + 1])
+        y = conv1d_same(h, w, torch.zeros(ch[l + 1]))
+        y = torch.minimum(torch.maximum(y * epi[0] + epi[1], epi[2]), epi[3])  # rows 4-7: same x 1/(1-rate)
         if dropout:
             y = rng.dropout_apply_torch(y, rng.stream_key(seed, l, pass_id), sample_ids, spec.blocks[l].dropout)
         h = y if l == 5 else y.to(torch.bfloat16).float()
