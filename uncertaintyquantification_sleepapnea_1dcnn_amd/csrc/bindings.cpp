@@ -27,7 +27,7 @@ namespace train {
 struct Layer {
   const void* wf; const void* wd; const float* bias; const float* gamma; const float* beta;
   float* mmean; float* mvar; float* gw; float* gb; float* ggamma; float* gbeta;
-  void* R; void* dY; float* st; float* bst; unsigned thr; float dsc;
+  void* R; void* dY; void* dZ; float* st; float* bst; unsigned thr; float dsc;
 };
 struct Args {
   Layer L[6];
@@ -139,7 +139,7 @@ void adam_step(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
 }
 
 // ctx: int64 CPU tensor of device pointers / scalars built once per workspace (ops/train_ops.py)
-constexpr int kCtxLayer = 17, kCtxLen = 6 * kCtxLayer + 20;
+constexpr int kCtxLayer = 18, kCtxLen = 6 * kCtxLayer + 20;
 
 float bits_to_float(int64_t v) {
   uint32_t u = static_cast<uint32_t>(v);
@@ -176,6 +176,7 @@ apneauq::train::Args args_from_ctx(const at::Tensor& ctx, int64_t pass_base) {
     L.bst = reinterpret_cast<float*>(q[14]);
     L.thr = static_cast<unsigned>(q[15]);
     L.dsc = bits_to_float(q[16]);
+    L.dZ = reinterpret_cast<void*>(q[17]);
   }
   const int64_t* g = c + 6 * kCtxLayer;
   A.x = reinterpret_cast<const void*>(g[0]);

@@ -38,6 +38,7 @@ ARCH = os.environ.get("APNEAUQ_OFFLOAD_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 DEBUG = os.environ.get("APNEAUQ_DEBUG", "0") not in ("", "0")
 HOST_SAN = os.environ.get("APNEAUQ_HOST_SANITIZE", "")
+EXTRA = os.environ.get("APNEAUQ_HIPCC_FLAGS", "").split()  # probe builds (e.g. -DAPNEAUQ_ABL=...)
 
 
 def _torch_paths():
@@ -73,7 +74,7 @@ def commands():
         obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
         san = (["-Xarch_host"] + host_san) if host_san else []
         cmds.append([_hipcc(), f"--offload-arch={ARCH}", "-c", src, "-o", obj, "-ffp-contract=fast",
-                     "-munsafe-fp-atomics"] + san + common)
+                     "-munsafe-fp-atomics"] + san + common + EXTRA)
         objs.append(obj)
     py_inc = sysconfig.get_paths()["include"]
     for src in cpp:
@@ -94,7 +95,7 @@ def _stamp():
         with open(f, "rb") as fh:
             h.update(fh.read())
     h.update(ARCH.encode())
-    h.update(f"debug={DEBUG};san={HOST_SAN}".encode())
+    h.update(f"debug={DEBUG};san={HOST_SAN};extra={EXTRA}".encode())
     return h.hexdigest()
 
 

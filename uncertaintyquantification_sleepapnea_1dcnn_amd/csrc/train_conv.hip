@@ -14,7 +14,9 @@
 // forward, the wgrad of block l+1) recomputes  A_l = mask * (R_l * s + t) / (1-p)  while staging
 // into LDS, and the consumers of dZ_l (dgrad / wgrad of block l) recompute
 //   dZ_l = [R_l > 0] * gamma * rstd * (dY_l - mean(dY_l) - xhat * mean(dY_l * xhat))
-// from the per-channel sums accumulated by the producer's epilogue (fp32 atomics).
+// from the per-channel sums accumulated by the producer's epilogue (fp32 atomics).  dgrad_l also
+// writes its staged dZ_l rows to global memory, so wgrad_l (whose ci-blocked workgroups would each
+// recompute the whole dZ tile) stages it with a plain copy.
 //
 // Forward and dgrad are implicit GEMMs on v_mfma_f32_16x16x32_bf16 with the weights as the A operand
 // (pre-packed fragments from global/L2) and the staged activations as the B operand (LDS,
@@ -48,6 +50,7 @@ struct Layer {
   float* gbeta;
   __bf16* R;           // PL (rows, C) post-ReLU, pre-BN
   __bf16* dY;          // PL (rows, C) gradient wrt BN output (blocks 1..5)
+  __bf16* dZ;          // PL (rows, C) gradient wrt the conv pre-activation, written by dgrad_l (l >= 1)
   float* st;           // [groups][2][C] forward sums (sum r, sum r^2)
   float* bst;          // [2][C] backward sums (sum dY, sum dY * xhat)
   unsigned thr;        // dropout threshold (16-bit units) and 1/(1-p)
@@ -110,101 +113,180 @@ __device__ __forceinline__ unsigned layer_sample_key(const Args& A, int l, int s
   return sample_key(stream_key(A.seed, l, A.pass_base + g), A.window_offset + w);
 }
 
-// Stage A_l (= dropout(BN(R_l))) rows [row0, row0 + nrows) x channels [c0, c0 + ncw*8) of global
-// PL buffer into LDS (row stride ldsrs bytes).  Pad rows and rows outside the batch become 0.
-template <int l>
-__device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, int row0, int nrows, int c0, int ncw,
-                                          const float* s, const float* t, int g0, int g1, int tile_sample0) {
-  constexpr int Cc = C[l + 1];
-  const Layer& Ly = A.L[l];
-  (void)tile_sample0;
-  for (int i = threadIdx.x; i < nrows * ncw; i += kThreads) {
-    const int r = i / ncw, cw = i - r * ncw;
-    const int grow = row0 + r;
-    const int n = row_sample(grow), tt = row_time(grow);
-    const int c = c0 + cw * 8;
-    bf16x8 o;
-    if (grow < kHalo || n >= A.B || tt >= kL) {
+// Staging loops issue a batch of up to kStageU global loads per thread before the first LDS
+// write, so a tile's staging pays the memory latency ceil(items / (256 * kStageU)) times instead of
+// once per item (a plain load->use loop waits vmcnt(0) on every iteration).
+constexpr int kStageU = 8;
+
+struct bf16x16 {
+  bf16x8 a, b;
+};
+
+template <int N, int UMAX = kStageU, typename Load, typename Store>
+__device__ __forceinline__ void staged_loop(Load load, Store store) {
+  constexpr int IT = (N + kThreads - 1) / kThreads;
+  constexpr int U = IT < UMAX ? IT : UMAX;
+  using P = decltype(load(0));
+  // opaque thread index: inside a tile loop (wgrad) LICM would otherwise hoist every per-item
+  // index/address out of the loop and keep them live across the MFMAs (VGPR spills)
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (__bf16)0.f;
-    } else {
-      const bf16x8 v = gld<bf16x8>(Ly.R + (long long)grow * Cc + c);
-      const int g = n / A.n_win;
-      const float* sg = s + (g == g0 ? 0 : 256);
-      const float* tg = t + (g == g0 ? 0 : 256);
-      (void)g1;
-      unsigned key = 0;
-      if (A.dropout) key = layer_sample_key(A, l, n);
+  for (int b = 0; b < IT; b += U) {
+    P v[U];
 #pragma unroll
-      for (int j = 0; j < 8; j += 2) {
-        float a0 = (float)v[j] * sg[c + j] + tg[c + j];
-        float a1 = (float)v[j + 1] * sg[c + j + 1] + tg[c + j + 1];
-        if (A.dropout) {
-          const unsigned h = dropout_bits2(key, tt, c + j);
-          a0 = (h & 0xFFFFu) >= Ly.thr ? a0 * Ly.dsc : 0.f;
-          a1 = (h >> 16) >= Ly.thr ? a1 * Ly.dsc : 0.f;
-        }
-        o[j] = (__bf16)a0;
-        o[j + 1] = (__bf16)a1;
-      }
+    for (int u = 0; u < U; ++u) {
+      const int i = tid + (b + u) * kThreads;
+      if (b + u < IT && i < N) v[u] = load(i);
     }
-    *reinterpret_cast<bf16x8*>(lds + r * ldsrs + cw * 16) = o;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = tid + (b + u) * kThreads;
+      if (b + u < IT && i < N) store(i, v[u]);
+    }
   }
 }
 
-// dZ_l rows into LDS (rows [row0, row0+nrows), channels [c0, c0+ncw*8)).
-//   l == 5: dY_6 = dlogit[n] * w[c] / 60 * mask6 * dsc6 (recomputed; never stored)
-template <int l>
-__device__ __forceinline__ void stage_dz(const Args& A, char* lds, int ldsrs, int row0, int nrows, int c0, int ncw,
-                                         const float* gam_rstd, const float* mean, const float* rstd, const float* mdy,
-                                         const float* mdyx, float* colsum = nullptr) {
+__device__ __forceinline__ bf16x8 zero8() {
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (__bf16)0.f;
+  return o;
+}
+
+// Stage A_l (= dropout(BN(R_l))) rows [row0, row0 + NR) x channels [c0, c0 + NCW*8) of global
+// PL buffer into LDS (row stride ldsrs bytes).  Pad rows and rows outside the batch become 0.
+template <int l, int NR, int NCW, int UMAX = kStageU>
+__device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, int row0, int c0, const float* s,
+                                          const float* t, int g0) {
   constexpr int Cc = C[l + 1];
   const Layer& Ly = A.L[l];
-  for (int i = threadIdx.x; i < nrows * ncw; i += kThreads) {
-    const int r = i / ncw, cw = i - r * ncw;
-    const int grow = row0 + r;
+  auto valid = [&](int grow) {
     const int n = row_sample(grow), tt = row_time(grow);
-    const int c = c0 + cw * 8;
-    bf16x8 o;
-    if (grow < kHalo || n >= A.B || tt >= kL) {
+    return !(grow < kHalo || n >= A.B || tt >= kL);
+  };
+  staged_loop<NR * NCW, UMAX>(
+      [&](int i) -> bf16x8 {
+        const int r = i / NCW, cw = i - r * NCW;
+        const int grow = row0 + r;
+        return valid(grow) ? gld<bf16x8>(Ly.R + (long long)grow * Cc + c0 + cw * 8) : zero8();
+      },
+      [&](int i, const bf16x8& v) {
+        const int r = i / NCW, cw = i - r * NCW;
+        const int grow = row0 + r;
+        const int c = c0 + cw * 8;
+        bf16x8 o = zero8();
+        if (valid(grow)) {
+          const int n = row_sample(grow), tt = row_time(grow);
+          const int g = n / A.n_win;
+          const float* sg = s + (g == g0 ? 0 : 256);
+          const float* tg = t + (g == g0 ? 0 : 256);
+          unsigned key = 0;
+          if (A.dropout) key = layer_sample_key(A, l, n);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (__bf16)0.f;
-    } else {
-      const bf16x8 rv = gld<bf16x8>(Ly.R + (long long)grow * Cc + c);
-      float dy[8];
-      if constexpr (l == 5) {
-        const float dl = A.dlogit[n] * (1.0f / kL);
-        const unsigned key = A.dropout ? layer_sample_key(A, 5, n) : 0u;
-#pragma unroll
-        for (int j = 0; j < 8; j += 2) {
-          float d0 = dl * A.dense_w[c + j], d1 = dl * A.dense_w[c + j + 1];
-          if (A.dropout) {
-            const unsigned h = dropout_bits2(key, tt, c + j);
-            d0 = (h & 0xFFFFu) >= Ly.thr ? d0 * Ly.dsc : 0.f;
-            d1 = (h >> 16) >= Ly.thr ? d1 * Ly.dsc : 0.f;
+          for (int j = 0; j < 8; j += 2) {
+            float a0 = (float)v[j] * sg[c + j] + tg[c + j];
+            float a1 = (float)v[j + 1] * sg[c + j + 1] + tg[c + j + 1];
+            if (A.dropout) {
+              const unsigned h = dropout_bits2(key, tt, c + j);
+              a0 = (h & 0xFFFFu) >= Ly.thr ? a0 * Ly.dsc : 0.f;
+              a1 = (h >> 16) >= Ly.thr ? a1 * Ly.dsc : 0.f;
+            }
+            o[j] = (__bf16)a0;
+            o[j + 1] = (__bf16)a1;
           }
-          dy[j] = d0;
-          dy[j + 1] = d1;
         }
-      } else {
-        const bf16x8 dv = gld<bf16x8>(Ly.dY + (long long)grow * Cc + c);
+        *reinterpret_cast<bf16x8*>(lds + r * ldsrs + cw * 16) = o;
+      });
+}
+
+// dZ_l rows into LDS (rows [row0, row0+NR), channels [c0, c0+NCW*8)); rows [own_lo, own_hi) are
+// also written to ``gout`` (dgrad materialises dZ_l for wgrad).
+//   l == 5: dY_6 = dlogit[n] * w[c] / 60 * mask6 * dsc6 (recomputed; never stored)
+template <int l, int NR, int NCW>
+__device__ __forceinline__ void stage_dz(const Args& A, char* lds, int ldsrs, int row0, int c0,
+                                         const float* gam_rstd, const float* mean, const float* rstd, const float* mdy,
+                                         const float* mdyx, float* colsum = nullptr, __bf16* gout = nullptr,
+                                         int own_lo = 0, int own_hi = 0) {
+  constexpr int Cc = C[l + 1];
+  const Layer& Ly = A.L[l];
+  auto valid = [&](int grow) {
+    const int n = row_sample(grow), tt = row_time(grow);
+    return !(grow < kHalo || n >= A.B || tt >= kL);
+  };
+  // payload: R_l (pre-BN activation) and dY_l, both loaded in the batched first phase
+  staged_loop<NR * NCW, kStageU / 2>(
+      [&](int i) -> bf16x16 {
+        const int r = i / NCW, cw = i - r * NCW;
+        const int grow = row0 + r;
+        bf16x16 q;
+        q.a = valid(grow) ? gld<bf16x8>(Ly.R + (long long)grow * Cc + c0 + cw * 8) : zero8();
+        if constexpr (l < 5) q.b = valid(grow) ? gld<bf16x8>(Ly.dY + (long long)grow * Cc + c0 + cw * 8) : zero8();
+        return q;
+      },
+      [&](int i, const bf16x16& q) {
+        const bf16x8& rv = q.a;
+        const int r = i / NCW, cw = i - r * NCW;
+        const int grow = row0 + r;
+        const int c = c0 + cw * 8;
+        bf16x8 o = zero8();
+        if (valid(grow)) {
+          const int n = row_sample(grow), tt = row_time(grow);
+          float dy[8];
+          if constexpr (l == 5) {
+            const float dl = A.dlogit[n] * (1.0f / kL);
+            const unsigned key = A.dropout ? layer_sample_key(A, 5, n) : 0u;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) dy[j] = (float)dv[j];
-      }
+            for (int j = 0; j < 8; j += 2) {
+              float d0 = dl * A.dense_w[c + j], d1 = dl * A.dense_w[c + j + 1];
+              if (A.dropout) {
+                const unsigned h = dropout_bits2(key, tt, c + j);
+                d0 = (h & 0xFFFFu) >= Ly.thr ? d0 * Ly.dsc : 0.f;
+                d1 = (h >> 16) >= Ly.thr ? d1 * Ly.dsc : 0.f;
+              }
+              dy[j] = d0;
+              dy[j + 1] = d1;
+            }
+          } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float rr = (float)rv[j];
-        const float xh = (rr - mean[c + j]) * rstd[c + j];
-        const float dz = gam_rstd[c + j] * (dy[j] - mdy[c + j] - xh * mdyx[c + j]);
-        o[j] = (__bf16)(rr > 0.f ? dz : 0.f);
-      }
-      if (colsum) {
+            for (int j = 0; j < 8; ++j) dy[j] = (float)q.b[j];
+          }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) atomicAdd(colsum + (c - c0) + j, (float)o[j]);
-      }
-    }
-    *reinterpret_cast<bf16x8*>(lds + r * ldsrs + cw * 16) = o;
-  }
+          for (int j = 0; j < 8; ++j) {
+            const float rr = (float)rv[j];
+            const float xh = (rr - mean[c + j]) * rstd[c + j];
+            const float dz = gam_rstd[c + j] * (dy[j] - mdy[c + j] - xh * mdyx[c + j]);
+            o[j] = (__bf16)(rr > 0.f ? dz : 0.f);
+          }
+          if (colsum) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) atomicAdd(colsum + (c - c0) + j, (float)o[j]);
+          }
+        }
+        *reinterpret_cast<bf16x8*>(lds + r * ldsrs + cw * 16) = o;
+        if (gout != nullptr && r >= own_lo && r < own_hi)
+          *reinterpret_cast<bf16x8*>(gout + (long long)grow * Cc + c) = o;  // pad rows get their zeros too
+      });
+}
+
+// Plain copy of materialised dZ rows (see dgrad) into LDS, with the optional bias-gradient sums.
+template <int l, int NR, int NCW, int UMAX>
+__device__ __forceinline__ void stage_dz_copy(const Args& A, char* lds, int ldsrs, int row0, int c0, float* colsum) {
+  constexpr int Cc = C[l + 1];
+  const Layer& Ly = A.L[l];
+  staged_loop<NR * NCW, UMAX>(
+      [&](int i) -> bf16x8 {
+        const int r = i / NCW, cw = i - r * NCW;
+        return gld<bf16x8>(Ly.dZ + (long long)(row0 + r) * Cc + c0 + cw * 8);
+      },
+      [&](int i, const bf16x8& o) {
+        const int r = i / NCW, cw = i - r * NCW;
+        *reinterpret_cast<bf16x8*>(lds + r * ldsrs + cw * 16) = o;
+        if (colsum) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) atomicAdd(colsum + cw * 8 + j, (float)o[j]);
+        }
+      });
 }
 
 // Implicit-GEMM conv tile: D^T[co][row] over the 128-row tile, weights = packed A fragments.
@@ -227,6 +309,7 @@ struct Conv {
     for (int c = 0; c < CT; ++c)
 #pragma unroll
       for (int r = 0; r < RT; ++r) acc[c][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const char* bbase = lds + (kHalo + row0 - PAD) * ldsrs + 16 * h;
     auto load_b = [&](int s, int r) -> bf16x8 {
       if constexpr (FIRST) {
         const char* base = lds + (kHalo + row0 + r * 16 - PAD) * ldsrs + (32 * s + 8 * h) * 2;
@@ -234,9 +317,11 @@ struct Conv {
         const bf16x4 hi = *reinterpret_cast<const bf16x4*>(base + 8);
         return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       } else {
+        // lane base + uniform step offset + compile-time row-tile offset (see fused_forward.hip)
         constexpr int CB = CIN / 32;
         const int tap = s / CB, cb = s - tap * CB;
-        return *reinterpret_cast<const bf16x8*>(lds + (kHalo + row0 + r * 16 + tap - PAD) * ldsrs + (cb * 32 + 8 * h) * 2);
+        const int soff = __builtin_amdgcn_readfirstlane(tap * ldsrs + cb * 64);
+        return *reinterpret_cast<const bf16x8*>(bbase + soff + r * 16 * ldsrs);
       }
     };
     auto load_a = [&](int s, bf16x8 (&a)[CT]) {
@@ -304,13 +389,14 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
   const int g0 = min(smp0, A.B - 1) / A.n_win, g1 = min(smp0 + 1, A.B - 1) / A.n_win;
   constexpr int IN_RS = (l == 0) ? 8 : kRS;
   if constexpr (l == 0) {
-    for (int i = threadIdx.x; i < kRows * 8 / 16; i += kThreads)
-      reinterpret_cast<f32x4*>(act)[i] = gld<f32x4>(A.x + (long long)row0 * 4 + i * 8);
+    staged_loop<kRows * 8 / 16>(
+        [&](int i) -> bf16x8 { return gld<bf16x8>(A.x + (long long)row0 * 4 + i * 8); },
+        [&](int i, const bf16x8& v) { reinterpret_cast<bf16x8*>(act)[i] = v; });
   } else {
     bn_affine_to_lds(A, l - 1, g0, prm, prm + 512, nullptr, nullptr);
     if (g1 != g0) bn_affine_to_lds(A, l - 1, g1, prm + 256, prm + 768, nullptr, nullptr);
     __syncthreads();
-    stage_act<l - 1>(A, act, kRS, row0, kRows, 0, CIN / 8, prm, prm + 512, g0, g1, smp0);
+    stage_act<l - 1, kRows, CIN / 8>(A, act, kRS, row0, 0, prm, prm + 512, g0);
   }
   __syncthreads();
   f32x4 acc[CV::CT][CV::RT];
@@ -498,7 +584,8 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
     bn_affine_to_lds(A, l - 1, 0, s_prev, t_prev, mean_prev, rstd_prev);
   }
   __syncthreads();
-  stage_dz<l>(A, act, kRS, row0, kRows, 0, CIN / 8, gr, mean, rstd, mdy, mdyx);
+  stage_dz<l, kRows, CIN / 8>(A, act, kRS, row0, 0, gr, mean, rstd, mdy, mdyx, nullptr, A.L[l].dZ, kHalo,
+                              kHalo + kR);
   __syncthreads();
   f32x4 acc[CV::CT][CV::RT];
   CV::run(A.L[l].wd, act, kRS, acc);
@@ -562,15 +649,14 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
 // with ds_read_b64_tr_b16 from row-major LDS tiles.  Block 1 stages an im2col (kk = tap*4+ci).
 // ------------------------------------------------------------------------------------------------
 template <int l> struct WgCfg;
-//                               CI_BLK CO_BLK WCO WCI
-template <> struct WgCfg<0> { static constexpr int CIB = 32, COB = 128, WCO = 4, WCI = 1; };  // im2col kk=32
-template <> struct WgCfg<1> { static constexpr int CIB = 32, COB = 192, WCO = 2, WCI = 2; };
-template <> struct WgCfg<2> { static constexpr int CIB = 32, COB = 224, WCO = 2, WCI = 2; };
-template <> struct WgCfg<3> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2; };
-template <> struct WgCfg<4> { static constexpr int CIB = 16, COB = 128, WCO = 4, WCI = 1; };
-template <> struct WgCfg<5> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2; };
-
-constexpr int kWgRowTiles = 16;  // 128-row tiles summed in registers per workgroup
+// CI_BLK CO_BLK WCO WCI, RTILES = 128-row tiles summed in registers per workgroup (sized so a
+// batch of 1024 gives >= 256 workgroups without multiplying the output atomics needlessly)
+template <> struct WgCfg<0> { static constexpr int CIB = 32, COB = 128, WCO = 4, WCI = 1, RTILES = 2; };  // im2col kk=32
+template <> struct WgCfg<1> { static constexpr int CIB = 32, COB = 192, WCO = 2, WCI = 2, RTILES = 8; };
+template <> struct WgCfg<2> { static constexpr int CIB = 32, COB = 224, WCO = 2, WCI = 2, RTILES = 8; };
+template <> struct WgCfg<3> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16; };
+template <> struct WgCfg<4> { static constexpr int CIB = 16, COB = 128, WCO = 4, WCI = 1, RTILES = 16; };
+template <> struct WgCfg<5> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16; };
 
 __device__ __forceinline__ bf16x8 tr_frag(const char* lds, int ldsrs, int row_base, int col0) {
   // fragment for a 16x16x32 operand whose K index is the LDS row: lane (m, h) gets rows
@@ -612,17 +698,19 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_kernel(Args A) {
   float* mdyx = prm + 1024;
   float* sp = prm + 1280;   // block l-1 affine (scale | shift) for staging A_{l-1}
   float* tp = prm + 1536;
-  float* colsum = prm + 2048;  // bias-gradient column sums (ci-block 0 only)
   const int nci_blk = FIRST ? 1 : CIN / W::CIB;
   const int nco_blk = COUT / W::COB;
   const int blk = blockIdx.x % (nci_blk * nco_blk);
   const int rg = blockIdx.x / (nci_blk * nco_blk);
   const int ci0 = (blk % nci_blk) * W::CIB, co0 = (blk / nci_blk) * W::COB;
+#ifdef APNEAUQ_WG_NOBIAS  // probe: skip the bias-gradient column sums (wrong db, timing only)
+  const bool do_bias = false;
+#else
   const bool do_bias = (ci0 == 0);
+#endif
   {
     const Layer& Ly = A.L[l];
     bn_affine_to_lds(A, l, 0, gr, mdy, mean, rstd);
-    for (int c = threadIdx.x; c < 256; c += kThreads) colsum[c] = 0.f;
     __syncthreads();
     for (int c = threadIdx.x; c < COUT; c += kThreads) {
       gr[c] = Ly.gamma[c] * rstd[c];
@@ -642,14 +730,27 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_kernel(Args A) {
     for (int b = 0; b < NCI; ++b)
 #pragma unroll
       for (int a = 0; a < NCO; ++a) acc[k][b][a] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // bias gradient on the matrix cores (a column sum of dZ = ones^T dZ): the waves of ci-block 0 with
+  // wci == 0 carry NCO extra accumulators.  (Per-element LDS atomics for these sums contended on the
+  // same 128-256 addresses and cost 3-4x the whole wgrad.)
+  const bool bias_wave = do_bias && wci == 0;
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.f;
+  f32x4 accb[NCO];
+#pragma unroll
+  for (int a = 0; a < NCO; ++a) accb[a] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int ntiles = (A.B + 1) / 2;
-  for (int it = 0; it < kWgRowTiles; ++it) {
-    const int tile = rg * kWgRowTiles + it;
+  for (int it = 0; it < W::RTILES; ++it) {
+    const int tile = rg * W::RTILES + it;
     if (tile >= ntiles) break;
     const int row0 = kR * tile;
     __syncthreads();
-    stage_dz<l>(A, dz_lds, DZRS, row0 + kHalo, kR, co0, W::COB / 8, gr, mean, rstd, mdy, mdyx,
-                do_bias ? colsum : nullptr);
+    if constexpr (FIRST)  // no dgrad for block 1: dZ_1 is recomputed here (a single ci block)
+      stage_dz<l, kR, W::COB / 8>(A, dz_lds, DZRS, row0 + kHalo, co0, gr, mean, rstd, mdy, mdyx,
+                                  nullptr);
+    else
+      stage_dz_copy<l, kR, W::COB / 8, 4>(A, dz_lds, DZRS, row0 + kHalo, co0, nullptr);
     if constexpr (FIRST) {
       // im2col of the raw input: col kk = tap*4 + ci (kk < 28), rows = tile rows
       for (int i = threadIdx.x; i < kR * 32; i += kThreads) {
@@ -660,7 +761,7 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_kernel(Args A) {
         *reinterpret_cast<__bf16*>(a_lds + r * ARS + kk * 2) = v;
       }
     } else {
-      stage_act<l - 1>(A, a_lds, ARS, row0, kRows, ci0, W::CIB / 8, sp, tp, 0, 0, 2 * tile);
+      stage_act<l - 1, kRows, W::CIB / 8, 4>(A, a_lds, ARS, row0, ci0, sp, tp, 0);
     }
     __syncthreads();
 #pragma unroll
@@ -668,14 +769,22 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_kernel(Args A) {
       bf16x8 fb[NCO];
 #pragma unroll
       for (int a = 0; a < NCO; ++a) fb[a] = tr_frag(dz_lds, DZRS, ks * 32, (wco * NCO + a) * 16);
+      if (bias_wave) {  // db[co] = sum_rows dZ[row][co]: one MFMA with an all-ones A fragment
+#pragma unroll
+        for (int a = 0; a < NCO; ++a) accb[a] = mfma16(ones, fb[a], accb[a]);
+      }
 #pragma unroll
       for (int k = 0; k < NTAP; ++k) {
 #pragma unroll
         for (int b = 0; b < NCI; ++b) {
           const int arow = FIRST ? ks * 32 : kHalo + ks * 32 + k - PAD;
           const bf16x8 fa = tr_frag(a_lds, ARS, arow, (wci * NCI + b) * 16);
+#ifndef APNEAUQ_WG_NOMFMA  // probe: staging only (wrong dW, timing only)
 #pragma unroll
           for (int a = 0; a < NCO; ++a) acc[k][b][a] = mfma16(fa, fb[a], acc[k][b][a]);
+#else
+          if (fa[0] == (__bf16)123.f) acc[k][b][0][0] += 1.f;
+#endif
         }
       }
     }
@@ -693,17 +802,26 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_kernel(Args A) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int rowi = (wci * NCI + b) * 16 + 4 * h + i;  // ci (or kk for block 1)
+#ifdef APNEAUQ_WG_NOATOMIC  // probe: plain stores instead of atomics (wrong results, timing only)
+          if constexpr (FIRST) {
+            const int tap = rowi >> 2, ci = rowi & 3;
+            if (tap < K) Ly.gw[(tap * CIN + ci) * COUT + co] = acc[k][b][a][i];
+          } else {
+            Ly.gw[(k * CIN + ci0 + rowi) * COUT + co] = acc[k][b][a][i];
+          }
+#else
           if constexpr (FIRST) {
             const int tap = rowi >> 2, ci = rowi & 3;
             if (tap < K) atomicAdd(Ly.gw + (tap * CIN + ci) * COUT + co, acc[k][b][a][i]);
           } else {
             atomicAdd(Ly.gw + (k * CIN + ci0 + rowi) * COUT + co, acc[k][b][a][i]);
           }
+#endif
         }
       }
-  if (do_bias) {
-    __syncthreads();
-    for (int c = threadIdx.x; c < W::COB; c += kThreads) atomicAdd(Ly.gb + co0 + c, colsum[c]);
+  if (bias_wave && h == 0) {  // row 0 of each ones^T dZ tile: lanes 0-15 hold its 16 column sums
+#pragma unroll
+    for (int a = 0; a < NCO; ++a) atomicAdd(Ly.gb + co0 + (wco * NCO + a) * 16 + m, accb[a][0]);
   }
 }
 
@@ -812,7 +930,7 @@ static void wg_launch(const Args& A, hipStream_t st) {
   const int nci = (l == 0) ? 1 : train::C[l] / W::CIB;
   const int nco = train::C[l + 1] / W::COB;
   const int tiles = (A.B + 1) / 2;
-  const int rgs = (tiles + train::kWgRowTiles - 1) / train::kWgRowTiles;
+  const int rgs = (tiles + train::WgCfg<l>::RTILES - 1) / train::WgCfg<l>::RTILES;
   hipLaunchKernelGGL(train::wgrad_kernel<l>, dim3(nci * nco * rgs), dim3(256), lds_wgrad<l>(), st, A);
 }
 

@@ -81,6 +81,9 @@ class TrainWorkspace:
         self.R = [torch.zeros(rows, ch[l + 1], dtype=bf, device=dev) for l in range(6)]
         self.dY = [torch.zeros(rows, ch[l + 1], dtype=bf, device=dev) if (with_backward and l < 5)
                    else torch.zeros(16, dtype=bf, device=dev) for l in range(6)]
+        # dZ_l materialised by dgrad_l for wgrad_l (block 1 has no dgrad)
+        self.dZ = [torch.zeros(rows, ch[l + 1], dtype=bf, device=dev) if (with_backward and l >= 1)
+                   else torch.zeros(16, dtype=bf, device=dev) for l in range(6)]
         self.st_all = torch.zeros(sum(self.groups * 2 * ch[l + 1] for l in range(6)), device=dev)
         self.bst_all = torch.zeros(sum(2 * ch[l + 1] for l in range(6)), device=dev)
         self.st, self.bst = [], []
@@ -127,7 +130,7 @@ class TrainWorkspace:
                      g[f"conv1d_{i}/kernel"].data_ptr(), g[f"conv1d_{i}/bias"].data_ptr(),
                      g[f"batchnorm_{i}/gamma"].data_ptr(), g[f"batchnorm_{i}/beta"].data_ptr(),
                      self.R[l].data_ptr(), self.dY[l].data_ptr(), self.st[l].data_ptr(), self.bst[l].data_ptr(),
-                     rng.dropout_threshold(p), _fbits(1.0 / (1.0 - p) if p < 1 else 0.0)]
+                     rng.dropout_threshold(p), _fbits(1.0 / (1.0 - p) if p < 1 else 0.0), self.dZ[l].data_ptr()]
         vals += [self.x.data_ptr(), self.y.data_ptr(), v["output_layer/kernel"].data_ptr(),
                  v["output_layer/bias"].data_ptr(), g["output_layer/kernel"].data_ptr(),
                  g["output_layer/bias"].data_ptr(), self.logits.data_ptr(), self.dlogit.data_ptr(),
