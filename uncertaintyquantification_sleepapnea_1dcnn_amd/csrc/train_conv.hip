@@ -89,13 +89,26 @@ __device__ __forceinline__ T gld(const void* p) {
 __device__ __forceinline__ int row_sample(int grow) { return (grow - kHalo) >> 6; }  // may be -1 / >= B
 __device__ __forceinline__ int row_time(int grow) { return (grow - kHalo) & 63; }
 
+// BN moment sums are accumulated into kStatSlots interleaved copies (slot = workgroup % kStatSlots)
+// so that the ~512 workgroups of a layer do not serialise on the same 2*C L2 atomic addresses;
+// readers add the slots.  Layout per layer: st[slot][group][2][C], bst[slot][2][C].
+constexpr int kStatSlots = 16;
+__device__ __forceinline__ int st_stride(const Args& A, int Cc) { return A.groups * 2 * Cc; }
+__device__ __forceinline__ float slot_sum(const float* p, int stride) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < kStatSlots; ++i) s += p[i * stride];
+  return s;
+}
+
 // Per-channel BN affine of block l for stats group g, into LDS: s[c], t[c], mean[c], rstd[c].
 __device__ __forceinline__ void bn_affine_to_lds(const Args& A, int l, int g, float* s, float* t, float* mean,
                                                  float* rstd) {
   const int Cc = C[l + 1];
   const Layer& Ly = A.L[l];
   for (int c = threadIdx.x; c < Cc; c += kThreads) {
-    const float s1 = Ly.st[(g * 2 + 0) * Cc + c], s2 = Ly.st[(g * 2 + 1) * Cc + c];
+    const int ss = st_stride(A, Cc);
+    const float s1 = slot_sum(Ly.st + (g * 2 + 0) * Cc + c, ss), s2 = slot_sum(Ly.st + (g * 2 + 1) * Cc + c, ss);
     const float mu = s1 * A.inv_count;
     const float var = fmaxf(s2 * A.inv_count - mu * mu, 0.f);
     const float rs = rsqrtf(var + A.eps);
@@ -428,16 +441,17 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
         else { s1[1][i] += q; s2[1][i] += q * q; }
       }
     }
+    float* st = Ly.st + (blockIdx.x % kStatSlots) * st_stride(A, COUT);
     if (g0 == g1) {
       s1[0] += s1[1];
       s2[0] += s2[1];
-      atomic_channel_sums(Ly.st + (g0 * 2 + 0) * COUT, co0, s1[0], m == 0);
-      atomic_channel_sums(Ly.st + (g0 * 2 + 1) * COUT, co0, s2[0], m == 0);
+      atomic_channel_sums(st + (g0 * 2 + 0) * COUT, co0, s1[0], m == 0);
+      atomic_channel_sums(st + (g0 * 2 + 1) * COUT, co0, s2[0], m == 0);
     } else {
-      atomic_channel_sums(Ly.st + (g0 * 2 + 0) * COUT, co0, s1[0], m == 0);
-      atomic_channel_sums(Ly.st + (g0 * 2 + 1) * COUT, co0, s2[0], m == 0);
-      atomic_channel_sums(Ly.st + (g1 * 2 + 0) * COUT, co0, s1[1], m == 0);
-      atomic_channel_sums(Ly.st + (g1 * 2 + 1) * COUT, co0, s2[1], m == 0);
+      atomic_channel_sums(st + (g0 * 2 + 0) * COUT, co0, s1[0], m == 0);
+      atomic_channel_sums(st + (g0 * 2 + 1) * COUT, co0, s2[0], m == 0);
+      atomic_channel_sums(st + (g1 * 2 + 0) * COUT, co0, s1[1], m == 0);
+      atomic_channel_sums(st + (g1 * 2 + 1) * COUT, co0, s2[1], m == 0);
     }
   }
   __syncthreads();
@@ -457,12 +471,13 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kThreads) void head_kernel(Args A, int backward) {
   constexpr int Cc = C[6];
-  float* dw = reinterpret_cast<float*>(smem);  // [dW 128 | dsum 128 | dxsum 128]
+  float* dw = reinterpret_cast<float*>(smem);  // [dW 128 | dsum 128 | dxsum 128 | loss, db]
   float* bsum0 = dw + 128;
   float* bsum1 = dw + 256;
+  float* red = dw + 384;  // per-workgroup loss / dense-bias sums: one global atomic per workgroup
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n = blockIdx.x * 4 + wave;
-  for (int c = threadIdx.x; c < 384; c += kThreads) dw[c] = 0.f;
+  for (int c = threadIdx.x; c < 386; c += kThreads) dw[c] = 0.f;
   __syncthreads();
   const Layer& Ly = A.L[5];
   if (n < A.B) {
@@ -472,8 +487,9 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A, int backward) {
     for (int q = 0; q < 2; ++q) {
       const int c = lane + 64 * q;
       if (c < Cc) {
-        const float m1 = Ly.st[(g * 2) * Cc + c] * A.inv_count;
-        const float var = fmaxf(Ly.st[(g * 2 + 1) * Cc + c] * A.inv_count - m1 * m1, 0.f);
+        const int ss = st_stride(A, Cc);
+        const float m1 = slot_sum(Ly.st + (g * 2) * Cc + c, ss) * A.inv_count;
+        const float var = fmaxf(slot_sum(Ly.st + (g * 2 + 1) * Cc + c, ss) * A.inv_count - m1 * m1, 0.f);
         rs[q] = rsqrtf(var + A.eps);
         mu[q] = m1;
         sc[q] = Ly.gamma[c] * rs[q];
@@ -509,9 +525,9 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A, int backward) {
       const float dl = (p - yv) * A.inv_batch;
       if (lane == 0) {
         const float loss = fmaxf(z, 0.f) - z * yv + log1pf(__expf(-fabsf(z)));  // BCE on logits
-        atomicAdd(A.loss_sum, loss);
+        atomicAdd(&red[0], loss);
         A.dlogit[n] = dl;
-        atomicAdd(A.g_dense_b, dl);
+        atomicAdd(&red[1], dl);
       }
       float b0[2] = {0.f, 0.f}, b1[2] = {0.f, 0.f};
       for (int tt = 0; tt < kL; ++tt) {
@@ -541,9 +557,14 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A, int backward) {
   if (backward) {
     __syncthreads();
     for (int c = threadIdx.x; c < Cc; c += kThreads) {
+      if (c == 0) {
+        atomicAdd(A.loss_sum, red[0]);
+        atomicAdd(A.g_dense_b, red[1]);
+      }
       atomicAdd(A.g_dense_w + c, dw[c]);
-      atomicAdd(Ly.bst + c, bsum0[c]);
-      atomicAdd(Ly.bst + Cc + c, bsum1[c]);
+      float* bst = Ly.bst + (blockIdx.x % kStatSlots) * 2 * Cc;
+      atomicAdd(bst + c, bsum0[c]);
+      atomicAdd(bst + Cc + c, bsum1[c]);
     }
   }
 }
@@ -578,8 +599,8 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
     __syncthreads();
     for (int c = threadIdx.x; c < CIN; c += kThreads) {
       gr[c] = Ly.gamma[c] * rstd[c];
-      mdy[c] = Ly.bst[c] * A.inv_count;
-      mdyx[c] = Ly.bst[CIN + c] * A.inv_count;
+      mdy[c] = slot_sum(Ly.bst + c, 2 * CIN) * A.inv_count;
+      mdyx[c] = slot_sum(Ly.bst + CIN + c, 2 * CIN) * A.inv_count;
     }
     bn_affine_to_lds(A, l - 1, 0, s_prev, t_prev, mean_prev, rstd_prev);
   }
@@ -631,8 +652,9 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
         }
       }
     }
-    atomic_channel_sums(Lp.bst, co0, b0, m == 0);
-    atomic_channel_sums(Lp.bst + COUT, co0, b1, m == 0);
+    float* bst = Lp.bst + (blockIdx.x % kStatSlots) * 2 * COUT;
+    atomic_channel_sums(bst, co0, b0, m == 0);
+    atomic_channel_sums(bst + COUT, co0, b1, m == 0);
   }
   __syncthreads();
   constexpr int CW = COUT / 8;
@@ -714,8 +736,8 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_kernel(Args A) {
     __syncthreads();
     for (int c = threadIdx.x; c < COUT; c += kThreads) {
       gr[c] = Ly.gamma[c] * rstd[c];
-      mdy[c] = Ly.bst[c] * A.inv_count;
-      mdyx[c] = Ly.bst[COUT + c] * A.inv_count;
+      mdy[c] = slot_sum(Ly.bst + c, 2 * COUT) * A.inv_count;
+      mdyx[c] = slot_sum(Ly.bst + COUT + c, 2 * COUT) * A.inv_count;
     }
     if constexpr (!FIRST) bn_affine_to_lds(A, l - 1, 0, sp, tp, nullptr, nullptr);
   }
@@ -835,15 +857,16 @@ __global__ void bn_finalize_kernel(Args A, int update_moving, int grads) {
   for (int c = threadIdx.x; c < Cc; c += blockDim.x) {
     if (update_moving) {
       for (int g = 0; g < A.groups; ++g) {  // one Keras call (= one moving update) per group
-        const float mu = Ly.st[(g * 2) * Cc + c] * A.inv_count;
-        const float var = fmaxf(Ly.st[(g * 2 + 1) * Cc + c] * A.inv_count - mu * mu, 0.f);
+        const int ss = st_stride(A, Cc);
+        const float mu = slot_sum(Ly.st + (g * 2) * Cc + c, ss) * A.inv_count;
+        const float var = fmaxf(slot_sum(Ly.st + (g * 2 + 1) * Cc + c, ss) * A.inv_count - mu * mu, 0.f);
         Ly.mmean[c] = Ly.mmean[c] * A.momentum + mu * (1.f - A.momentum);
         Ly.mvar[c] = Ly.mvar[c] * A.momentum + var * (1.f - A.momentum);
       }
     }
     if (grads) {
-      Ly.gbeta[c] = Ly.bst[c];
-      Ly.ggamma[c] = Ly.bst[Cc + c];
+      Ly.gbeta[c] = slot_sum(Ly.bst + c, 2 * Cc);
+      Ly.ggamma[c] = slot_sum(Ly.bst + Cc + c, 2 * Cc);
     }
   }
 }
@@ -907,7 +930,7 @@ hipError_t train_launch_fwd(const Args& A, int l, hipStream_t st) {
 }
 
 hipError_t train_launch_head(const Args& A, int backward, hipStream_t st) {
-  hipLaunchKernelGGL(train::head_kernel, dim3((A.B + 3) / 4), dim3(256), 384 * 4, st, A, backward);
+  hipLaunchKernelGGL(train::head_kernel, dim3((A.B + 3) / 4), dim3(256), 386 * 4, st, A, backward);
   return hipGetLastError();
 }
 

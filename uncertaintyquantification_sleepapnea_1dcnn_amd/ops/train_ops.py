@@ -30,6 +30,7 @@ from . import _ext, fused, rng
 
 SR, HALO, ROWS_PER_TILE = 64, 4, 128
 TRAIN_PASS_BASE = 1 << 30
+STAT_SLOTS = 16  # must equal kStatSlots in csrc/train_conv.hip
 
 
 def supports(spec: ModelSpec) -> bool:
@@ -84,12 +85,15 @@ class TrainWorkspace:
         # dZ_l materialised by dgrad_l for wgrad_l (block 1 has no dgrad)
         self.dZ = [torch.zeros(rows, ch[l + 1], dtype=bf, device=dev) if (with_backward and l >= 1)
                    else torch.zeros(16, dtype=bf, device=dev) for l in range(6)]
-        self.st_all = torch.zeros(sum(self.groups * 2 * ch[l + 1] for l in range(6)), device=dev)
-        self.bst_all = torch.zeros(sum(2 * ch[l + 1] for l in range(6)), device=dev)
+        # BN moment sums: STAT_SLOTS interleaved copies per layer (kernels add into slot wg % S and
+        # readers sum the slots; train_conv.hip kStatSlots) -> st[S][groups][2][C], bst[S][2][C]
+        S = STAT_SLOTS
+        self.st_all = torch.zeros(sum(S * self.groups * 2 * ch[l + 1] for l in range(6)), device=dev)
+        self.bst_all = torch.zeros(sum(S * 2 * ch[l + 1] for l in range(6)), device=dev)
         self.st, self.bst = [], []
         o1 = o2 = 0
         for l in range(6):
-            n1, n2 = self.groups * 2 * ch[l + 1], 2 * ch[l + 1]
+            n1, n2 = S * self.groups * 2 * ch[l + 1], S * 2 * ch[l + 1]
             self.st.append(self.st_all[o1: o1 + n1])
             self.bst.append(self.bst_all[o2: o2 + n2])
             o1 += n1
