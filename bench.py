@@ -60,6 +60,10 @@ def main(argv=None):
     ap.add_argument("--passes", type=int, default=50, help="MC Dropout passes T")
     ap.add_argument("--members", type=int, default=8, help="Deep Ensemble members M")
     ap.add_argument("--seed", type=int, default=2025)
+    ap.add_argument("--bn-mode", choices=["running", "batch"], default="running",
+                    help="MC-Dropout BatchNorm: running statistics (standard MC Dropout, fused kernel) or "
+                         "per-pass batch statistics over the whole window set = the reference's "
+                         "model(x, training=True) (layer-wise HIP kernels + SyncBN across ranks)")
     a = ap.parse_args(argv)
 
     info = pdist.init()
@@ -87,10 +91,24 @@ def main(argv=None):
                             for m in mem_ids])
 
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    if a.bn_mode == "batch":
+        from uncertaintyquantification_sleepapnea_1dcnn_amd.models.cnn import AlarconCNN1D
+        from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import train_ops
+
+        mcd_model = AlarconCNN1D(seed=a.seed, device=dev, params={k: v.to(dev) for k, v in synthetic_params(a.seed).items()})
+        sync = torch.distributed.all_reduce if world > 1 else None
+
+    def mcd_probs(i):
+        if a.bn_mode == "running":
+            return pinf.mcd_probs_local(blob_mcd, x_loc, a.passes, a.seed + i, start)
+        # reference semantics: every pass normalises with the batch statistics of ALL windows
+        return train_ops.forward_batch_stats(mcd_model, x_loc, a.passes, pass_base=i * a.passes, seed=a.seed,
+                                             update_moving=True, sync=sync, window_offset=start, global_n=n_glob,
+                                             max_samples=1 << 18)
 
     def step(i):
         ev[0].record()
-        pm = pinf.mcd_probs_local(blob_mcd, x_loc, a.passes, a.seed + i, start)
+        pm = mcd_probs(i)
         m_mcd = uq_ops.metrics(pm)
         s_mcd = pinf.aggregate_sums(m_mcd, y_loc)
         ev[1].record()
@@ -151,7 +169,7 @@ def main(argv=None):
                                                if member_parallel else " (window-sharded, members replicated)"),
                 "mcd_passes": a.passes,
                 "de_members": a.members,
-                "bn_mode_mcd": "running",
+                "bn_mode_mcd": a.bn_mode,
                 "windows_per_gpu_per_step": n_loc,
             },
             "extra": {
