@@ -1,0 +1,64 @@
+"""Deep-Ensemble training throughput (BASELINE.json config "DE M=8 training across 8 x MI355X").
+
+Ensemble parallel as in ``parallel/ensemble.py``: member m trains on rank m % G (one process per GPU,
+``torchrun --nproc-per-node G``), every member runs Keras-semantics steps (batch 1024, Adam,
+BCE, dropout, batch-statistics BN) on synthetic SHHS2-shaped windows through the HIP training
+kernels.  One "step" = one optimizer step of EVERY member; windows/s counts all members' samples
+over all GPUs (weak scaling in members per GPU when G | M).
+
+    python -m bench.train_bench --members 8 --steps 20             # 1 GPU, members sequential
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m bench.train_bench --members 8
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import time
+
+import torch
+
+from uncertaintyquantification_sleepapnea_1dcnn_amd.models.cnn import AlarconCNN1D
+from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel import dist as pdist
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--members", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--seed", type=int, default=2025)
+    a = ap.parse_args(argv)
+    info = pdist.init()
+    dev = info.device
+    mine = pdist.members_of_rank(a.members, info.rank, info.world)
+    models = [AlarconCNN1D(seed=a.seed + m, device=dev) for m in mine]
+    g = torch.Generator().manual_seed(a.seed + info.rank)
+    x = torch.randn(a.batch, 60, 4, generator=g).to(dev)
+    y = (torch.rand(a.batch, generator=g) < 0.3).float().to(dev)
+
+    def step():
+        for mdl in models:
+            mdl.train_step(x, y)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    pdist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    pdist.barrier()
+    dt = pdist.all_reduce_max(time.perf_counter() - t0)
+    if info.rank == 0:
+        samples = a.members * a.batch * a.steps
+        print(json.dumps({"metric": "DE training windows/s (all members, all GPUs)", "value": round(samples / dt, 1),
+                          "n_gpus": info.world, "members": a.members, "batch": a.batch, "steps": a.steps,
+                          "ms_per_step_all_members": round(dt * 1e3 / a.steps, 3), "dtype": "bf16",
+                          "data": "synthetic", "parallelism": f"ensemble-parallel over {info.world} GPU(s)"}))
+    pdist.shutdown()
+
+
+if __name__ == "__main__":
+    main()
