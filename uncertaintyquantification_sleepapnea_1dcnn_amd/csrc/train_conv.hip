@@ -23,6 +23,8 @@
 // ds_read_b128).  wgrad reduces over rows, so both operands are read with the CDNA4 transposing
 // LDS read ds_read_b64_tr_b16 from row-major tiles; each workgroup sums 16 row tiles in registers
 // and adds its output block to the fp32 gradient with global atomics.
+#include <algorithm>
+
 #include "common.h"
 
 namespace apneauq {
@@ -395,73 +397,118 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
   using CV = Conv<CIN, COUT, KS[l], T::WM, T::WN, l == 0>;
   char* act = smem;                                  // staged input, then staged output
   float* prm = reinterpret_cast<float*>(smem + kRows * kRS);  // [s 512 | t 512]
-  const int tile = blockIdx.x;
-  APNEAUQ_DASSERT(2 * tile < A.B + 1 && blockDim.x == kThreads);
-  const int row0 = kR * tile;                        // first staged row (global PL index)
-  const int smp0 = 2 * tile;
-  const int g0 = min(smp0, A.B - 1) / A.n_win, g1 = min(smp0 + 1, A.B - 1) / A.n_win;
   constexpr int IN_RS = (l == 0) ? 8 : kRS;
-  if constexpr (l == 0) {
-    staged_loop<kRows * 8 / 16>(
-        [&](int i) -> bf16x8 { return gld<bf16x8>(A.x + (long long)row0 * 4 + i * 8); },
-        [&](int i, const bf16x8& v) { reinterpret_cast<bf16x8*>(act)[i] = v; });
-  } else {
-    bn_affine_to_lds(A, l - 1, g0, prm, prm + 512, nullptr, nullptr);
-    if (g1 != g0) bn_affine_to_lds(A, l - 1, g1, prm + 256, prm + 768, nullptr, nullptr);
-    __syncthreads();
-    stage_act<l - 1, kRows, CIN / 8>(A, act, kRS, row0, 0, prm, prm + 512, g0);
-  }
-  __syncthreads();
-  f32x4 acc[CV::CT][CV::RT];
-  CV::run(A.L[l].wf, act, IN_RS, acc);
-  __syncthreads();  // all waves done reading the staged input; reuse it for the output tile
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave / T::WN, wn = wave % T::WN;
   const int m = lane & 15, h = lane >> 4;
   const Layer& Ly = A.L[l];
-#pragma unroll
-  for (int c = 0; c < CV::CT; ++c) {
-    const int co0 = (wn * CV::CT + c) * 16 + 4 * h;
-    const f32x4 bias = gld<f32x4>(Ly.bias + co0);
-    f32x4 s1[kSlots] = {}, s2[kSlots] = {};
-#pragma unroll
-    for (int r = 0; r < CV::RT; ++r) {
-      const int row = wm * CV::RT * 16 + r * 16 + m;  // 0..127 within the tile
-      const int slot = row >> 6, tt = row & 63;
-      const bool valid = tt < kL && (smp0 + slot) < A.B;
-      f32x4 v;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = valid ? fmaxf(acc[c][r][i] + bias[i], 0.f) : 0.f;
-      bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
-      *reinterpret_cast<bf16x4*>(act + row * kRS + co0 * 2) = o;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float q = (float)o[i];  // moments of the values the consumers will normalise
-        if (slot == 0) { s1[0][i] += q; s2[0][i] += q * q; }
-        else { s1[1][i] += q; s2[1][i] += q * q; }
+  // Each workgroup owns a contiguous range of tiles (so the stats group changes rarely) and sums the
+  // per-tile channel moments in LDS (lstat, 2 waves per address at most); the global atomics are
+  // issued once per run of tiles of one stats group instead of once per tile (with ~10^5 tiles per
+  // call the per-tile atomics were ~20 % of the kernel).
+  const int tiles = (A.B + 1) / 2;
+  const int tpw = (tiles + gridDim.x - 1) / gridDim.x;
+  const int t_begin = blockIdx.x * tpw;
+  const int t_end = min(tiles, t_begin + tpw);
+  float* lstat = prm + 1024;  // [2][COUT]: sum r, sum r^2 of the current group run
+  for (int c = threadIdx.x; c < 2 * COUT; c += kThreads) lstat[c] = 0.f;
+  int gcur = -1;
+  float* st = Ly.st + (blockIdx.x % kStatSlots) * st_stride(A, COUT);
+  auto flush = [&]() {  // workgroup-uniform
+    __syncthreads();
+    if (gcur >= 0) {
+      for (int c = threadIdx.x; c < COUT; c += kThreads) {
+        atomicAdd(st + (gcur * 2 + 0) * COUT + c, lstat[c]);
+        atomicAdd(st + (gcur * 2 + 1) * COUT + c, lstat[COUT + c]);
+        lstat[c] = lstat[COUT + c] = 0.f;
       }
     }
-    float* st = Ly.st + (blockIdx.x % kStatSlots) * st_stride(A, COUT);
-    if (g0 == g1) {
-      s1[0] += s1[1];
-      s2[0] += s2[1];
-      atomic_channel_sums(st + (g0 * 2 + 0) * COUT, co0, s1[0], m == 0);
-      atomic_channel_sums(st + (g0 * 2 + 1) * COUT, co0, s2[0], m == 0);
+    __syncthreads();
+  };
+  int gaff = -1;  // stats group whose BN affine (of block l-1) is in prm
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    APNEAUQ_DASSERT(2 * tile < A.B + 1 && blockDim.x == kThreads);
+    const int row0 = kR * tile;                        // first staged row (global PL index)
+    const int smp0 = 2 * tile;
+    const int g0 = min(smp0, A.B - 1) / A.n_win, g1 = min(smp0 + 1, A.B - 1) / A.n_win;
+    __syncthreads();  // previous tile's copy-out has read the LDS tile
+    if constexpr (l == 0) {
+      staged_loop<kRows * 8 / 16>(
+          [&](int i) -> bf16x8 { return gld<bf16x8>(A.x + (long long)row0 * 4 + i * 8); },
+          [&](int i, const bf16x8& v) { reinterpret_cast<bf16x8*>(act)[i] = v; });
     } else {
-      atomic_channel_sums(st + (g0 * 2 + 0) * COUT, co0, s1[0], m == 0);
-      atomic_channel_sums(st + (g0 * 2 + 1) * COUT, co0, s2[0], m == 0);
-      atomic_channel_sums(st + (g1 * 2 + 0) * COUT, co0, s1[1], m == 0);
-      atomic_channel_sums(st + (g1 * 2 + 1) * COUT, co0, s2[1], m == 0);
+      if (g0 != gaff || g1 != g0) {  // (re)load the affine of block l-1 for this tile's group(s)
+        bn_affine_to_lds(A, l - 1, g0, prm, prm + 512, nullptr, nullptr);
+        if (g1 != g0) bn_affine_to_lds(A, l - 1, g1, prm + 256, prm + 768, nullptr, nullptr);
+        gaff = (g1 == g0) ? g0 : -1;
+        __syncthreads();
+      }
+      stage_act<l - 1, kRows, CIN / 8>(A, act, kRS, row0, 0, prm, prm + 512, g0);
+    }
+    __syncthreads();
+    f32x4 acc[CV::CT][CV::RT];
+    CV::run(Ly.wf, act, IN_RS, acc);
+    __syncthreads();  // all waves done reading the staged input; reuse it for the output tile
+    // epilogue over the rows of sample slot `sel` (-1: both): bias + ReLU -> bf16 LDS tile, and the
+    // moments of the stored values into lstat (group gcur)
+    auto epi = [&](int sel) {
+#pragma unroll
+      for (int c = 0; c < CV::CT; ++c) {
+        const int co0 = (wn * CV::CT + c) * 16 + 4 * h;
+        const f32x4 bias = gld<f32x4>(Ly.bias + co0);
+        f32x4 p1 = {0.f, 0.f, 0.f, 0.f}, p2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < CV::RT; ++r) {
+          const int row = wm * CV::RT * 16 + r * 16 + m;  // 0..127 within the tile
+          const int slot = row >> 6, tt = row & 63;
+          if (sel >= 0 && slot != sel) continue;
+          const bool valid = tt < kL && (smp0 + slot) < A.B;
+          f32x4 v;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = valid ? fmaxf(acc[c][r][i] + bias[i], 0.f) : 0.f;
+          bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+          *reinterpret_cast<bf16x4*>(act + row * kRS + co0 * 2) = o;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float q = (float)o[i];  // moments of the values the consumers will normalise
+            p1[i] += q;
+            p2[i] += q * q;
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float t1 = group16_sum(p1[i]), t2 = group16_sum(p2[i]);
+          if (m == 0) {
+            atomicAdd(&lstat[co0 + i], t1);
+            atomicAdd(&lstat[COUT + co0 + i], t2);
+          }
+        }
+      }
+    };
+    if (g0 == g1) {
+      if (g0 != gcur) {
+        flush();
+        gcur = g0;
+      }
+      epi(-1);
+    } else {  // a tile straddling two stats groups (MC-Dropout pass boundary)
+      flush();
+      gcur = g0;
+      epi(0);
+      flush();
+      gcur = g1;
+      epi(1);
+    }
+    __syncthreads();
+    // coalesced copy-out of the 128 tile rows (16 B per thread-iteration)
+    constexpr int CW = COUT / 8;
+    for (int i = threadIdx.x; i < kR * CW; i += kThreads) {
+      const int r = i / CW, cw = i - r * CW;
+      *reinterpret_cast<bf16x8*>(Ly.R + (long long)(row0 + kHalo + r) * COUT + cw * 8) =
+          *reinterpret_cast<const bf16x8*>(act + r * kRS + cw * 16);
     }
   }
-  __syncthreads();
-  // coalesced copy-out of the 128 tile rows (16 B per thread-iteration)
-  constexpr int CW = COUT / 8;
-  for (int i = threadIdx.x; i < kR * CW; i += kThreads) {
-    const int r = i / CW, cw = i - r * CW;
-    *reinterpret_cast<bf16x8*>(Ly.R + (long long)(row0 + kHalo + r) * COUT + cw * 8) =
-        *reinterpret_cast<const bf16x8*>(act + r * kRS + cw * 16);
-  }
+  flush();
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -905,7 +952,7 @@ __global__ void pack_kernel(const float* __restrict__ w, int k, int cin, int cou
 // ------------------------------------------------------------------------------------------------ host
 using train::Args;
 
-constexpr int lds_fwd() { return train::kRows * train::kRS + 1024 * 4; }
+constexpr int lds_fwd() { return train::kRows * train::kRS + (1024 + 2 * 256) * 4; }  // tile + affine + lstat
 constexpr int lds_dgrad() { return train::kRows * train::kRS + 2304 * 4; }
 template <int l>
 constexpr int lds_wgrad() {
@@ -916,7 +963,8 @@ int train_args_size() { return (int)sizeof(Args); }
 int train_layer_size() { return (int)sizeof(train::Layer); }
 
 hipError_t train_launch_fwd(const Args& A, int l, hipStream_t st) {
-  const int tiles = (A.B + 1) / 2;
+  // persistent forward: at most 4 workgroups per CU-slot pair, each over a contiguous tile range
+  const int tiles = std::min((A.B + 1) / 2, 256 * 8);
   switch (l) {
     case 0: hipLaunchKernelGGL(train::fwd_kernel<0>, dim3(tiles), dim3(256), lds_fwd(), st, A); break;
     case 1: hipLaunchKernelGGL(train::fwd_kernel<1>, dim3(tiles), dim3(256), lds_fwd(), st, A); break;
