@@ -96,3 +96,31 @@ def test_hip_training_reduces_loss():
     h = m.fit(x, y.astype(np.float32), batch_size=256, epochs=3, validation_split=0.1, verbose=0)
     assert h.history["loss"][-1] < h.history["loss"][0]
     assert h.history["val_accuracy"][-1] > 0.8
+
+
+def test_graphed_training_step_matches_eager(monkeypatch):
+    """The HIP-graph replay of the training step (device-side dropout pass / Adam step counters)
+    follows the eager HIP step: same losses and (up to fp32 atomic summation order) same weights."""
+    _ext.require()
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.data.synthetic import synthetic_windows
+
+    x, y, _ = synthetic_windows(256, seed=5)
+    x = torch.as_tensor(x, dtype=torch.float32).cuda()
+    y = torch.as_tensor(y, dtype=torch.float32).cuda()
+    runs = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("APNEAUQ_TRAIN_GRAPH", mode)
+        m = AlarconCNN1D(seed=3, device="cuda")
+        losses = [float(m.train_step(x[i * 64:(i + 1) * 64], y[i * 64:(i + 1) * 64])) for i in range(4)]
+        runs[mode] = (losses, m.store.flat.clone(), m.optimizer.iterations, m._train_step_counter)
+        if mode == "1":
+            assert 64 in getattr(m, "_train_graphs", {})  # the graph path really ran
+    (le, we, ie, ce), (lg, wg, ig, cg) = runs["0"], runs["1"]
+    assert (ie, ce) == (ig, cg) == (4, 4)
+    assert abs(lg[0] - le[0]) < 1e-4 * abs(le[0])  # step 1: identical weights, masks, inputs
+    np.testing.assert_allclose(lg, le, rtol=5e-3, atol=1e-3)  # fp32 atomics: order-dependent sums
+    # Adam moves every weight by ~lr whatever its gradient size, so a near-zero gradient whose sign
+    # depends on the atomic summation order moves by +-lr: compare whole-vector norms, not max-abs
+    w0 = AlarconCNN1D(seed=3, device="cuda").store.flat
+    rel = ((wg - we).norm() / (we - w0).norm()).item()
+    assert rel < 0.2, rel

@@ -4,14 +4,21 @@
 //   m += (g - m) * (1 - b1);  v += (g^2 - v) * (1 - b2)
 //   p -= alpha * m / (sqrt(v) + eps),   alpha = lr * sqrt(1 - b2^t) / (1 - b1^t),  eps = 1e-7
 // One launch updates all 26 trainable tensors (851,457 values): 16-B vector loads/stores, grid
-// sized to the chip and grid-strided.  Optionally averages a data-parallel gradient (scale).
+// sized to the chip and grid-strided.  Optionally averages a data-parallel gradient (scale).  With
+// step_dev the bias correction is computed on the device from the iteration counter, so a captured
+// HIP graph of the training step replays correctly (ops/train_ops.py:GraphedTrainStep).
 #include "common.h"
 
 namespace apneauq {
 
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v, long long n,
-                                                    float b1, float b2, float alpha, float eps, float gscale) {
+                                                    float b1, float b2, float alpha, float eps, float gscale,
+                                                    const int* __restrict__ step_dev) {
+  if (step_dev != nullptr) {  // HIP-graph replays: alpha_t from the device iteration counter (alpha = lr)
+    const float t = (float)(*step_dev + 1);
+    alpha = alpha * sqrtf(1.f - powf(b2, t)) / (1.f - powf(b1, t));
+  }
   const long long n4 = n >> 2;
   const long long stride = (long long)gridDim.x * blockDim.x;
   const float c1 = 1.f - b1, c2 = 1.f - b2;
@@ -43,12 +50,13 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
 }
 
 hipError_t launch_adam(float* p, const float* g, float* m, float* v, long long n, float b1, float b2, float alpha,
-                       float eps, float gscale, hipStream_t stream) {
+                       float eps, float gscale, const int* step_dev, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
   long long blocks = ((n >> 2) + 255) / 256;
   if (blocks < 1) blocks = 1;
   if (blocks > 1024) blocks = 1024;
-  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p, g, m, v, n, b1, b2, alpha, eps, gscale);
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p, g, m, v, n, b1, b2, alpha, eps, gscale,
+                     step_dev);
   return hipGetLastError();
 }
 

@@ -22,7 +22,8 @@ hipError_t launch_uq_reduce(const float* probs, int t_count, int n, float* out, 
 hipError_t launch_bootstrap(const float* metrics, const int* y, const int* idx, unsigned seed, int n, int n_boot,
                             double* out, hipStream_t stream);
 hipError_t launch_adam(float* p, const float* g, float* m, float* v, long long n, float b1, float b2, float alpha,
-                       float eps, float gscale, hipStream_t stream);
+                       float eps, float gscale, const int* step_dev, hipStream_t stream);
+hipError_t train_bump_counters(int* c, int n, hipStream_t st);
 namespace train {
 struct Layer {
   const void* wf; const void* wd; const float* bias; const float* gamma; const float* beta;
@@ -34,7 +35,7 @@ struct Args {
   const void* x; const float* y; const float* dense_w; const float* dense_b; float* g_dense_w; float* g_dense_b;
   float* logits; float* dlogit; float* loss_sum;
   int B; int n_win; int groups; unsigned pass_base; unsigned window_offset; unsigned long long seed; int dropout;
-  float inv_count; float inv_batch; float eps; float momentum;
+  float inv_count; float inv_batch; float eps; float momentum; const unsigned* pass_dev;
 };
 }  // namespace train
 int train_args_size();
@@ -126,20 +127,34 @@ at::Tensor bootstrap(const at::Tensor& metrics, const at::Tensor& y, const c10::
 }
 
 void adam_step(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v, double b1, double b2, double alpha,
-               double eps, double gscale) {
+               double eps, double gscale, const c10::optional<at::Tensor>& counters) {
   TORCH_CHECK(p.is_cuda() && g.is_cuda() && m.is_cuda() && v.is_cuda(), "adam_step: GPU tensors required");
   for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&p, &g, &m, &v})
     TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == p.numel() &&
                     reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
                 "adam_step: contiguous, 16-B aligned fp32 tensors of equal size required");
   const at::DeviceGuard guard(p.device());
+  const int* step_dev = nullptr;
+  if (counters.has_value()) {  // [pass offset, iterations]: alpha = lr, corrected on the device
+    TORCH_CHECK(counters->is_cuda() && counters->scalar_type() == at::kInt && counters->numel() >= 2,
+                "adam_step: counters must be an int32 GPU tensor [pass, iterations]");
+    step_dev = counters->data_ptr<int>() + 1;
+  }
   check(apneauq::launch_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
-                             p.numel(), (float)b1, (float)b2, (float)alpha, (float)eps, (float)gscale, cur_stream()),
+                             p.numel(), (float)b1, (float)b2, (float)alpha, (float)eps, (float)gscale, step_dev,
+                             cur_stream()),
         "adam_step");
 }
 
+void bump_counters(at::Tensor& counters) {
+  TORCH_CHECK(counters.is_cuda() && counters.scalar_type() == at::kInt && counters.numel() <= 64,
+              "bump_counters: int32 GPU tensor of <= 64 counters");
+  const at::DeviceGuard guard(counters.device());
+  check(apneauq::train_bump_counters(counters.data_ptr<int>(), (int)counters.numel(), cur_stream()), "bump_counters");
+}
+
 // ctx: int64 CPU tensor of device pointers / scalars built once per workspace (ops/train_ops.py)
-constexpr int kCtxLayer = 18, kCtxLen = 6 * kCtxLayer + 20;
+constexpr int kCtxLayer = 18, kCtxLen = 6 * kCtxLayer + 21;
 
 float bits_to_float(int64_t v) {
   uint32_t u = static_cast<uint32_t>(v);
@@ -199,6 +214,7 @@ apneauq::train::Args args_from_ctx(const at::Tensor& ctx, int64_t pass_base) {
   A.inv_batch = bits_to_float(g[17]);
   A.eps = bits_to_float(g[18]);
   A.momentum = bits_to_float(g[19]);
+  A.pass_dev = reinterpret_cast<const unsigned*>(g[20]);
   return A;
 }
 
@@ -254,7 +270,8 @@ TORCH_LIBRARY(apneauq, m) {
   m.def("train_call(Tensor ctx, int op, int layer, int flag, int pass_base, int device) -> ()", &train_call);
   m.def("train_pack(Tensor w, int k, int cin, int cout, Tensor(a!) fwd, Tensor(b!) dgr) -> ()");
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, float b1, float b2, float alpha, float eps, "
-        "float gscale) -> ()");
+        "float gscale, Tensor? counters=None) -> ()");
+  m.def("bump_counters(Tensor(a!) counters) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
@@ -262,5 +279,6 @@ TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
   m.impl("uq_reduce", &uq_reduce);
   m.impl("bootstrap", &bootstrap);
   m.impl("adam_step", &adam_step);
+  m.impl("bump_counters", &bump_counters);
   m.impl("train_pack", &train_pack);
 }

@@ -81,6 +81,7 @@ struct Args {
   float inv_batch;     // 1 / global batch size — BCE mean
   float eps;
   float momentum;
+  const unsigned* pass_dev;  // optional device step counter added to pass_base (HIP-graph replays)
 };
 
 template <typename T>
@@ -125,7 +126,8 @@ __device__ __forceinline__ void bn_affine_to_lds(const Args& A, int l, int g, fl
 __device__ __forceinline__ unsigned layer_sample_key(const Args& A, int l, int sample) {
   const unsigned g = (unsigned)(sample / A.n_win);
   const unsigned w = (unsigned)(sample - (int)g * A.n_win);
-  return sample_key(stream_key(A.seed, l, A.pass_base + g), A.window_offset + w);
+  const unsigned pb = A.pass_base + (A.pass_dev != nullptr ? *A.pass_dev : 0u);
+  return sample_key(stream_key(A.seed, l, pb + g), A.window_offset + w);
 }
 
 // Staging loops issue a batch of up to kStageU global loads per thread before the first LDS
@@ -517,91 +519,133 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
 // each lane owning channels (lane, lane + 64).
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kThreads) void head_kernel(Args A, int backward) {
-  constexpr int Cc = C[6];
-  float* dw = reinterpret_cast<float*>(smem);  // [dW 128 | dsum 128 | dxsum 128 | loss, db]
-  float* bsum0 = dw + 128;
-  float* bsum1 = dw + 256;
-  float* red = dw + 384;  // per-workgroup loss / dense-bias sums: one global atomic per workgroup
+  // One sample per wave.  Lane (cw, ph) = (lane % 12, lane / 12), lanes 0..59: channels
+  // [8cw, 8cw+8) of rows ph, ph+5, ..., ph+55 — twelve 16-B loads per lane, all in flight at once
+  // (the previous per-channel/per-row scalar loop was load-latency bound: ~50 us at any batch size).
+  constexpr int Cc = C[6], NCW = Cc / 8, NPH = 5, NJ = kL / NPH;
+  static_assert(NCW * NPH <= 64 && NJ * NPH == kL, "head lane map");
+  float* prm = reinterpret_cast<float*>(smem);  // [mu | rs | sc | sh | w] x 96, then sums
+  float* pmu = prm, *prs = prm + Cc, *psc = prm + 2 * Cc, *psh = prm + 3 * Cc, *pw = prm + 4 * Cc;
+  float* dw = prm + 5 * Cc;     // dense-weight gradient sums
+  float* bsum0 = dw + Cc;       // sum dY, sum dY * xhat (backward BN sums of block 6)
+  float* bsum1 = bsum0 + Cc;
+  float* red = bsum1 + Cc;      // per-workgroup loss / dense-bias sums: one global atomic per workgroup
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n = blockIdx.x * 4 + wave;
-  for (int c = threadIdx.x; c < 386; c += kThreads) dw[c] = 0.f;
-  __syncthreads();
   const Layer& Ly = A.L[5];
-  if (n < A.B) {
+  const int g_first = min(blockIdx.x * 4, A.B - 1) / A.n_win;
+  const int g_last = min(blockIdx.x * 4 + 3, A.B - 1) / A.n_win;
+  for (int c = threadIdx.x; c < 3 * Cc + 2; c += kThreads) dw[c] = 0.f;
+  auto params = [&](int g) {
+    for (int c = threadIdx.x; c < Cc; c += kThreads) {
+      const int ss = st_stride(A, Cc);
+      const float m1 = slot_sum(Ly.st + (g * 2) * Cc + c, ss) * A.inv_count;
+      const float var = fmaxf(slot_sum(Ly.st + (g * 2 + 1) * Cc + c, ss) * A.inv_count - m1 * m1, 0.f);
+      const float r = rsqrtf(var + A.eps);
+      pmu[c] = m1;
+      prs[c] = r;
+      psc[c] = Ly.gamma[c] * r;
+      psh[c] = Ly.beta[c] - m1 * Ly.gamma[c] * r;
+      pw[c] = A.dense_w[c];
+    }
+  };
+  params(g_first);
+  __syncthreads();
+  // (a workgroup whose 4 samples span two stats groups — an MC-Dropout pass boundary with n_win
+  //  not a multiple of 4 — recomputes its per-lane parameters from the global sums directly)
+  const bool mixed = g_first != g_last;
+  const int cw = lane % NCW, ph = lane / NCW;
+  const bool active = n < A.B && lane < NCW * NPH;
+  const int c0 = cw * 8;
+  float mu[8], rs[8], sc[8], sh[8], w[8];
+  if (active) {
     const int g = n / A.n_win;
-    float sc[2] = {0.f, 0.f}, sh[2] = {0.f, 0.f}, mu[2] = {0.f, 0.f}, rs[2] = {0.f, 0.f}, w[2] = {0.f, 0.f};
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int c = lane + 64 * q;
-      if (c < Cc) {
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      if (mixed && g != g_first) {
         const int ss = st_stride(A, Cc);
         const float m1 = slot_sum(Ly.st + (g * 2) * Cc + c, ss) * A.inv_count;
         const float var = fmaxf(slot_sum(Ly.st + (g * 2 + 1) * Cc + c, ss) * A.inv_count - m1 * m1, 0.f);
-        rs[q] = rsqrtf(var + A.eps);
-        mu[q] = m1;
-        sc[q] = Ly.gamma[c] * rs[q];
-        sh[q] = Ly.beta[c] - m1 * sc[q];
-        w[q] = A.dense_w[c];
+        rs[j] = rsqrtf(var + A.eps);
+        mu[j] = m1;
+        sc[j] = Ly.gamma[c] * rs[j];
+        sh[j] = Ly.beta[c] - m1 * sc[j];
+      } else {
+        mu[j] = pmu[c];
+        rs[j] = prs[c];
+        sc[j] = psc[c];
+        sh[j] = psh[c];
       }
+      w[j] = pw[c];
     }
-    const unsigned key = A.dropout ? layer_sample_key(A, 5, n) : 0u;
-    const __bf16* base = Ly.R + (long long)(kHalo + n * kSR) * Cc;
-    auto keep = [&](int tt, int c) -> bool {
-      const unsigned hh = dropout_bits2(key, tt, c & ~1);
-      return ((c & 1) ? (hh >> 16) : (hh & 0xFFFFu)) >= Ly.thr;
-    };
-    float gap[2] = {0.f, 0.f};
-    for (int tt = 0; tt < kL; ++tt) {
+  }
+  bf16x8 v[NJ];
+  unsigned keep[NJ];  // bit j: channel c0 + j kept by dropout at row ph + 5 k
+  float gap[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (active) {
+    const __bf16* base = Ly.R + (long long)(kHalo + n * kSR) * Cc + c0;
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int c = lane + 64 * q;
-        if (c < Cc) {
-          float a = (float)base[tt * Cc + c] * sc[q] + sh[q];
-          if (A.dropout) a = keep(tt, c) ? a * Ly.dsc : 0.f;
-          gap[q] += a;
+    for (int k = 0; k < NJ; ++k) v[k] = gld<bf16x8>(base + (long long)(ph + NPH * k) * Cc);
+    const unsigned key = A.dropout ? layer_sample_key(A, 5, n) : 0u;
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) {
+      const int tt = ph + NPH * k;
+      unsigned kb = 0xFFu;
+      if (A.dropout) {
+        kb = 0u;
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+          const unsigned hh = dropout_bits2(key, tt, c0 + j);
+          kb |= ((hh & 0xFFFFu) >= Ly.thr ? 1u : 0u) << j;
+          kb |= ((hh >> 16) >= Ly.thr ? 1u : 0u) << (j + 1);
         }
       }
+      keep[k] = kb;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float a = (float)v[k][j] * sc[j] + sh[j];
+        gap[j] += ((kb >> j) & 1u) ? (A.dropout ? a * Ly.dsc : a) : 0.f;
+      }
     }
-    gap[0] *= (1.0f / kL);
-    gap[1] *= (1.0f / kL);
-    const float z = wave_sum(gap[0] * w[0] + gap[1] * w[1]) + A.dense_b[0];
-    if (lane == 0) A.logits[n] = z;
-    if (backward) {
-      const float p = 1.0f / (1.0f + __expf(-z));
+  }
+  float part = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) part += gap[j] * w[j];
+  const float z = wave_sum(active ? part : 0.f) * (1.0f / kL) + A.dense_b[0];
+  if (n < A.B && lane == 0) A.logits[n] = z;
+  if (backward) {
+    if (n < A.B) {
+      const float pz = 1.0f / (1.0f + __expf(-z));
       const float yv = A.y[n];
-      const float dl = (p - yv) * A.inv_batch;
+      const float dl = (pz - yv) * A.inv_batch;
       if (lane == 0) {
         const float loss = fmaxf(z, 0.f) - z * yv + log1pf(__expf(-fabsf(z)));  // BCE on logits
         atomicAdd(&red[0], loss);
         A.dlogit[n] = dl;
         atomicAdd(&red[1], dl);
       }
-      float b0[2] = {0.f, 0.f}, b1[2] = {0.f, 0.f};
-      for (int tt = 0; tt < kL; ++tt) {
+      if (active) {
+        float b0[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, b1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const int c = lane + 64 * q;
-          if (c < Cc) {
-            float dy = dl * w[q] * (1.0f / kL);
-            if (A.dropout) dy = keep(tt, c) ? dy * Ly.dsc : 0.f;
-            const float xh = ((float)base[tt * Cc + c] - mu[q]) * rs[q];
-            b0[q] += dy;
-            b1[q] += dy * xh;
+        for (int k = 0; k < NJ; ++k) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float dy = dl * w[j] * (1.0f / kL);
+            if (A.dropout) dy = ((keep[k] >> j) & 1u) ? dy * Ly.dsc : 0.f;
+            const float xh = ((float)v[k][j] - mu[j]) * rs[j];
+            b0[j] += dy;
+            b1[j] += dy * xh;
           }
         }
-      }
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int c = lane + 64 * q;
-        if (c < Cc) {
-          atomicAdd(&dw[c], dl * gap[q]);
-          atomicAdd(&bsum0[c], b0[q]);
-          atomicAdd(&bsum1[c], b1[q]);
+        for (int j = 0; j < 8; ++j) {
+          atomicAdd(&dw[c0 + j], dl * gap[j] * (1.0f / kL));
+          atomicAdd(&bsum0[c0 + j], b0[j]);
+          atomicAdd(&bsum1[c0 + j], b1[j]);
         }
       }
     }
-  }
-  if (backward) {
     __syncthreads();
     for (int c = threadIdx.x; c < Cc; c += kThreads) {
       if (c == 0) {
@@ -810,8 +854,12 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_kernel(Args A) {
 #pragma unroll
   for (int a = 0; a < NCO; ++a) accb[a] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int ntiles = (A.B + 1) / 2;
-  for (int it = 0; it < W::RTILES; ++it) {
-    const int tile = rg * W::RTILES + it;
+  // row tiles per workgroup: RTILES at large batches, fewer when the batch is small (the launcher
+  // sizes the grid for >= ~512 workgroups)
+  const int rgs = gridDim.x / (nci_blk * nco_blk);
+  const int rt = (ntiles + rgs - 1) / rgs;
+  for (int it = 0; it < rt; ++it) {
+    const int tile = rg * rt + it;
     if (tile >= ntiles) break;
     const int row0 = kR * tile;
     __syncthreads();
@@ -962,6 +1010,15 @@ constexpr int lds_wgrad() {
 int train_args_size() { return (int)sizeof(Args); }
 int train_layer_size() { return (int)sizeof(train::Layer); }
 
+__global__ void bump_counters_kernel(int* c, int n) {
+  if (threadIdx.x < n) c[threadIdx.x] += 1;
+}
+
+hipError_t train_bump_counters(int* c, int n, hipStream_t st) {
+  hipLaunchKernelGGL(bump_counters_kernel, dim3(1), dim3(64), 0, st, c, n);
+  return hipGetLastError();
+}
+
 hipError_t train_launch_fwd(const Args& A, int l, hipStream_t st) {
   // persistent forward: at most 4 workgroups per CU-slot pair, each over a contiguous tile range
   const int tiles = std::min((A.B + 1) / 2, 256 * 8);
@@ -978,7 +1035,7 @@ hipError_t train_launch_fwd(const Args& A, int l, hipStream_t st) {
 }
 
 hipError_t train_launch_head(const Args& A, int backward, hipStream_t st) {
-  hipLaunchKernelGGL(train::head_kernel, dim3((A.B + 3) / 4), dim3(256), 386 * 4, st, A, backward);
+  hipLaunchKernelGGL(train::head_kernel, dim3((A.B + 3) / 4), dim3(256), (8 * train::C[6] + 2) * 4, st, A, backward);
   return hipGetLastError();
 }
 
@@ -1001,7 +1058,10 @@ static void wg_launch(const Args& A, hipStream_t st) {
   const int nci = (l == 0) ? 1 : train::C[l] / W::CIB;
   const int nco = train::C[l + 1] / W::COB;
   const int tiles = (A.B + 1) / 2;
-  const int rgs = (tiles + train::WgCfg<l>::RTILES - 1) / train::WgCfg<l>::RTILES;
+  // RTILES row tiles per workgroup, but never fewer than ~512 workgroups while tiles remain
+  const int nblk = nci * nco;
+  const int rt = std::max(1, std::min(train::WgCfg<l>::RTILES, (tiles * nblk + 511) / 512));
+  const int rgs = (tiles + rt - 1) / rt;
   hipLaunchKernelGGL(train::wgrad_kernel<l>, dim3(nci * nco * rgs), dim3(256), lds_wgrad<l>(), st, A);
 }
 

@@ -117,10 +117,13 @@ class TrainWorkspace:
         self.ch = ch
         self._ctx_key = None
         self.ctx = None
+        # [dropout pass offset, Adam iterations] on the device: read by the kernels when the step
+        # is replayed from a captured HIP graph (see GraphedTrainStep)
+        self.counters = torch.zeros(2, dtype=torch.int32, device=dev)
 
     def build_ctx(self, n: int, n_win: int, groups: int, window_offset: int, seed: int, dropout: bool,
-                  inv_count: float, inv_batch: float):
-        key = (n, n_win, groups, window_offset, seed, dropout, inv_count, inv_batch)
+                  inv_count: float, inv_batch: float, device_counters: bool = False):
+        key = (n, n_win, groups, window_offset, seed, dropout, inv_count, inv_batch, device_counters)
         if key == self._ctx_key:
             return self.ctx
         spec, v, g = self.model.spec, self.model.store.views, self.gviews
@@ -140,7 +143,8 @@ class TrainWorkspace:
                  g["output_layer/bias"].data_ptr(), self.logits.data_ptr(), self.dlogit.data_ptr(),
                  self.loss.data_ptr(), n, n_win, groups, TRAIN_PASS_BASE, window_offset,
                  int(seed) & ((1 << 63) - 1), int(bool(dropout)), _fbits(inv_count), _fbits(inv_batch),
-                 _fbits(spec.bn_epsilon), _fbits(spec.bn_momentum)]
+                 _fbits(spec.bn_epsilon), _fbits(spec.bn_momentum),
+                 self.counters.data_ptr() if device_counters else 0]
         self.ctx = torch.tensor(vals, dtype=torch.int64)
         self._ctx_key = key
         return self.ctx
@@ -206,6 +210,92 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, syn
         scale = grad_allreduce(ws.grad)
     model.optimizer.step(model.store.flat, ws.grad, grad_scale=scale)
     return ws.loss.double().sum(), torch.sigmoid(ws.logits[:n])
+
+
+class GraphedTrainStep:
+    """The whole HIP training step of one batch size captured once as a HIP graph and replayed.
+
+    At batch 128-256 the eager step is bound by ~25 kernel launches + ~20 small tensor ops issued
+    from Python (~0.8 ms/step whatever the batch); a replay is one graph launch.  The dropout pass id
+    and Adam's bias-correction step come from the workspace's device counters, bumped by the last
+    node of the graph, so replays are exactly the steps the eager path would run (the host mirrors
+    ``model._train_step_counter`` / ``optimizer.iterations`` advance in lockstep and the device
+    counters are re-synced if they were changed outside, e.g. by an eager step or a restore).
+    Single device only (a data-parallel step all-reduces through torch.distributed).
+    """
+
+    def __init__(self, model, batch: int):
+        self.model = model
+        self.batch = int(batch)
+        dev = model.store.device
+        self.ws = TrainWorkspace(model, self.batch)
+        self.x_in = torch.zeros(self.batch, 60, self.ws.ch[0], device=dev)
+        self.y_in = torch.zeros(self.batch, device=dev)
+        n = self.batch
+        self.ctx = self.ws.build_ctx(n, n, 1, 0, model.seed, True, 1.0 / (n * 60), 1.0 / n, device_counters=True)
+        model.optimizer._ensure(model.store.flat)
+        self._sync_counters()
+        self.graph = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(self.graph, stream=side):
+                self.loss_out, self.probs_out = self._body()
+        torch.cuda.current_stream(dev).wait_stream(side)
+
+    def _state(self):
+        return (int(self.model._train_step_counter), int(self.model.optimizer.iterations))
+
+    def _sync_counters(self):
+        st = self._state()
+        self.ws.counters.copy_(torch.tensor(st, dtype=torch.int32))
+        self._dev_state = st
+
+    def _body(self):
+        ws, n, o = self.ws, self.batch, _ext.ops()
+        dev = self.x_in.device.index or 0
+        ws.x[HALO: HALO + SR * n].view(n, SR, ws.ch[0])[:, :60].copy_(self.x_in)
+        ws.y[:n].copy_(self.y_in)
+        ws.st_all.zero_()
+        ws.bst_all.zero_()
+        ws.grad.zero_()
+        ws.loss.zero_()
+        ws.pack()
+        for l in range(6):
+            _call(self.ctx, 0, l, 0, TRAIN_PASS_BASE, dev)
+        _call(self.ctx, 1, 0, 1, TRAIN_PASS_BASE, dev)
+        for l in range(5, 0, -1):
+            _call(self.ctx, 2, l, 0, TRAIN_PASS_BASE, dev)
+            _call(self.ctx, 3, l, 0, TRAIN_PASS_BASE, dev)
+        _call(self.ctx, 3, 0, 0, TRAIN_PASS_BASE, dev)
+        _call(self.ctx, 4, 1, 1, TRAIN_PASS_BASE, dev)
+        opt = self.model.optimizer
+        o.adam_step(self.model.store.flat, ws.grad, opt.m, opt.v, opt.beta_1, opt.beta_2, opt.learning_rate,
+                    opt.epsilon, 1.0, ws.counters)
+        o.bump_counters(ws.counters)
+        return ws.loss.double().sum(), torch.sigmoid(ws.logits[:n])
+
+    def __call__(self, x: torch.Tensor, y: torch.Tensor):
+        """One step; returns (loss_sum, probs) views of static buffers (valid until the next replay)."""
+        if self._state() != self._dev_state:
+            self._sync_counters()
+        self.x_in.copy_(x)
+        self.y_in.copy_(y.reshape(-1))
+        self.graph.replay()
+        self.model.optimizer.iterations += 1
+        self._dev_state = (self._dev_state[0] + 1, self._dev_state[1] + 1)
+        return self.loss_out, self.probs_out
+
+
+def graph_train_step(model, x: torch.Tensor, y: torch.Tensor):
+    """Replay (capturing on first use) the graphed step for this batch size."""
+    g = getattr(model, "_train_graphs", None)
+    if g is None:
+        g = model._train_graphs = {}
+    n = int(x.shape[0])
+    if n not in g:
+        g[n] = GraphedTrainStep(model, n)
+    return g[n](x, y)
 
 
 @torch.no_grad()

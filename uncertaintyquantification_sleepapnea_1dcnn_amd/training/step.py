@@ -30,6 +30,11 @@ def _backend(model) -> str:
     return "torch"
 
 
+def _use_graphs() -> bool:
+    """HIP-graph replay of the single-device HIP step (``APNEAUQ_TRAIN_GRAPH=0`` disables)."""
+    return os.environ.get("APNEAUQ_TRAIN_GRAPH", "1") != "0"
+
+
 def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, dp_step=None):
     """``dp_step = (global_batch, offset)`` when the model trains data-parallel (``model.dp``)."""
     backend = _backend(model)
@@ -47,6 +52,8 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, dp_
 
             return train_ops.train_step(model, x, y, grad_allreduce=_gar, sync=dp.all_reduce_, global_batch=gn,
                                         window_offset=off)
+        if grad_allreduce is None and _use_graphs():
+            return train_ops.graph_train_step(model, x, y)
         return train_ops.train_step(model, x, y, grad_allreduce=grad_allreduce)
     store = model.store
     flat = store.flat.detach().requires_grad_(True)
