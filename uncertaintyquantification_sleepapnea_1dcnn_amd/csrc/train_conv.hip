@@ -223,7 +223,7 @@ __device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, i
 template <int l, int NR, int NCW>
 __device__ __forceinline__ void stage_dz(const Args& A, char* lds, int ldsrs, int row0, int c0,
                                          const float* gam_rstd, const float* mean, const float* rstd, const float* mdy,
-                                         const float* mdyx, float* colsum = nullptr, __bf16* gout = nullptr,
+                                         const float* mdyx, __bf16* gout = nullptr,
                                          int own_lo = 0, int own_hi = 0) {
   constexpr int Cc = C[l + 1];
   const Layer& Ly = A.L[l];
@@ -275,10 +275,6 @@ __device__ __forceinline__ void stage_dz(const Args& A, char* lds, int ldsrs, in
             const float dz = gam_rstd[c + j] * (dy[j] - mdy[c + j] - xh * mdyx[c + j]);
             o[j] = (__bf16)(rr > 0.f ? dz : 0.f);
           }
-          if (colsum) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) atomicAdd(colsum + (c - c0) + j, (float)o[j]);
-          }
         }
         *reinterpret_cast<bf16x8*>(lds + r * ldsrs + cw * 16) = o;
         if (gout != nullptr && r >= own_lo && r < own_hi)
@@ -286,9 +282,9 @@ __device__ __forceinline__ void stage_dz(const Args& A, char* lds, int ldsrs, in
       });
 }
 
-// Plain copy of materialised dZ rows (see dgrad) into LDS, with the optional bias-gradient sums.
+// Plain copy of materialised dZ rows (see dgrad) into LDS.
 template <int l, int NR, int NCW, int UMAX>
-__device__ __forceinline__ void stage_dz_copy(const Args& A, char* lds, int ldsrs, int row0, int c0, float* colsum) {
+__device__ __forceinline__ void stage_dz_copy(const Args& A, char* lds, int ldsrs, int row0, int c0) {
   constexpr int Cc = C[l + 1];
   const Layer& Ly = A.L[l];
   staged_loop<NR * NCW, UMAX>(
@@ -299,10 +295,6 @@ __device__ __forceinline__ void stage_dz_copy(const Args& A, char* lds, int ldsr
       [&](int i, const bf16x8& o) {
         const int r = i / NCW, cw = i - r * NCW;
         *reinterpret_cast<bf16x8*>(lds + r * ldsrs + cw * 16) = o;
-        if (colsum) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) atomicAdd(colsum + cw * 8 + j, (float)o[j]);
-        }
       });
 }
 
@@ -696,8 +688,7 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
     bn_affine_to_lds(A, l - 1, 0, s_prev, t_prev, mean_prev, rstd_prev);
   }
   __syncthreads();
-  stage_dz<l, kRows, CIN / 8>(A, act, kRS, row0, 0, gr, mean, rstd, mdy, mdyx, nullptr, A.L[l].dZ, kHalo,
-                              kHalo + kR);
+  stage_dz<l, kRows, CIN / 8>(A, act, kRS, row0, 0, gr, mean, rstd, mdy, mdyx, A.L[l].dZ, kHalo, kHalo + kR);
   __syncthreads();
   f32x4 acc[CV::CT][CV::RT];
   CV::run(A.L[l].wd, act, kRS, acc);
@@ -864,10 +855,9 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_kernel(Args A) {
     const int row0 = kR * tile;
     __syncthreads();
     if constexpr (FIRST)  // no dgrad for block 1: dZ_1 is recomputed here (a single ci block)
-      stage_dz<l, kR, W::COB / 8>(A, dz_lds, DZRS, row0 + kHalo, co0, gr, mean, rstd, mdy, mdyx,
-                                  nullptr);
+      stage_dz<l, kR, W::COB / 8>(A, dz_lds, DZRS, row0 + kHalo, co0, gr, mean, rstd, mdy, mdyx);
     else
-      stage_dz_copy<l, kR, W::COB / 8, 4>(A, dz_lds, DZRS, row0 + kHalo, co0, nullptr);
+      stage_dz_copy<l, kR, W::COB / 8, 4>(A, dz_lds, DZRS, row0 + kHalo, co0);
     if constexpr (FIRST) {
       // im2col of the raw input: col kk = tap*4 + ci (kk < 28), rows = tile rows
       for (int i = threadIdx.x; i < kR * 32; i += kThreads) {
