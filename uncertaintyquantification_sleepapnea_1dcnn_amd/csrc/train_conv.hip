@@ -755,12 +755,14 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
 template <int l> struct WgCfg;
 // CI_BLK CO_BLK WCO WCI, RTILES = 128-row tiles summed in registers per workgroup (sized so a
 // batch of 1024 gives >= 256 workgroups without multiplying the output atomics needlessly)
-template <> struct WgCfg<0> { static constexpr int CIB = 32, COB = 128, WCO = 4, WCI = 1, RTILES = 2; };  // im2col kk=32
-template <> struct WgCfg<1> { static constexpr int CIB = 32, COB = 192, WCO = 2, WCI = 2, RTILES = 8; };
-template <> struct WgCfg<2> { static constexpr int CIB = 32, COB = 224, WCO = 2, WCI = 2, RTILES = 8; };
-template <> struct WgCfg<3> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16; };
-template <> struct WgCfg<4> { static constexpr int CIB = 16, COB = 128, WCO = 4, WCI = 1, RTILES = 16; };
-template <> struct WgCfg<5> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16; };
+// MINWG: the launcher lowers the row tiles per workgroup until at least this many workgroups
+// exist (measured at batch 1024: blocks 2-3 prefer fewer, longer workgroups, blocks 4-6 more)
+template <> struct WgCfg<0> { static constexpr int CIB = 32, COB = 128, WCO = 4, WCI = 1, RTILES = 2, MINWG = 512; };  // im2col kk=32
+template <> struct WgCfg<1> { static constexpr int CIB = 32, COB = 192, WCO = 2, WCI = 2, RTILES = 8, MINWG = 256; };
+template <> struct WgCfg<2> { static constexpr int CIB = 32, COB = 224, WCO = 2, WCI = 2, RTILES = 8, MINWG = 256; };
+template <> struct WgCfg<3> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = 512; };
+template <> struct WgCfg<4> { static constexpr int CIB = 16, COB = 128, WCO = 4, WCI = 1, RTILES = 16, MINWG = 512; };
+template <> struct WgCfg<5> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = 512; };
 
 __device__ __forceinline__ bf16x8 tr_frag(const char* lds, int ldsrs, int row_base, int col0) {
   // fragment for a 16x16x32 operand whose K index is the LDS row: lane (m, h) gets rows
@@ -1048,9 +1050,9 @@ static void wg_launch(const Args& A, hipStream_t st) {
   const int nci = (l == 0) ? 1 : train::C[l] / W::CIB;
   const int nco = train::C[l + 1] / W::COB;
   const int tiles = (A.B + 1) / 2;
-  // RTILES row tiles per workgroup, but never fewer than ~512 workgroups while tiles remain
+  // RTILES row tiles per workgroup, but never fewer than ~MINWG workgroups while tiles remain
   const int nblk = nci * nco;
-  const int rt = std::max(1, std::min(train::WgCfg<l>::RTILES, (tiles * nblk + 511) / 512));
+  const int rt = std::max(1, std::min(W::RTILES, (tiles * nblk + W::MINWG - 1) / W::MINWG));
   const int rgs = (tiles + rt - 1) / rt;
   hipLaunchKernelGGL(train::wgrad_kernel<l>, dim3(nci * nco * rgs), dim3(256), lds_wgrad<l>(), st, A);
 }
