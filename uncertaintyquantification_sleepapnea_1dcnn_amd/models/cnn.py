@@ -9,8 +9,9 @@ Execution backends (MI355X-first):
 
 * inference (``training=False`` / ``predict``) on the GPU runs the fused whole-network HIP
   kernel (``ops/fused.py``); the packed weight blob is cached and invalidated on any update;
-* training steps run the layer-wise path (autograd over the fp32 reference ops today, HIP
-  conv kernels where available) with the Keras BatchNorm/Dropout/Adam semantics;
+* training steps run the layer-wise HIP kernels (``ops/train_ops.py``; replayed from a captured
+  HIP graph on a single device) with the Keras BatchNorm/Dropout/Adam semantics, or fp32 autograd
+  over the reference ops where no kernel exists (CPU, non-default architectures);
 * ``model(x, training=True)`` reproduces Keras exactly: dropout on, BatchNorm on the statistics of
   the batch passed in, moving averages updated as a side effect (the reference's MC Dropout
   quirk).
@@ -108,6 +109,12 @@ class AlarconCNN1D:
         self.device = torch.device(device)
         self.store = self.store.to(self.device)
         self._blob = None
+        for attr in ("_train_ws", "_mcd_ws", "_train_graphs"):  # device workspaces / captured graphs
+            if hasattr(self, attr):
+                delattr(self, attr)
+        if self.optimizer.m is not None:
+            self.optimizer.m = self.optimizer.m.to(self.device)
+            self.optimizer.v = self.optimizer.v.to(self.device)
         return self
 
     # ------------------------------------------------------------------ inference

@@ -234,6 +234,9 @@ class GraphedTrainStep:
         n = self.batch
         self.ctx = self.ws.build_ctx(n, n, 1, 0, model.seed, True, 1.0 / (n * 60), 1.0 / n, device_counters=True)
         model.optimizer._ensure(model.store.flat)
+        # the graph bakes these buffers' addresses: a replay is only valid while they are the same
+        # tensor objects (a restored optimizer state or a moved model triggers a re-capture)
+        self.bound = (model.store.flat, model.optimizer.m, model.optimizer.v)
         self._sync_counters()
         self.graph = torch.cuda.CUDAGraph()
         side = torch.cuda.Stream(device=dev)
@@ -293,9 +296,11 @@ def graph_train_step(model, x: torch.Tensor, y: torch.Tensor):
     if g is None:
         g = model._train_graphs = {}
     n = int(x.shape[0])
-    if n not in g:
-        g[n] = GraphedTrainStep(model, n)
-    return g[n](x, y)
+    opt = model.optimizer
+    cur = g.get(n)
+    if cur is None or any(a is not b for a, b in zip(cur.bound, (model.store.flat, opt.m, opt.v))):
+        g[n] = cur = GraphedTrainStep(model, n)
+    return cur(x, y)
 
 
 @torch.no_grad()
