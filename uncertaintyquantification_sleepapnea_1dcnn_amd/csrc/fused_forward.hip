@@ -36,7 +36,8 @@ constexpr int kRS = 256 * 2 + 32;              // activation row stride in bytes
 constexpr int kX0RS = kCin * 2;                // input row stride in bytes
 constexpr int kActBytes = kRows * kRS;
 constexpr int kX0Bytes = kRows * kX0RS;
-constexpr int kHeadBytes = 64;
+constexpr int kHeadOut = 2 * 6;                // head partials: [channel tile][slot] (block 6: 6 tiles)
+constexpr int kHeadBytes = (kHeadOut + 2) * 4 + 8;
 constexpr int kLdsBytes = kActBytes + kX0Bytes + kHeadBytes;
 constexpr int kThreads = 256;
 static_assert(kActBytes % 16 == 0 && kX0Bytes % 16 == 0, "LDS carve must stay 16-B aligned");
@@ -126,13 +127,22 @@ __device__ unsigned g_stamp_cu[kStampWG];
 #endif
 
 // One Conv1D(relu) -> BN -> Dropout block as an LDS-resident implicit GEMM.
-//   WM x WN waves tile (rows x output channels);  CT/RT = 16-wide tiles per wave.
+//
+// Wave tiling (WM x WN = 4 waves over rows x output channels):
+//   * WM = 1: every wave covers all kRT row tiles (both samples) and NF channel tiles, so no
+//     weight fragment is loaded twice per workgroup.  With HALF, channel tiles that do not split
+//     4 ways (Cout = 224 -> 14 tiles) are shared by wave pairs: a pair owns 2*NF+1 tiles, each wave
+//     NF full ones plus half (one sample's row tiles) of the middle one, so all waves issue the same
+//     MFMA count;
+//   * WM = 2: a wave covers one sample (kRT/2 row tiles) and NF channel tiles; the two wave rows
+//     load the same weight fragments.  Used for Cout = 96 (6 tiles), where the pair split above
+//     doubles the B-operand (LDS) reads per MFMA and measured 10-19 % slower per layer
+//     (profiles/fused_ablation_r1.md, v8).
 #ifndef APNEAUQ_BLOCK_INLINE
 #define APNEAUQ_BLOCK_INLINE __forceinline__
 #endif
 
-// Per-block context passed by value to the (deliberately non-inlined) block functions: keeping
-// each block a separate function bounds register allocation to one block's live state.
+// Per-block context passed by value to the block functions.
 struct BlockCtx {
   const guint8* blob;  // this member's packed parameters
   unsigned skey0, skey1;  // dropout sample keys of the two slots (0 if no dropout)
@@ -142,7 +152,7 @@ struct BlockCtx {
   int out_logits;
 };
 
-template <int LAYER, int WM, int WN, int PD, bool HEAD, bool DROP>
+template <int LAYER, int WM, int NF, bool HALF, int PD, bool HEAD, bool DROP>
 __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
   char* act = smem;
   const char* x0 = smem + kActBytes;
@@ -152,36 +162,59 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
   constexpr bool FIRST = (LAYER == 0);
   constexpr int NSTEP = ksteps(LAYER);
   constexpr int NCT = COUT / 16;
-  constexpr int CT = NCT / WN;
-  constexpr int RT = kRT / WM;
+  constexpr int NW = kThreads / kWave;
   constexpr int PAD = (K - 1) / 2;
-  static_assert(NCT % WN == 0 && kRT % WM == 0 && WM * WN == kThreads / kWave, "wave tiling");
+  constexpr int NA = NF + (HALF ? 1 : 0);  // weight fragments per wave per k-step
+  constexpr int HRT = kRT / 2;             // row tiles of one sample (= of the shared half tile)
+  constexpr int NRT = kRT / WM;            // row tiles per wave
+  static_assert(WM == 1 || (WM == 2 && !HALF), "wave rows");
+  static_assert(HALF ? NCT == (NW / 2) * (2 * NF + 1) : NCT == (NW / WM) * NF, "wave tiling");
   static_assert(FIRST || CIN % 32 == 0, "k-step must stay inside one tap");
-  static_assert(!HEAD || WM == kSlots, "head needs one sample slot per wave row");
+  static_assert(kRT == 8 && kSR == 64 && kSlots == 2, "row-tile -> (slot, t) mapping below");
+  static_assert(!HEAD || 2 * NCT <= kHeadOut, "head partials fit in LDS");
 
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int wm = wave / WN, wn = wave % WN;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int m = lane & 15, h = lane >> 4;
+  // channel tiles of this wave: NF full ones from ctf, the half tile cth (local rows r < HRT);
+  // local row tile r (0 .. NRT-1) is tile (r + ho) mod 8 of the workgroup.  ho is a multiple of 4
+  // (one sample = 4 row tiles), so t = 16 (r mod 4) + m is compile-time in r and only the sample
+  // slot of local rows r < HRT (slot 1 iff ho != 0) depends on the wave.
+  int ctf, cth = 0, ho = 0;
+  if constexpr (HALF) {
+    const int pair = wave >> 1, odd = wave & 1;
+    ctf = pair * (2 * NF + 1) + (odd ? NF + 1 : 0);
+    cth = pair * (2 * NF + 1) + NF;
+    ho = odd * HRT;
+  } else if constexpr (WM == 2) {
+    ctf = (wave % (NW / 2)) * NF;
+    ho = (wave / (NW / 2)) * HRT;
+  } else {
+    ctf = wave * NF;
+  }
+  const int rt_lo = ho, rt_hi = (ho + HRT) & (kRT - 1);
 
-  const gbf16x8* wp = reinterpret_cast<const gbf16x8*>(blob + woff(LAYER)) + (wn * CT) * 64 + lane;
-  const int row0 = wm * RT * 16 + m;  // this lane's first output row (time row) in the tile
+  const gbf16x8* wpf = reinterpret_cast<const gbf16x8*>(blob + woff(LAYER)) + ctf * 64 + lane;
+  const gbf16x8* wph = reinterpret_cast<const gbf16x8*>(blob + woff(LAYER)) + cth * 64 + lane;
 
-  f32x4 acc[CT][RT];
+  f32x4 acc[NA][NRT];
 #pragma unroll
-  for (int c = 0; c < CT; ++c)
+  for (int c = 0; c < NA; ++c)
 #pragma unroll
-    for (int r = 0; r < RT; ++r) acc[c][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < NRT; ++r) acc[c][r] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const char* bbase = act + (kHalo + row0 - PAD) * kRS + 16 * h;
-  // B fragment (activations, LDS) of row tile r at k-step s
+  const char* bb_lo = act + (kHalo + rt_lo * 16 + m - PAD) * kRS + 16 * h;
+  const char* bb_hi = act + (kHalo + rt_hi * 16 + m - PAD) * kRS + 16 * h;
+  const char* xb_lo = x0 + (kHalo + rt_lo * 16 + m - PAD) * kX0RS + 16 * h;
+  const char* xb_hi = x0 + (kHalo + rt_hi * 16 + m - PAD) * kX0RS + 16 * h;
+  // B fragment (activations, LDS) of local row tile r at k-step s
   auto load_b = [&](int s, int r) -> bf16x8 {
     if constexpr ((APNEAUQ_ABL & 4) != 0) {
       const __bf16 v = (__bf16)(float)(lane + s + r);
       return bf16x8{v, v, v, v, v, v, v, v};
     } else if constexpr (FIRST) {
       // k = tap*4 + ci: 8 consecutive k = two consecutive rows x 4 channels (16 B, 8-B aligned)
-      const char* base = x0 + (kHalo + row0 + r * 16 - PAD) * kX0RS + (32 * s + 8 * h) * 2;
+      const char* base = (r < HRT ? xb_lo : xb_hi) + (r % HRT) * 16 * kX0RS + 64 * s;
       const bf16x4 lo = *reinterpret_cast<const bf16x4*>(base);
       const bf16x4 hi = *reinterpret_cast<const bf16x4*>(base + 8);
       return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -190,29 +223,32 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
       constexpr int CB = CIN / 32;
       const int tap = s / CB, cb = s - tap * CB;
       const int soff = __builtin_amdgcn_readfirstlane(tap * kRS + cb * 64);
-      return *reinterpret_cast<const bf16x8*>(bbase + soff + r * 16 * kRS);
+      return *reinterpret_cast<const bf16x8*>((r < HRT ? bb_lo : bb_hi) + soff + (r % HRT) * 16 * kRS);
     }
   };
-  // A fragments (weights, global/L2) of k-step s
-  auto load_a = [&](int s, bf16x8 (&a)[CT]) {
+  // A fragments (weights, global/L2) of k-step s: NF full tiles, then the half tile
+  auto load_a = [&](int s, bf16x8 (&a)[NA]) {
 #pragma unroll
-    for (int c = 0; c < CT; ++c) {
+    for (int c = 0; c < NA; ++c) {
       if constexpr ((APNEAUQ_ABL & 8) != 0) {
         const __bf16 v = (__bf16)(float)(lane + s + c);
         a[c] = bf16x8{v, v, v, v, v, v, v, v};
       } else {
-        a[c] = wp[(s * NCT + c) * 64];
+        a[c] = (c < NF ? wpf + c * 64 : wph)[s * NCT * 64];
       }
     }
   };
-  // (B fragments are read just in time: a DB-deep register ring over the (k-step, row-tile)
-  // sequence measured 0.5-1 % slower on MI355X — the co-resident wave already hides LDS latency.)
-  auto step = [&](int s, const bf16x8 (&a)[CT]) {
+  // (B fragments are read just in time: a register ring over the (k-step, row-tile) sequence
+  // measured 0.5-1 % slower on MI355X — the co-resident wave already hides LDS latency.)
+  auto step = [&](int s, const bf16x8 (&a)[NA]) {
 #pragma unroll
-    for (int r = 0; r < RT; ++r) {
+    for (int r = 0; r < NRT; ++r) {
       const bf16x8 b = load_b(s, r);
 #pragma unroll
-      for (int c = 0; c < CT; ++c) acc[c][r] = mfma16(a[c], b, acc[c][r]);
+      for (int c = 0; c < NF; ++c) acc[c][r] = mfma16(a[c], b, acc[c][r]);
+      if constexpr (HALF) {
+        if (r < HRT) acc[NF][r] = mfma16(a[NF], b, acc[NF][r]);
+      }
     }
   };
 
@@ -224,7 +260,7 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
   __builtin_amdgcn_s_setprio(APNEAUQ_PRIO_K);  // probe: wave priority during the MFMA phase
 #endif
   constexpr int NS = PD + 1;
-  bf16x8 a[NS][CT];
+  bf16x8 a[NS][NA];
 #pragma unroll
   for (int j = 0; j < PD; ++j) load_a(j < NSTEP ? j : NSTEP - 1, a[j]);
 
@@ -247,9 +283,12 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
   // relu(acc + b) * s + t == clamp(fma(acc, s, b*s + t), lo, hi) (host-folded constants, one v_fma +
   // one v_med3 per element); MC Dropout reads a second copy pre-scaled by 1/(1-rate).  Rows t >= 60
   // of a slot are the next block's zero halo: they are simply never written (zeroed at kernel start).
-  // row0 = wm*RT*16 + m with RT*16 a multiple of 64, so t = (16r mod 64) + m is compile-time up to m.
   const gfloat* epi = reinterpret_cast<const gfloat*>(blob + eoff(LAYER)) + (DROP ? 4 * COUT : 0);
   const bool tail_lane = m >= kL - 48;  // lanes whose row in a 48..63 row tile is a halo row
+  const bool swap = ho != 0;            // local rows 0..3 belong to sample slot 1
+  const unsigned key_lo = swap ? X.skey1 : X.skey0, key_hi = swap ? X.skey0 : X.skey1;
+  char* ob_lo = act + (kHalo + rt_lo * 16 + m) * kRS;
+  char* ob_hi = act + (kHalo + rt_hi * 16 + m) * kRS;
 
   if constexpr (!HEAD) APNEAUQ_SYNC();  // every wave has finished reading this block's input
   APNEAUQ_STAMP(4 + 4 * LAYER);  // epilogue start (after the barrier)
@@ -257,29 +296,33 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
   __builtin_amdgcn_s_setprio(APNEAUQ_PRIO_E);  // probe: wave priority during the VALU epilogue
 #endif
 
-  float gap = 0.f;  // HEAD: this lane's share of sum_t sum_co w[co] * y[t][co]
+  // HEAD: this lane's share of sum_t sum_co w[co] * y[t][co], per (channel tile, slot).  Every
+  // (tile, slot) sum is formed by exactly one wave and combined in tile order, so a sample's logit
+  // does not depend on the slot it occupies (bitwise sharding invariance).
+  float gap[NA][kSlots];
 #pragma unroll
-  for (int c = 0; c < CT; ++c) {
-    const int co0 = (wn * CT + c) * 16 + 4 * h;
+  for (int c = 0; c < NA; ++c) gap[c][0] = gap[c][1] = 0.f;
+#pragma unroll
+  for (int c = 0; c < NA; ++c) {
+    const int co0 = (c < NF ? ctf + c : cth) * 16 + 4 * h;
     const f32x4 sc = *reinterpret_cast<const gf32x4*>(epi + co0);
     const f32x4 sh = *reinterpret_cast<const gf32x4*>(epi + COUT + co0);
     const f32x4 lo = *reinterpret_cast<const gf32x4*>(epi + 2 * COUT + co0);
     const f32x4 hi = *reinterpret_cast<const gf32x4*>(epi + 3 * COUT + co0);
     f32x4 dw;
     if constexpr (HEAD) dw = *reinterpret_cast<const gf32x4*>(reinterpret_cast<const gfloat*>(blob + kDenseOff) + co0);
+    const int nr = (HALF && c == NF) ? HRT : NRT;  // compile-time after unrolling
 #pragma unroll
-    for (int r = 0; r < RT; ++r) {
-      const int row = row0 + r * 16;
-      constexpr int kTail = 48;  // (16 r) mod 64 of the row tile that holds t = 48..63
-      const bool tail_tile = ((r * 16) % kSR) == kTail;
-      const int slot = (wm * RT * 16 + r * 16) / kSR;
-      const int t = (r * 16) % kSR + m;
+    for (int r = 0; r < NRT; ++r) {
+      if (r >= nr) break;
+      const bool tail_tile = (r % 4) == 3;  // the row tile holding t = 48..63 of its sample
+      const int t = (r % 4) * 16 + m;
       f32x4 v = acc[c][r];
       if constexpr ((APNEAUQ_ABL & 1) == 0) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = __builtin_amdgcn_fmed3f(__builtin_fmaf(v[i], sc[i], sh[i]), lo[i], hi[i]);
         if constexpr (DROP) {
-          const unsigned k = slot ? X.skey1 : X.skey0;
+          const unsigned k = r < HRT ? key_lo : key_hi;
 #if (APNEAUQ_ABL & 32)
           auto cheap = [](unsigned x) { x ^= x >> 13; x ^= x << 7; x ^= x >> 17; return x; };
           const unsigned b01 = cheap(k ^ ((t << 9) | (co0 >> 1)));
@@ -299,10 +342,10 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
       }
       if constexpr (HEAD) {
         const float g = v[0] * dw[0] + v[1] * dw[1] + v[2] * dw[2] + v[3] * dw[3];
-        gap += (tail_tile && tail_lane) ? 0.f : g;
+        gap[c][r < HRT ? 0 : 1] += (tail_tile && tail_lane) ? 0.f : g;  // [0]: local rows 0..3
       } else {
         bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
-        bf16x4* dst = reinterpret_cast<bf16x4*>(act + (kHalo + row) * kRS + co0 * 2);
+        bf16x4* dst = reinterpret_cast<bf16x4*>((r < HRT ? ob_lo : ob_hi) + (r % HRT) * 16 * kRS + co0 * 2);
         if constexpr ((APNEAUQ_ABL & 2) != 0) {
           if (v[0] == 123.f) *dst = o;
         } else if (!(tail_tile && tail_lane)) {
@@ -312,16 +355,24 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
     }
   }
   if constexpr (HEAD) {
-    gap = wave_sum(gap);
-    if (lane == 0) head[wm * WN + wn] = gap;
+#pragma unroll
+    for (int c = 0; c < NA; ++c) {
+      const int ct = c < NF ? ctf + c : cth;
+#pragma unroll
+      for (int j = 0; j < kSlots; ++j) {
+        if (((HALF && c == NF) || WM == 2) && j == 1) break;  // only local rows 0..3
+        const float g = wave_sum(gap[c][j]);
+        if (lane == 0) head[2 * ct + (j ^ (swap ? 1 : 0))] = g;
+      }
+    }
     __syncthreads();
     if (threadIdx.x < kSlots) {
       const int sl = threadIdx.x;
       float s = 0.f;
 #pragma unroll
-      for (int j = 0; j < WN; ++j) s += head[sl * WN + j];
+      for (int ct = 0; ct < NCT; ++ct) s += head[2 * ct + sl];
       const float logit = s * (1.0f / kL) + reinterpret_cast<const gfloat*>(blob + kDenseOff)[C[6]];
-      head[8 + sl] = X.out_logits ? logit : 1.0f / (1.0f + __expf(-logit));
+      head[kHeadOut + sl] = X.out_logits ? logit : 1.0f / (1.0f + __expf(-logit));
     }
   } else {
     APNEAUQ_STAMP(5 + 4 * LAYER);  // epilogue done, before the barrier
@@ -405,16 +456,16 @@ __global__ __launch_bounds__(kThreads, 2) void fused_forward_kernel(Args A) {
     X.skey0 = sample_key(stream_key(A.seed, L, A.pass_offset + pass[0]), A.window_offset + win[0]);      \
     X.skey1 = sample_key(stream_key(A.seed, L, A.pass_offset + pass[1]), A.window_offset + win[1]);      \
   }
-    APNEAUQ_CTX(0) block<0, 1, 4, APNEAUQ_PD0, false, DROP>(X);
-    APNEAUQ_CTX(1) block<1, 1, 4, APNEAUQ_PD1, false, DROP>(X);
-    APNEAUQ_CTX(2) block<2, 2, 2, APNEAUQ_PD2, false, DROP>(X);
-    APNEAUQ_CTX(3) block<3, 2, 2, APNEAUQ_PD3, false, DROP>(X);
-    APNEAUQ_CTX(4) block<4, 1, 4, APNEAUQ_PD4, false, DROP>(X);
-    APNEAUQ_CTX(5) block<5, 2, 2, APNEAUQ_PD5, true, DROP>(X);
+    APNEAUQ_CTX(0) block<0, 1, 2, false, APNEAUQ_PD0, false, DROP>(X);
+    APNEAUQ_CTX(1) block<1, 1, 3, false, APNEAUQ_PD1, false, DROP>(X);
+    APNEAUQ_CTX(2) block<2, 1, 3, true, APNEAUQ_PD2, false, DROP>(X);
+    APNEAUQ_CTX(3) block<3, 2, 3, false, APNEAUQ_PD3, false, DROP>(X);
+    APNEAUQ_CTX(4) block<4, 1, 4, false, APNEAUQ_PD4, false, DROP>(X);
+    APNEAUQ_CTX(5) block<5, 2, 3, false, APNEAUQ_PD5, true, DROP>(X);
 #undef APNEAUQ_CTX
     if (threadIdx.x < kSlots && valid[threadIdx.x]) {
       const int sl = threadIdx.x;
-      A.out[((long long)member * A.n_pass + pass[sl]) * A.n_win + win[sl]] = head[8 + sl];
+      A.out[((long long)member * A.n_pass + pass[sl]) * A.n_win + win[sl]] = head[kHeadOut + sl];
     }
     APNEAUQ_STAMP(1);
   }
