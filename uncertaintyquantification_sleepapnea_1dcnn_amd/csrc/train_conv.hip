@@ -27,6 +27,8 @@
 
 #include "common.h"
 
+#include <type_traits>
+
 namespace apneauq {
 namespace train {
 
@@ -95,6 +97,12 @@ __device__ __forceinline__ int row_time(int grow) { return (grow - kHalo) & 63; 
 // BN moment sums are accumulated into kStatSlots interleaved copies (slot = workgroup % kStatSlots)
 // so that the ~512 workgroups of a layer do not serialise on the same 2*C L2 atomic addresses;
 // readers add the slots.  Layout per layer: st[slot][group][2][C], bst[slot][2][C].
+// Probe hooks for timing the forward kernel's phases (always 0 in the library build; nonzero
+// values compute garbage): 4 = no copy-out, 8 = no conv MFMAs.
+#ifndef APNEAUQ_FWD_ABL
+#define APNEAUQ_FWD_ABL 0
+#endif
+
 constexpr int kStatSlots = 16;
 __device__ __forceinline__ int st_stride(const Args& A, int Cc) { return A.groups * 2 * Cc; }
 __device__ __forceinline__ float slot_sum(const float* p, int stride) {
@@ -173,116 +181,201 @@ __device__ __forceinline__ bf16x8 zero8() {
 
 // Stage A_l (= dropout(BN(R_l))) rows [row0, row0 + NR) x channels [c0, c0 + NCW*8) of global
 // PL buffer into LDS (row stride ldsrs bytes).  Pad rows and rows outside the batch become 0.
+// row0 is a tile start (a multiple of 128), so the rows hold samples smp0 = row0/64 and smp0 + 1
+// (plus the halo rows of the neighbours: pad rows, or rows whose outputs are discarded).
+//
+// Each thread owns one 8-channel chunk (cw = tid % NCW) for all its rows, so the BN affine of the
+// chunk (x 1/(1-rate) when dropping) and the two samples' dropout keys are loaded / derived once per
+// call instead of per 16-B item; the affine of the second stats group (a tile straddling an
+// MC-Dropout pass boundary, g1 = s/t + 256) is selected per row only when it differs.
 template <int l, int NR, int NCW, int UMAX = kStageU>
 __device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, int row0, int c0, const float* s,
                                           const float* t, int g0) {
   constexpr int Cc = C[l + 1];
+  constexpr int RP = kThreads / NCW;  // rows per pass over the workgroup
+  constexpr int NK = (NR + RP - 1) / RP;
+  constexpr int U = NK < UMAX ? NK : UMAX;
   const Layer& Ly = A.L[l];
+  // opaque thread index (see staged_loop): keeps the per-row addresses out of enclosing tile loops
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  const int cw = tid % NCW, rin = tid / NCW;
+  const bool active = rin < RP;
+  const int c = c0 + cw * 8;
+  const int smp0 = row0 >> 6;
+  const int g1 = min(smp0 + 1, A.B - 1) / A.n_win;
+  const bool two = g1 != g0;  // workgroup-uniform
+  const bool drop = A.dropout != 0;
+  const float dsc = drop ? Ly.dsc : 1.f;
+  float s0[8], t0[8], s1[8], t1[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    s0[j] = s[c + j] * dsc;
+    t0[j] = t[c + j] * dsc;
+    s1[j] = two ? s[256 + c + j] * dsc : s0[j];
+    t1[j] = two ? t[256 + c + j] * dsc : t0[j];
+  }
+  unsigned key0 = 0u, key1 = 0u;
+  if (drop) {
+    key0 = layer_sample_key(A, l, min(smp0, A.B - 1));
+    key1 = layer_sample_key(A, l, min(smp0 + 1, A.B - 1));
+  }
   auto valid = [&](int grow) {
     const int n = row_sample(grow), tt = row_time(grow);
     return !(grow < kHalo || n >= A.B || tt >= kL);
   };
-  staged_loop<NR * NCW, UMAX>(
-      [&](int i) -> bf16x8 {
-        const int r = i / NCW, cw = i - r * NCW;
+#pragma unroll
+  for (int b = 0; b < NK; b += U) {
+    bf16x8 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = rin + (b + u) * RP;
+      const int grow = row0 + r;
+      if (b + u < NK) v[u] = (active && r < NR && valid(grow)) ? gld<bf16x8>(Ly.R + (long long)grow * Cc + c) : zero8();
+    }
+    auto store = [&](auto two_groups) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int r = rin + (b + u) * RP;
+        if (b + u >= NK || !active || r >= NR) continue;
         const int grow = row0 + r;
-        return valid(grow) ? gld<bf16x8>(Ly.R + (long long)grow * Cc + c0 + cw * 8) : zero8();
-      },
-      [&](int i, const bf16x8& v) {
-        const int r = i / NCW, cw = i - r * NCW;
-        const int grow = row0 + r;
-        const int c = c0 + cw * 8;
         bf16x8 o = zero8();
         if (valid(grow)) {
-          const int n = row_sample(grow), tt = row_time(grow);
-          const int g = n / A.n_win;
-          const float* sg = s + (g == g0 ? 0 : 256);
-          const float* tg = t + (g == g0 ? 0 : 256);
-          unsigned key = 0;
-          if (A.dropout) key = layer_sample_key(A, l, n);
+          const int tt = row_time(grow);
+          const bool hi = row_sample(grow) != smp0;
+          const unsigned key = hi ? key1 : key0;
 #pragma unroll
           for (int j = 0; j < 8; j += 2) {
-            float a0 = (float)v[j] * sg[c + j] + tg[c + j];
-            float a1 = (float)v[j + 1] * sg[c + j + 1] + tg[c + j + 1];
-            if (A.dropout) {
+            float a0, a1;
+            if constexpr (decltype(two_groups)::value) {
+              a0 = (float)v[u][j] * (hi ? s1[j] : s0[j]) + (hi ? t1[j] : t0[j]);
+              a1 = (float)v[u][j + 1] * (hi ? s1[j + 1] : s0[j + 1]) + (hi ? t1[j + 1] : t0[j + 1]);
+            } else {
+              a0 = (float)v[u][j] * s0[j] + t0[j];
+              a1 = (float)v[u][j + 1] * s0[j + 1] + t0[j + 1];
+            }
+            if (drop) {
               const unsigned h = dropout_bits2(key, tt, c + j);
-              a0 = (h & 0xFFFFu) >= Ly.thr ? a0 * Ly.dsc : 0.f;
-              a1 = (h >> 16) >= Ly.thr ? a1 * Ly.dsc : 0.f;
+              a0 = (h & 0xFFFFu) >= Ly.thr ? a0 : 0.f;
+              a1 = (h >> 16) >= Ly.thr ? a1 : 0.f;
             }
             o[j] = (__bf16)a0;
             o[j + 1] = (__bf16)a1;
           }
         }
         *reinterpret_cast<bf16x8*>(lds + r * ldsrs + cw * 16) = o;
-      });
+      }
+    };
+    if (two)
+      store(std::true_type{});
+    else
+      store(std::false_type{});
+  }
 }
 
 // dZ_l rows into LDS (rows [row0, row0+NR), channels [c0, c0+NCW*8)); rows [own_lo, own_hi) are
 // also written to ``gout`` (dgrad materialises dZ_l for wgrad).
 //   l == 5: dY_6 = dlogit[n] * w[c] / 60 * mask6 * dsc6 (recomputed; never stored)
+// As in stage_act, each thread owns one 8-channel chunk, and the BN backward
+//   dz = relu'(r) * g*rstd * (dy - mean(dy) - xhat * mean(dy*xhat)),  xhat = (r - mean) * rstd
+// is folded per channel into dz = relu'(r) * (al * dy + be * r + ga), evaluated from registers.
 template <int l, int NR, int NCW>
 __device__ __forceinline__ void stage_dz(const Args& A, char* lds, int ldsrs, int row0, int c0,
                                          const float* gam_rstd, const float* mean, const float* rstd, const float* mdy,
                                          const float* mdyx, __bf16* gout = nullptr,
                                          int own_lo = 0, int own_hi = 0) {
   constexpr int Cc = C[l + 1];
+  constexpr int RP = kThreads / NCW;
+  constexpr int NK = (NR + RP - 1) / RP;
+  constexpr int U = NK < kStageU / 2 ? NK : kStageU / 2;
   const Layer& Ly = A.L[l];
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  const int cw = tid % NCW, rin = tid / NCW;
+  const bool active = rin < RP;
+  const int c = c0 + cw * 8;
+  const int smp0 = (row0 >> 7) * 2;  // row0 is a tile start, or a tile start + kHalo
+  float al[8], be[8], ga[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float g = gam_rstd[c + j], q = rstd[c + j] * mdyx[c + j];
+    al[j] = g;
+    be[j] = -g * q;
+    ga[j] = g * (q * mean[c + j] - mdy[c + j]);
+  }
+  // block 6: dY is recomputed from dlogit, the dense weights and the dropout mask of block 6
+  float dw[8] = {}, dl0 = 0.f, dl1 = 0.f;
+  unsigned key0 = 0u, key1 = 0u;
+  if constexpr (l == 5) {
+    const float dsc = A.dropout ? Ly.dsc : 1.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dw[j] = A.dense_w[c + j] * dsc;
+    dl0 = A.dlogit[min(smp0, A.B - 1)] * (1.0f / kL);
+    dl1 = A.dlogit[min(smp0 + 1, A.B - 1)] * (1.0f / kL);
+    if (A.dropout) {
+      key0 = layer_sample_key(A, 5, min(smp0, A.B - 1));
+      key1 = layer_sample_key(A, 5, min(smp0 + 1, A.B - 1));
+    }
+  }
   auto valid = [&](int grow) {
     const int n = row_sample(grow), tt = row_time(grow);
     return !(grow < kHalo || n >= A.B || tt >= kL);
   };
-  // payload: R_l (pre-BN activation) and dY_l, both loaded in the batched first phase
-  staged_loop<NR * NCW, kStageU / 2>(
-      [&](int i) -> bf16x16 {
-        const int r = i / NCW, cw = i - r * NCW;
-        const int grow = row0 + r;
-        bf16x16 q;
-        q.a = valid(grow) ? gld<bf16x8>(Ly.R + (long long)grow * Cc + c0 + cw * 8) : zero8();
-        if constexpr (l < 5) q.b = valid(grow) ? gld<bf16x8>(Ly.dY + (long long)grow * Cc + c0 + cw * 8) : zero8();
-        return q;
-      },
-      [&](int i, const bf16x16& q) {
-        const bf16x8& rv = q.a;
-        const int r = i / NCW, cw = i - r * NCW;
-        const int grow = row0 + r;
-        const int c = c0 + cw * 8;
-        bf16x8 o = zero8();
-        if (valid(grow)) {
-          const int n = row_sample(grow), tt = row_time(grow);
-          float dy[8];
-          if constexpr (l == 5) {
-            const float dl = A.dlogit[n] * (1.0f / kL);
-            const unsigned key = A.dropout ? layer_sample_key(A, 5, n) : 0u;
 #pragma unroll
-            for (int j = 0; j < 8; j += 2) {
-              float d0 = dl * A.dense_w[c + j], d1 = dl * A.dense_w[c + j + 1];
-              if (A.dropout) {
-                const unsigned h = dropout_bits2(key, tt, c + j);
-                d0 = (h & 0xFFFFu) >= Ly.thr ? d0 * Ly.dsc : 0.f;
-                d1 = (h >> 16) >= Ly.thr ? d1 * Ly.dsc : 0.f;
-              }
-              dy[j] = d0;
-              dy[j + 1] = d1;
+  for (int b = 0; b < NK; b += U) {
+    // payload: R_l (pre-BN activation) and dY_l, both loaded in the batched first phase
+    bf16x16 q[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = rin + (b + u) * RP;
+      const int grow = row0 + r;
+      if (b + u >= NK) continue;
+      const bool ok = active && r < NR && valid(grow);
+      q[u].a = ok ? gld<bf16x8>(Ly.R + (long long)grow * Cc + c) : zero8();
+      if constexpr (l < 5) q[u].b = ok ? gld<bf16x8>(Ly.dY + (long long)grow * Cc + c) : zero8();
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = rin + (b + u) * RP;
+      if (b + u >= NK || !active || r >= NR) continue;
+      const int grow = row0 + r;
+      bf16x8 o = zero8();
+      if (valid(grow)) {
+        float dy[8];
+        if constexpr (l == 5) {
+          const int tt = row_time(grow);
+          const bool hi = row_sample(grow) != smp0;
+          const float dl = hi ? dl1 : dl0;
+          const unsigned key = hi ? key1 : key0;
+#pragma unroll
+          for (int j = 0; j < 8; j += 2) {
+            float d0 = dl * dw[j], d1 = dl * dw[j + 1];
+            if (A.dropout) {
+              const unsigned h = dropout_bits2(key, tt, c + j);
+              d0 = (h & 0xFFFFu) >= Ly.thr ? d0 : 0.f;
+              d1 = (h >> 16) >= Ly.thr ? d1 : 0.f;
             }
-          } else {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) dy[j] = (float)q.b[j];
+            dy[j] = d0;
+            dy[j + 1] = d1;
           }
+        } else {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float rr = (float)rv[j];
-            const float xh = (rr - mean[c + j]) * rstd[c + j];
-            const float dz = gam_rstd[c + j] * (dy[j] - mdy[c + j] - xh * mdyx[c + j]);
-            o[j] = (__bf16)(rr > 0.f ? dz : 0.f);
-          }
+          for (int j = 0; j < 8; ++j) dy[j] = (float)q[u].b[j];
         }
-        *reinterpret_cast<bf16x8*>(lds + r * ldsrs + cw * 16) = o;
-        if (gout != nullptr && r >= own_lo && r < own_hi)
-          *reinterpret_cast<bf16x8*>(gout + (long long)grow * Cc + c) = o;  // pad rows get their zeros too
-      });
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float rr = (float)q[u].a[j];
+          const float dz = __builtin_fmaf(al[j], dy[j], __builtin_fmaf(be[j], rr, ga[j]));
+          o[j] = (__bf16)(rr > 0.f ? dz : 0.f);
+        }
+      }
+      *reinterpret_cast<bf16x8*>(lds + r * ldsrs + cw * 16) = o;
+      if (gout != nullptr && r >= own_lo && r < own_hi)
+        *reinterpret_cast<bf16x8*>(gout + (long long)grow * Cc + c) = o;  // pad rows get their zeros too
+    }
+  }
 }
 
-// Plain copy of materialised dZ rows (see dgrad) into LDS.
 template <int l, int NR, int NCW, int UMAX>
 __device__ __forceinline__ void stage_dz_copy(const Args& A, char* lds, int ldsrs, int row0, int c0) {
   constexpr int Cc = C[l + 1];
@@ -441,7 +534,14 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
     }
     __syncthreads();
     f32x4 acc[CV::CT][CV::RT];
+#if (APNEAUQ_FWD_ABL & 8)
+#pragma unroll
+    for (int c = 0; c < CV::CT; ++c)
+#pragma unroll
+      for (int r = 0; r < CV::RT; ++r) acc[c][r] = f32x4{(float)act[threadIdx.x], 0.f, 0.f, (float)r};
+#else
     CV::run(Ly.wf, act, IN_RS, acc);
+#endif
     __syncthreads();  // all waves done reading the staged input; reuse it for the output tile
     // epilogue over the rows of sample slot `sel` (-1: both): bias + ReLU -> bf16 LDS tile, and the
     // moments of the stored values into lstat (group gcur)
@@ -496,7 +596,7 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
     __syncthreads();
     // coalesced copy-out of the 128 tile rows (16 B per thread-iteration)
     constexpr int CW = COUT / 8;
-    for (int i = threadIdx.x; i < kR * CW; i += kThreads) {
+    for (int i = threadIdx.x; i < ((APNEAUQ_FWD_ABL & 4) ? 0 : kR * CW); i += kThreads) {
       const int r = i / CW, cw = i - r * CW;
       *reinterpret_cast<bf16x8*>(Ly.R + (long long)(row0 + kHalo + r) * COUT + cw * 8) =
           *reinterpret_cast<const bf16x8*>(act + r * kRS + cw * 16);
