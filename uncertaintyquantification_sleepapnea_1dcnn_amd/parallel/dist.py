@@ -61,7 +61,9 @@ def init(backend: Optional[str] = None, device: Optional[str] = None, timeout_s:
         dev = torch.device("cpu")
     be = "none"
     if world > 1:
-        be = backend or ("nccl" if use_gpu else "gloo")
+        # APNEAUQ_DIST_BACKEND=gloo rehearses a multi-rank GPU run on ONE card (RCCL refuses two ranks
+        # on one device); production multi-GPU runs use RCCL ("nccl").
+        be = backend or os.environ.get("APNEAUQ_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         if not dist.is_initialized():
