@@ -38,7 +38,13 @@ def test_checkpoint_roundtrip(tmp_path):
     m2 = load_model(path, device="cpu")
     for a, b in zip(m.get_weights(), m2.get_weights()):
         np.testing.assert_array_equal(a, b)
-    with np.load(path, allow_pickle=False) as z:
+    # a .keras path is a genuine Keras v3 archive (utils/keras_io.py); other names are .npz
+    import zipfile
+
+    with zipfile.ZipFile(path) as z:
+        assert {"config.json", "model.weights.h5"} <= set(z.namelist())
+    npz = m.save(str(tmp_path / "w.npz"))
+    with np.load(npz, allow_pickle=False) as z:
         assert "conv1d_1/kernel" in z.files and "output_layer/bias" in z.files
 
 
