@@ -24,6 +24,12 @@ hipError_t launch_bootstrap(const float* metrics, const int* y, const int* idx, 
 hipError_t launch_adam(float* p, const float* g, float* m, float* v, long long n, float b1, float b2, float alpha,
                        float eps, float gscale, const int* step_dev, hipStream_t stream);
 hipError_t train_bump_counters(int* c, int n, hipStream_t st);
+hipError_t launch_generic_conv(const void* x, const void* wfrag, const float* epi, void* y, int n, int L, int cin,
+                               int cout, int cout_pad, int ksize, int pool, int dropout, unsigned thr, int layer,
+                               int n_win, unsigned pass_offset, unsigned window_offset, unsigned long long seed,
+                               hipStream_t stream);
+hipError_t launch_generic_head(const void* y, const float* w, float b, int n, int L, int C, int out_logits, float* out,
+                               hipStream_t stream);
 namespace train {
 struct Layer {
   const void* wf; const void* wd; const float* bias; const float* gamma; const float* beta;
@@ -247,6 +253,45 @@ void train_pack(const at::Tensor& w, int64_t k, int64_t cin, int64_t cout, at::T
         "train_pack");
 }
 
+// Generic-spec conv block (csrc/generic_conv.hip): x (N, L, Cin) bf16 -> (N, L or L/2, Cout) bf16.
+at::Tensor generic_conv(const at::Tensor& x, const at::Tensor& wfrag, const at::Tensor& epi, int64_t cout,
+                        int64_t ksize, bool pool, bool dropout, int64_t thr, int64_t layer, int64_t n_win,
+                        int64_t pass_offset, int64_t window_offset, int64_t seed) {
+  TORCH_CHECK(x.is_cuda() && wfrag.is_cuda() && epi.is_cuda(), "generic_conv: tensors must be on the GPU");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() == 3, "generic_conv: x must be contiguous bf16 (N, L, C)");
+  TORCH_CHECK(wfrag.scalar_type() == at::kBFloat16 && wfrag.is_contiguous() && wfrag.dim() == 4 && wfrag.size(2) == 64 &&
+              wfrag.size(3) == 8, "generic_conv: wfrag must be (nstep, Cout_pad/16, 64, 8) bf16");
+  const int64_t n = x.size(0), L = x.size(1), cin = x.size(2), cout_pad = wfrag.size(1) * 16;
+  TORCH_CHECK(wfrag.size(0) == (ksize * cin + 31) / 32, "generic_conv: wfrag k-steps do not match k*Cin");
+  TORCH_CHECK(cout > 0 && cout % 4 == 0 && cout <= cout_pad && cout_pad - cout < 16, "generic_conv: Cout must be a multiple of 4");
+  TORCH_CHECK(cout_pad <= 1024 && L < (1 << 22), "generic_conv: dropout hash needs C <= 1024, L < 2^22");
+  TORCH_CHECK(epi.scalar_type() == at::kFloat && epi.is_contiguous() && epi.numel() == 8 * cout_pad, "generic_conv: epi must be (8, Cout_pad) fp32");
+  TORCH_CHECK(ksize % 2 == 1, "generic_conv: odd kernel sizes only ('same' padding)");
+  TORCH_CHECK(n_win >= 1 && n % n_win == 0, "generic_conv: N must be n_pass * n_win");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "generic_conv: 16-B alignment required");
+  TORCH_CHECK(n * L < (int64_t(1) << 31), "generic_conv: too many rows");
+  const at::DeviceGuard guard(x.device());
+  const int64_t lout = pool ? L / 2 : L;
+  auto y = at::empty({n, lout, cout}, x.options());
+  check(apneauq::launch_generic_conv(x.data_ptr(), wfrag.data_ptr(), epi.data_ptr<float>(), y.data_ptr(), (int)n, (int)L,
+                                     (int)cin, (int)cout, (int)cout_pad, (int)ksize, pool ? 1 : 0, dropout ? 1 : 0,
+                                     (unsigned)thr, (int)layer, (int)n_win, (unsigned)pass_offset, (unsigned)window_offset,
+                                     (unsigned long long)seed, cur_stream()),
+        "generic_conv");
+  return y;
+}
+
+at::Tensor generic_head(const at::Tensor& y, const at::Tensor& w, double b, bool out_logits) {
+  TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kBFloat16 && y.is_contiguous() && y.dim() == 3, "generic_head: y must be (N, L, C) bf16");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == y.size(2), "generic_head: w must be (C,) fp32");
+  const at::DeviceGuard guard(y.device());
+  auto out = at::empty({y.size(0)}, y.options().dtype(at::kFloat));
+  check(apneauq::launch_generic_head(y.data_ptr(), w.data_ptr<float>(), (float)b, (int)y.size(0), (int)y.size(1), (int)y.size(2),
+                                     out_logits ? 1 : 0, out.data_ptr<float>(), cur_stream()),
+        "generic_head");
+  return out;
+}
+
 std::vector<int64_t> fused_layout() {
   int w[6], e[6], d;
   apneauq::fused_layout(w, e, &d);
@@ -272,6 +317,9 @@ TORCH_LIBRARY(apneauq, m) {
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, float b1, float b2, float alpha, float eps, "
         "float gscale, Tensor? counters=None) -> ()");
   m.def("bump_counters(Tensor(a!) counters) -> ()");
+  m.def("generic_conv(Tensor x, Tensor wfrag, Tensor epi, int cout, int ksize, bool pool, bool dropout, int thr, "
+        "int layer, int n_win, int pass_offset, int window_offset, int seed) -> Tensor");
+  m.def("generic_head(Tensor y, Tensor w, float b, bool logits) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
@@ -281,4 +329,6 @@ TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
   m.impl("adam_step", &adam_step);
   m.impl("bump_counters", &bump_counters);
   m.impl("train_pack", &train_pack);
+  m.impl("generic_conv", &generic_conv);
+  m.impl("generic_head", &generic_head);
 }

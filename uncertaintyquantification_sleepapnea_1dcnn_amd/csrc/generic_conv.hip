@@ -1,0 +1,225 @@
+// Layer-wise inference kernels for ANY ModelSpec (gfx950 / MI355X): the opt-in MaxPool1D variant
+// (north star "Conv1D -> BN -> ReLU -> MaxPool1D -> Dropout"), other window shapes
+// (the "30 s single-channel" config: L = 30, C = 1), other filter / kernel sizes.
+//
+// The fused whole-network kernel (fused_forward.hip) is specialised to the reference's (60, 4)
+// no-pool architecture; this path trades its LDS residency for generality:
+//
+//   conv_block_kernel: one Conv1D(relu, same) -> BN(running) -> [MaxPool1D(2)] -> [Dropout] block as
+//     an implicit GEMM on v_mfma_f32_16x16x32_bf16.  D^T[co][row] = W^T[co][k] * X^T[k][row] with
+//     k = tap*Cin + ci; the weights are pre-packed A fragments (ops/fused.py:pack_conv_fragments, Cout
+//     zero-padded to 16), the activations are gathered straight from global memory (16-B loads when
+//     Cin % 8 == 0, so the 8 k of a lane lie in one tap; element loads otherwise).  Each lane's
+//     accumulator holds one time step x 4 channels, so the epilogue -- the bias + ReLU + BN affine
+//     folded into fma + med3, the 2:1 max pool as a lane-pair exchange (rows t, t^1 sit in lanes
+//     l, l^1), the counter-based dropout (ops/rng.py, keyed by the pooled time step) -- runs in
+//     registers and writes bf16 (N, L_out, Cout).
+//   head_kernel: GAP over time + Dense(C -> 1) (+ sigmoid), one wave per sample.
+//
+// Rows: sample n, step t map to GEMM row n*Lp + t, Lp = L rounded up to even when pooling (pairs
+// never straddle a 16-row tile).  A workgroup is 2 x 2 waves over 128 rows x 128 channels; each wave
+// owns 4 row tiles x 4 channel tiles, so a k-step costs 4 activation gathers + 4 weight-fragment
+// loads for 16 MFMAs (row gathers are shared through L1 by the two waves of a row half).
+#include "common.h"
+
+namespace apneauq {
+namespace generic {
+
+struct ConvArgs {
+  const __bf16* x;        // (N, L, Cin) bf16
+  const bf16x8* wfrag;    // (nstep, Cout_pad/16, 64, 8)
+  const float* epi;       // (8, Cout_pad): s, t', lo, hi, then the same x 1/(1-rate)
+  __bf16* y;              // (N, Lout, Cout)
+  int n, L, Lp, cin, cout, cout_pad, ksize, nstep, lout;
+  int pool, dropout;
+  unsigned thr;           // 16-bit dropout threshold
+  int layer;              // dropout stream layer id
+  int n_win;              // samples per pass (sample s: pass s / n_win, window s % n_win)
+  unsigned pass_offset, window_offset;
+  unsigned long long seed;
+};
+
+constexpr int kRT = 4, kCT = 4;  // row / channel tiles per wave; a workgroup is 2 x 2 waves
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void conv_block_kernel(ConvArgs A) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int m = lane & 15, h = lane >> 4;
+  const int wr = wave >> 1, wc = wave & 1;
+  const long long rows = (long long)A.n * A.Lp;
+  const long long row_base = (long long)blockIdx.x * (2 * kRT * 16) + wr * (kRT * 16);
+  const int nct = A.cout_pad / 16;
+  const int ct0 = (blockIdx.y * 2 + wc) * kCT;
+  if (ct0 >= nct) return;  // wave-uniform: no channel tile for this wave (no barriers below)
+  const int pad = (A.ksize - 1) / 2;
+  const int K = A.ksize * A.cin;
+
+  // this lane's B rows (one per row tile): sample n, step t
+  int rn[kRT], rt[kRT];
+  bool rok[kRT];
+#pragma unroll
+  for (int r = 0; r < kRT; ++r) {
+    const long long row = row_base + r * 16 + m;
+    const bool ok = row < rows;
+    rn[r] = ok ? (int)(row / A.Lp) : 0;
+    rt[r] = ok ? (int)(row - (long long)rn[r] * A.Lp) : 0;
+    rok[r] = ok && rt[r] < A.L;
+  }
+
+  f32x4 acc[kCT][kRT];
+#pragma unroll
+  for (int c = 0; c < kCT; ++c)
+#pragma unroll
+    for (int r = 0; r < kRT; ++r) acc[c][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // (tap, ci) of k = 32 s + 8 h, advanced incrementally (no per-step division)
+  int tap = (8 * h) / A.cin, ci = 8 * h - tap * A.cin;
+  for (int s = 0; s < A.nstep; ++s) {
+    const int kk0 = 32 * s + 8 * h;
+    bf16x8 b[kRT];
+#pragma unroll
+    for (int r = 0; r < kRT; ++r) {
+      const __bf16* xs = A.x + (long long)rn[r] * A.L * A.cin;
+      if constexpr (VEC) {
+        const int ts = rt[r] + tap - pad;
+        if (rok[r] && kk0 < K && ts >= 0 && ts < A.L) {
+          b[r] = *(const gbf16x8*)(xs + (long long)ts * A.cin + ci);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) b[r][j] = (__bf16)0.f;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int kk = kk0 + j;
+          const int tp = kk / A.cin, cc = kk - tp * A.cin;
+          const int ts = rt[r] + tp - pad;
+          b[r][j] = (rok[r] && kk < K && ts >= 0 && ts < A.L) ? xs[(long long)ts * A.cin + cc] : (__bf16)0.f;
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < kCT; ++c) {
+      const int ct = ct0 + c;
+      if (ct < nct) {  // wave-uniform
+        const bf16x8 a = ((const gbf16x8*)A.wfrag)[((long long)s * nct + ct) * 64 + lane];
+#pragma unroll
+        for (int r = 0; r < kRT; ++r) acc[c][r] = mfma16(a, b[r], acc[c][r]);
+      }
+    }
+    if constexpr (VEC) {
+      ci += 32;
+      while (ci >= A.cin) {
+        ci -= A.cin;
+        ++tap;
+      }
+    }
+  }
+
+  // epilogue: per row tile, the lane holds row (n, t) x channels co0 .. co0+3 of each channel tile
+  const float* epi = A.epi + (A.dropout ? 4 * A.cout_pad : 0);
+#pragma unroll
+  for (int r = 0; r < kRT; ++r) {
+    const int n = rn[r], t = rt[r];
+    unsigned key = 0u;
+    if (A.dropout) {
+      const unsigned pass = (unsigned)(n / A.n_win), win = (unsigned)(n - (int)pass * A.n_win);
+      key = sample_key(stream_key(A.seed, (unsigned)A.layer, A.pass_offset + pass), A.window_offset + win);
+    }
+    const int tout = A.pool ? (t >> 1) : t;
+    const bool store = rok[r] && (!A.pool || ((t & 1) == 0 && tout < A.lout));
+#pragma unroll
+    for (int c = 0; c < kCT; ++c) {
+      const int ct = ct0 + c;
+      if (ct >= nct) break;  // wave-uniform
+      const int co0 = ct * 16 + 4 * h;
+      f32x4 v = acc[c][r];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float sc = epi[co0 + i], sh = epi[A.cout_pad + co0 + i];
+        const float lo = epi[2 * A.cout_pad + co0 + i], hi = epi[3 * A.cout_pad + co0 + i];
+        v[i] = __builtin_amdgcn_fmed3f(__builtin_fmaf(v[i], sc, sh), lo, hi);
+      }
+      if (A.pool) {  // MaxPool1D(2, valid) after BN: rows t and t^1 live in lanes l and l^1
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i], __shfl_xor(v[i], 1, kWave));
+      }
+      if (A.dropout) {
+        const unsigned b01 = dropout_bits2(key, (unsigned)tout, (unsigned)co0);
+        const unsigned b23 = dropout_bits2(key, (unsigned)tout, (unsigned)co0 + 2);
+        v[0] = (b01 & 0xFFFFu) >= A.thr ? v[0] : 0.f;
+        v[1] = (b01 >> 16) >= A.thr ? v[1] : 0.f;
+        v[2] = (b23 & 0xFFFFu) >= A.thr ? v[2] : 0.f;
+        v[3] = (b23 >> 16) >= A.thr ? v[3] : 0.f;
+      }
+      if (store && co0 < A.cout) {
+        __bf16* dst = A.y + ((long long)n * A.lout + tout) * A.cout + co0;
+        *reinterpret_cast<bf16x4*>(dst) = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+      }
+    }
+  }
+}
+
+// GAP over time + Dense(C -> 1): one wave per sample, fp32 accumulation.
+__global__ __launch_bounds__(256) void head_kernel(const __bf16* y, const float* w, float b, int n, int L, int C,
+                                                   int out_logits, float* out) {
+  const int lane = threadIdx.x & 63;
+  const int s = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= n) return;
+  const __bf16* ys = y + (long long)s * L * C;
+  float acc = 0.f;
+  for (int i = lane; i < L * C; i += kWave) acc += (float)ys[i] * w[i % C];
+  acc = wave_sum(acc);
+  if (lane == 0) {
+    const float z = acc / (float)L + b;
+    out[s] = out_logits ? z : 1.0f / (1.0f + __expf(-z));
+  }
+}
+
+}  // namespace generic
+
+hipError_t launch_generic_conv(const void* x, const void* wfrag, const float* epi, void* y, int n, int L, int cin,
+                               int cout, int cout_pad, int ksize, int pool, int dropout, unsigned thr, int layer,
+                               int n_win, unsigned pass_offset, unsigned window_offset, unsigned long long seed,
+                               hipStream_t stream) {
+  generic::ConvArgs A;
+  A.x = reinterpret_cast<const __bf16*>(x);
+  A.wfrag = reinterpret_cast<const bf16x8*>(wfrag);
+  A.epi = epi;
+  A.y = reinterpret_cast<__bf16*>(y);
+  A.n = n;
+  A.L = L;
+  A.pool = pool;
+  A.Lp = pool ? (L + 1) / 2 * 2 : L;
+  A.cin = cin;
+  A.cout = cout;
+  A.cout_pad = cout_pad;
+  A.ksize = ksize;
+  A.nstep = (ksize * cin + 31) / 32;
+  A.lout = pool ? L / 2 : L;
+  A.dropout = dropout;
+  A.thr = thr;
+  A.layer = layer;
+  A.n_win = n_win;
+  A.pass_offset = pass_offset;
+  A.window_offset = window_offset;
+  A.seed = seed;
+  const long long rows = (long long)n * A.Lp;
+  if (rows == 0) return hipSuccess;
+  constexpr int kRowsWG = 2 * generic::kRT * 16, kChWG = 2 * generic::kCT;  // 128 rows x 8 channel tiles
+  const dim3 grid((unsigned)((rows + kRowsWG - 1) / kRowsWG), (unsigned)((cout_pad / 16 + kChWG - 1) / kChWG));
+  if (cin % 8 == 0)
+    hipLaunchKernelGGL(generic::conv_block_kernel<true>, grid, dim3(256), 0, stream, A);
+  else
+    hipLaunchKernelGGL(generic::conv_block_kernel<false>, grid, dim3(256), 0, stream, A);
+  return hipGetLastError();
+}
+
+hipError_t launch_generic_head(const void* y, const float* w, float b, int n, int L, int C, int out_logits, float* out,
+                               hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(generic::head_kernel, dim3((n + 3) / 4), dim3(256), 0, stream,
+                     reinterpret_cast<const __bf16*>(y), w, b, n, L, C, out_logits, out);
+  return hipGetLastError();
+}
+
+}  // namespace apneauq

@@ -906,8 +906,15 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_kernel(Args A) {
   float* tp = prm + 1536;
   const int nci_blk = FIRST ? 1 : CIN / W::CIB;
   const int nco_blk = COUT / W::COB;
-  const int blk = blockIdx.x % (nci_blk * nco_blk);
-  const int rg = blockIdx.x / (nci_blk * nco_blk);
+  // XCD-aware remap: hardware dispatch round-robins blockIdx over the 8 XCDs, so the nci*nco
+  // workgroups of one row group (which stage the same dZ / A rows) would land on 8 different L2s
+  // and each re-read the rows from HBM.  Contiguous logical ids per XCD keep a row group's blocks
+  // on one XCD, running together, so its rows come from HBM once (bijective for any grid size).
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xq = nwg / 8, xr = nwg % 8, xcd = bid % 8;
+  const int wg = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + bid / 8;
+  const int blk = wg % (nci_blk * nco_blk);
+  const int rg = wg / (nci_blk * nco_blk);
   const int ci0 = (blk % nci_blk) * W::CIB, co0 = (blk / nci_blk) * W::COB;
 #ifdef APNEAUQ_WG_NOBIAS  // probe: skip the bias-gradient column sums (wrong db, timing only)
   const bool do_bias = false;

@@ -109,6 +109,7 @@ class AlarconCNN1D:
         self.device = torch.device(device)
         self.store = self.store.to(self.device)
         self._blob = None
+        self._gpack = None
         for attr in ("_train_ws", "_mcd_ws", "_train_graphs"):  # device workspaces / captured graphs
             if hasattr(self, attr):
                 delattr(self, attr)
@@ -128,12 +129,44 @@ class AlarconCNN1D:
         return t
 
     def uses_fused(self) -> bool:
+        """The reference architecture on a GPU: the fused whole-network kernel."""
+        return self.device.type == "cuda" and fused.supports(self.spec)
+
+    def uses_generic(self) -> bool:
+        """Any other supported architecture on a GPU: the layer-wise HIP kernels (ops/generic.py)."""
+        from ..ops import generic
+
+        return self.device.type == "cuda" and not fused.supports(self.spec) and generic.supports(self.spec)
+
+    def uses_hip(self) -> bool:
+        """Inference (running-stat BN) runs on hand-written HIP kernels; warns once when it cannot."""
         if self.device.type != "cuda":
             return False
-        if not fused.supports(self.spec):
-            fused.warn_unsupported(self.spec, "inference")
-            return False
-        return True
+        if self.uses_fused() or self.uses_generic():
+            return True
+        fused.warn_unsupported(self.spec, "inference")
+        return False
+
+    def generic_pack(self):
+        if getattr(self, "_gpack", None) is None or self._gpack_version != self.store.version:
+            from ..ops import generic
+
+            self._gpack = generic.pack(self.spec, self.store.as_dict())
+            self._gpack_version = self.store.version
+        return self._gpack
+
+    def hip_forward(self, x_bf16: torch.Tensor, n_pass: int = 1, dropout: bool = False, seed: Optional[int] = None,
+                    pass_offset: int = 0, window_offset: int = 0, logits: bool = False) -> torch.Tensor:
+        """(n_pass, N) fp32 probabilities (or logits) with running-stat BN on the HIP kernels."""
+        _ext.require()
+        seed = self.seed if seed is None else seed
+        if self.uses_fused():
+            return fused.fused_forward(x_bf16, self.fused_blob(), self.spec, n_pass=n_pass, dropout=dropout, seed=seed,
+                                       pass_offset=pass_offset, window_offset=window_offset, logits=logits)[0]
+        from ..ops import generic
+
+        return generic.forward(self.generic_pack(), self.spec, x_bf16, n_pass=n_pass, dropout=dropout, seed=seed,
+                               pass_offset=pass_offset, window_offset=window_offset, logits=logits)
 
     def fused_blob(self) -> torch.Tensor:
         """Packed parameters for the fused HIP kernel (cached per weight version)."""
@@ -148,13 +181,11 @@ class AlarconCNN1D:
         x = self._as_input(x)
         use_drop = training if dropout is None else dropout
         use_batch = training if bn_batch_stats is None else bn_batch_stats
-        if not use_batch and self.uses_fused():
-            _ext.require()
+        if not use_batch and self.uses_hip() and (sample_ids is None or not isinstance(sample_ids, torch.Tensor)):
             sid = 0 if sample_ids is None else int(sample_ids)
-            out = fused.fused_forward(x.to(torch.bfloat16).contiguous(), self.fused_blob(), self.spec, n_pass=1,
-                                      dropout=use_drop, seed=self.seed if seed is None else seed,
-                                      pass_offset=0 if pass_id is None else pass_id, window_offset=sid, logits=True)
-            return out[0, 0].reshape(-1, 1)
+            out = self.hip_forward(x.to(torch.bfloat16).contiguous(), n_pass=1, dropout=use_drop, seed=seed,
+                                   pass_offset=0 if pass_id is None else pass_id, window_offset=sid, logits=True)
+            return out[0].reshape(-1, 1)
         upd = use_batch if update_moving is None else update_moving
         with torch.no_grad():
             out = R.forward(self.spec, self.store.as_dict(), x, dropout=use_drop, bn_batch_stats=use_batch,
@@ -183,7 +214,7 @@ class AlarconCNN1D:
         CPU path's memory (results are independent of it).
         """
         x = self._as_input(x)
-        if self.uses_fused():
+        if self.uses_hip():
             return torch.sigmoid(self.logits(x)).cpu().numpy()
         outs = []
         step = max(int(batch_size), 4096)

@@ -67,7 +67,7 @@ def _gather_members(local: torch.Tensor, ids: List[int], n_members: int, world: 
 def mc_dropout_predict_sharded(model, x_test_data, n_pred: int = 50, bn_mode: str = "batch",
                                seed: Optional[int] = None) -> torch.Tensor:
     """(T, N, 1) float32 on every rank; each rank computes its window shard."""
-    from ..ops import bn_batch, fused
+    from ..ops import bn_batch
 
     world, rank = dist.get_world_size(), dist.get_rank()
     x = model._as_input(x_test_data)
@@ -76,9 +76,9 @@ def mc_dropout_predict_sharded(model, x_test_data, n_pred: int = 50, bn_mode: st
     xl = x[s:e]
     seed = model.seed if seed is None else seed
     if bn_mode == "running":
-        if model.uses_fused():
-            loc = fused.fused_forward(xl.to(torch.bfloat16).contiguous(), model.fused_blob(), model.spec, n_pass=n_pred,
-                                      dropout=True, seed=seed, window_offset=s)[0]
+        if model.uses_hip():
+            loc = model.hip_forward(xl.to(torch.bfloat16).contiguous(), n_pass=n_pred, dropout=True, seed=seed,
+                                    window_offset=s)
         else:
             ids = torch.arange(s, e, device=x.device)
             loc = torch.stack([torch.sigmoid(model.logits(xl, dropout=True, bn_batch_stats=False, pass_id=t, seed=seed,
@@ -104,6 +104,9 @@ def deep_ensembles_predict_sharded(ensemble_models: List, x_test_data) -> torch.
         x = mine[0]._as_input(x_test_data).to(torch.bfloat16).contiguous()
         blobs = torch.cat([m.fused_blob().to(mine[0].device) for m in mine])
         loc = fused.fused_forward(x, blobs, mine[0].spec)[:, 0]
+    elif mine and all(m.uses_hip() for m in mine):
+        x = mine[0]._as_input(x_test_data).to(torch.bfloat16).contiguous()
+        loc = torch.stack([m.hip_forward(x)[0] for m in mine])
     elif mine:
         loc = torch.stack([torch.as_tensor(np.asarray(m.predict(x_test_data, verbose=0))).reshape(-1) for m in mine])
     else:

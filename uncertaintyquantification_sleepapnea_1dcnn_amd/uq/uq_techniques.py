@@ -69,12 +69,10 @@ def mc_dropout_predict(model, x_test_data, n_pred: int = 50, bn_mode: str = "bat
 
     if (D.active() if distributed is None else distributed):
         out = D.mc_dropout_predict_sharded(model, x_test_data, n_pred, bn_mode, seed)
-    elif bn_mode == "running" and getattr(model, "uses_fused", lambda: False)():
-        from ..ops import fused
-
+    elif bn_mode == "running" and getattr(model, "uses_hip", lambda: False)():
+        # fused whole-network kernel (reference architecture) or the layer-wise HIP kernels (any spec)
         x = model._as_input(x_test_data).to(torch.bfloat16).contiguous()
-        out = fused.fused_forward(x, model.fused_blob(), model.spec, n_pass=n_pred, dropout=True,
-                                  seed=model.seed if seed is None else seed)[0].unsqueeze(-1)
+        out = model.hip_forward(x, n_pass=n_pred, dropout=True, seed=seed).unsqueeze(-1)
     elif bn_mode == "running":
         x = model._as_input(x_test_data)
         out = torch.stack([torch.sigmoid(model.logits(x, dropout=True, bn_batch_stats=False, pass_id=t,
@@ -107,6 +105,11 @@ def deep_ensembles_predict(ensemble_models: List, x_test_data, as_numpy: bool = 
         x = m0._as_input(x_test_data).to(torch.bfloat16).contiguous()
         blobs = torch.cat([m.fused_blob().to(m0.device) for m in ensemble_models])
         out = fused.fused_forward(x, blobs, m0.spec)[:, 0].unsqueeze(-1)
+        out = out.float().cpu().numpy() if as_numpy else out
+    elif ensemble_models and all(getattr(m, "uses_hip", lambda: False)() for m in ensemble_models):
+        m0 = ensemble_models[0]
+        x = m0._as_input(x_test_data).to(torch.bfloat16).contiguous()
+        out = torch.stack([m.hip_forward(x.to(m.device))[0].to(m0.device) for m in ensemble_models]).unsqueeze(-1)
         out = out.float().cpu().numpy() if as_numpy else out
     else:
         preds = [np.asarray(m.predict(x_test_data, verbose=0)) for m in ensemble_models]
