@@ -32,8 +32,8 @@ import sysconfig
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 SO_NAME = "_apneauq_hip.so"
-SO_PATH = os.path.join(PKG, SO_NAME)
-BUILD_DIR = os.path.join(HERE, "build")
+SO_PATH = os.environ.get("APNEAUQ_SO_OUT") or os.path.join(PKG, SO_NAME)  # probe variants: another path
+BUILD_DIR = os.path.join(HERE, "build" + ("_" + hashlib.sha1(os.environ.get("APNEAUQ_SO_OUT", "").encode()).hexdigest()[:8] if os.environ.get("APNEAUQ_SO_OUT") else ""))
 ARCH = os.environ.get("APNEAUQ_OFFLOAD_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 DEBUG = os.environ.get("APNEAUQ_DEBUG", "0") not in ("", "0")

@@ -102,6 +102,12 @@ __device__ __forceinline__ int row_time(int grow) { return (grow - kHalo) & 63; 
 #ifndef APNEAUQ_FWD_ABL
 #define APNEAUQ_FWD_ABL 0
 #endif
+// dgrad probe hooks (0 in the library build; nonzero values compute garbage): 1 = epilogue without
+// the R_{l-1} loads, 2 = stage_dz without the global dZ write, 4 = no dY copy-out, 8 = no MFMAs,
+// 16 = stage_dz without its global loads
+#ifndef APNEAUQ_DG_ABL
+#define APNEAUQ_DG_ABL 0
+#endif
 
 constexpr int kStatSlots = 16;
 __device__ __forceinline__ int st_stride(const Args& A, int Cc) { return A.groups * 2 * Cc; }
@@ -128,6 +134,19 @@ __device__ __forceinline__ void bn_affine_to_lds(const Args& A, int l, int g, fl
     t[c] = Ly.beta[c] - mu * sc;
     if (mean) mean[c] = mu;
     if (rstd) rstd[c] = rs;
+  }
+}
+
+// Per-channel batch mean and 1/sqrt(var + eps) of block l, stats group g, into LDS.
+__device__ __forceinline__ void bn_stats_to_lds(const Args& A, int l, int g, float* mean, float* rstd) {
+  const int Cc = C[l + 1];
+  const Layer& Ly = A.L[l];
+  for (int c = threadIdx.x; c < Cc; c += kThreads) {
+    const int ss = st_stride(A, Cc);
+    const float s1 = slot_sum(Ly.st + (g * 2 + 0) * Cc + c, ss), s2 = slot_sum(Ly.st + (g * 2 + 1) * Cc + c, ss);
+    const float mu = s1 * A.inv_count;
+    mean[c] = mu;
+    rstd[c] = rsqrtf(fmaxf(s2 * A.inv_count - mu * mu, 0.f) + A.eps);
   }
 }
 
@@ -330,7 +349,7 @@ __device__ __forceinline__ void stage_dz(const Args& A, char* lds, int ldsrs, in
       const int r = rin + (b + u) * RP;
       const int grow = row0 + r;
       if (b + u >= NK) continue;
-      const bool ok = active && r < NR && valid(grow);
+      const bool ok = active && r < NR && valid(grow) && !(APNEAUQ_DG_ABL & 16);
       q[u].a = ok ? gld<bf16x8>(Ly.R + (long long)grow * Cc + c) : zero8();
       if constexpr (l < 5) q[u].b = ok ? gld<bf16x8>(Ly.dY + (long long)grow * Cc + c) : zero8();
     }
@@ -370,7 +389,7 @@ __device__ __forceinline__ void stage_dz(const Args& A, char* lds, int ldsrs, in
         }
       }
       *reinterpret_cast<bf16x8*>(lds + r * ldsrs + cw * 16) = o;
-      if (gout != nullptr && r >= own_lo && r < own_hi)
+      if (gout != nullptr && r >= own_lo && r < own_hi && !(APNEAUQ_DG_ABL & 2))
         *reinterpret_cast<bf16x8*>(gout + (long long)grow * Cc + c) = o;  // pad rows get their zeros too
     }
   }
@@ -761,6 +780,8 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
   constexpr int CIN = C[l + 1], COUT = C[l];  // conv^T: input = dZ_l channels, output = block l-1 channels
   using T = Tiling<COUT>;
   using CV = Conv<CIN, COUT, KS[l], T::WM, T::WN, false>;
+  // LDS: the staged tile + 7 x 256 per-channel floats = 79.25 KiB, so TWO workgroups fit per CU
+  // (with the previous 9 x 256 floats it was 81.25 KiB and dgrad ran one workgroup per CU)
   char* act = smem;
   float* prm = reinterpret_cast<float*>(smem + kRows * kRS);
   float* gr = prm;           // gamma*rstd of block l
@@ -768,10 +789,8 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
   float* rstd = prm + 512;
   float* mdy = prm + 768;
   float* mdyx = prm + 1024;
-  float* s_prev = prm + 1280;     // block l-1 affine (unused here) and its mean / rstd for xhat
-  float* t_prev = prm + 1536;
-  float* mean_prev = prm + 1792;
-  float* rstd_prev = prm + 2048;
+  float* mean_prev = prm + 1280;  // block l-1 mean / rstd for xhat
+  float* rstd_prev = prm + 1536;
   const int tile = blockIdx.x;
   APNEAUQ_DASSERT(2 * tile < A.B + 1 && blockDim.x == kThreads);
   const int row0 = kR * tile;
@@ -785,13 +804,20 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
       mdy[c] = slot_sum(Ly.bst + c, 2 * CIN) * A.inv_count;
       mdyx[c] = slot_sum(Ly.bst + CIN + c, 2 * CIN) * A.inv_count;
     }
-    bn_affine_to_lds(A, l - 1, 0, s_prev, t_prev, mean_prev, rstd_prev);
+    bn_stats_to_lds(A, l - 1, 0, mean_prev, rstd_prev);
   }
   __syncthreads();
   stage_dz<l, kRows, CIN / 8>(A, act, kRS, row0, 0, gr, mean, rstd, mdy, mdyx, A.L[l].dZ, kHalo, kHalo + kR);
   __syncthreads();
   f32x4 acc[CV::CT][CV::RT];
+#if (APNEAUQ_DG_ABL & 8)
+#pragma unroll
+  for (int c = 0; c < CV::CT; ++c)
+#pragma unroll
+    for (int r = 0; r < CV::RT; ++r) acc[c][r] = f32x4{(float)act[threadIdx.x], 0.f, 0.f, (float)r};
+#else
   CV::run(A.L[l].wd, act, kRS, acc);
+#endif
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave / T::WN, wn = wave % T::WN;
@@ -824,7 +850,11 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
       bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
       *reinterpret_cast<bf16x4*>(act + row * kRS + co0 * 2) = o;
       if (valid) {
+#if (APNEAUQ_DG_ABL & 1)
+        const bf16x4 rr = o;
+#else
         const bf16x4 rr = gld<bf16x4>(Lp.R + (long long)(row0 + kHalo + row) * COUT + co0);
+#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float q = (float)o[i];
@@ -840,7 +870,7 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
   }
   __syncthreads();
   constexpr int CW = COUT / 8;
-  for (int i = threadIdx.x; i < kR * CW; i += kThreads) {
+  for (int i = threadIdx.x; i < ((APNEAUQ_DG_ABL & 4) ? 0 : kR * CW); i += kThreads) {
     const int r = i / CW, cw = i - r * CW;
     *reinterpret_cast<bf16x8*>(Lp.dY + (long long)(row0 + kHalo + r) * COUT + cw * 8) =
         *reinterpret_cast<const bf16x8*>(act + r * kRS + cw * 16);
@@ -1100,10 +1130,11 @@ __global__ void pack_kernel(const float* __restrict__ w, int k, int cin, int cou
 using train::Args;
 
 constexpr int lds_fwd() { return train::kRows * train::kRS + (1024 + 2 * 256) * 4; }  // tile + affine + lstat
-constexpr int lds_dgrad() { return train::kRows * train::kRS + 2304 * 4; }
+constexpr int lds_dgrad() { return train::kRows * train::kRS + 1792 * 4; }
+static_assert(2 * lds_dgrad() <= 160 * 1024, "dgrad must fit two workgroups per CU");
 template <int l>
 constexpr int lds_wgrad() {
-  return train::kR * (train::WgCfg<l>::COB * 2 + 16) + train::kRows * (train::WgCfg<l>::CIB * 2 + 16) + 2304 * 4;
+  return train::kR * (train::WgCfg<l>::COB * 2 + 16) + train::kRows * (train::WgCfg<l>::CIB * 2 + 16) + 1792 * 4;
 }
 
 int train_args_size() { return (int)sizeof(Args); }

@@ -13,7 +13,8 @@ import threading
 import torch
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SO_PATH = os.path.join(_PKG, "_apneauq_hip.so")
+# APNEAUQ_SO_PATH loads a probe variant built with csrc/build.py APNEAUQ_SO_OUT=... (timing ablations only)
+SO_PATH = os.environ.get("APNEAUQ_SO_PATH") or os.path.join(_PKG, "_apneauq_hip.so")
 _lock = threading.Lock()
 _state = {"loaded": False, "error": None}
 
