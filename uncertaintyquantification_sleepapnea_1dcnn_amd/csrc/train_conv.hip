@@ -887,12 +887,15 @@ template <int l> struct WgCfg;
 // batch of 1024 gives >= 256 workgroups without multiplying the output atomics needlessly)
 // MINWG: the launcher lowers the row tiles per workgroup until at least this many workgroups
 // exist (measured at batch 1024: blocks 2-3 prefer fewer, longer workgroups, blocks 4-6 more)
-template <> struct WgCfg<0> { static constexpr int CIB = 32, COB = 128, WCO = 4, WCI = 1, RTILES = 2, MINWG = 512; };  // im2col kk=32
-template <> struct WgCfg<1> { static constexpr int CIB = 32, COB = 192, WCO = 2, WCI = 2, RTILES = 8, MINWG = 256; };
-template <> struct WgCfg<2> { static constexpr int CIB = 32, COB = 224, WCO = 2, WCI = 2, RTILES = 8, MINWG = 256; };
-template <> struct WgCfg<3> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = 512; };
-template <> struct WgCfg<4> { static constexpr int CIB = 16, COB = 128, WCO = 4, WCI = 1, RTILES = 16, MINWG = 512; };
-template <> struct WgCfg<5> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = 512; };
+// U: dZ staging loads in flight per thread; MINB: workgroups per CU the register budget targets
+// (batch-8192 probes, tools/probes/so_variants.sh: U 4 -> 8 saves 10-13 % on blocks 2, 3, 5; three
+// workgroups per CU save 17 % on block 4 and spill on block 6)
+template <> struct WgCfg<0> { static constexpr int CIB = 32, COB = 128, WCO = 4, WCI = 1, RTILES = 2, MINWG = 512, U = 4, MINB = 2; };  // im2col kk=32
+template <> struct WgCfg<1> { static constexpr int CIB = 32, COB = 192, WCO = 2, WCI = 2, RTILES = 8, MINWG = 256, U = 8, MINB = 2; };
+template <> struct WgCfg<2> { static constexpr int CIB = 32, COB = 224, WCO = 2, WCI = 2, RTILES = 8, MINWG = 256, U = 8, MINB = 2; };
+template <> struct WgCfg<3> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = 512, U = 8, MINB = 3; };
+template <> struct WgCfg<4> { static constexpr int CIB = 16, COB = 128, WCO = 4, WCI = 1, RTILES = 16, MINWG = 512, U = 8, MINB = 3; };
+template <> struct WgCfg<5> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = 512, U = 4, MINB = 2; };
 
 __device__ __forceinline__ bf16x8 tr_frag(const char* lds, int ldsrs, int row_base, int col0) {
   // fragment for a 16x16x32 operand whose K index is the LDS row: lane (m, h) gets rows
@@ -914,7 +917,7 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* lds, int ldsrs, int row_ba
 }
 
 template <int l>
-__global__ __launch_bounds__(kThreads, 2) void wgrad_kernel(Args A) {
+__global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A) {
   using W = WgCfg<l>;
   constexpr int CIN = C[l], COUT = C[l + 1], K = KS[l], PAD = (K - 1) / 2;
   constexpr bool FIRST = (l == 0);
@@ -995,8 +998,11 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_kernel(Args A) {
     __syncthreads();
     if constexpr (FIRST)  // no dgrad for block 1: dZ_1 is recomputed here (a single ci block)
       stage_dz<l, kR, W::COB / 8>(A, dz_lds, DZRS, row0 + kHalo, co0, gr, mean, rstd, mdy, mdyx);
-    else
-      stage_dz_copy<l, kR, W::COB / 8, 4>(A, dz_lds, DZRS, row0 + kHalo, co0);
+    else {
+#ifndef APNEAUQ_WG_NODZ  // probe: no dZ staging (wrong dW, timing only)
+      stage_dz_copy<l, kR, W::COB / 8, W::U>(A, dz_lds, DZRS, row0 + kHalo, co0);
+#endif
+    }
     if constexpr (FIRST) {
       // im2col of the raw input: col kk = tap*4 + ci (kk < 28), rows = tile rows
       for (int i = threadIdx.x; i < kR * 32; i += kThreads) {
@@ -1007,7 +1013,9 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad_kernel(Args A) {
         *reinterpret_cast<__bf16*>(a_lds + r * ARS + kk * 2) = v;
       }
     } else {
+#ifndef APNEAUQ_WG_NOA  // probe: no A_{l-1} staging (wrong dW, timing only)
       stage_act<l - 1, kRows, W::CIB / 8, 4>(A, a_lds, ARS, row0, ci0, sp, tp, 0);
+#endif
     }
     __syncthreads();
 #pragma unroll
