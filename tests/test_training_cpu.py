@@ -107,3 +107,33 @@ def test_training_learns_cpu():
     m = AlarconCNN1D(seed=3, device="cpu")
     h = m.fit(x, y.astype(np.float32), batch_size=64, epochs=2, validation_split=0.1, verbose=0)
     assert h.history["loss"][1] < h.history["loss"][0]
+
+
+@pytest.mark.parametrize("pooled", [False, True])
+def test_generic_train_emulation_matches_autograd(pooled, monkeypatch):
+    """The bf16-dataflow oracle of the generic HIP training path (tests/generic_train_emulation.py)
+    is exact fp32 backprop once its quantisation points are switched off (pool routing, dropout,
+    BN backward, dgrad/wgrad index algebra)."""
+    import dataclasses
+
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.models import reference as R
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.models.spec import BlockSpec, ModelSpec
+
+    from . import generic_train_emulation as E
+
+    monkeypatch.setattr(E, "bf", lambda t: t.float())
+    spec = ModelSpec(31, 3, tuple(BlockSpec(f, k, r, pooled and i != 1) for i, (f, k, r) in
+                                  enumerate([(8, 5, 0.3), (12, 3, 0.2), (16, 1, 0.5)])))
+    p = R.synthetic_params(spec, 3)
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(9, 31, 3, generator=g)
+    y = (torch.rand(9, generator=g) > 0.5).float()
+    loss, _, eg, _ = E.emulate_generic_step(spec, p, x, y, seed=4, pass_id=7)
+    q = {k: (v.clone().requires_grad_(True) if not k.endswith(("moving_mean", "moving_variance")) else v.clone())
+         for k, v in p.items()}
+    lg = R.forward(spec, q, x, dropout=True, bn_batch_stats=True, seed=4, pass_id=7, return_logits=True)
+    lv = torch.nn.functional.binary_cross_entropy_with_logits(lg.reshape(-1), y, reduction="none")
+    lv.mean().backward()
+    assert abs(lv.sum().item() - loss) < 1e-4 * max(1.0, loss)
+    for k, v in eg.items():
+        torch.testing.assert_close(v.reshape(q[k].grad.shape), q[k].grad, atol=1e-5, rtol=1e-4)

@@ -27,7 +27,19 @@ hipError_t train_bump_counters(int* c, int n, hipStream_t st);
 hipError_t launch_generic_conv(const void* x, const void* wfrag, const float* epi, void* y, int n, int L, int cin,
                                int cout, int cout_pad, int ksize, int pool, int dropout, unsigned thr, int layer,
                                int n_win, unsigned pass_offset, unsigned window_offset, unsigned long long seed,
-                               hipStream_t stream);
+                               hipStream_t stream, int mode, int in_rs, int in_off, float* stats);
+hipError_t launch_gt_bn_finalize(const float* st, int C, float inv_count, const float* gamma, const float* beta,
+                                 float eps, float momentum, float* mmean, float* mvar, int update, float* bn,
+                                 hipStream_t stream);
+hipError_t launch_gt_apply(const void* z, const float* bn, void* out, int n, int L, int C, int pool, int out_rs,
+                           int out_off, int dropout, unsigned thr, float inv_keep, unsigned skey,
+                           unsigned window_offset, hipStream_t stream);
+hipError_t launch_gt_bwd(int dz_mode, const void* z, const float* bn, const void* dh, const float* dlog,
+                         const float* w, float invL, int n, int L, int C, int pool, int dropout, unsigned thr,
+                         float inv_keep, unsigned skey, unsigned window_offset, float* bst, const float* coef,
+                         const float* gamma, void* dz, int dz_rs, int dz_off, float* gbias, hipStream_t stream);
+hipError_t launch_gt_bwd_finalize(const float* bst, int C, float inv_count, float* coef, float* ggamma, float* gbeta,
+                                  hipStream_t stream);
 hipError_t launch_generic_head(const void* y, const float* w, float b, int n, int L, int C, int out_logits, float* out,
                                hipStream_t stream);
 namespace train {
@@ -276,9 +288,148 @@ at::Tensor generic_conv(const at::Tensor& x, const at::Tensor& wfrag, const at::
   check(apneauq::launch_generic_conv(x.data_ptr(), wfrag.data_ptr(), epi.data_ptr<float>(), y.data_ptr(), (int)n, (int)L,
                                      (int)cin, (int)cout, (int)cout_pad, (int)ksize, pool ? 1 : 0, dropout ? 1 : 0,
                                      (unsigned)thr, (int)layer, (int)n_win, (unsigned)pass_offset, (unsigned)window_offset,
-                                     (unsigned long long)seed, cur_stream()),
+                                     (unsigned long long)seed, cur_stream(), 0, (int)L, 0, nullptr),
         "generic_conv");
   return y;
+}
+
+// ---- generic-spec training (csrc/generic_train.hip); every buffer is preallocated by ops/generic_train.py ----
+inline void need_rows(const at::Tensor& t, int64_t rows, int64_t c, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.is_contiguous(), what, ": bf16 contiguous GPU tensor required");
+  TORCH_CHECK(t.numel() >= rows * c, what, ": buffer too small (", t.numel(), " < ", rows * c, ")");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, what, ": 16-B alignment required");
+}
+inline void need_f32(const at::Tensor& t, int64_t n, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() >= n, what,
+              ": fp32 contiguous GPU tensor of >= ", n, " elements required");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, what, ": 16-B alignment required");
+}
+constexpr int64_t kGtSlots = 16;
+
+// mode 1: y = relu(conv(x) + bias) (N, L, Cout) + BN moment slots; mode 2: y = conv(x) (dgrad).
+// x row (n, t) lives at n * in_rs + in_off + t (zero-padded layouts); the conv reads rows
+// in_off - pad .. in_off + L - 1 + pad of each sample, all of which must exist.
+void gt_conv(const at::Tensor& x, const at::Tensor& wfrag, const c10::optional<at::Tensor>& bias, at::Tensor& y,
+             const c10::optional<at::Tensor>& stats, int64_t n, int64_t L, int64_t cin, int64_t cout, int64_t ksize,
+             int64_t mode, int64_t in_rs, int64_t in_off) {
+  TORCH_CHECK(mode == 1 || mode == 2, "gt_conv: mode must be 1 (train) or 2 (linear)");
+  TORCH_CHECK(ksize % 2 == 1 && cout % 4 == 0 && cout <= 1024 && n >= 0 && L >= 1, "gt_conv: bad shape");
+  TORCH_CHECK(wfrag.is_cuda() && wfrag.scalar_type() == at::kBFloat16 && wfrag.is_contiguous() && wfrag.dim() == 4 &&
+              wfrag.size(0) == (ksize * cin + 31) / 32 && wfrag.size(2) == 64 && wfrag.size(3) == 8 &&
+              wfrag.size(1) * 16 >= cout && wfrag.size(1) * 16 - cout < 16, "gt_conv: wfrag shape mismatch");
+  const int64_t pad = (ksize - 1) / 2;
+  TORCH_CHECK(in_rs >= L && in_off >= 0, "gt_conv: bad input row layout");
+  if (n > 0) need_rows(x, (n - 1) * in_rs + in_off + L, cin, "gt_conv x");
+  (void)pad;  // rows outside [0, L) of a sample are masked in the kernel, never read
+  need_rows(y, n * L, cout, "gt_conv y");
+  const float* bp = nullptr;
+  float* sp = nullptr;
+  if (mode == 1) {
+    TORCH_CHECK(bias.has_value() && stats.has_value(), "gt_conv: mode 1 needs bias and stats");
+    need_f32(*bias, cout, "gt_conv bias");
+    need_f32(*stats, kGtSlots * 2 * cout, "gt_conv stats");
+    bp = bias->data_ptr<float>();
+    sp = stats->data_ptr<float>();
+  }
+  TORCH_CHECK(n * L < (int64_t(1) << 31), "gt_conv: too many rows");
+  const at::DeviceGuard guard(y.device());
+  check(apneauq::launch_generic_conv(x.data_ptr(), wfrag.data_ptr(), bp, y.data_ptr(), (int)n, (int)L, (int)cin,
+                                     (int)cout, (int)(wfrag.size(1) * 16), (int)ksize, 0, 0, 0u, 0, 1, 0u, 0u, 0ull,
+                                     cur_stream(), (int)mode, (int)in_rs, (int)in_off, sp),
+        "gt_conv");
+}
+
+void gt_bn_finalize(const at::Tensor& st, int64_t C, double inv_count, const at::Tensor& gamma, const at::Tensor& beta,
+                    double eps, double momentum, at::Tensor& mmean, at::Tensor& mvar, bool update, at::Tensor& bn) {
+  need_f32(st, kGtSlots * 2 * C, "gt_bn_finalize st");
+  TORCH_CHECK(gamma.is_cuda() && gamma.numel() == C && beta.numel() == C && mmean.numel() == C && mvar.numel() == C,
+              "gt_bn_finalize: per-channel tensors must have C elements");
+  need_f32(bn, 4 * C, "gt_bn_finalize bn");
+  const at::DeviceGuard guard(bn.device());
+  check(apneauq::launch_gt_bn_finalize(st.data_ptr<float>(), (int)C, (float)inv_count, gamma.data_ptr<float>(),
+                                       beta.data_ptr<float>(), (float)eps, (float)momentum, mmean.data_ptr<float>(),
+                                       mvar.data_ptr<float>(), update ? 1 : 0, bn.data_ptr<float>(), cur_stream()),
+        "gt_bn_finalize");
+}
+
+void gt_apply(const at::Tensor& z, const at::Tensor& bn, at::Tensor& out, int64_t n, int64_t L, int64_t C, bool pool,
+              int64_t out_rs, int64_t out_off, bool dropout, int64_t thr, double inv_keep, int64_t skey,
+              int64_t window_offset) {
+  TORCH_CHECK(C % 4 == 0 && C <= 1024 && L >= 1, "gt_apply: bad shape");
+  const int64_t lout = pool ? L / 2 : L;
+  need_rows(z, n * L, C, "gt_apply z");
+  need_f32(bn, 4 * C, "gt_apply bn");
+  TORCH_CHECK(out_rs >= lout && out_off >= 0, "gt_apply: bad output row layout");
+  if (n > 0) need_rows(out, (n - 1) * out_rs + out_off + lout, C, "gt_apply out");
+  const at::DeviceGuard guard(out.device());
+  check(apneauq::launch_gt_apply(z.data_ptr(), bn.data_ptr<float>(), out.data_ptr(), (int)n, (int)L, (int)C, pool ? 1 : 0,
+                                 (int)out_rs, (int)out_off, dropout ? 1 : 0, (unsigned)thr, (float)inv_keep,
+                                 (unsigned)skey, (unsigned)window_offset, cur_stream()),
+        "gt_apply");
+}
+
+// dz_mode 0: BN-backward sums into bst; 1: dz (zero-padded rows) + bias gradient.  The upstream
+// gradient is dh (N, L/2 or L, C) bf16, or (head mode, dh undefined) dlog[n] * w[c] * invL.
+void gt_bwd(bool dz_mode, const at::Tensor& z, const at::Tensor& bn, const c10::optional<at::Tensor>& dh,
+            const c10::optional<at::Tensor>& dlog, const c10::optional<at::Tensor>& w, double invL, int64_t n, int64_t L,
+            int64_t C, bool pool, bool dropout, int64_t thr, double inv_keep, int64_t skey, int64_t window_offset,
+            const c10::optional<at::Tensor>& bst, const c10::optional<at::Tensor>& coef,
+            const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& dz, int64_t dz_rs, int64_t dz_off,
+            const c10::optional<at::Tensor>& gbias) {
+  TORCH_CHECK(C % 4 == 0 && C <= 1024 && L >= 1, "gt_bwd: bad shape");
+  const int64_t lout = pool ? L / 2 : L;
+  need_rows(z, n * L, C, "gt_bwd z");
+  need_f32(bn, 4 * C, "gt_bwd bn");
+  const void* dhp = nullptr;
+  const float *dlp = nullptr, *wp = nullptr;
+  if (dh.has_value()) {
+    need_rows(*dh, n * lout, C, "gt_bwd dh");
+    dhp = dh->data_ptr();
+  } else {
+    TORCH_CHECK(dlog.has_value() && w.has_value(), "gt_bwd: need dh or (dlog, w)");
+    need_f32(*dlog, n, "gt_bwd dlog");
+    need_f32(*w, C, "gt_bwd w");
+    dlp = dlog->data_ptr<float>();
+    wp = w->data_ptr<float>();
+  }
+  float* bp = nullptr;
+  const float *cp = nullptr, *gp = nullptr;
+  void* dzp = nullptr;
+  float* gbp = nullptr;
+  if (!dz_mode) {
+    TORCH_CHECK(bst.has_value(), "gt_bwd: stats mode needs bst");
+    need_f32(*bst, kGtSlots * 2 * C, "gt_bwd bst");
+    bp = bst->data_ptr<float>();
+  } else {
+    TORCH_CHECK(coef.has_value() && gamma.has_value() && dz.has_value() && gbias.has_value(), "gt_bwd: dz mode args");
+    need_f32(*coef, 2 * C, "gt_bwd coef");
+    TORCH_CHECK(gamma->is_cuda() && gamma->numel() == C, "gt_bwd gamma");
+    TORCH_CHECK(dz_rs >= L && dz_off >= 0, "gt_bwd: bad dz row layout");
+    if (n > 0) need_rows(*dz, (n - 1) * dz_rs + dz_off + L, C, "gt_bwd dz");
+    TORCH_CHECK(gbias->is_cuda() && gbias->scalar_type() == at::kFloat && gbias->numel() == C, "gt_bwd gbias");
+    cp = coef->data_ptr<float>();
+    gp = gamma->data_ptr<float>();
+    dzp = dz->data_ptr();
+    gbp = gbias->data_ptr<float>();
+  }
+  const at::DeviceGuard guard(z.device());
+  check(apneauq::launch_gt_bwd(dz_mode ? 1 : 0, z.data_ptr(), bn.data_ptr<float>(), dhp, dlp, wp, (float)invL, (int)n,
+                               (int)L, (int)C, pool ? 1 : 0, dropout ? 1 : 0, (unsigned)thr, (float)inv_keep,
+                               (unsigned)skey, (unsigned)window_offset, bp, cp, gp, dzp, (int)dz_rs, (int)dz_off, gbp,
+                               cur_stream()),
+        "gt_bwd");
+}
+
+void gt_bwd_finalize(const at::Tensor& bst, int64_t C, double inv_count, at::Tensor& coef, at::Tensor& ggamma,
+                     at::Tensor& gbeta) {
+  need_f32(bst, kGtSlots * 2 * C, "gt_bwd_finalize bst");
+  need_f32(coef, 2 * C, "gt_bwd_finalize coef");
+  TORCH_CHECK(ggamma.is_cuda() && ggamma.scalar_type() == at::kFloat && ggamma.numel() == C && gbeta.numel() == C,
+              "gt_bwd_finalize: grads must have C elements");
+  const at::DeviceGuard guard(coef.device());
+  check(apneauq::launch_gt_bwd_finalize(bst.data_ptr<float>(), (int)C, (float)inv_count, coef.data_ptr<float>(),
+                                        ggamma.data_ptr<float>(), gbeta.data_ptr<float>(), cur_stream()),
+        "gt_bwd_finalize");
 }
 
 at::Tensor generic_head(const at::Tensor& y, const at::Tensor& w, double b, bool out_logits) {
@@ -320,6 +471,16 @@ TORCH_LIBRARY(apneauq, m) {
   m.def("generic_conv(Tensor x, Tensor wfrag, Tensor epi, int cout, int ksize, bool pool, bool dropout, int thr, "
         "int layer, int n_win, int pass_offset, int window_offset, int seed) -> Tensor");
   m.def("generic_head(Tensor y, Tensor w, float b, bool logits) -> Tensor");
+  m.def("gt_conv(Tensor x, Tensor wfrag, Tensor? bias, Tensor(a!) y, Tensor(b!)? stats, int n, int L, int cin, "
+        "int cout, int ksize, int mode, int in_rs, int in_off) -> ()");
+  m.def("gt_bn_finalize(Tensor st, int C, float inv_count, Tensor gamma, Tensor beta, float eps, float momentum, "
+        "Tensor(a!) mmean, Tensor(b!) mvar, bool update, Tensor(c!) bn) -> ()");
+  m.def("gt_apply(Tensor z, Tensor bn, Tensor(a!) out, int n, int L, int C, bool pool, int out_rs, int out_off, "
+        "bool dropout, int thr, float inv_keep, int skey, int window_offset) -> ()");
+  m.def("gt_bwd(bool dz_mode, Tensor z, Tensor bn, Tensor? dh, Tensor? dlog, Tensor? w, float invL, int n, int L, "
+        "int C, bool pool, bool dropout, int thr, float inv_keep, int skey, int window_offset, Tensor(a!)? bst, "
+        "Tensor? coef, Tensor? gamma, Tensor(b!)? dz, int dz_rs, int dz_off, Tensor(c!)? gbias) -> ()");
+  m.def("gt_bwd_finalize(Tensor bst, int C, float inv_count, Tensor(a!) coef, Tensor(b!) ggamma, Tensor(c!) gbeta) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
@@ -331,4 +492,9 @@ TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
   m.impl("train_pack", &train_pack);
   m.impl("generic_conv", &generic_conv);
   m.impl("generic_head", &generic_head);
+  m.impl("gt_conv", &gt_conv);
+  m.impl("gt_bn_finalize", &gt_bn_finalize);
+  m.impl("gt_apply", &gt_apply);
+  m.impl("gt_bwd", &gt_bwd);
+  m.impl("gt_bwd_finalize", &gt_bwd_finalize);
 }

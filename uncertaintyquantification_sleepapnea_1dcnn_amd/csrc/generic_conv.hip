@@ -37,11 +37,19 @@ struct ConvArgs {
   int n_win;              // samples per pass (sample s: pass s / n_win, window s % n_win)
   unsigned pass_offset, window_offset;
   unsigned long long seed;
+  int in_rs, in_off;      // input row addressing: sample n, step t at row n * in_rs + in_off + t
+  float* stats;           // kTrain: BN moment sums (kStatSlots, 2, Cout)
 };
+
+// Epilogue modes: kInfer = bias + ReLU + BN(running) [+ pool] [+ dropout] (the folded epi rows);
+// kTrain = relu(acc + bias) stored as the pre-BN activation z, with the per-channel BN moments
+// (sum, sum of squares) accumulated into kStatSlots interleaved copies; kLinear = acc as is (dgrad).
+enum { kInfer = 0, kTrain = 1, kLinear = 2 };
+constexpr int kStatSlots = 16;
 
 constexpr int kRT = 4, kCT = 4;  // row / channel tiles per wave; a workgroup is 2 x 2 waves
 
-template <bool VEC>
+template <bool VEC, int MODE>
 __global__ __launch_bounds__(256) void conv_block_kernel(ConvArgs A) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int m = lane & 15, h = lane >> 4;
@@ -78,7 +86,7 @@ __global__ __launch_bounds__(256) void conv_block_kernel(ConvArgs A) {
     bf16x8 b[kRT];
 #pragma unroll
     for (int r = 0; r < kRT; ++r) {
-      const __bf16* xs = A.x + (long long)rn[r] * A.L * A.cin;
+      const __bf16* xs = A.x + ((long long)rn[r] * A.in_rs + A.in_off) * A.cin;
       if constexpr (VEC) {
         const int ts = rt[r] + tap - pad;
         if (rok[r] && kk0 < K && ts >= 0 && ts < A.L) {
@@ -115,6 +123,55 @@ __global__ __launch_bounds__(256) void conv_block_kernel(ConvArgs A) {
     }
   }
 
+  if constexpr (MODE != kInfer) {
+    // training / dgrad epilogue: no pool, no dropout; y is (N, L, Cout)
+    float* st = A.stats + (blockIdx.x % kStatSlots) * 2 * A.cout;
+#pragma unroll
+    for (int c = 0; c < kCT; ++c) {
+      const int ct = ct0 + c;
+      if (ct >= nct) break;  // wave-uniform
+      const int co0 = ct * 16 + 4 * h;
+      const bool cok = co0 < A.cout;
+      float bi[4] = {0.f, 0.f, 0.f, 0.f};
+      if (MODE == kTrain && cok) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bi[i] = A.epi[co0 + i];
+      }
+      float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < kRT; ++r) {
+        f32x4 v = acc[c][r];
+        if constexpr (MODE == kTrain) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            v[i] = fmaxf(v[i] + bi[i], 0.f);
+            const float u = rok[r] ? v[i] : 0.f;
+            s1[i] += u;
+            s2[i] += u * u;
+          }
+        }
+        if (rok[r] && cok) {
+          __bf16* dst = A.y + ((long long)rn[r] * A.L + rt[r]) * A.cout + co0;
+          *reinterpret_cast<bf16x4*>(dst) = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+        }
+      }
+      if constexpr (MODE == kTrain) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          s1[i] = group16_sum(s1[i]);
+          s2[i] = group16_sum(s2[i]);
+        }
+        if (m == 0 && cok) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            atomicAdd(st + co0 + i, s1[i]);
+            atomicAdd(st + A.cout + co0 + i, s2[i]);
+          }
+        }
+      }
+    }
+    return;
+  }
   // epilogue: per row tile, the lane holds row (n, t) x channels co0 .. co0+3 of each channel tile
   const float* epi = A.epi + (A.dropout ? 4 * A.cout_pad : 0);
 #pragma unroll
@@ -180,7 +237,7 @@ __global__ __launch_bounds__(256) void head_kernel(const __bf16* y, const float*
 hipError_t launch_generic_conv(const void* x, const void* wfrag, const float* epi, void* y, int n, int L, int cin,
                                int cout, int cout_pad, int ksize, int pool, int dropout, unsigned thr, int layer,
                                int n_win, unsigned pass_offset, unsigned window_offset, unsigned long long seed,
-                               hipStream_t stream) {
+                               hipStream_t stream, int mode, int in_rs, int in_off, float* stats) {
   generic::ConvArgs A;
   A.x = reinterpret_cast<const __bf16*>(x);
   A.wfrag = reinterpret_cast<const bf16x8*>(wfrag);
@@ -203,14 +260,32 @@ hipError_t launch_generic_conv(const void* x, const void* wfrag, const float* ep
   A.pass_offset = pass_offset;
   A.window_offset = window_offset;
   A.seed = seed;
+  A.in_rs = in_rs > 0 ? in_rs : L;
+  A.in_off = in_off;
+  A.stats = stats;
+  if (mode != generic::kInfer) {
+    A.pool = 0;
+    A.Lp = L;
+    A.lout = L;
+    A.dropout = 0;
+  }
   const long long rows = (long long)n * A.Lp;
   if (rows == 0) return hipSuccess;
   constexpr int kRowsWG = 2 * generic::kRT * 16, kChWG = 2 * generic::kCT;  // 128 rows x 8 channel tiles
   const dim3 grid((unsigned)((rows + kRowsWG - 1) / kRowsWG), (unsigned)((cout_pad / 16 + kChWG - 1) / kChWG));
-  if (cin % 8 == 0)
-    hipLaunchKernelGGL(generic::conv_block_kernel<true>, grid, dim3(256), 0, stream, A);
-  else
-    hipLaunchKernelGGL(generic::conv_block_kernel<false>, grid, dim3(256), 0, stream, A);
+#define APNEAUQ_GCONV(M)                                                                   \
+  if (cin % 8 == 0)                                                                        \
+    hipLaunchKernelGGL((generic::conv_block_kernel<true, M>), grid, dim3(256), 0, stream, A); \
+  else                                                                                     \
+    hipLaunchKernelGGL((generic::conv_block_kernel<false, M>), grid, dim3(256), 0, stream, A);
+  if (mode == generic::kTrain) {
+    APNEAUQ_GCONV(generic::kTrain)
+  } else if (mode == generic::kLinear) {
+    APNEAUQ_GCONV(generic::kLinear)
+  } else {
+    APNEAUQ_GCONV(generic::kInfer)
+  }
+#undef APNEAUQ_GCONV
   return hipGetLastError();
 }
 

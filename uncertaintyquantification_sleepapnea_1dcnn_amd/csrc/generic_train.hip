@@ -1,0 +1,332 @@
+// Layer-wise HIP training kernels for ANY ModelSpec (gfx950 / MI355X): the opt-in MaxPool1D blocks,
+// other window shapes (the "30 s single-channel" ModelSpec(30, 1)), other filter / kernel sizes.
+// Reference semantics: one Keras train_on_batch of the SURVEY §2.2 stack (cnn_baseline_train.py:55-102):
+//   z = relu(conv(h) + b);  y = BN_batch(z);  [y = MaxPool1D(2)(y)];  h' = Dropout(y)
+// The reference architecture has its own persistent, LDS-resident kernels (train_conv.hip); this
+// path is built from the generic implicit-GEMM MFMA conv (generic_conv.hip, modes kTrain / kLinear)
+// plus the memory-bound pieces below, each one pass over bf16 activations:
+//
+//   bn_finalize   moment slots -> (scale, shift, mean, rstd) + Keras moving-average update
+//   apply         BN affine + 2:1 max pool + counter-based dropout -> next layer's input, written in
+//                 the consumer's zero-padded row layout (so wgrad is a plain strided GEMM)
+//   bwd_stats     upstream grad routed back through dropout (same keys) and the pool (argmax
+//                 recomputed from z) -> per-channel sum(dy), sum(dy * xhat)
+//   bwd_finalize  -> dgamma, dbeta and the two BN-backward coefficients
+//   bwd_dz        dz = relu'(z) * gamma * rstd * (dy - E[dy] - xhat E[dy xhat]) written zero-padded,
+//                 bias gradient as a fused column sum
+//
+// Channel-group mapping of the elementwise kernels: a thread owns 4 consecutive channels of one
+// row (8-byte bf16x4 accesses), G = C/4 <= 256 groups across the block, 256 / G rows per sweep.
+#include "common.h"
+
+namespace apneauq {
+namespace gtrain {
+
+constexpr int kSlots = 16;  // == generic::kStatSlots
+
+__global__ void bn_finalize_kernel(const float* st, int C, float inv_count, const float* gamma, const float* beta,
+                                   float eps, float momentum, float* mmean, float* mvar, int update, float* bn) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int s = 0; s < kSlots; ++s) {
+    s1 += st[s * 2 * C + c];
+    s2 += st[s * 2 * C + C + c];
+  }
+  const double meand = s1 * inv_count;
+  const float mean = (float)meand;
+  const float var = (float)fmax(s2 * inv_count - meand * meand, 0.0);
+  const float rstd = rsqrtf(var + eps);
+  const float scale = gamma[c] * rstd;
+  bn[c] = scale;
+  bn[C + c] = beta[c] - mean * scale;
+  bn[2 * C + c] = mean;
+  bn[3 * C + c] = rstd;
+  if (update) {
+    mmean[c] = mmean[c] * momentum + mean * (1.f - momentum);
+    mvar[c] = mvar[c] * momentum + var * (1.f - momentum);
+  }
+}
+
+__device__ __forceinline__ f32x4 load4(const __bf16* p) {
+  const bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
+  return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+
+struct ApplyArgs {
+  const __bf16* z;  // (N, L, C) pre-BN activations
+  const float* bn;  // (4, C): scale, shift, mean, rstd
+  __bf16* out;      // row (n, t) at n * out_rs + out_off + t
+  int n, L, C, pool, lout, out_rs, out_off, dropout;
+  unsigned thr;
+  float inv_keep;
+  unsigned skey;  // stream_key(seed, layer, pass)
+  unsigned window_offset;
+};
+
+__global__ __launch_bounds__(256) void apply_kernel(ApplyArgs A) {
+  const int G = A.C >> 2;
+  const long long total = (long long)A.n * A.lout * G;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int c = (int)(i % G) * 4;
+    const long long row = i / G;
+    const int ns = (int)(row / A.lout), to = (int)(row - (long long)ns * A.lout);
+    const int t0 = A.pool ? 2 * to : to;
+    const __bf16* zr = A.z + ((long long)ns * A.L + t0) * A.C + c;
+    const f32x4 sc = *reinterpret_cast<const f32x4*>(A.bn + c);
+    const f32x4 sh = *reinterpret_cast<const f32x4*>(A.bn + A.C + c);
+    f32x4 y = load4(zr);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y[j] = __builtin_fmaf(y[j], sc[j], sh[j]);
+    if (A.pool) {
+      const f32x4 y1 = load4(zr + A.C);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) y[j] = fmaxf(y[j], __builtin_fmaf(y1[j], sc[j], sh[j]));
+    }
+    if (A.dropout) {
+      const unsigned key = sample_key(A.skey, A.window_offset + (unsigned)ns);
+      const unsigned b01 = dropout_bits2(key, (unsigned)to, (unsigned)c);
+      const unsigned b23 = dropout_bits2(key, (unsigned)to, (unsigned)c + 2);
+      y[0] = (b01 & 0xFFFFu) >= A.thr ? y[0] * A.inv_keep : 0.f;
+      y[1] = (b01 >> 16) >= A.thr ? y[1] * A.inv_keep : 0.f;
+      y[2] = (b23 & 0xFFFFu) >= A.thr ? y[2] * A.inv_keep : 0.f;
+      y[3] = (b23 >> 16) >= A.thr ? y[3] * A.inv_keep : 0.f;
+    }
+    __bf16* dst = A.out + ((long long)ns * A.out_rs + A.out_off + to) * A.C + c;
+    *reinterpret_cast<bf16x4*>(dst) = bf16x4{(__bf16)y[0], (__bf16)y[1], (__bf16)y[2], (__bf16)y[3]};
+  }
+}
+
+struct BwdArgs {
+  const __bf16* z;     // (N, L, C)
+  const float* bn;     // (4, C)
+  const __bf16* dh;    // (N, lout, C) upstream gradient, or nullptr in head mode
+  const float* dlog;   // head mode: dh[n, t, c] = dlog[n] * w[c] * invL
+  const float* w;
+  float invL;
+  int n, L, C, pool, lout, dropout;
+  unsigned thr;
+  float inv_keep;
+  unsigned skey, window_offset;
+  float* bst;          // bwd_stats: (kSlots, 2, C) sums of dy, dy * xhat
+  const float* coef;   // bwd_dz: (2, C) E[dy], E[dy xhat]
+  const float* gamma;
+  __bf16* dz;          // bwd_dz: row (n, t) at n * dz_rs + dz_off + t
+  int dz_rs, dz_off;
+  float* gbias;        // bwd_dz: bias gradient (C,)
+};
+
+// Gradient w.r.t. the BN output y at pre-pool row (ns, t), channels c .. c+3.
+__device__ __forceinline__ f32x4 upstream_dy(const BwdArgs& A, int ns, int t, int c, const f32x4& sc,
+                                             const f32x4& sh) {
+  f32x4 g = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int to = A.pool ? (t >> 1) : t;
+  if (to >= A.lout) return g;  // odd L with pool: the last step is dropped by the valid pool
+  if (A.dh != nullptr) {
+    g = load4(A.dh + ((long long)ns * A.lout + to) * A.C + c);
+  } else {
+    const float d = A.dlog[ns] * A.invL;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) g[j] = d * A.w[c + j];
+  }
+  if (A.dropout) {
+    const unsigned key = sample_key(A.skey, A.window_offset + (unsigned)ns);
+    const unsigned b01 = dropout_bits2(key, (unsigned)to, (unsigned)c);
+    const unsigned b23 = dropout_bits2(key, (unsigned)to, (unsigned)c + 2);
+    g[0] = (b01 & 0xFFFFu) >= A.thr ? g[0] * A.inv_keep : 0.f;
+    g[1] = (b01 >> 16) >= A.thr ? g[1] * A.inv_keep : 0.f;
+    g[2] = (b23 & 0xFFFFu) >= A.thr ? g[2] * A.inv_keep : 0.f;
+    g[3] = (b23 >> 16) >= A.thr ? g[3] * A.inv_keep : 0.f;
+  }
+  if (A.pool) {  // max-pool backward: the gradient goes to the (first) maximum of the pair
+    const __bf16* zr = A.z + (long long)ns * A.L * A.C + c;
+    const f32x4 za = load4(zr + (long long)t * A.C), zb = load4(zr + (long long)(t ^ 1) * A.C);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float ya = __builtin_fmaf(za[j], sc[j], sh[j]), yb = __builtin_fmaf(zb[j], sc[j], sh[j]);
+      const bool win = (t & 1) == 0 ? ya >= yb : ya > yb;
+      g[j] = win ? g[j] : 0.f;
+    }
+  }
+  return g;
+}
+
+// Block reduction of 8 per-thread partial sums per channel group; returns in threads tid < G.
+__device__ __forceinline__ void block_reduce8(float* lds, float (&v)[8], int G, int rpb) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) lds[j * 256 + tid] = v[j];
+  __syncthreads();
+  if (tid < G) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float s = 0.f;
+      for (int r = 1; r < rpb; ++r) s += lds[j * 256 + r * G + tid];
+      v[j] += s;
+    }
+  }
+}
+
+template <bool DZ>
+__global__ __launch_bounds__(256) void bwd_kernel(BwdArgs A) {
+  __shared__ float lds[8 * 256];
+  const int G = A.C >> 2;
+  const int rpb = 256 / G;
+  const int cg = threadIdx.x % G, rl = threadIdx.x / G;
+  const int c = cg * 4;
+  const bool active = rl < rpb;
+  const long long rows = (long long)A.n * A.L;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (active) {
+    const f32x4 sc = *reinterpret_cast<const f32x4*>(A.bn + c);
+    const f32x4 sh = *reinterpret_cast<const f32x4*>(A.bn + A.C + c);
+    const f32x4 mu = *reinterpret_cast<const f32x4*>(A.bn + 2 * A.C + c);
+    const f32x4 rs = *reinterpret_cast<const f32x4*>(A.bn + 3 * A.C + c);
+    f32x4 k0 = f32x4{0.f, 0.f, 0.f, 0.f}, k1 = k0, gr = k0;
+    if constexpr (DZ) {
+      k0 = *reinterpret_cast<const f32x4*>(A.coef + c);
+      k1 = *reinterpret_cast<const f32x4*>(A.coef + A.C + c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) gr[j] = A.gamma[c + j] * rs[j];
+    }
+    for (long long row = (long long)blockIdx.x * rpb + rl; row < rows; row += (long long)gridDim.x * rpb) {
+      const int ns = (int)(row / A.L), t = (int)(row - (long long)ns * A.L);
+      const f32x4 dy = upstream_dy(A, ns, t, c, sc, sh);
+      const f32x4 z = load4(A.z + row * A.C + c);
+      if constexpr (!DZ) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[j] += dy[j];
+          acc[4 + j] += dy[j] * (z[j] - mu[j]) * rs[j];
+        }
+      } else {
+        f32x4 d;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float xh = (z[j] - mu[j]) * rs[j];
+          d[j] = z[j] > 0.f ? gr[j] * (dy[j] - k0[j] - xh * k1[j]) : 0.f;
+          acc[j] += d[j];
+        }
+        __bf16* dst = A.dz + ((long long)ns * A.dz_rs + A.dz_off + t) * A.C + c;
+        *reinterpret_cast<bf16x4*>(dst) = bf16x4{(__bf16)d[0], (__bf16)d[1], (__bf16)d[2], (__bf16)d[3]};
+      }
+    }
+  }
+  block_reduce8(lds, acc, G, rpb);
+  if (threadIdx.x < G) {
+    if constexpr (!DZ) {
+      float* st = A.bst + (blockIdx.x % kSlots) * 2 * A.C;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        atomicAdd(st + c + j, acc[j]);
+        atomicAdd(st + A.C + c + j, acc[4 + j]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) atomicAdd(A.gbias + c + j, acc[j]);
+    }
+  }
+}
+
+__global__ void bwd_finalize_kernel(const float* bst, int C, float inv_count, float* coef, float* ggamma,
+                                    float* gbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s1 = 0.f, s2 = 0.f;
+  for (int s = 0; s < kSlots; ++s) {
+    s1 += bst[s * 2 * C + c];
+    s2 += bst[s * 2 * C + C + c];
+  }
+  gbeta[c] = s1;
+  ggamma[c] = s2;
+  coef[c] = s1 * inv_count;
+  coef[C + c] = s2 * inv_count;
+}
+
+inline int elem_grid(long long items, int per_block) {
+  long long g = (items + per_block - 1) / per_block;
+  return (int)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
+}
+
+}  // namespace gtrain
+
+hipError_t launch_gt_bn_finalize(const float* st, int C, float inv_count, const float* gamma, const float* beta,
+                                 float eps, float momentum, float* mmean, float* mvar, int update, float* bn,
+                                 hipStream_t stream) {
+  hipLaunchKernelGGL(gtrain::bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, st, C, inv_count, gamma,
+                     beta, eps, momentum, mmean, mvar, update, bn);
+  return hipGetLastError();
+}
+
+hipError_t launch_gt_apply(const void* z, const float* bn, void* out, int n, int L, int C, int pool, int out_rs,
+                           int out_off, int dropout, unsigned thr, float inv_keep, unsigned skey,
+                           unsigned window_offset, hipStream_t stream) {
+  gtrain::ApplyArgs A;
+  A.z = reinterpret_cast<const __bf16*>(z);
+  A.bn = bn;
+  A.out = reinterpret_cast<__bf16*>(out);
+  A.n = n;
+  A.L = L;
+  A.C = C;
+  A.pool = pool;
+  A.lout = pool ? L / 2 : L;
+  A.out_rs = out_rs;
+  A.out_off = out_off;
+  A.dropout = dropout;
+  A.thr = thr;
+  A.inv_keep = inv_keep;
+  A.skey = skey;
+  A.window_offset = window_offset;
+  const long long items = (long long)n * A.lout * (C / 4);
+  if (items == 0) return hipSuccess;
+  hipLaunchKernelGGL(gtrain::apply_kernel, dim3(gtrain::elem_grid(items, 256)), dim3(256), 0, stream, A);
+  return hipGetLastError();
+}
+
+hipError_t launch_gt_bwd(int dz_mode, const void* z, const float* bn, const void* dh, const float* dlog,
+                         const float* w, float invL, int n, int L, int C, int pool, int dropout, unsigned thr,
+                         float inv_keep, unsigned skey, unsigned window_offset, float* bst, const float* coef,
+                         const float* gamma, void* dz, int dz_rs, int dz_off, float* gbias, hipStream_t stream) {
+  gtrain::BwdArgs A;
+  A.z = reinterpret_cast<const __bf16*>(z);
+  A.bn = bn;
+  A.dh = reinterpret_cast<const __bf16*>(dh);
+  A.dlog = dlog;
+  A.w = w;
+  A.invL = invL;
+  A.n = n;
+  A.L = L;
+  A.C = C;
+  A.pool = pool;
+  A.lout = pool ? L / 2 : L;
+  A.dropout = dropout;
+  A.thr = thr;
+  A.inv_keep = inv_keep;
+  A.skey = skey;
+  A.window_offset = window_offset;
+  A.bst = bst;
+  A.coef = coef;
+  A.gamma = gamma;
+  A.dz = reinterpret_cast<__bf16*>(dz);
+  A.dz_rs = dz_rs;
+  A.dz_off = dz_off;
+  A.gbias = gbias;
+  const int rpb = 256 / (C / 4);
+  const long long rows = (long long)n * L;
+  if (rows == 0) return hipSuccess;
+  const dim3 grid(gtrain::elem_grid(rows, rpb * 4));  // ~4 rows per thread
+  if (dz_mode)
+    hipLaunchKernelGGL(gtrain::bwd_kernel<true>, grid, dim3(256), 0, stream, A);
+  else
+    hipLaunchKernelGGL(gtrain::bwd_kernel<false>, grid, dim3(256), 0, stream, A);
+  return hipGetLastError();
+}
+
+hipError_t launch_gt_bwd_finalize(const float* bst, int C, float inv_count, float* coef, float* ggamma, float* gbeta,
+                                  hipStream_t stream) {
+  hipLaunchKernelGGL(gtrain::bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, bst, C, inv_count,
+                     coef, ggamma, gbeta);
+  return hipGetLastError();
+}
+
+}  // namespace apneauq

@@ -110,7 +110,7 @@ class AlarconCNN1D:
         self.store = self.store.to(self.device)
         self._blob = None
         self._gpack = None
-        for attr in ("_train_ws", "_mcd_ws", "_train_graphs"):  # device workspaces / captured graphs
+        for attr in ("_train_ws", "_mcd_ws", "_train_graphs", "_gtrain_ws", "_gfwd_ws"):  # device workspaces / captured graphs
             if hasattr(self, attr):
                 delattr(self, attr)
         if self.optimizer.m is not None:

@@ -69,6 +69,25 @@ def mc_dropout_batch_bn(model, x, n_pred: int, seed: Optional[int] = None, windo
                                                 global_n=global_n, max_samples=chunk_rows or (1 << 20))
             model._call_counter = base + n_pred
             return out.unsqueeze(-1)
+        from . import generic_train
+
+        if generic_train.supports(model.spec):
+            sync = None
+            if distributed:
+                import torch.distributed as dist
+
+                if dist.is_available() and dist.is_initialized():
+                    sync = dist.all_reduce
+            base = model._call_counter
+            out = generic_train.forward_batch_stats(model, xt, n_pred, pass_base=base,
+                                                    seed=model.seed if seed is None else seed,
+                                                    update_moving=update_moving, sync=sync,
+                                                    window_offset=window_offset, global_n=global_n)
+            model._call_counter = base + n_pred
+            return out.unsqueeze(-1)
+        from . import fused
+
+        fused.warn_unsupported(model.spec, "batch-statistics MC Dropout")
     sample_ids = torch.arange(window_offset, window_offset + n, device=xt.device)
     hook = _moments_hook() if distributed else None
     outs = []

@@ -9,8 +9,8 @@ GAP + Dense head launch, with bf16 activations between blocks.
 
 Dropout masks are the same pure function of (seed, layer, pass, window, t, channel) as everywhere
 else (``ops/rng.py``), so results match the fp32 reference's masks exactly and do not depend on
-chunking or sharding.  BatchNorm with batch statistics (``bn_mode="batch"``, training) stays on
-the PyTorch path for these architectures.
+chunking or sharding.  BatchNorm with batch statistics (``bn_mode="batch"``, training) runs on the
+generic training kernels (``ops/generic_train.py``).
 """
 from __future__ import annotations
 

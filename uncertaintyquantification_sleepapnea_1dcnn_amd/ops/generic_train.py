@@ -1,0 +1,240 @@
+"""Host orchestration of the HIP training kernels for ANY :class:`ModelSpec`.
+
+The reference architecture trains on its own LDS-resident kernels (``ops/train_ops.py``).  Every
+other architecture the spec expresses -- the opt-in ``MaxPool1D(2)`` blocks (the
+north star's "Conv1D -> BN -> ReLU -> MaxPool1D -> Dropout" stack), the "30 s single-channel"
+``ModelSpec(30, 1)``, other filter / kernel sizes -- trains here, with the reference's Keras
+semantics (``models/cnn_baseline_train.py:55-102``: Conv1D(relu) -> BN(batch stats, moving
+update) -> [pool] -> Dropout, BCE, Adam):
+
+  per block, forward       ``gt_conv`` mode 1   z = relu(conv(h) + b) + BN moment slots (MFMA)
+                           ``gt_bn_finalize``   scale / shift / mean / rstd + moving update
+                           ``gt_apply``         BN + pool + dropout -> next input (zero-padded rows)
+  head                     GAP + Dense + BCE + dlogit + dense grads (a few fused torch ops)
+  per block, backward      ``gt_bwd`` stats     sum(dy), sum(dy xhat) (dropout/pool routed back)
+                           ``gt_bwd_finalize``  dgamma, dbeta, BN-backward coefficients
+                           ``gt_bwd`` dz        dz (zero-padded rows) + bias gradient
+                           ``gt_conv`` mode 2   dgrad = conv(dz, flipped W^T) (MFMA)
+                           wgrad                one strided-batched hipBLASLt GEMM over the k taps:
+                                                dW[tap] = Xpad[tap : tap + R]^T dZpad
+  Adam                     one multi-tensor launch over the flat buffer (``csrc/adam.hip``)
+
+The zero-padded row layout (every sample's rows framed by k//2 zero rows, plus k//2 guard rows
+at both ends) is what makes wgrad a plain GEMM: the rows of tap ``j`` are the contiguous slice
+starting at row ``j`` of the padded input, so no im2col buffer is materialised.
+
+Dropout masks are the pure function of (seed, layer, pass, window, t, channel) used everywhere
+(``ops/rng.py``), keyed by the global window id, so data-parallel shards draw exactly the masks of
+the single-device batch.  ``sync`` (SyncBN) all-reduces the forward moment slots and the backward
+sums.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional
+
+import torch
+
+from ..models.spec import ModelSpec
+from . import _ext, fused, generic, rng
+
+TRAIN_PASS_BASE = 1 << 30  # == training/step.py
+SLOTS = 16  # == kStatSlots (csrc/generic_conv.hip, csrc/generic_train.hip)
+
+
+def supports(spec: ModelSpec) -> bool:
+    """True if the generic HIP training kernels implement ``spec`` (the same shapes as the generic
+    inference kernels).  On a GPU box a missing extension raises unless APNEAUQ_ALLOW_FALLBACK=1."""
+    if not generic.supports(spec):
+        return False
+    if _ext.available():
+        return True
+    if not _ext.fallback_allowed():
+        _ext.require()
+    return False
+
+
+class GenericTrainWorkspace:
+    """Device buffers of one model for batches of up to ``batch`` windows."""
+
+    def __init__(self, model, batch: int, with_backward: bool = True):
+        spec: ModelSpec = model.spec
+        dev = model.store.device
+        self.model = model
+        self.B = int(batch)
+        self.with_backward = with_backward
+        B, bf = self.B, torch.bfloat16
+        self.L = spec.lengths()
+        self.ch = spec.channels()
+        self.ks = [b.kernel_size for b in spec.blocks]
+        self.pads = [(k - 1) // 2 for k in self.ks]
+        self.rs = [self.L[l] + 2 * self.pads[l] for l in range(len(spec.blocks))]
+        nl = len(spec.blocks)
+        # layer inputs in the zero-padded row layout: data row (n, t) at n * rs + 2 p + t
+        self.xin = [torch.zeros(2 * self.pads[l] + B * self.rs[l], self.ch[l], dtype=bf, device=dev) for l in range(nl)]
+        self.z = [torch.empty(B * self.L[l], self.ch[l + 1], dtype=bf, device=dev) for l in range(nl)]
+        self.hlast = torch.empty(B * self.L[-1], self.ch[-1], dtype=bf, device=dev)
+        sizes = [SLOTS * 2 * self.ch[l + 1] for l in range(nl)]
+        self.st_all = torch.zeros(sum(sizes), device=dev)
+        self.st = list(torch.split(self.st_all, sizes))
+        self.bn = [torch.zeros(4 * self.ch[l + 1], device=dev) for l in range(nl)]
+        if with_backward:
+            # dz of block l, zero-padded rows (n, t) at n * rs + p + t; dh[l] = dL/d(input of block l)
+            self.dzp = [torch.zeros(B * self.rs[l], self.ch[l + 1], dtype=bf, device=dev) for l in range(nl)]
+            self.dh = [torch.empty(B * self.L[l], self.ch[l], dtype=bf, device=dev) if l > 0 else None
+                       for l in range(nl)]
+            self.bst_all = torch.zeros(sum(sizes), device=dev)
+            self.bst = list(torch.split(self.bst_all, sizes))
+            self.coef = [torch.zeros(2 * self.ch[l + 1], device=dev) for l in range(nl)]
+            store = model.store
+            self.grad = torch.zeros_like(store.flat)
+            self.gviews = {}
+            for n in store.trainable:
+                off = store.offsets[n]
+                self.gviews[n] = self.grad[off: off + store.views[n].numel()].view(store.shapes[n])
+
+    def load_input(self, x: torch.Tensor) -> None:
+        n, p = x.shape[0], self.pads[0]
+        self.xin[0][p: p + n * self.rs[0]].view(n, self.rs[0], self.ch[0])[:, p: p + self.L[0]].copy_(x)
+
+    def pack(self, backward: bool):
+        """bf16 MFMA fragments of every conv kernel (forward; + dgrad orientation when training)."""
+        v = self.model.store.views
+        wf, wd = [], []
+        for l in range(len(self.ks)):
+            w = v[f"conv1d_{l + 1}/kernel"].float()
+            wf.append(_frag(w))
+            wd.append(_frag(w.flip(0).transpose(1, 2)) if backward and l > 0 else None)
+        return wf, wd
+
+
+def _frag(w: torch.Tensor) -> torch.Tensor:
+    cout = w.shape[2]
+    cpad = (cout + 15) // 16 * 16
+    return fused.pack_conv_fragments(torch.nn.functional.pad(w, (0, cpad - cout)))
+
+
+def _get_ws(model, batch: int, with_backward: bool = True) -> GenericTrainWorkspace:
+    attr = "_gtrain_ws" if with_backward else "_gfwd_ws"
+    ws = getattr(model, attr, None)
+    if ws is None or ws.B < batch:
+        ws = GenericTrainWorkspace(model, batch, with_backward=with_backward)
+        setattr(model, attr, ws)
+    return ws
+
+
+def _forward(ws: GenericTrainWorkspace, n: int, global_n: int, seed: int, pass_id: int, window_offset: int,
+             dropout: bool, update_moving: bool, sync: Optional[Callable], wf) -> torch.Tensor:
+    """Batch-statistics forward of ``n`` windows already loaded in ``ws.xin[0]``; returns the
+    last block's output (n, L_out, C) bf16."""
+    o = _ext.ops()
+    spec, v = ws.model.spec, ws.model.store.views
+    nl = len(spec.blocks)
+    ws.st_all.zero_()
+    for l, b in enumerate(spec.blocks):
+        i = l + 1
+        cin, cout, L = ws.ch[l], ws.ch[l + 1], ws.L[l]
+        o.gt_conv(ws.xin[l], wf[l], v[f"conv1d_{i}/bias"], ws.z[l], ws.st[l], n, L, cin, cout, ws.ks[l], 1,
+                  ws.rs[l], 2 * ws.pads[l])
+        if sync is not None:
+            sync(ws.st[l])
+        o.gt_bn_finalize(ws.st[l], cout, 1.0 / (global_n * L), v[f"batchnorm_{i}/gamma"], v[f"batchnorm_{i}/beta"],
+                         spec.bn_epsilon, spec.bn_momentum, v[f"batchnorm_{i}/moving_mean"],
+                         v[f"batchnorm_{i}/moving_variance"], bool(update_moving), ws.bn[l])
+        if l + 1 < nl:
+            out, out_rs, out_off = ws.xin[l + 1], ws.rs[l + 1], 2 * ws.pads[l + 1]
+        else:
+            out, out_rs, out_off = ws.hlast, ws.L[-1], 0
+        drop = bool(dropout and b.dropout > 0)
+        o.gt_apply(ws.z[l], ws.bn[l], out, n, L, cout, bool(b.pool), out_rs, out_off, drop,
+                   rng.dropout_threshold(b.dropout), _inv_keep(b.dropout), rng.stream_key(seed, l, pass_id),
+                   int(window_offset))
+    return ws.hlast[: n * ws.L[-1]].view(n, ws.L[-1], ws.ch[-1])
+
+
+def _inv_keep(rate: float) -> float:
+    return 1.0 / (1.0 - rate) if rate < 1.0 else 0.0
+
+
+def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, sync: Optional[Callable] = None,
+               global_batch: Optional[int] = None, window_offset: int = 0, sync_world: int = 1):
+    """One Keras-semantics optimizer step on the generic HIP kernels; returns (loss_sum, probs)."""
+    spec: ModelSpec = model.spec
+    n = int(x.shape[0])
+    gb = int(global_batch or n)
+    ws = _get_ws(model, n)
+    o = _ext.ops()
+    v, g = model.store.views, ws.gviews
+    nl = len(spec.blocks)
+    ws.load_input(x)
+    wf, wd = ws.pack(backward=True)
+    pass_id = TRAIN_PASS_BASE + model._train_step_counter
+    seed = model.seed
+    h = _forward(ws, n, gb, seed, pass_id, window_offset, True, True, sync, wf)
+    # head: GAP + Dense + BCE(logits), mean over the global batch
+    gap = h.float().mean(dim=1)
+    wdense = v["output_layer/kernel"].reshape(-1)
+    logit = torch.addmv(v["output_layer/bias"], gap, wdense)
+    yv = y.reshape(-1).float()
+    lv = torch.nn.functional.binary_cross_entropy_with_logits(logit, yv, reduction="none")
+    prob = torch.sigmoid(logit)
+    dlog = ((prob - yv) / gb).contiguous()
+    ws.grad.zero_()
+    torch.mv(gap.t(), dlog, out=g["output_layer/kernel"].view(-1))
+    g["output_layer/bias"].copy_(dlog.sum().reshape(1))
+    ws.bst_all.zero_()
+    for l in range(nl - 1, -1, -1):
+        i, b = l + 1, spec.blocks[l]
+        cin, cout, L, p, k = ws.ch[l], ws.ch[l + 1], ws.L[l], ws.pads[l], ws.ks[l]
+        drop = b.dropout > 0
+        thr, ik, skey = rng.dropout_threshold(b.dropout), _inv_keep(b.dropout), rng.stream_key(seed, l, pass_id)
+        if l == nl - 1:
+            up = dict(dh=None, dlog=dlog, w=wdense, invL=1.0 / ws.L[-1])
+        else:
+            up = dict(dh=ws.dh[l + 1], dlog=None, w=None, invL=1.0)
+        o.gt_bwd(False, ws.z[l], ws.bn[l], up["dh"], up["dlog"], up["w"], up["invL"], n, L, cout, bool(b.pool), drop,
+                 thr, ik, skey, int(window_offset), ws.bst[l], None, None, None, 0, 0, None)
+        if sync is not None:
+            sync(ws.bst[l])
+        o.gt_bwd_finalize(ws.bst[l], cout, 1.0 / (gb * L), ws.coef[l], g[f"batchnorm_{i}/gamma"],
+                          g[f"batchnorm_{i}/beta"])
+        o.gt_bwd(True, ws.z[l], ws.bn[l], up["dh"], up["dlog"], up["w"], up["invL"], n, L, cout, bool(b.pool), drop,
+                 thr, ik, skey, int(window_offset), None, ws.coef[l], v[f"batchnorm_{i}/gamma"], ws.dzp[l], ws.rs[l], p,
+                 g[f"conv1d_{i}/bias"])
+        if l > 0:
+            o.gt_conv(ws.dzp[l], wd[l], None, ws.dh[l], None, n, L, cout, cin, k, 2, ws.rs[l], p)
+        # wgrad: dW[tap] = Xpad[tap : tap + R]^T dZpad (R = n * rs rows), fp32 out of one batched GEMM
+        R = n * ws.rs[l]
+        xs = ws.xin[l].as_strided((k, cin, R), (cin, 1, cin))
+        dzs = ws.dzp[l][:R].unsqueeze(0).expand(k, R, cout)
+        g[f"conv1d_{i}/kernel"].copy_(torch.bmm(xs, dzs, out_dtype=torch.float32))
+    if sync is not None and sync_world > 1:  # the synced sums made dgamma / dbeta global already
+        for i in range(1, nl + 1):
+            g[f"batchnorm_{i}/gamma"].div_(sync_world)
+            g[f"batchnorm_{i}/beta"].div_(sync_world)
+    scale = 1.0
+    if grad_allreduce is not None:
+        scale = grad_allreduce(ws.grad)
+    model.optimizer.step(model.store.flat, ws.grad, grad_scale=scale)
+    return lv.detach().sum().double(), prob.detach()
+
+
+@torch.no_grad()
+def forward_batch_stats(model, x: torch.Tensor, n_pass: int, pass_base: int, seed: int, update_moving: bool = True,
+                        sync: Optional[Callable] = None, window_offset: int = 0,
+                        global_n: Optional[int] = None) -> torch.Tensor:
+    """MC Dropout with BN on per-pass batch statistics of the whole set (the reference's
+    ``model(x, training=True)``) for any spec: (T, N) probabilities, one layer-synchronous
+    sweep per pass."""
+    n = int(x.shape[0])
+    gn = int(global_n or n)
+    ws = _get_ws(model, n, with_backward=False)
+    ws.load_input(x)
+    wf, _ = ws.pack(backward=False)
+    v = model.store.views
+    wdense = v["output_layer/kernel"].reshape(-1)
+    out = torch.empty(n_pass, n, device=x.device)
+    for t in range(n_pass):
+        h = _forward(ws, n, gn, seed, pass_base + t, window_offset, True, update_moving, sync, wf)
+        out[t] = torch.sigmoid(torch.addmv(v["output_layer/bias"], h.float().mean(dim=1), wdense))
+    model.store.bump()
+    return out

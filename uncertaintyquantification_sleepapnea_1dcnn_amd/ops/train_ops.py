@@ -37,7 +37,6 @@ def supports(spec: ModelSpec) -> bool:
     """True if the HIP training kernels implement ``spec``.  On a GPU machine a missing extension
     raises (no silent eager fallback) unless ``APNEAUQ_ALLOW_FALLBACK=1``."""
     if not fused.supports(spec):
-        fused.warn_unsupported(spec, "training")
         return False
     if _ext.available():
         return True
@@ -169,15 +168,16 @@ def _get_ws(model, batch: int) -> TrainWorkspace:
 
 
 def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, sync: Optional[Callable] = None,
-               global_batch: Optional[int] = None, window_offset: int = 0):
-    """One Keras-semantics optimizer step with the HIP kernels; returns (loss_sum, probs)."""
+               global_batch: Optional[int] = None, window_offset: int = 0, sync_world: int = 1):
+    """One Keras-semantics optimizer step with the HIP kernels; returns (loss_sum, probs).
+
+    ``sync`` (data parallel, ``sync_world`` ranks) all-reduces the BN moments and backward sums, so
+    the dgamma / dbeta the finalize writes are already global; they are pre-divided by
+    ``sync_world`` because ``grad_allreduce`` sums the whole flat gradient once more.
+    """
     n = x.shape[0]
     ws = _get_ws(model, n)
     gb = global_batch or n
-    sync = sync or getattr(model, "bn_sync", None)
-    if sync is not None and global_batch is None:
-        gb = getattr(model, "dp_global_batch", lambda b: b)(n)
-        window_offset = getattr(model, "dp_window_offset", lambda b: 0)(n)
     ctx = ws.build_ctx(n, n, 1, window_offset, model.seed, True, 1.0 / (gb * 60), 1.0 / gb)
     dev = x.device.index or 0
     # inputs in padded-row layout (pad rows stay zero)
@@ -205,6 +205,10 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, syn
         _call(ctx, 3, l, 0, pb, dev)
     _call(ctx, 3, 0, 0, pb, dev)
     _call(ctx, 4, 1, 1, pb, dev)
+    if sync is not None and sync_world > 1:
+        for i in range(1, 7):
+            ws.gviews[f"batchnorm_{i}/gamma"].div_(sync_world)
+            ws.gviews[f"batchnorm_{i}/beta"].div_(sync_world)
     scale = 1.0
     if grad_allreduce is not None:
         scale = grad_allreduce(ws.grad)

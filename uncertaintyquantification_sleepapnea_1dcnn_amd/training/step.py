@@ -1,7 +1,9 @@
 """One Keras-semantics optimizer step (forward in training mode, BCE-on-logits, backward, Adam).
 
 Backends:
-* ``"hip"``  — layer-wise HIP kernels (``ops/train_ops.py``) when the extension provides them;
+* ``"hip"``  — the reference architecture's layer-wise HIP kernels (``ops/train_ops.py``);
+* ``"hip_generic"`` — any other architecture (pool blocks, other window shapes) on the generic
+  HIP kernels (``ops/generic_train.py``);
 * ``"torch"``— autograd over the fp32 reference ops (CPU, and the fallback/oracle on GPU).
 
 Gradients land in ONE flat fp32 buffer (views of ``ParamStore.flat``), so the data-parallel
@@ -27,6 +29,13 @@ def _backend(model) -> str:
 
         if train_ops.supports(model.spec):
             return "hip"
+        from ..ops import generic_train
+
+        if generic_train.supports(model.spec):
+            return "hip_generic"
+        from ..ops import fused
+
+        fused.warn_unsupported(model.spec, "training")
     return "torch"
 
 
@@ -42,6 +51,14 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, dp_
     if dp is not None and dp.size == 1:
         dp = None
     gn, off = dp_step if (dp is not None and dp_step is not None) else (x.shape[0], 0)
+    if backend == "hip_generic":
+        from ..ops import generic_train
+
+        if dp is not None:
+            return generic_train.train_step(model, x, y, grad_allreduce=lambda g: (dp.all_reduce_(g), 1.0)[1],
+                                            sync=dp.all_reduce_, global_batch=gn, window_offset=off,
+                                            sync_world=dp.size)
+        return generic_train.train_step(model, x, y, grad_allreduce=grad_allreduce)
     if backend == "hip":
         from ..ops import train_ops
 
@@ -51,7 +68,7 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, dp_
                 return 1.0  # kernels already scale by 1/global batch
 
             return train_ops.train_step(model, x, y, grad_allreduce=_gar, sync=dp.all_reduce_, global_batch=gn,
-                                        window_offset=off)
+                                        window_offset=off, sync_world=dp.size)
         if grad_allreduce is None and _use_graphs():
             return train_ops.graph_train_step(model, x, y)
         return train_ops.train_step(model, x, y, grad_allreduce=grad_allreduce)
