@@ -406,7 +406,7 @@ void gt_bwd(bool dz_mode, const at::Tensor& z, const at::Tensor& bn, const c10::
     TORCH_CHECK(gamma->is_cuda() && gamma->numel() == C, "gt_bwd gamma");
     TORCH_CHECK(dz_rs >= L && dz_off >= 0, "gt_bwd: bad dz row layout");
     if (n > 0) need_rows(*dz, (n - 1) * dz_rs + dz_off + L, C, "gt_bwd dz");
-    TORCH_CHECK(gbias->is_cuda() && gbias->scalar_type() == at::kFloat && gbias->numel() == C, "gt_bwd gbias");
+    need_f32(*gbias, kGtSlots * C, "gt_bwd gbias slots");
     cp = coef->data_ptr<float>();
     gp = gamma->data_ptr<float>();
     dzp = dz->data_ptr();

@@ -13,7 +13,8 @@
 //                 recomputed from z) -> per-channel sum(dy), sum(dy * xhat)
 //   bwd_finalize  -> dgamma, dbeta and the two BN-backward coefficients
 //   bwd_dz        dz = relu'(z) * gamma * rstd * (dy - E[dy] - xhat E[dy xhat]) written zero-padded,
-//                 bias gradient as a fused column sum
+//                 bias gradient as a fused column sum (kSlots interleaved copies: one
+//                 same-address atomic per block and channel serialised at L2 cost 5x the kernel)
 //
 // Channel-group mapping of the elementwise kernels: a thread owns 4 consecutive channels of one
 // row (8-byte bf16x4 accesses), G = C/4 <= 256 groups across the block, 256 / G rows per sweep.
@@ -113,7 +114,7 @@ struct BwdArgs {
   const float* gamma;
   __bf16* dz;          // bwd_dz: row (n, t) at n * dz_rs + dz_off + t
   int dz_rs, dz_off;
-  float* gbias;        // bwd_dz: bias gradient (C,)
+  float* gbias;        // bwd_dz: bias-gradient slots (kSlots, C), summed by the host
 };
 
 // Gradient w.r.t. the BN output y at pre-pool row (ns, t), channels c .. c+3.
@@ -223,7 +224,7 @@ __global__ __launch_bounds__(256) void bwd_kernel(BwdArgs A) {
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) atomicAdd(A.gbias + c + j, acc[j]);
+      for (int j = 0; j < 4; ++j) atomicAdd(A.gbias + (blockIdx.x % kSlots) * A.C + c + j, acc[j]);
     }
   }
 }

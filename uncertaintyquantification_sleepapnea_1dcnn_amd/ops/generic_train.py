@@ -84,6 +84,9 @@ class GenericTrainWorkspace:
                        for l in range(nl)]
             self.bst_all = torch.zeros(sum(sizes), device=dev)
             self.bst = list(torch.split(self.bst_all, sizes))
+            # bias-gradient slots (SLOTS, C) per block, zeroed with bst_all
+            self.dbs_all = torch.zeros(sum(sizes) // 2, device=dev)
+            self.dbs = [t.view(SLOTS, -1) for t in torch.split(self.dbs_all, [s // 2 for s in sizes])]
             self.coef = [torch.zeros(2 * self.ch[l + 1], device=dev) for l in range(nl)]
             store = model.store
             self.grad = torch.zeros_like(store.flat)
@@ -182,6 +185,7 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, syn
     torch.mv(gap.t(), dlog, out=g["output_layer/kernel"].view(-1))
     g["output_layer/bias"].copy_(dlog.sum().reshape(1))
     ws.bst_all.zero_()
+    ws.dbs_all.zero_()
     for l in range(nl - 1, -1, -1):
         i, b = l + 1, spec.blocks[l]
         cin, cout, L, p, k = ws.ch[l], ws.ch[l + 1], ws.L[l], ws.pads[l], ws.ks[l]
@@ -199,14 +203,22 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, syn
                           g[f"batchnorm_{i}/beta"])
         o.gt_bwd(True, ws.z[l], ws.bn[l], up["dh"], up["dlog"], up["w"], up["invL"], n, L, cout, bool(b.pool), drop,
                  thr, ik, skey, int(window_offset), None, ws.coef[l], v[f"batchnorm_{i}/gamma"], ws.dzp[l], ws.rs[l], p,
-                 g[f"conv1d_{i}/bias"])
+                 ws.dbs[l])
+        torch.sum(ws.dbs[l], 0, out=g[f"conv1d_{i}/bias"])
         if l > 0:
             o.gt_conv(ws.dzp[l], wd[l], None, ws.dh[l], None, n, L, cout, cin, k, 2, ws.rs[l], p)
         # wgrad: dW[tap] = Xpad[tap : tap + R]^T dZpad (R = n * rs rows), fp32 out of one batched GEMM
         R = n * ws.rs[l]
-        xs = ws.xin[l].as_strided((k, cin, R), (cin, 1, cin))
-        dzs = ws.dzp[l][:R].unsqueeze(0).expand(k, R, cout)
-        g[f"conv1d_{i}/kernel"].copy_(torch.bmm(xs, dzs, out_dtype=torch.float32))
+        if cin >= 16:
+            xs = ws.xin[l].as_strided((k, cin, R), (cin, 1, cin))
+            dzs = ws.dzp[l][:R].unsqueeze(0).expand(k, R, cout)
+            g[f"conv1d_{i}/kernel"].copy_(torch.bmm(xs, dzs, out_dtype=torch.float32))
+        else:
+            # few input channels (block 1): a (R, k * Cin) im2col is small, and one plain GEMM avoids
+            # the ~10 ms host-side solution search hipBLASLt runs for a lda < 16 strided batch
+            xcol = ws.xin[l].as_strided((R, k * cin), (cin, 1)).contiguous()
+            g[f"conv1d_{i}/kernel"].view(k * cin, cout).copy_(
+                torch.mm(xcol.t(), ws.dzp[l][:R], out_dtype=torch.float32))
     if sync is not None and sync_world > 1:  # the synced sums made dgamma / dbeta global already
         for i in range(1, nl + 1):
             g[f"batchnorm_{i}/gamma"].div_(sync_world)
