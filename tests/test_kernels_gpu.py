@@ -60,3 +60,27 @@ def test_adam_kernel_matches_eager():
         a.step(pa, gr)
         b.step(pb, gr.cuda())
     torch.testing.assert_close(pb.cpu(), pa, rtol=1e-6, atol=1e-6)
+
+
+def test_metrics_kernel_matches_bucketize():
+    """K10 (csrc/metrics.hip): device accuracy / AUC counters == the host bucketize path, including
+    predictions exactly on thresholds, and no host sync per batch."""
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.training import metrics as TM
+
+    _ext.require()
+    g = torch.Generator().manual_seed(0)
+    thr = torch.tensor(TM.keras_thresholds(), dtype=torch.float32)
+    p = torch.cat([torch.rand(5000, generator=g), thr[1:-1], torch.tensor([0.0, 1.0, 0.5])])
+    y = (torch.rand(p.numel(), generator=g) > 0.6).float()
+    acc_d, auc_d, acc_h, auc_h = TM.BinaryAccuracy(), TM.AUC(), TM.BinaryAccuracy(), TM.AUC()
+    for s in range(0, p.numel(), 1024):
+        acc_d.update_state(y[s: s + 1024].cuda(), p[s: s + 1024].cuda())
+        auc_d.update_state(y[s: s + 1024].cuda(), p[s: s + 1024].cuda())
+        acc_h.update_state(y[s: s + 1024], p[s: s + 1024])
+        auc_h.update_state(y[s: s + 1024], p[s: s + 1024])
+    assert auc_d._counts is not None and acc_d._counts is not None  # accumulated on the device
+    np.testing.assert_array_equal(auc_d.confusion()[0], auc_h.confusion()[0])
+    np.testing.assert_array_equal(auc_d.pos_hist, auc_h.pos_hist)
+    np.testing.assert_array_equal(auc_d.neg_hist, auc_h.neg_hist)
+    assert acc_d.result() == acc_h.result()
+    assert abs(auc_d.result() - auc_h.result()) < 1e-12

@@ -40,6 +40,8 @@ hipError_t launch_gt_bwd(int dz_mode, const void* z, const float* bn, const void
                          const float* gamma, void* dz, int dz_rs, int dz_off, float* gbias, hipStream_t stream);
 hipError_t launch_gt_bwd_finalize(const float* bst, int C, float inv_count, float* coef, float* ggamma, float* gbeta,
                                   hipStream_t stream);
+hipError_t launch_metrics_update(const float* p, const float* y, long long n, const float* thr, int n_thr,
+                                 unsigned long long* counts, hipStream_t stream);
 hipError_t launch_generic_head(const void* y, const float* w, float b, int n, int L, int C, int out_logits, float* out,
                                hipStream_t stream);
 namespace train {
@@ -443,6 +445,22 @@ at::Tensor generic_head(const at::Tensor& y, const at::Tensor& w, double b, bool
   return out;
 }
 
+// K10 (csrc/metrics.hip): counts (int64, 1 + 2 (n_thr + 1)) += accuracy / AUC-bucket counts of a batch.
+void metrics_update(const at::Tensor& p, const at::Tensor& y, const at::Tensor& thr, at::Tensor& counts) {
+  TORCH_CHECK(p.is_cuda() && y.is_cuda() && thr.is_cuda() && counts.is_cuda(), "metrics_update: GPU tensors required");
+  TORCH_CHECK(p.scalar_type() == at::kFloat && y.scalar_type() == at::kFloat && thr.scalar_type() == at::kFloat &&
+              p.is_contiguous() && y.is_contiguous() && thr.is_contiguous() && p.numel() == y.numel(),
+              "metrics_update: contiguous fp32 p, y of equal size and fp32 thresholds required");
+  TORCH_CHECK(thr.numel() >= 1 && thr.numel() <= 1024, "metrics_update: 1..1024 thresholds");
+  TORCH_CHECK(counts.scalar_type() == at::kLong && counts.is_contiguous() && counts.numel() == 1 + 2 * (thr.numel() + 1),
+              "metrics_update: counts must be int64 (1 + 2 (n_thr + 1))");
+  const at::DeviceGuard guard(p.device());
+  check(apneauq::launch_metrics_update(p.data_ptr<float>(), y.data_ptr<float>(), p.numel(), thr.data_ptr<float>(),
+                                       (int)thr.numel(), reinterpret_cast<unsigned long long*>(counts.data_ptr<int64_t>()),
+                                       cur_stream()),
+        "metrics_update");
+}
+
 std::vector<int64_t> fused_layout() {
   int w[6], e[6], d;
   apneauq::fused_layout(w, e, &d);
@@ -471,6 +489,7 @@ TORCH_LIBRARY(apneauq, m) {
   m.def("generic_conv(Tensor x, Tensor wfrag, Tensor epi, int cout, int ksize, bool pool, bool dropout, int thr, "
         "int layer, int n_win, int pass_offset, int window_offset, int seed) -> Tensor");
   m.def("generic_head(Tensor y, Tensor w, float b, bool logits) -> Tensor");
+  m.def("metrics_update(Tensor p, Tensor y, Tensor thr, Tensor(a!) counts) -> ()");
   m.def("gt_conv(Tensor x, Tensor wfrag, Tensor? bias, Tensor(a!) y, Tensor(b!)? stats, int n, int L, int cin, "
         "int cout, int ksize, int mode, int in_rs, int in_off) -> ()");
   m.def("gt_bn_finalize(Tensor st, int C, float inv_count, Tensor gamma, Tensor beta, float eps, float momentum, "
@@ -492,6 +511,7 @@ TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
   m.impl("train_pack", &train_pack);
   m.impl("generic_conv", &generic_conv);
   m.impl("generic_head", &generic_head);
+  m.impl("metrics_update", &metrics_update);
   m.impl("gt_conv", &gt_conv);
   m.impl("gt_bn_finalize", &gt_bn_finalize);
   m.impl("gt_apply", &gt_apply);

@@ -31,6 +31,8 @@ from .metrics import AUC, BinaryAccuracy, MeanMetric
 def _sync_metrics(dp, loss_acc: torch.Tensor, acc_m, auc_m) -> None:
     """Sum the epoch's per-rank metric state over the data-parallel group."""
     dev = loss_acc.device
+    acc_m.flush()
+    auc_m.flush()
     buf = torch.tensor([acc_m.total, acc_m.count], dtype=torch.float64, device=dev)
     hist = torch.tensor(np.concatenate([auc_m.pos_hist, auc_m.neg_hist]), dtype=torch.float64, device=dev)
     dp.all_reduce_(loss_acc)
@@ -52,15 +54,17 @@ def evaluate_arrays(model, x: torch.Tensor, y: torch.Tensor, batch_size: int = 1
     """Inference-mode loss / accuracy / AUC over (x, y) (device tensors)."""
     loss_m, acc_m, auc_m = MeanMetric(), BinaryAccuracy(), AUC()
     n = x.shape[0]
+    loss_sum = torch.zeros((), dtype=torch.float64, device=x.device)
     with torch.no_grad():
         for s in range(0, n, batch_size):
             xb, yb = x[s: s + batch_size], y[s: s + batch_size]
             logits = model.logits(xb, training=False)
             l = torch.nn.functional.binary_cross_entropy_with_logits(logits.reshape(-1), yb.float(), reduction="sum")
             p = torch.sigmoid(logits)
-            loss_m.update(l.item(), yb.numel())
+            loss_sum += l
             acc_m.update_state(yb, p)
             auc_m.update_state(yb, p)
+    loss_m.update(loss_sum.item(), n)
     return loss_m.result(), acc_m.result(), auc_m.result()
 
 
