@@ -27,7 +27,7 @@ hipError_t train_bump_counters(int* c, int n, hipStream_t st);
 hipError_t launch_generic_conv(const void* x, const void* wfrag, const float* epi, void* y, int n, int L, int cin,
                                int cout, int cout_pad, int ksize, int pool, int dropout, unsigned thr, int layer,
                                int n_win, unsigned pass_offset, unsigned window_offset, unsigned long long seed,
-                               hipStream_t stream, int mode, int in_rs, int in_off, float* stats);
+                               hipStream_t stream, int mode, int in_rs, int in_off, float* stats, long long x_rows);
 hipError_t launch_gt_bn_finalize(const float* st, int C, float inv_count, const float* gamma, const float* beta,
                                  float eps, float momentum, float* mmean, float* mvar, int update, float* bn,
                                  hipStream_t stream);
@@ -290,7 +290,7 @@ at::Tensor generic_conv(const at::Tensor& x, const at::Tensor& wfrag, const at::
   check(apneauq::launch_generic_conv(x.data_ptr(), wfrag.data_ptr(), epi.data_ptr<float>(), y.data_ptr(), (int)n, (int)L,
                                      (int)cin, (int)cout, (int)cout_pad, (int)ksize, pool ? 1 : 0, dropout ? 1 : 0,
                                      (unsigned)thr, (int)layer, (int)n_win, (unsigned)pass_offset, (unsigned)window_offset,
-                                     (unsigned long long)seed, cur_stream(), 0, (int)L, 0, nullptr),
+                                     (unsigned long long)seed, cur_stream(), 0, (int)L, 0, nullptr, n * L),
         "generic_conv");
   return y;
 }
@@ -337,7 +337,7 @@ void gt_conv(const at::Tensor& x, const at::Tensor& wfrag, const c10::optional<a
   const at::DeviceGuard guard(y.device());
   check(apneauq::launch_generic_conv(x.data_ptr(), wfrag.data_ptr(), bp, y.data_ptr(), (int)n, (int)L, (int)cin,
                                      (int)cout, (int)(wfrag.size(1) * 16), (int)ksize, 0, 0, 0u, 0, 1, 0u, 0u, 0ull,
-                                     cur_stream(), (int)mode, (int)in_rs, (int)in_off, sp),
+                                     cur_stream(), (int)mode, (int)in_rs, (int)in_off, sp, x.numel() / cin),
         "gt_conv");
 }
 

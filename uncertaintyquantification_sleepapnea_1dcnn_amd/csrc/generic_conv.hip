@@ -39,6 +39,8 @@ struct ConvArgs {
   unsigned long long seed;
   int in_rs, in_off;      // input row addressing: sample n, step t at row n * in_rs + in_off + t
   float* stats;           // kTrain: BN moment sums (kStatSlots, 2, Cout)
+  long long x_rows;       // rows of the input buffer (staging bound)
+  int lds_rows, lds_stride;  // conv_lds_kernel: staged rows, bytes per LDS row
 };
 
 // Epilogue modes: kInfer = bias + ReLU + BN(running) [+ pool] [+ dropout] (the folded epi rows);
@@ -49,80 +51,11 @@ constexpr int kStatSlots = 16;
 
 constexpr int kRT = 4, kCT = 4;  // row / channel tiles per wave; a workgroup is 2 x 2 waves
 
-template <bool VEC, int MODE>
-__global__ __launch_bounds__(256) void conv_block_kernel(ConvArgs A) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int m = lane & 15, h = lane >> 4;
-  const int wr = wave >> 1, wc = wave & 1;
-  const long long rows = (long long)A.n * A.Lp;
-  const long long row_base = (long long)blockIdx.x * (2 * kRT * 16) + wr * (kRT * 16);
-  const int nct = A.cout_pad / 16;
-  const int ct0 = (blockIdx.y * 2 + wc) * kCT;
-  if (ct0 >= nct) return;  // wave-uniform: no channel tile for this wave (no barriers below)
-  const int pad = (A.ksize - 1) / 2;
-  const int K = A.ksize * A.cin;
-
-  // this lane's B rows (one per row tile): sample n, step t
-  int rn[kRT], rt[kRT];
-  bool rok[kRT];
-#pragma unroll
-  for (int r = 0; r < kRT; ++r) {
-    const long long row = row_base + r * 16 + m;
-    const bool ok = row < rows;
-    rn[r] = ok ? (int)(row / A.Lp) : 0;
-    rt[r] = ok ? (int)(row - (long long)rn[r] * A.Lp) : 0;
-    rok[r] = ok && rt[r] < A.L;
-  }
-
-  f32x4 acc[kCT][kRT];
-#pragma unroll
-  for (int c = 0; c < kCT; ++c)
-#pragma unroll
-    for (int r = 0; r < kRT; ++r) acc[c][r] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // (tap, ci) of k = 32 s + 8 h, advanced incrementally (no per-step division)
-  int tap = (8 * h) / A.cin, ci = 8 * h - tap * A.cin;
-  for (int s = 0; s < A.nstep; ++s) {
-    const int kk0 = 32 * s + 8 * h;
-    bf16x8 b[kRT];
-#pragma unroll
-    for (int r = 0; r < kRT; ++r) {
-      const __bf16* xs = A.x + ((long long)rn[r] * A.in_rs + A.in_off) * A.cin;
-      if constexpr (VEC) {
-        const int ts = rt[r] + tap - pad;
-        if (rok[r] && kk0 < K && ts >= 0 && ts < A.L) {
-          b[r] = *(const gbf16x8*)(xs + (long long)ts * A.cin + ci);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) b[r][j] = (__bf16)0.f;
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int kk = kk0 + j;
-          const int tp = kk / A.cin, cc = kk - tp * A.cin;
-          const int ts = rt[r] + tp - pad;
-          b[r][j] = (rok[r] && kk < K && ts >= 0 && ts < A.L) ? xs[(long long)ts * A.cin + cc] : (__bf16)0.f;
-        }
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < kCT; ++c) {
-      const int ct = ct0 + c;
-      if (ct < nct) {  // wave-uniform
-        const bf16x8 a = ((const gbf16x8*)A.wfrag)[((long long)s * nct + ct) * 64 + lane];
-#pragma unroll
-        for (int r = 0; r < kRT; ++r) acc[c][r] = mfma16(a, b[r], acc[c][r]);
-      }
-    }
-    if constexpr (VEC) {
-      ci += 32;
-      while (ci >= A.cin) {
-        ci -= A.cin;
-        ++tap;
-      }
-    }
-  }
-
+// Epilogue of one wave: acc[c][r] holds rows (rn[r], rt[r]) x channels ct*16 + 4h .. +3 per lane.
+template <int MODE>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& A, f32x4 (&acc)[kCT][kRT], const int (&rn)[kRT],
+                                              const int (&rt)[kRT], const bool (&rok)[kRT], int ct0, int nct,
+                                              int m, int h) {
   if constexpr (MODE != kInfer) {
     // training / dgrad epilogue: no pool, no dropout; y is (N, L, Cout)
     float* st = A.stats + (blockIdx.x % kStatSlots) * 2 * A.cout;
@@ -216,6 +149,169 @@ __global__ __launch_bounds__(256) void conv_block_kernel(ConvArgs A) {
   }
 }
 
+template <bool VEC, int MODE>
+__global__ __launch_bounds__(256) void conv_block_kernel(ConvArgs A) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int m = lane & 15, h = lane >> 4;
+  const int wr = wave >> 1, wc = wave & 1;
+  const long long rows = (long long)A.n * A.Lp;
+  const long long row_base = (long long)blockIdx.x * (2 * kRT * 16) + wr * (kRT * 16);
+  const int nct = A.cout_pad / 16;
+  const int ct0 = (blockIdx.y * 2 + wc) * kCT;
+  if (ct0 >= nct) return;  // wave-uniform: no channel tile for this wave (no barriers below)
+  const int pad = (A.ksize - 1) / 2;
+  const int K = A.ksize * A.cin;
+
+  // this lane's B rows (one per row tile): sample n, step t
+  int rn[kRT], rt[kRT];
+  bool rok[kRT];
+#pragma unroll
+  for (int r = 0; r < kRT; ++r) {
+    const long long row = row_base + r * 16 + m;
+    const bool ok = row < rows;
+    rn[r] = ok ? (int)(row / A.Lp) : 0;
+    rt[r] = ok ? (int)(row - (long long)rn[r] * A.Lp) : 0;
+    rok[r] = ok && rt[r] < A.L;
+  }
+
+  f32x4 acc[kCT][kRT];
+#pragma unroll
+  for (int c = 0; c < kCT; ++c)
+#pragma unroll
+    for (int r = 0; r < kRT; ++r) acc[c][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // (tap, ci) of k = 32 s + 8 h, advanced incrementally (no per-step division)
+  int tap = (8 * h) / A.cin, ci = 8 * h - tap * A.cin;
+  for (int s = 0; s < A.nstep; ++s) {
+    const int kk0 = 32 * s + 8 * h;
+    bf16x8 b[kRT];
+#pragma unroll
+    for (int r = 0; r < kRT; ++r) {
+      const __bf16* xs = A.x + ((long long)rn[r] * A.in_rs + A.in_off) * A.cin;
+      if constexpr (VEC) {
+        const int ts = rt[r] + tap - pad;
+        if (rok[r] && kk0 < K && ts >= 0 && ts < A.L) {
+          b[r] = *(const gbf16x8*)(xs + (long long)ts * A.cin + ci);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) b[r][j] = (__bf16)0.f;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int kk = kk0 + j;
+          const int tp = kk / A.cin, cc = kk - tp * A.cin;
+          const int ts = rt[r] + tp - pad;
+          b[r][j] = (rok[r] && kk < K && ts >= 0 && ts < A.L) ? xs[(long long)ts * A.cin + cc] : (__bf16)0.f;
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < kCT; ++c) {
+      const int ct = ct0 + c;
+      if (ct < nct) {  // wave-uniform
+        const bf16x8 a = ((const gbf16x8*)A.wfrag)[((long long)s * nct + ct) * 64 + lane];
+#pragma unroll
+        for (int r = 0; r < kRT; ++r) acc[c][r] = mfma16(a, b[r], acc[c][r]);
+      }
+    }
+    if constexpr (VEC) {
+      ci += 32;
+      while (ci >= A.cin) {
+        ci -= A.cin;
+        ++tap;
+      }
+    }
+  }
+
+  conv_epilogue<MODE>(A, acc, rn, rt, rok, ct0, nct, m, h);
+}
+
+// LDS-staged variant (Cin % 8 == 0, host-checked LDS budget): the workgroup's input rows -- one
+// contiguous range of the (row-addressed) input, 128 output rows plus the halo and any per-sample
+// padding rows in between -- are staged once into LDS with coalesced 16-B loads, and the K loop
+// reads B fragments with ds_read_b128 instead of one 16-B global gather per lane, row tile and
+// k-step.  Taps that cross a sample boundary are masked per lane (t + tap - pad outside [0, L)).
+// The row stride is padded by 16 B so the 16 rows a lane group reads fall into different banks.
+template <int MODE>
+__global__ __launch_bounds__(256) void conv_lds_kernel(ConvArgs A) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int m = lane & 15, h = lane >> 4;
+  const int wr = wave >> 1, wc = wave & 1;
+  const long long rows = (long long)A.n * A.Lp;
+  const long long wg_row0 = (long long)blockIdx.x * (2 * kRT * 16);
+  const int pad = (A.ksize - 1) / 2;
+  const int K = A.ksize * A.cin;
+  // first input row the workgroup can touch: (sample, step) of its first output row, minus the halo
+  const int n0 = (int)(wg_row0 / A.Lp), t0 = (int)(wg_row0 - (long long)n0 * A.Lp);
+  const long long xbase = (long long)n0 * A.in_rs + A.in_off + t0 - pad;
+  const int cpr = A.cin >> 3;  // 16-B chunks per row
+  for (int i = threadIdx.x; i < A.lds_rows * cpr; i += 256) {
+    const int lr = i / cpr, cc = i - lr * cpr;
+    const long long xr = xbase + lr;
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
+    if (xr >= 0 && xr < A.x_rows) v = *(const gbf16x8*)(A.x + xr * A.cin + cc * 8);
+    *reinterpret_cast<bf16x8*>(smem + lr * A.lds_stride + cc * 16) = v;
+  }
+  __syncthreads();
+  const long long row_base = wg_row0 + wr * (kRT * 16);
+  const int nct = A.cout_pad / 16;
+  const int ct0 = (blockIdx.y * 2 + wc) * kCT;
+  if (ct0 >= nct) return;  // wave-uniform, after the only barrier
+
+  int rn[kRT], rt[kRT], lr0[kRT];
+  bool rok[kRT];
+#pragma unroll
+  for (int r = 0; r < kRT; ++r) {
+    const long long row = row_base + r * 16 + m;
+    const bool ok = row < rows;
+    rn[r] = ok ? (int)(row / A.Lp) : 0;
+    rt[r] = ok ? (int)(row - (long long)rn[r] * A.Lp) : 0;
+    rok[r] = ok && rt[r] < A.L;
+    // LDS row of tap 0 (input step t - pad)
+    lr0[r] = rok[r] ? (int)((long long)rn[r] * A.in_rs + A.in_off + rt[r] - pad - xbase) : 0;
+    APNEAUQ_DASSERT(!rok[r] || (lr0[r] >= 0 && lr0[r] + A.ksize <= A.lds_rows));
+  }
+
+  f32x4 acc[kCT][kRT];
+#pragma unroll
+  for (int c = 0; c < kCT; ++c)
+#pragma unroll
+    for (int r = 0; r < kRT; ++r) acc[c][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int tap = (8 * h) / A.cin, ci = 8 * h - tap * A.cin;
+  const bf16x8 zero8 = bf16x8{(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f,
+                              (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
+  for (int s = 0; s < A.nstep; ++s) {
+    const bool kok = 32 * s + 8 * h < K;
+    bf16x8 b[kRT];
+#pragma unroll
+    for (int r = 0; r < kRT; ++r) {
+      const int ts = rt[r] + tap - pad;
+      const bool ok = rok[r] && kok && ts >= 0 && ts < A.L;
+      const int lrow = ok ? lr0[r] + tap : 0;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + lrow * A.lds_stride + ci * 2);
+      b[r] = ok ? v : zero8;
+    }
+#pragma unroll
+    for (int c = 0; c < kCT; ++c) {
+      const int ct = ct0 + c;
+      if (ct < nct) {  // wave-uniform
+        const bf16x8 a = ((const gbf16x8*)A.wfrag)[((long long)s * nct + ct) * 64 + lane];
+#pragma unroll
+        for (int r = 0; r < kRT; ++r) acc[c][r] = mfma16(a, b[r], acc[c][r]);
+      }
+    }
+    ci += 32;
+    while (ci >= A.cin) {
+      ci -= A.cin;
+      ++tap;
+    }
+  }
+  conv_epilogue<MODE>(A, acc, rn, rt, rok, ct0, nct, m, h);
+}
+
 // GAP over time + Dense(C -> 1): one wave per sample, fp32 accumulation.
 __global__ __launch_bounds__(256) void head_kernel(const __bf16* y, const float* w, float b, int n, int L, int C,
                                                    int out_logits, float* out) {
@@ -237,7 +333,7 @@ __global__ __launch_bounds__(256) void head_kernel(const __bf16* y, const float*
 hipError_t launch_generic_conv(const void* x, const void* wfrag, const float* epi, void* y, int n, int L, int cin,
                                int cout, int cout_pad, int ksize, int pool, int dropout, unsigned thr, int layer,
                                int n_win, unsigned pass_offset, unsigned window_offset, unsigned long long seed,
-                               hipStream_t stream, int mode, int in_rs, int in_off, float* stats) {
+                               hipStream_t stream, int mode, int in_rs, int in_off, float* stats, long long x_rows) {
   generic::ConvArgs A;
   A.x = reinterpret_cast<const __bf16*>(x);
   A.wfrag = reinterpret_cast<const bf16x8*>(wfrag);
@@ -273,6 +369,25 @@ hipError_t launch_generic_conv(const void* x, const void* wfrag, const float* ep
   if (rows == 0) return hipSuccess;
   constexpr int kRowsWG = 2 * generic::kRT * 16, kChWG = 2 * generic::kCT;  // 128 rows x 8 channel tiles
   const dim3 grid((unsigned)((rows + kRowsWG - 1) / kRowsWG), (unsigned)((cout_pad / 16 + kChWG - 1) / kChWG));
+  // LDS staging when every row a workgroup can touch fits: 128 output rows span at most
+  // 127 + ceil(127 / Lp) * max(0, in_rs - Lp) input rows, plus the 2 * pad halo
+  const long long extra = (long long)(127 + A.Lp - 1) / A.Lp * (A.in_rs > A.Lp ? A.in_rs - A.Lp : 0);
+  const long long span = 128 + extra + 2 * (long long)((ksize - 1) / 2);
+  const int stride = 2 * cin + 16;
+  A.x_rows = x_rows;
+  A.lds_rows = (int)span;
+  A.lds_stride = stride;
+  const bool use_lds = cin % 8 == 0 && span * stride <= 80 * 1024 && x_rows > 0;
+  if (use_lds) {
+    const size_t lds = (size_t)span * stride;
+    if (mode == generic::kTrain)
+      hipLaunchKernelGGL(generic::conv_lds_kernel<generic::kTrain>, grid, dim3(256), lds, stream, A);
+    else if (mode == generic::kLinear)
+      hipLaunchKernelGGL(generic::conv_lds_kernel<generic::kLinear>, grid, dim3(256), lds, stream, A);
+    else
+      hipLaunchKernelGGL(generic::conv_lds_kernel<generic::kInfer>, grid, dim3(256), lds, stream, A);
+    return hipGetLastError();
+  }
 #define APNEAUQ_GCONV(M)                                                                   \
   if (cin % 8 == 0)                                                                        \
     hipLaunchKernelGGL((generic::conv_block_kernel<true, M>), grid, dim3(256), 0, stream, A); \
