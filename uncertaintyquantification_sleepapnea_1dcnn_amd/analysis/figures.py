@@ -26,6 +26,21 @@ import matplotlib.pyplot as plt  # noqa: E402
 from scipy.stats import gaussian_kde, pearsonr  # noqa: E402
 
 
+def load_data(csv_path: str) -> Optional[pd.DataFrame]:
+    """``final_plot_uq_overview_figures.py:26-37``: the CSV as a DataFrame, or None if it is missing
+    or unreadable (reported, not raised)."""
+    if not os.path.exists(csv_path):
+        print(f"ERROR: File not found - {csv_path}")
+        return None
+    try:
+        df = pd.read_csv(csv_path)
+    except Exception as e:  # noqa: BLE001 -- the reference reports and returns None
+        print(f"Error loading {csv_path}: {e}")
+        return None
+    print(f"Loaded {csv_path}, shape: {df.shape}")
+    return df
+
+
 def _hist_kde(ax, v, bins=20):
     v = np.asarray(v, dtype=float)
     v = v[np.isfinite(v)]

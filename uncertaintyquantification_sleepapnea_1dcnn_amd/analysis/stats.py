@@ -1,7 +1,8 @@
 """Statistical tests of the thesis analysis (``uq_analysis/``).
 
 * :func:`patient_correlation` — ``patient_accuracy_entropy_correlation.py:15-46``: Pearson r between
-  a patient summary's ``mean_entropy`` and ``patient_accuracy`` (rows with NaN dropped jointly).
+  a patient summary's ``mean_entropy`` and ``patient_accuracy`` (rows with NaN dropped jointly);
+  :func:`calculate_and_print_correlation` is the reference's file-path entry point.
 * :func:`entropy_mannwhitney` — ``window_uncertainty_vs_correctness_mannwhitney.py:18``: one-sided
   Mann-Whitney U (incorrect > correct) on per-window predictive entropy.  The reference script is
   labelled "Deep Ensembles" whatever file it reads; here the method is a parameter.
@@ -31,6 +32,27 @@ def patient_correlation(summary: Union[str, pd.DataFrame], method: str = "MC Dro
         print(f"Pearson r = {r:.4f}")
         print(f"P-value = {p:.4g}")
     return float(r), float(p)
+
+
+def calculate_and_print_correlation(csv_path: str, method_name: str, x_col: str = "mean_entropy",
+                                    y_col: str = "patient_accuracy") -> Tuple[Optional[float], Optional[float]]:
+    """Reference entry point (``patient_accuracy_entropy_correlation.py:15-46``): (r, p) or (None, None)
+    when the file or columns are missing or fewer than two rows survive the joint NaN drop."""
+    import os
+
+    if not os.path.exists(csv_path):
+        print(f"ERROR: File not found - {csv_path}")
+        return None, None
+    try:
+        df = pd.read_csv(csv_path)
+    except Exception as e:  # noqa: BLE001 -- the reference reports and returns (None, None)
+        print(f"Error processing {csv_path}: {e}")
+        return None, None
+    if x_col in df.columns and y_col in df.columns:
+        n_drop = len(df) - len(df[[x_col, y_col]].dropna())
+        if n_drop:
+            print(f"Warning: Dropped {n_drop} rows with NaN values.")
+    return patient_correlation(df, method_name, x_col, y_col)
 
 
 def entropy_mannwhitney(detail: Union[str, pd.DataFrame], method: str = "Deep Ensembles", metric: str = "Predictive_Entropy",

@@ -103,7 +103,7 @@ def evaluate_mc_dropout(model, X, y, patient_ids=None, model_eval_label: str = "
     if probs is None or probs.shape[0] != n_passes or probs.shape[1] != len(y):
         print(f"MC Dropout prediction failed or returned unexpected shape for {model_eval_label}")
         return None
-    if raw_pred_path is None:
+    if raw_pred_path is None:  # "" skips the dump
         raw_pred_path = f"./mc_raw_pred0505_{model_eval_label}.npy"
     return _finish(probs, y, patient_ids, model_eval_label, save_detailed_csv, output_csv_dir, output_plot_dir,
                    n_bootstrap, seed, raw_pred_path, make_plots)
@@ -124,6 +124,29 @@ def evaluate_deep_ensemble(models: List, X, y, patient_ids=None, model_eval_labe
         return None
     return _finish(probs, y, patient_ids, model_eval_label, save_detailed_csv, output_csv_dir, output_plot_dir,
                    n_bootstrap, seed, raw_pred_path, make_plots)
+
+
+def evaluate_mc_dropout_global(model, X_data_reshaped, y_data, model_eval_label: str, n_passes: int = 50,
+                               n_bootstrap: int = 100, seed: int = 2025, bn_mode: str = "batch",
+                               output_plot_dir: str = "./uq_plots/mc_dropout", make_plots: bool = True) -> Optional[Dict]:
+    """``evaluate_mcd_global.py:45-94`` signature ``evaluate_mc_dropout(model, X, y, label)``: MC Dropout
+    + ``evaluate_uq_methods``, no per-window CSV or raw dump (exported under the reference name by
+    ``cli/evaluate_mcd_global.py``)."""
+    return evaluate_mc_dropout(model, X_data_reshaped, y_data, None, model_eval_label, save_detailed_csv=False,
+                               n_passes=n_passes, n_bootstrap=n_bootstrap, seed=seed, bn_mode=bn_mode,
+                               output_plot_dir=output_plot_dir, raw_pred_path="", make_plots=make_plots)
+
+
+def evaluate_ensemble(models: List, X_data, y_data, model_eval_label: str, n_bootstrap: int = 100, seed: int = 2025,
+                      output_plot_dir: str = "./uq_plots/deep_ensemble", make_plots: bool = True) -> Optional[Dict]:
+    """``evaluate_de_global.py:40-80``: Deep Ensemble predictions + ``evaluate_uq_methods`` for a 3-D
+    window array (anything else is rejected, ``:48-50``)."""
+    if np.ndim(X_data) != 3:
+        print(f"ERROR: Expected 3D input data (samples, steps, features) for model, but got shape {np.shape(X_data)}")
+        return None
+    return evaluate_deep_ensemble(models, X_data, y_data, None, model_eval_label, save_detailed_csv=False,
+                                  n_bootstrap=n_bootstrap, seed=seed, output_plot_dir=output_plot_dir,
+                                  raw_pred_path="", make_plots=make_plots)
 
 
 def convergence_sweep(predict_fn, counts, X_unbalanced, y_unbalanced, X_balanced, y_balanced, output_csv: str):
