@@ -13,6 +13,15 @@ REF_FUNCS = {
     "analyze_de_patient_level": ["load_ensemble", "evaluate_deep_ensemble"],
     "patient_accuracy_entropy_correlation": ["calculate_and_print_correlation"],
     "final_plot_uq_overview_figures": ["load_data"],
+    "cnn_baseline_train": ["al_1d_cnn_create_model", "run_cnn_experiment"],
+    "train_deep_ensemble_cnns": ["al_1d_cnn_create_model", "train_ensemble"],
+    "shhs_signal_quality": ["analyze_signal_quality"],
+    "shhs_cohort_analysis": ["analyze_cohort"],
+    "hyperparameter_plot_mcd_or_de_pass_convergence": ["plot_variance_convergence"],
+    "preprocess_shhs_raw": ["check_artifacts_and_missing_values", "calculate_sleep_time", "remove_artifacts",
+                            "get_edf_channels", "resample_signals", "parse_xml_annotations",
+                            "segment_and_label_edf_data", "process_single_file", "process_all_files", "main"],
+    "prepare_numpy_datasets": ["reshape_flat_to_3d", "standardize_per_window", "prepare_final_datasets"],
 }
 
 

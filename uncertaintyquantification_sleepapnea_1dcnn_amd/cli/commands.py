@@ -76,6 +76,15 @@ def train_deep_ensemble_cnns(argv=None):
                    batch_size=a.batch_size, patience=a.patience)
 
 
+def reference_train_ensemble(model_type: str = "cnn", num_models: int = 5, seed_base: int = SEED,
+                             data_dir: str = "./processed_datasets", save_dir: str = "./models/ensemble_cnn_no_pool"):
+    """``train_deep_ensemble_cnns.py:81`` signature ``train_ensemble(model_type, num_models, seed_base)``:
+    loads the SMOTE training set from ``data_dir`` and trains the members (skip-if-exists resume)."""
+    argv = ["--model_type", model_type, "--num_models", str(num_models), "--seed_base", str(seed_base),
+            "--data_dir", data_dir, "--save_dir", save_dir]
+    train_deep_ensemble_cnns(argv)
+
+
 def _load_test(data_dir):
     from ..data.prepare import load_processed
 
