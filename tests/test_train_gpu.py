@@ -124,3 +124,31 @@ def test_graphed_training_step_matches_eager(monkeypatch):
     w0 = AlarconCNN1D(seed=3, device="cuda").store.flat
     rel = ((wg - we).norm() / (we - w0).norm()).item()
     assert rel < 0.2, rel
+
+
+def test_fit_concurrent_on_streams_matches_sequential():
+    """Three members trained concurrently on HIP streams (training/trainer.py:fit_concurrent) track
+    back-to-back fits (atomics make the kernels order-nondeterministic, so loss histories are
+    compared to 2 %), and train_ensemble on one GPU uses the concurrent path."""
+    import os
+    import tempfile
+
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel.ensemble import load_ensemble_prefix, train_ensemble
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.training.trainer import fit_concurrent
+
+    _ext.require()
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(3072, 60, 4, generator=g)
+    y = (x[:, :, 0].mean(1) > 0).float()
+    kw = dict(epochs=3, batch_size=512, validation_split=0.1, verbose=0)
+    seq = [AlarconCNN1D(seed=20 + i, device="cuda") for i in range(3)]
+    h_seq = [m.fit(x, y, **kw) for m in seq]
+    con = [AlarconCNN1D(seed=20 + i, device="cuda") for i in range(3)]
+    h_con = fit_concurrent(con, x, y, **kw)
+    for hs, hc in zip(h_seq, h_con):
+        np.testing.assert_allclose(hc.history["loss"], hs.history["loss"], rtol=2e-2)
+    with tempfile.TemporaryDirectory() as d:
+        paths = train_ensemble(x.numpy(), y.numpy(), num_models=3, save_dir=d, prefix="m", name_offset=0, epochs=2,
+                               batch_size=512, verbose=0, epoch_backup=False)
+        assert all(os.path.exists(p) for p in paths)
+        assert len(load_ensemble_prefix(os.path.join(d, "m"), 3, device="cuda")) == 3

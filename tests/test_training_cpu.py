@@ -137,3 +137,22 @@ def test_generic_train_emulation_matches_autograd(pooled, monkeypatch):
     assert abs(lv.sum().item() - loss) < 1e-4 * max(1.0, loss)
     for k, v in eg.items():
         torch.testing.assert_close(v.reshape(q[k].grad.shape), q[k].grad, atol=1e-5, rtol=1e-4)
+
+
+def test_fit_concurrent_equals_sequential_fit():
+    """Members stepped round-robin (training/trainer.py:fit_concurrent) train exactly like
+    back-to-back fit() calls: same histories and bitwise-equal weights (CPU, no streams)."""
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.training.trainer import fit_concurrent
+
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(96, 60, 4, generator=g)
+    y = (x[:, :, 0].mean(1) > 0).float()
+    kw = dict(epochs=2, batch_size=32, validation_split=0.25, verbose=0)
+    seq = [AlarconCNN1D(seed=10 + i, device="cpu") for i in range(3)]
+    h_seq = [m.fit(x, y, callbacks=[EarlyStopping(patience=1)], **kw) for m in seq]
+    con = [AlarconCNN1D(seed=10 + i, device="cpu") for i in range(3)]
+    h_con = fit_concurrent(con, x, y, callbacks=[[EarlyStopping(patience=1)] for _ in con], **kw)
+    for a, b, hs, hc in zip(seq, con, h_seq, h_con):
+        assert hs.history == hc.history
+        for wa, wb in zip(a.get_weights(), b.get_weights()):
+            np.testing.assert_array_equal(wa, wb)

@@ -18,7 +18,7 @@ def run(models, x, y, streams, steps):
     for _ in range(steps):
         for i, m in enumerate(models):
             with torch.cuda.stream(streams[i % len(streams)]):
-                m.train_step(x, y)
+                m.train_step(x, y, return_probs=True)  # device tensors: no host sync per step
     torch.cuda.synchronize()
     return (time.perf_counter() - t) / steps
 

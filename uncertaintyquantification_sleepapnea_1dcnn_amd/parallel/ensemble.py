@@ -9,6 +9,9 @@ Training replaces the reference's sequential member loop (``train_deep_ensemble_
 * **resume** at member granularity: a member whose checkpoint exists is skipped (the reference's
   skip-if-exists, ``:130-132``) — a killed job rerun retrains only the missing members; checkpoints
   are written atomically (tmp + rename) so a crash never leaves a half-written member;
+* **concurrent members**: the members one rank owns (``world < M``) train at the same time on
+  separate HIP streams (``training/trainer.py:fit_concurrent``; a batch-1024 step fills only part of
+  the GPU), then are saved in member order;
 * **resume** at epoch granularity inside a member (``epoch_backup``): a per-member
   ``BackupAndRestore`` file holds weights + Adam state + epoch, so a member killed mid-training
   continues from its last finished epoch (fault sites for tests: ``utils/faults.py``).
@@ -29,6 +32,7 @@ import torch.distributed as dist
 from ..utils.faults import maybe_fail
 from ..models.cnn import AlarconCNN1D, load_model
 from ..training.callbacks import BackupAndRestore, EarlyStopping
+from ..training.trainer import fit_concurrent
 from . import dist as pdist
 from .data_parallel import DPContext
 
@@ -51,7 +55,8 @@ def train_ensemble(x_train, y_train, num_models: int = 5, seed_base: int = 2025,
                    prefix: str = MODEL_PREFIX, name_offset: int = 21, epochs: int = 50, batch_size: int = 1024,
                    patience: int = 5, validation_split: float = 0.1, verbose: int = 2, resume: bool = True,
                    device=None, input_shape: Optional[Sequence[int]] = None, epoch_backup: bool = True,
-                   extra_callbacks: Optional[Sequence] = None) -> List[str]:
+                   extra_callbacks: Optional[Sequence] = None, concurrent: Optional[bool] = None) -> List[str]:
+    """Train the members this rank owns; ``concurrent`` (default: on a GPU) overlaps them on streams."""
     info = pdist.init()
     world, rank = info.world, info.rank
     groups = plan(num_models, world)
@@ -65,6 +70,7 @@ def train_ensemble(x_train, y_train, num_models: int = 5, seed_base: int = 2025,
     os.makedirs(save_dir, exist_ok=True)
     shape = tuple(input_shape) if input_shape is not None else tuple(np.asarray(x_train).shape[1:])
     paths = []
+    jobs = []  # (member, ranks, model, callbacks) this rank trains
     for m, ranks in enumerate(groups):
         path = member_path(save_dir, m, prefix, name_offset)
         paths.append(path)
@@ -74,8 +80,6 @@ def train_ensemble(x_train, y_train, num_models: int = 5, seed_base: int = 2025,
             if verbose:
                 print(f"\n--- Model {m + 1}/{num_models} (Seed: {seed_base + m}) already exists. Skipping training. ---")
             continue
-        if verbose:
-            print(f"\n--- Training Model {m + 1}/{num_models} (Seed: {seed_base + m}) on ranks {ranks} ---")
         model = AlarconCNN1D(input_shape=shape, seed=seed_base + m, device=dev)
         if len(ranks) > 1:
             model.dp = DPContext(pgroups[m], len(ranks), ranks.index(rank))
@@ -83,11 +87,30 @@ def train_ensemble(x_train, y_train, num_models: int = 5, seed_base: int = 2025,
         cbs = [es] + list(extra_callbacks or [])
         if epoch_backup:  # a member killed mid-training resumes at its last finished epoch
             cbs.append(BackupAndRestore(os.path.join(save_dir, ".backup_" + os.path.splitext(os.path.basename(path))[0])))
-        hist = model.fit(x_train, y_train, epochs=epochs, batch_size=batch_size, validation_split=validation_split,
-                         callbacks=cbs, verbose=verbose if ranks.index(rank) == 0 else 0)
+        jobs.append((m, ranks, model, cbs))
+    if concurrent is None:
+        concurrent = torch.device(dev).type == "cuda"
+    together = [j for j in jobs if len(j[1]) == 1] if concurrent else []
+    if len(together) > 1:
+        if verbose:
+            print(f"\n--- Training Models {[j[0] + 1 for j in together]} concurrently on rank {rank} ---")
+        hists = fit_concurrent([j[2] for j in together], x_train, y_train, callbacks=[j[3] for j in together],
+                               epochs=epochs, batch_size=batch_size, validation_split=validation_split,
+                               verbose=verbose)
+        done = {j[0]: h for j, h in zip(together, hists)}
+    else:
+        done = {}
+    for m, ranks, model, cbs in jobs:
+        if m in done:
+            hist = done[m]
+        else:
+            if verbose:
+                print(f"\n--- Training Model {m + 1}/{num_models} (Seed: {seed_base + m}) on ranks {ranks} ---")
+            hist = model.fit(x_train, y_train, epochs=epochs, batch_size=batch_size, validation_split=validation_split,
+                             callbacks=cbs, verbose=verbose if ranks.index(rank) == 0 else 0)
         maybe_fail("ensemble.before_save", member=m)
         if ranks.index(rank) == 0:
-            model.save(path)
+            model.save(paths[m])
             if verbose:
                 print(f"Model {m + 1} saved successfully (Trained for {len(hist.history.get('loss', []))} epochs).")
     pdist.barrier()

@@ -71,6 +71,67 @@ def evaluate_arrays(model, x: torch.Tensor, y: torch.Tensor, batch_size: int = 1
 def fit(model, x, y, batch_size: int = 32, epochs: int = 1, verbose: int = 1, callbacks: Optional[List[Callback]] = None,
         validation_split: float = 0.0, validation_data=None, shuffle: bool = True, seed: Optional[int] = None,
         initial_epoch: int = 0, grad_allreduce=None) -> History:
+    """Keras ``model.fit`` semantics (``cnn_baseline_train.py:210-217``); runs :func:`fit_steps` to the end."""
+    it = fit_steps(model, x, y, batch_size, epochs, verbose, callbacks, validation_split, validation_data, shuffle,
+                   seed, initial_epoch, grad_allreduce)
+    while True:
+        try:
+            next(it)
+        except StopIteration as stop:
+            return stop.value
+
+
+def fit_concurrent(models: List, x, y, streams: Optional[List] = None, **fit_kwargs) -> List[History]:
+    """Train several independent models (ensemble members sharing one GPU) at the same time.
+
+    Each model's :func:`fit_steps` runs on its own HIP stream and the host round-robins one
+    optimizer step per model, so the kernels of different members overlap on the device (a
+    batch-1024 step of this small CNN fills only part of the GPU: 8 members on 3 streams train
+    1.39-1.48x faster than back to back, ``profiles/multistream_train_r1.json``).  Every model keeps its own data
+    order, callbacks (EarlyStopping, BackupAndRestore) and epoch-end host synchronisation; results
+    are identical to sequential ``fit`` calls.  ``fit_kwargs`` as for :func:`fit`; per-model
+    ``callbacks`` may be given as a list of lists.
+    """
+    import contextlib
+
+    cbs = fit_kwargs.pop("callbacks", None)
+    per_cbs = cbs if (cbs and isinstance(cbs[0], (list, tuple))) else [cbs] * len(models)
+    dev = models[0].device if models else torch.device("cpu")
+    x, y = _to_device(x, dev), _to_device(y, dev)  # one device copy shared by every member
+    if streams is None:
+        # 3 streams + the default one fit HIP's 4 hardware queues per process (GPU_MAX_HW_QUEUES);
+        # more streams share queues and measured no faster (profiles/multistream_train_r1.json)
+        streams = [torch.cuda.Stream(device=dev) for _ in range(min(3, len(models)))] if dev.type == "cuda" else [None]
+    cur = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
+    for s in streams:
+        if s is not None:
+            s.wait_stream(cur)  # inputs produced on the current stream
+    ctx = [(torch.cuda.stream(streams[i % len(streams)]) if streams[i % len(streams)] is not None
+            else contextlib.nullcontext()) for i in range(len(models))]
+    gens = []
+    for i, m in enumerate(models):
+        with ctx[i]:
+            gens.append(fit_steps(m, x, y, callbacks=per_cbs[i], **fit_kwargs))
+    hist: List[Optional[History]] = [None] * len(models)
+    live = list(range(len(models)))
+    while live:
+        for i in list(live):
+            with ctx[i]:
+                try:
+                    next(gens[i])
+                except StopIteration as stop:
+                    hist[i] = stop.value
+                    live.remove(i)
+    for s in streams:
+        if s is not None and cur is not None:
+            cur.wait_stream(s)
+    return hist
+
+
+def fit_steps(model, x, y, batch_size: int = 32, epochs: int = 1, verbose: int = 1,
+              callbacks: Optional[List[Callback]] = None, validation_split: float = 0.0, validation_data=None,
+              shuffle: bool = True, seed: Optional[int] = None, initial_epoch: int = 0, grad_allreduce=None):
+    """Generator form of :func:`fit`: yields after every optimizer step, returns the History."""
     dev = model.device
     X = _to_device(x, dev)
     Y = _to_device(y, dev)
@@ -122,6 +183,7 @@ def fit(model, x, y, batch_size: int = 32, epochs: int = 1, verbose: int = 1, ca
             n_seen += int(gidx.numel())
             acc_m.update_state(yb, p)
             auc_m.update_state(yb, p)
+            yield
         if dp is not None and dp.size > 1:
             _sync_metrics(dp, loss_acc, acc_m, auc_m)
         loss_m.update(loss_acc.item(), n_seen)
