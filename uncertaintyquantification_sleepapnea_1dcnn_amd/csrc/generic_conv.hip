@@ -20,6 +20,8 @@
 // never straddle a 16-row tile).  A workgroup is 2 x 2 waves over 128 rows x 128 channels; each wave
 // owns 4 row tiles x 4 channel tiles, so a k-step costs 4 activation gathers + 4 weight-fragment
 // loads for 16 MFMAs (row gathers are shared through L1 by the two waves of a row half).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace apneauq {
@@ -50,10 +52,9 @@ enum { kInfer = 0, kTrain = 1, kLinear = 2 };
 constexpr int kStatSlots = 16;
 
 constexpr int kRT = 4, kCT = 4;  // row / channel tiles per wave; a workgroup is 2 x 2 waves
-constexpr int kLdsRT = 8, kLdsCT = 4;  // conv_lds_kernel: 1 x 4 waves over 128 rows x 256 channels
 
 // Epilogue of one wave: acc[c][r] holds rows (rn[r], rt[r]) x channels ct*16 + 4h .. +3 per lane.
-template <int MODE, int kRT, int kCT>
+template <int MODE>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& A, f32x4 (&acc)[kCT][kRT], const int (&rn)[kRT],
                                               const int (&rt)[kRT], const bool (&rok)[kRT], int ct0, int nct,
                                               int m, int h) {
@@ -224,7 +225,7 @@ __global__ __launch_bounds__(256) void conv_block_kernel(ConvArgs A) {
     }
   }
 
-  conv_epilogue<MODE, kRT, kCT>(A, acc, rn, rt, rok, ct0, nct, m, h);
+  conv_epilogue<MODE>(A, acc, rn, rt, rok, ct0, nct, m, h);
 }
 
 // LDS-staged variant (Cin % 8 == 0, host-checked LDS budget): the workgroup's input rows -- one
@@ -233,17 +234,14 @@ __global__ __launch_bounds__(256) void conv_block_kernel(ConvArgs A) {
 // reads B fragments with ds_read_b128 instead of one 16-B global gather per lane, row tile and
 // k-step.  Taps that cross a sample boundary are masked per lane (t + tap - pad outside [0, L)).
 // The row stride is padded by 16 B so the 16 rows a lane group reads fall into different banks.
-// Wave layout 1 x 4: every wave covers all 128 staged rows (8 row tiles) x 4 channel tiles, so a
-// workgroup spans 256 output channels and each weight fragment feeds 8 MFMAs (the 2 x 2 layout of
-// conv_block_kernel loads every fragment twice per workgroup and feeds 4).
 template <int MODE>
 __global__ __launch_bounds__(256) void conv_lds_kernel(ConvArgs A) {
-  constexpr int kRT = kLdsRT, kCT = kLdsCT;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int m = lane & 15, h = lane >> 4;
+  const int wr = wave >> 1, wc = wave & 1;
   const long long rows = (long long)A.n * A.Lp;
-  const long long wg_row0 = (long long)blockIdx.x * (kRT * 16);
+  const long long wg_row0 = (long long)blockIdx.x * (2 * kRT * 16);
   const int pad = (A.ksize - 1) / 2;
   const int K = A.ksize * A.cin;
   // first input row the workgroup can touch: (sample, step) of its first output row, minus the halo
@@ -260,9 +258,9 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvArgs A) {
     *reinterpret_cast<bf16x8*>(smem + lr * A.lds_stride + cc * 16) = v;
   }
   __syncthreads();
-  const long long row_base = wg_row0;
+  const long long row_base = wg_row0 + wr * (kRT * 16);
   const int nct = A.cout_pad / 16;
-  const int ct0 = (blockIdx.y * 4 + wave) * kCT;
+  const int ct0 = (blockIdx.y * 2 + wc) * kCT;
   if (ct0 >= nct) return;  // wave-uniform, after the only barrier
 
   int rn[kRT], rt[kRT], lr0[kRT];
@@ -287,8 +285,19 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvArgs A) {
   int tap = (8 * h) / A.cin, ci = 8 * h - tap * A.cin;
   const bf16x8 zero8 = bf16x8{(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f,
                               (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
+  // weight fragments are software-pipelined one k-step ahead: the global (L2) load of step s + 1
+  // is in flight while the MFMAs of step s run
+  const gbf16x8* wf = (const gbf16x8*)A.wfrag + (long long)ct0 * 64 + lane;
+  const int nc = nct - ct0 < kCT ? nct - ct0 : kCT;  // wave-uniform
+  bf16x8 a[kCT];
+#pragma unroll
+  for (int c = 0; c < kCT; ++c) a[c] = c < nc ? wf[c * 64] : zero8;
   for (int s = 0; s < A.nstep; ++s) {
     const bool kok = 32 * s + 8 * h < K;
+    bf16x8 an[kCT];
+    const gbf16x8* wn = wf + (long long)(s + 1 < A.nstep ? s + 1 : s) * nct * 64;
+#pragma unroll
+    for (int c = 0; c < kCT; ++c) an[c] = c < nc ? wn[c * 64] : zero8;
     bf16x8 b[kRT];
 #pragma unroll
     for (int r = 0; r < kRT; ++r) {
@@ -300,20 +309,20 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvArgs A) {
     }
 #pragma unroll
     for (int c = 0; c < kCT; ++c) {
-      const int ct = ct0 + c;
-      if (ct < nct) {  // wave-uniform
-        const bf16x8 a = ((const gbf16x8*)A.wfrag)[((long long)s * nct + ct) * 64 + lane];
+      if (c < nc) {  // wave-uniform
 #pragma unroll
-        for (int r = 0; r < kRT; ++r) acc[c][r] = mfma16(a, b[r], acc[c][r]);
+        for (int r = 0; r < kRT; ++r) acc[c][r] = mfma16(a[c], b[r], acc[c][r]);
       }
     }
+#pragma unroll
+    for (int c = 0; c < kCT; ++c) a[c] = an[c];
     ci += 32;
     while (ci >= A.cin) {
       ci -= A.cin;
       ++tap;
     }
   }
-  conv_epilogue<MODE, kRT, kCT>(A, acc, rn, rt, rok, ct0, nct, m, h);
+  conv_epilogue<MODE>(A, acc, rn, rt, rok, ct0, nct, m, h);
 }
 
 // GAP over time + Dense(C -> 1): one wave per sample, fp32 accumulation.
@@ -381,10 +390,13 @@ hipError_t launch_generic_conv(const void* x, const void* wfrag, const float* ep
   A.x_rows = x_rows;
   A.lds_rows = (int)span;
   A.lds_stride = stride;
-  const bool use_lds = cin % 8 == 0 && span * stride <= 80 * 1024 && x_rows > 0;
+  static const bool lds_enabled = [] {  // APNEAUQ_GCONV_LDS=0 forces the direct-gather kernel (A/B runs)
+    const char* e = getenv("APNEAUQ_GCONV_LDS");
+    return !(e && e[0] == '0');
+  }();
+  const bool use_lds = lds_enabled && cin % 8 == 0 && span * stride <= 80 * 1024 && x_rows > 0;
   if (use_lds) {
     const size_t lds = (size_t)span * stride;
-    const dim3 grid((unsigned)((rows + 127) / 128), (unsigned)((cout_pad / 16 + 4 * generic::kLdsCT - 1) / (4 * generic::kLdsCT)));
     if (mode == generic::kTrain)
       hipLaunchKernelGGL(generic::conv_lds_kernel<generic::kTrain>, grid, dim3(256), lds, stream, A);
     else if (mode == generic::kLinear)
