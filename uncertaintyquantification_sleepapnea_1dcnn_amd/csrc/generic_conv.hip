@@ -152,7 +152,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& A, f32x4 (&acc)[kC
 }
 
 template <bool VEC, int MODE>
-__global__ __launch_bounds__(256) void conv_block_kernel(ConvArgs A) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void conv_block_kernel(ConvArgs A) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int m = lane & 15, h = lane >> 4;
   const int wr = wave >> 1, wc = wave & 1;
@@ -235,7 +235,7 @@ __global__ __launch_bounds__(256) void conv_block_kernel(ConvArgs A) {
 // k-step.  Taps that cross a sample boundary are masked per lane (t + tap - pad outside [0, L)).
 // The row stride is padded by 16 B so the 16 rows a lane group reads fall into different banks.
 template <int MODE>
-__global__ __launch_bounds__(256) void conv_lds_kernel(ConvArgs A) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void conv_lds_kernel(ConvArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int m = lane & 15, h = lane >> 4;
