@@ -183,8 +183,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     for (int r = 0; r < kRT; ++r) acc[c][r] = f32x4{0.f, 0.f, 0.f, 0.f};
   // (tap, ci) of k = 32 s + 8 h, advanced incrementally (no per-step division)
   int tap = (8 * h) / A.cin, ci = 8 * h - tap * A.cin;
+  // weight fragments of k-step s + 1 are loaded while step s runs (as in conv_lds_kernel)
+  const gbf16x8* wf = (const gbf16x8*)A.wfrag + (long long)ct0 * 64 + lane;
+  const int nc = nct - ct0 < kCT ? nct - ct0 : kCT;  // wave-uniform
+  bf16x8 a[kCT];
+#pragma unroll
+  for (int c = 0; c < kCT; ++c) {
+    if (c < nc) {
+      a[c] = wf[c * 64];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[c][j] = (__bf16)0.f;
+    }
+  }
   for (int s = 0; s < A.nstep; ++s) {
     const int kk0 = 32 * s + 8 * h;
+    // (the element-gather variant has no registers to spare for the prefetch: it loads step s here)
+    bf16x8 an[kCT];
+    const gbf16x8* wn = wf + (long long)(VEC ? (s + 1 < A.nstep ? s + 1 : s) : s) * nct * 64;
+#pragma unroll
+    for (int c = 0; c < kCT; ++c) {
+      if constexpr (VEC)
+        an[c] = c < nc ? wn[c * 64] : a[c];
+      else if (c < nc)
+        a[c] = wn[c * 64];
+    }
     bf16x8 b[kRT];
 #pragma unroll
     for (int r = 0; r < kRT; ++r) {
@@ -209,14 +232,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     }
 #pragma unroll
     for (int c = 0; c < kCT; ++c) {
-      const int ct = ct0 + c;
-      if (ct < nct) {  // wave-uniform
-        const bf16x8 a = ((const gbf16x8*)A.wfrag)[((long long)s * nct + ct) * 64 + lane];
+      if (c < nc) {  // wave-uniform
 #pragma unroll
-        for (int r = 0; r < kRT; ++r) acc[c][r] = mfma16(a, b[r], acc[c][r]);
+        for (int r = 0; r < kRT; ++r) acc[c][r] = mfma16(a[c], b[r], acc[c][r]);
       }
     }
     if constexpr (VEC) {
+#pragma unroll
+      for (int c = 0; c < kCT; ++c) a[c] = an[c];
       ci += 32;
       while (ci >= A.cin) {
         ci -= A.cin;
