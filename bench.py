@@ -1,22 +1,35 @@
 #!/usr/bin/env python3
 """Headline benchmark: 30s-windows/sec for MC Dropout T=50 & Deep Ensemble M=8 UQ inference.
 
-Driver contract (one rank per GPU; ``torchrun --nproc-per-node N bench.py --gpus N ...``):
-one *step* processes a fixed batch of ``--windows`` windows PER GPU (weak scaling) through the
+Driver contract: ``python bench.py --gpus N --steps K --warmup W`` (self-launches N ranks, one per
+GPU, when not already under torchrun) or ``torchrun --nproc-per-node N bench.py --gpus N ...``.
+One *step* processes a fixed batch of ``--windows`` windows PER GPU (weak scaling) through the
 complete UQ inference of both methods the reference evaluates
 (``uncertainty_quantification/analyze_mcd_patient_level.py`` / ``analyze_de_patient_level.py``):
 
-  1. MC Dropout, T=50 stochastic passes (fused HIP kernel, counter-based dropout masks, BN on
-     running statistics = standard MC Dropout) over this rank's window shard, then the per-window
-     mean / variance / entropy / expected entropy / MI reduction (HIP ``uq_reduce``);
-  2. Deep Ensemble, M=8 members (inference BN, no dropout) placed member-parallel over the GPUs,
-     RCCL all_to_all of member probabilities over xGMI, then the same reduction;
+  1. MC Dropout, T=50 stochastic passes with the reference's semantics (``uq_techniques.py:22``,
+     ``model(x, training=True)``): every pass normalises each BatchNorm with the batch statistics
+     of the WHOLE window set (all ranks: SyncBN all-reduce per layer) and updates the moving
+     averages; layer-synchronous HIP kernels (``csrc/train_conv.hip``), counter-based dropout
+     masks keyed by the global window index; then the per-window mean / variance / entropy /
+     expected entropy / MI reduction (HIP ``uq_reduce``);
+  2. Deep Ensemble, M=8 members (inference BN, no dropout; ``uq_techniques.py:29``), fused
+     whole-network HIP kernel, member-parallel over the GPUs with an RCCL all_to_all of member
+     probabilities over xGMI, then the same reduction;
   3. the 6 aggregate UQ scalars of each method, all-reduced over ranks.
 
-``value`` = windows fully UQ-evaluated (both methods) per second over ALL GPUs.  Model: the
-reference Alarcón 1D-CNN (853,441 params, 60 x 4 windows), random-init weights with non-trivial
-BN statistics, synthetic standardised windows.  Timing: W untimed warmup steps, then K steps
-bracketed by barrier + synchronize; the max over ranks is reported.
+``value`` = windows fully UQ-evaluated (both methods) per second over ALL GPUs, for the
+reference-semantics MCD (``--bn-mode batch``, the default).  The same run also times standard MC
+Dropout (BN on running statistics, the fused whole-network kernel) and reports it under
+``extra.running_bn``, and an fp32 deviation block: the bf16 HIP paths against the fp32 PyTorch
+reference model (``models/reference.py``) on a fixed window subset.
+
+Model: the reference Alarcón 1D-CNN (853,441 params, 60 x 4 windows), random-init weights with
+non-trivial BN statistics, synthetic standardised windows.  Timing: W untimed warmup steps, then K
+steps bracketed by barrier + synchronize; the max over ranks is reported.
+
+``--device cpu`` is a dry run of the same launcher / collectives / metrics on gloo with the fp32
+reference model (CPU tests); its numbers are not performance claims.
 """
 from __future__ import annotations
 
@@ -30,123 +43,175 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-import torch  # noqa: E402
-
-from uncertaintyquantification_sleepapnea_1dcnn_amd.models import reference as R  # noqa: E402
-from uncertaintyquantification_sleepapnea_1dcnn_amd.models.spec import DEFAULT_SPEC as SPEC  # noqa: E402
-from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import fused, uq as uq_ops  # noqa: E402
-from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel import dist as pdist  # noqa: E402
-from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel import inference as pinf  # noqa: E402
-
 METRIC = "30s-windows/sec for MCD T=50 & DE M=8 inference at 1/2/4/8 MI355X"
 # The reference publishes no throughput number.  vs_baseline divides by OUR
 # measurement of its exact loops in eager fp32 PyTorch on 1 x MI355X (bench/comparator.py, N=16384,
 # MCD T=50 with BN batch statistics as the reference runs it + DE M=8 predict(batch 32) + NumPy UQ
-# metrics): profiles/comparator_eager_fp32_batchbn_r1.json.  It is the faster of the two comparator
-# modes (BN running statistics: 3102 windows/s), so the ratio is the conservative one.
+# metrics): profiles/comparator_eager_fp32_batchbn_r1.json — the same MCD semantics as the headline.
 BASELINE = 4925.9
+BASELINE_BASIS = ("eager fp32 PyTorch running the reference's loops (MCD: 50 x model(X, training=True) with BN batch "
+                  "stats; DE: 8 x predict(batch 32)) on 1 x MI355X, profiles/comparator_eager_fp32_batchbn_r1.json")
 
 
-def synthetic_params(seed: int):
-    return R.synthetic_params(SPEC, seed)
-
-
-def main(argv=None):
-    ap = argparse.ArgumentParser(description=__doc__)
-    ap.add_argument("--gpus", type=int, default=1)
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); self-launched unless under torchrun")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--windows", type=int, default=16384, help="windows per GPU per step")
     ap.add_argument("--passes", type=int, default=50, help="MC Dropout passes T")
     ap.add_argument("--members", type=int, default=8, help="Deep Ensemble members M")
     ap.add_argument("--seed", type=int, default=2025)
-    ap.add_argument("--bn-mode", choices=["running", "batch"], default="running",
-                    help="MC-Dropout BatchNorm: running statistics (standard MC Dropout, fused kernel) or "
-                         "per-pass batch statistics over the whole window set = the reference's "
-                         "model(x, training=True) (layer-wise HIP kernels + SyncBN across ranks)")
-    a = ap.parse_args(argv)
+    ap.add_argument("--bn-mode", choices=["batch", "running"], default="batch",
+                    help="MC-Dropout BatchNorm of the headline: per-pass batch statistics over the whole window set "
+                         "(the reference's model(x, training=True); default) or running statistics (standard MC "
+                         "Dropout, fused kernel)")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the other BN mode's timing")
+    ap.add_argument("--no-deviation", action="store_true", help="skip the fp32 deviation block")
+    ap.add_argument("--deviation-windows", type=int, default=1024)
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
+                    help="cpu = dry run of launcher + collectives on gloo with the fp32 reference model")
+    return ap.parse_args(argv)
 
-    info = pdist.init()
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    a = parse(argv)
+    # ---- launcher: spawn one worker per GPU BEFORE anything (incl. torch) touches the GPU
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel import launch
+
+    rc = launch.maybe_spawn(a.gpus, __file__, argv)
+    if rc is not None:
+        sys.exit(rc)
+    if a.device == "cpu":
+        os.environ.setdefault("APNEAUQ_DIST_BACKEND", "gloo")
+        os.environ["CUDA_VISIBLE_DEVICES"] = ""
+    run(a)
+
+
+def run(a):
+    import torch
+
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.models import reference as R
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.models.spec import DEFAULT_SPEC as SPEC
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import uq as uq_ops
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel import dist as pdist
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel import inference as pinf
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel import launch
+
+    cpu = a.device == "cpu"
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if cpu:
+        torch.set_num_threads(max(1, (os.cpu_count() or 2) // max(1, world_env)))
+    launch.check_world(a.gpus, world_env, None if cpu else torch.cuda.device_count(), "cpu" if cpu else "cuda")
+    info = pdist.init(device="cpu" if cpu else None)
     dev = info.device
-    if dev.type != "cuda":
-        raise SystemExit("bench.py needs a GPU")
+    if not cpu and dev.type != "cuda":
+        raise SystemExit("bench.py needs a GPU (use --device cpu for the dry run)")
     world, rank = info.world, info.rank
     n_loc = a.windows
     n_glob = n_loc * world
 
-    # ---- resident data: the whole synthetic window set lives in HBM on every rank (bf16)
+    # ---- resident data: the whole synthetic window set lives in HBM on every rank
     g = torch.Generator(device="cpu").manual_seed(a.seed)
-    x_glob = torch.randn(n_glob, 60, 4, generator=g).to(torch.bfloat16).to(dev)
-    y_glob = (torch.rand(n_glob, generator=g) < 0.3).to(torch.int32).to(dev)
+    x32_glob = torch.randn(n_glob, 60, 4, generator=g)
+    y_glob = (torch.rand(n_glob, generator=g) < 0.3).to(torch.int32)
+    xdt = torch.float32 if cpu else torch.bfloat16
+    x_glob = x32_glob.to(xdt).to(dev)
+    y_glob = y_glob.to(dev)
     start, stop = pdist.shard_range(n_glob, rank, world)
     x_loc = x_glob[start:stop].contiguous()
     y_loc = y_glob[start:stop].contiguous()
 
-    # ---- models: one MC-Dropout model; M ensemble members, member-parallel when G | M
-    blob_mcd = fused.pack_blob(SPEC, {k: v.to(dev) for k, v in synthetic_params(a.seed).items()}).unsqueeze(0)
+    params_mcd = {k: v.to(dev) for k, v in R.synthetic_params(SPEC, a.seed).items()}
     member_parallel = world > 1 and a.members % world == 0
     mem_ids = (list(range(rank * (a.members // world), (rank + 1) * (a.members // world)))
                if member_parallel else list(range(a.members)))
-    blobs_de = torch.stack([fused.pack_blob(SPEC, {k: v.to(dev) for k, v in synthetic_params(a.seed + 100 + m).items()})
-                            for m in mem_ids])
+    params_de = [{k: v.to(dev) for k, v in R.synthetic_params(SPEC, a.seed + 100 + m).items()} for m in mem_ids]
+    sync = (lambda t: torch.distributed.all_reduce(t)) if world > 1 else None
 
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-    if a.bn_mode == "batch":
-        from uncertaintyquantification_sleepapnea_1dcnn_amd.models.cnn import AlarconCNN1D
-        from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import train_ops
+    if cpu:
+        engine = _CpuEngine(R, SPEC, params_mcd, params_de, world, start, n_glob, a.seed, a.passes)
+    else:
+        engine = _HipEngine(R, SPEC, params_mcd, params_de, world, start, n_glob, a.seed, a.passes, sync)
 
-        mcd_model = AlarconCNN1D(seed=a.seed, device=dev, params={k: v.to(dev) for k, v in synthetic_params(a.seed).items()})
-        sync = torch.distributed.all_reduce if world > 1 else None
+    def timed(mode: str, steps: int, warmup: int, step_base: int):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if not cpu else None
+        phase = [0.0, 0.0]
 
-    def mcd_probs(i):
-        if a.bn_mode == "running":
-            return pinf.mcd_probs_local(blob_mcd, x_loc, a.passes, a.seed + i, start)
-        # reference semantics: every pass normalises with the batch statistics of ALL windows
-        return train_ops.forward_batch_stats(mcd_model, x_loc, a.passes, pass_base=i * a.passes, seed=a.seed,
-                                             update_moving=True, sync=sync, window_offset=start, global_n=n_glob,
-                                             max_samples=1 << 18)
+        def step(i):
+            if ev:
+                ev[0].record()
+            t0 = time.perf_counter()
+            pm = engine.mcd(mode, x_loc, step_base + i)
+            s_mcd = pinf.aggregate_sums(uq_ops.metrics(pm), y_loc)
+            if ev:
+                ev[1].record()
+            t1 = time.perf_counter()
+            if member_parallel:
+                pd = pinf.all_to_all_members(engine.de(x_glob), world)
+            else:
+                pd = engine.de(x_loc)
+            s_de = pinf.aggregate_sums(uq_ops.metrics(pd), y_loc)
+            sums = torch.stack([s_mcd, s_de])
+            pdist.all_reduce_sum_(sums)
+            if ev:
+                ev[2].record()
+            return sums, (t0, t1, time.perf_counter())
 
-    def step(i):
-        ev[0].record()
-        pm = mcd_probs(i)
-        m_mcd = uq_ops.metrics(pm)
-        s_mcd = pinf.aggregate_sums(m_mcd, y_loc)
-        ev[1].record()
-        if member_parallel:
-            pd = pinf.de_probs_member_parallel(blobs_de, x_glob, world)
-        else:
-            pd = fused.fused_forward(x_loc, blobs_de, SPEC)[:, 0]
-        m_de = uq_ops.metrics(pd)
-        s_de = pinf.aggregate_sums(m_de, y_loc)
-        sums = torch.stack([s_mcd, s_de])
-        pdist.all_reduce_sum_(sums)
-        ev[2].record()
-        return sums
+        for i in range(warmup):
+            step(i)
+        if not cpu:
+            torch.cuda.synchronize()
+        pdist.barrier()
+        if not cpu:
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sums = None
+        for i in range(steps):
+            sums, tt = step(warmup + i)
+            if ev and steps <= 64:
+                torch.cuda.synchronize()  # per-step split of the two phases (events)
+                phase[0] += ev[0].elapsed_time(ev[1])
+                phase[1] += ev[1].elapsed_time(ev[2])
+            elif cpu:
+                phase[0] += (tt[1] - tt[0]) * 1e3
+                phase[1] += (tt[2] - tt[1]) * 1e3
+        if not cpu:
+            torch.cuda.synchronize()
+        pdist.barrier()
+        if not cpu:
+            torch.cuda.synchronize()
+        elapsed = pdist.all_reduce_max(time.perf_counter() - t0)
+        return elapsed, sums, phase
 
-    for i in range(a.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    pdist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    mcd_ms = de_ms = 0.0
-    for i in range(a.steps):
-        sums = step(a.warmup + i)
-        if a.steps <= 64:
-            torch.cuda.synchronize()  # per-step split of the two phases (events)
-            mcd_ms += ev[0].elapsed_time(ev[1])
-            de_ms += ev[1].elapsed_time(ev[2])
-    torch.cuda.synchronize()
-    pdist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    elapsed = pdist.all_reduce_max(elapsed)
+    elapsed, sums, phase = timed(a.bn_mode, a.steps, a.warmup, 0)
     agg_mcd = pinf.finalize_aggregates(sums[0])
     agg_de = pinf.finalize_aggregates(sums[1])
-
     ms = elapsed * 1e3 / a.steps
     value = n_glob * a.steps / elapsed
+
+    secondary = None
+    if not a.no_secondary:
+        other = "running" if a.bn_mode == "batch" else "batch"
+        k2 = max(1, min(a.steps, 10))
+        e2, s2, ph2 = timed(other, k2, 1, 10_000)
+        secondary = {
+            "bn_mode_mcd": other,
+            "value": round(n_glob * k2 / e2, 1),
+            "ms_per_step": round(e2 * 1e3 / k2, 3),
+            "steps": k2,
+            "mcd_phase_ms": round(ph2[0] / k2, 3),
+            "mcd_windows_per_s_per_gpu": round(n_loc / (ph2[0] / k2 / 1e3), 1) if ph2[0] else None,
+            "mcd_mean_entropy": round(pinf.finalize_aggregates(s2[0])["mean_total_pred_entropy"], 6),
+        }
+
+    deviation = None
+    if not cpu and not a.no_deviation:
+        deviation = engine.deviation(x32_glob[: a.deviation_windows].to(dev), y_glob[: a.deviation_windows])
+
     macs = SPEC.forward_macs()
+    devices = pdist.gather_device_ids()  # collective: every rank
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -158,32 +223,156 @@ def main(argv=None):
             "ms_per_step": round(ms, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": None if BASELINE is None else value / BASELINE,
-            "dtype": "bf16",
+            "vs_baseline": None if (BASELINE is None or cpu) else round(value / BASELINE, 3),
+            "vs_baseline_basis": BASELINE_BASIS if a.bn_mode == "batch" else
+            BASELINE_BASIS + " (NOTE: headline run in bn_mode=running; semantics differ)",
+            "dtype": "fp32" if cpu else "bf16",
             "data": "synthetic (random standardized 60x4 windows, random-init weights)",
             "config": {
                 "model": "Alarcon 1D-CNN (6x[Conv1D-ReLU-BN-Dropout]+GAP+Dense, 853,441 params), input (60, 4)",
                 "global_batch": n_glob,
                 "seq_len": 60,
-                "parallelism": f"dp{world}" + (f" (MCD: window-sharded; DE: member-parallel {a.members // world}/GPU + all_to_all)"
-                                               if member_parallel else " (window-sharded, members replicated)"),
+                "parallelism": f"dp{world}" + (f" (MCD: window-sharded + SyncBN; DE: member-parallel {a.members // world}/GPU"
+                                               " + all_to_all)" if member_parallel else
+                                               (" (MCD: window-sharded + SyncBN; DE: members replicated)" if world > 1 else "")),
                 "mcd_passes": a.passes,
                 "de_members": a.members,
                 "bn_mode_mcd": a.bn_mode,
                 "windows_per_gpu_per_step": n_loc,
             },
+            "backend": info.backend,
+            "devices": devices,
             "extra": {
-                "mcd_phase_ms": round(mcd_ms / max(a.steps, 1), 3),
-                "de_phase_ms": round(de_ms / max(a.steps, 1), 3),
-                "mcd_windows_per_s_per_gpu": round(n_loc / (mcd_ms / a.steps / 1e3), 1) if mcd_ms else None,
-                "de_windows_per_s_per_gpu": round(n_loc / (de_ms / a.steps / 1e3), 1) if de_ms else None,
+                "mcd_phase_ms": round(phase[0] / max(a.steps, 1), 3),
+                "de_phase_ms": round(phase[1] / max(a.steps, 1), 3),
+                "mcd_windows_per_s_per_gpu": round(n_loc / (phase[0] / a.steps / 1e3), 1) if phase[0] else None,
+                "de_windows_per_s_per_gpu": round(n_loc / (phase[1] / a.steps / 1e3), 1) if phase[1] else None,
                 "effective_tflops_per_gpu": round(n_loc * (a.passes + a.members) * 2 * macs / (ms / 1e3) / 1e12, 1),
                 "mcd_mean_entropy": round(agg_mcd["mean_total_pred_entropy"], 6),
                 "de_mean_mutual_info": round(agg_de["mean_mutual_info"], 6),
+                ("running_bn" if a.bn_mode == "batch" else "batch_bn"): secondary,
+                "fp32_deviation": deviation,
             },
         }
         print(json.dumps(out), flush=True)
     pdist.shutdown()
+
+
+class _HipEngine:
+    """bf16 HIP kernels: batch-BN MCD on the layer-wise kernels, running-BN MCD and DE fused."""
+
+    def __init__(self, R, spec, params_mcd, params_de, world, start, n_glob, seed, passes, sync):
+        import torch
+
+        from uncertaintyquantification_sleepapnea_1dcnn_amd.models.cnn import AlarconCNN1D
+        from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import fused
+
+        self.R, self.spec, self.fused = R, spec, fused
+        self.world, self.start, self.n_glob, self.seed, self.passes, self.sync = world, start, n_glob, seed, passes, sync
+        self.params_mcd = params_mcd
+        self.params_de = params_de
+        self.blob_mcd = fused.pack_blob(spec, params_mcd).unsqueeze(0)
+        self.blobs_de = torch.stack([fused.pack_blob(spec, p) for p in params_de])
+        # the batch-BN model owns its own parameter copy: its moving statistics are mutated every pass
+        self.model = AlarconCNN1D(seed=seed, device=params_mcd["conv1d_1/kernel"].device,
+                                  params={k: v.clone() for k, v in params_mcd.items()})
+
+    def mcd(self, mode, x_loc, i):
+        from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import train_ops
+        from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel import inference as pinf
+
+        if mode == "running":
+            return pinf.mcd_probs_local(self.blob_mcd, x_loc, self.passes, self.seed + i, self.start)
+        # reference semantics: every pass normalises with the batch statistics of ALL windows
+        return train_ops.forward_batch_stats(self.model, x_loc, self.passes, pass_base=i * self.passes, seed=self.seed,
+                                             update_moving=True, sync=self.sync, window_offset=self.start,
+                                             global_n=self.n_glob, max_samples=1 << 18)
+
+    def de(self, x):
+        return self.fused.fused_forward(x, self.blobs_de, self.spec)[:, 0]
+
+    def deviation(self, x32, y):
+        """bf16 HIP results vs the fp32 PyTorch reference on the same windows, masks and weights."""
+        import torch
+
+        from uncertaintyquantification_sleepapnea_1dcnn_amd.models.cnn import AlarconCNN1D
+        from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import train_ops, uq as uq_ops
+        from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel import inference as pinf
+
+        R, spec = self.R, self.spec
+        n = x32.shape[0]
+        xb = x32.to(torch.bfloat16)
+        ids = torch.arange(n, device=x32.device)
+        out = {"windows": n, "reference": "models/reference.py forward in fp32 (same weights, masks, fp32 input)"}
+        with torch.no_grad():
+            # deterministic forward (DE member 0, inference BN)
+            p_hip = self.fused.fused_forward(xb, self.blobs_de[:1], spec)[0, 0]
+            p_ref = R.forward(spec, self.params_de[0], x32, training=False).reshape(-1)
+            out["de_member_max_abs_dp"] = float((p_hip - p_ref).abs().max())
+            # MC Dropout, T passes, both BN modes; identical counter-based masks on both sides
+            T, seed, base = self.passes, self.seed + 555, 777
+            agg = {}
+            for mode in ("batch", "running"):
+                if mode == "batch":
+                    model = AlarconCNN1D(seed=seed, device=x32.device,
+                                         params={k: v.clone() for k, v in self.params_mcd.items()})
+                    ph = train_ops.forward_batch_stats(model, xb, T, pass_base=base, seed=seed, update_moving=False)
+                else:
+                    ph = self.fused.fused_forward(xb, self.blob_mcd, spec, n_pass=T, dropout=True, seed=seed,
+                                                  pass_offset=base)[0]
+                pr = torch.stack([R.forward(spec, self.params_mcd, x32, dropout=True, bn_batch_stats=(mode == "batch"),
+                                            seed=seed, pass_id=base + t, sample_ids=ids).reshape(-1) for t in range(T)])
+                ah = pinf.finalize_aggregates(pinf.aggregate_sums(uq_ops.metrics(ph), y))
+                ar = pinf.finalize_aggregates(pinf.aggregate_sums(uq_ops.metrics_eager(pr), y))
+                agg[mode] = {
+                    "max_abs_dp": float((ph - pr).abs().max()),
+                    "mean_abs_dp": float((ph - pr).abs().mean()),
+                    "aggregates_hip": {k: round(v, 6) for k, v in ah.items()},
+                    "aggregates_delta": {k: float(f"{ah[k] - ar[k]:.3e}") for k in ah},
+                }
+            out["mcd_T"] = T
+            out["mcd_batch_bn"] = agg["batch"]
+            out["mcd_running_bn"] = agg["running"]
+        return out
+
+
+class _CpuEngine:
+    """fp32 reference model on the CPU (dry run of the distributed bench on gloo)."""
+
+    def __init__(self, R, spec, params_mcd, params_de, world, start, n_glob, seed, passes):
+        self.R, self.spec, self.world, self.start, self.n_glob = R, spec, world, start, n_glob
+        self.seed, self.passes = seed, passes
+        self.params_mcd, self.params_de = params_mcd, params_de
+
+    def _sync_hook(self, h):
+        import torch
+        import torch.distributed as dist
+
+        s = torch.stack([h.sum(dim=(0, 1)), (h * h).sum(dim=(0, 1))]).double()
+        cnt = torch.tensor([float(h.shape[0] * h.shape[1])], dtype=torch.float64)
+        if dist.is_initialized() and self.world > 1:
+            dist.all_reduce(s)
+            dist.all_reduce(cnt)
+        mean = s[0] / cnt
+        var = (s[1] / cnt - mean * mean).clamp_min(0)
+        return mean.float(), var.float()
+
+    def mcd(self, mode, x_loc, i):
+        import torch
+
+        ids = torch.arange(self.start, self.start + x_loc.shape[0])
+        with torch.no_grad():
+            return torch.stack([self.R.forward(self.spec, self.params_mcd, x_loc, dropout=True,
+                                               bn_batch_stats=(mode == "batch"), seed=self.seed,
+                                               pass_id=i * self.passes + t, sample_ids=ids,
+                                               bn_stats_hook=self._sync_hook if mode == "batch" else None).reshape(-1)
+                                for t in range(self.passes)])
+
+    def de(self, x):
+        import torch
+
+        with torch.no_grad():
+            return torch.stack([self.R.forward(self.spec, p, x, training=False).reshape(-1) for p in self.params_de])
 
 
 if __name__ == "__main__":

@@ -6,23 +6,27 @@ BCE, dropout, batch-statistics BN) on synthetic SHHS2-shaped windows through the
 kernels.  One "step" = one optimizer step of EVERY member; windows/s counts all members' samples
 over all GPUs (weak scaling in members per GPU when G | M).
 
-    python -m bench.train_bench --members 8 --steps 20             # 1 GPU, members sequential
-    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m bench.train_bench --members 8
+    python -m bench.train_bench --members 8 --steps 20             # 1 GPU, members on 3 streams
+    python -m bench.train_bench --gpus 8 --members 8               # self-launches 8 ranks (one per GPU)
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m bench.train_bench --gpus 8 --members 8
 """
 from __future__ import annotations
 
 import argparse
 import json
+import os
+import sys
 import time
 
-import torch
-
-from uncertaintyquantification_sleepapnea_1dcnn_amd.models.cnn import AlarconCNN1D
-from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel import dist as pdist
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
 
 
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); self-launched unless under torchrun")
     ap.add_argument("--members", type=int, default=8)
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--steps", type=int, default=20)
@@ -31,6 +35,17 @@ def main(argv=None):
     ap.add_argument("--streams", type=int, default=3, help="HIP streams the members of one GPU round-robin over "
                     "(3 + the default stream fit the 4 hardware queues HIP uses per process)")
     a = ap.parse_args(argv)
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel import launch
+
+    rc = launch.maybe_spawn(a.gpus, __file__, argv)  # before anything touches the GPU
+    if rc is not None:
+        sys.exit(rc)
+    import torch
+
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.models.cnn import AlarconCNN1D
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel import dist as pdist
+
+    launch.check_world(a.gpus, int(os.environ.get("WORLD_SIZE", "1")), torch.cuda.device_count())
     info = pdist.init()
     dev = info.device
     mine = pdist.members_of_rank(a.members, info.rank, info.world)
@@ -60,12 +75,14 @@ def main(argv=None):
     torch.cuda.synchronize()
     pdist.barrier()
     dt = pdist.all_reduce_max(time.perf_counter() - t0)
+    devices = pdist.gather_device_ids()
     if info.rank == 0:
         samples = a.members * a.batch * a.steps
         print(json.dumps({"metric": "DE training windows/s (all members, all GPUs)", "value": round(samples / dt, 1),
                           "n_gpus": info.world, "members": a.members, "batch": a.batch, "steps": a.steps,
                           "ms_per_step_all_members": round(dt * 1e3 / a.steps, 3), "dtype": "bf16",
-                          "data": "synthetic", "parallelism": f"ensemble-parallel over {info.world} GPU(s), {len(streams)} stream(s)/GPU"}))
+                          "data": "synthetic", "backend": info.backend, "devices": devices,
+                          "parallelism": f"ensemble-parallel over {info.world} GPU(s), {len(streams)} stream(s)/GPU"}))
     pdist.shutdown()
 
 

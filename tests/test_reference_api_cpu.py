@@ -69,3 +69,19 @@ def test_global_drivers_reference_signatures():
     for res in (de, mcd):
         assert "mean_predictive_variance" in res or any("variance" in k for k in res)
         assert sum(k.endswith("_ci_lower") for k in res) == 6
+
+
+def test_mc_dropout_running_calls_draw_fresh_masks():
+    """Like model(x, training=True), consecutive mc_dropout_predict calls differ."""
+    import numpy as np
+
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.models.cnn import AlarconCNN1D
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.uq import uq_techniques as U
+
+    m = AlarconCNN1D(seed=3, device="cpu")
+    x = np.random.default_rng(0).standard_normal((6, 60, 4)).astype(np.float32)
+    a = U.mc_dropout_predict(m, x, n_pred=2, bn_mode="running")
+    b = U.mc_dropout_predict(m, x, n_pred=2, bn_mode="running")
+    assert a.shape == b.shape == (2, 6, 1)
+    assert not np.array_equal(a, b)
+    assert m._call_counter == 4

@@ -156,3 +156,15 @@ def test_fit_concurrent_equals_sequential_fit():
         assert hs.history == hc.history
         for wa, wb in zip(a.get_weights(), b.get_weights()):
             np.testing.assert_array_equal(wa, wb)
+
+
+def test_graph_bound_key_tracks_optimizer_scalars():
+    """A captured training graph is re-captured when lr / betas / epsilon change."""
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.models.cnn import AlarconCNN1D
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import train_ops
+
+    m = AlarconCNN1D(seed=1, device="cpu")
+    k1 = train_ops.bound_key(m)
+    assert train_ops._same_bound(k1, train_ops.bound_key(m))
+    m.optimizer.learning_rate = 5e-4
+    assert not train_ops._same_bound(k1, train_ops.bound_key(m))

@@ -216,6 +216,18 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, syn
     return ws.loss.double().sum(), torch.sigmoid(ws.logits[:n])
 
 
+def bound_key(model):
+    """What a captured training graph bakes in: buffer identities and the optimizer's scalars
+    (learning rate / betas / epsilon are kernel arguments of the captured Adam launch)."""
+    opt = model.optimizer
+    return (model.store.flat, opt.m, opt.v, float(opt.learning_rate), float(opt.beta_1), float(opt.beta_2),
+            float(opt.epsilon))
+
+
+def _same_bound(a, b) -> bool:
+    return all(x is y for x, y in zip(a[:3], b[:3])) and tuple(a[3:]) == tuple(b[3:])
+
+
 class GraphedTrainStep:
     """The whole HIP training step of one batch size captured once as a HIP graph and replayed.
 
@@ -240,7 +252,7 @@ class GraphedTrainStep:
         model.optimizer._ensure(model.store.flat)
         # the graph bakes these buffers' addresses: a replay is only valid while they are the same
         # tensor objects (a restored optimizer state or a moved model triggers a re-capture)
-        self.bound = (model.store.flat, model.optimizer.m, model.optimizer.v)
+        self.bound = bound_key(model)
         self._sync_counters()
         self.graph = torch.cuda.CUDAGraph()
         side = torch.cuda.Stream(device=dev)
@@ -302,7 +314,7 @@ def graph_train_step(model, x: torch.Tensor, y: torch.Tensor):
     n = int(x.shape[0])
     opt = model.optimizer
     cur = g.get(n)
-    if cur is None or any(a is not b for a, b in zip(cur.bound, (model.store.flat, opt.m, opt.v))):
+    if cur is None or not _same_bound(cur.bound, bound_key(model)):
         g[n] = cur = GraphedTrainStep(model, n)
     return cur(x, y)
 

@@ -53,18 +53,28 @@ def init(backend: Optional[str] = None, device: Optional[str] = None, timeout_s:
     world = env_world()
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    use_gpu = torch.cuda.is_available() and device != "cpu"
+    use_gpu = device != "cpu" and torch.cuda.is_available()
+    # APNEAUQ_DIST_BACKEND=gloo rehearses a multi-rank GPU run on ONE card (RCCL refuses two ranks
+    # on one device); production multi-GPU runs use RCCL ("nccl").  APNEAUQ_FORCE_PG=1 creates the
+    # process group even for one rank (exercises the RCCL path on a 1-GPU box).
+    force_pg = os.environ.get("APNEAUQ_FORCE_PG", "0") == "1"
+    be = "none"
+    if world > 1 or force_pg:
+        be = backend or os.environ.get("APNEAUQ_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
     if use_gpu:
-        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+        n_dev = torch.cuda.device_count()
+        if local >= n_dev and be != "gloo":
+            raise RuntimeError(f"LOCAL_RANK {local} has no GPU ({n_dev} visible); one rank per GPU over RCCL")
+        torch.cuda.set_device(local % max(1, n_dev))
         dev = torch.device("cuda", torch.cuda.current_device())
     else:
         dev = torch.device("cpu")
-    be = "none"
-    if world > 1:
-        # APNEAUQ_DIST_BACKEND=gloo rehearses a multi-rank GPU run on ONE card (RCCL refuses two ranks
-        # on one device); production multi-GPU runs use RCCL ("nccl").
-        be = backend or os.environ.get("APNEAUQ_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
+    if be != "none":
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1 and "MASTER_PORT" not in os.environ:
+            from .launch import free_port
+
+            os.environ["MASTER_PORT"] = str(free_port())
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         if not dist.is_initialized():
             kw = dict(backend=be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
@@ -126,3 +136,15 @@ def member_groups(n_members: int, world: int) -> List[List[int]]:
         return [[m % world] for m in range(n_members)]
     per = world // n_members
     return [list(range(m * per, (m + 1) * per)) for m in range(n_members)]
+
+
+def gather_device_ids() -> List[str]:
+    """``host:device`` of every rank, in rank order (reported by the benches)."""
+    import socket
+
+    me = f"{socket.gethostname()}:{info().device}"
+    if not (dist.is_available() and dist.is_initialized()):
+        return [me]
+    out: List[Optional[str]] = [None] * dist.get_world_size()
+    dist.all_gather_object(out, me)
+    return [str(o) for o in out]

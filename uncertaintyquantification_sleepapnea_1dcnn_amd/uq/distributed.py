@@ -76,13 +76,16 @@ def mc_dropout_predict_sharded(model, x_test_data, n_pred: int = 50, bn_mode: st
     xl = x[s:e]
     seed = model.seed if seed is None else seed
     if bn_mode == "running":
+        base = model._call_counter  # fresh masks per call, identical on every rank
         if model.uses_hip():
             loc = model.hip_forward(xl.to(torch.bfloat16).contiguous(), n_pass=n_pred, dropout=True, seed=seed,
-                                    window_offset=s)
+                                    window_offset=s, pass_offset=base)
         else:
             ids = torch.arange(s, e, device=x.device)
-            loc = torch.stack([torch.sigmoid(model.logits(xl, dropout=True, bn_batch_stats=False, pass_id=t, seed=seed,
-                                                          sample_ids=ids)).reshape(-1) for t in range(n_pred)])
+            loc = torch.stack([torch.sigmoid(model.logits(xl, dropout=True, bn_batch_stats=False, pass_id=base + t,
+                                                          seed=seed, sample_ids=ids)).reshape(-1)
+                               for t in range(n_pred)])
+        model._call_counter = base + n_pred
     else:
         loc = bn_batch.mc_dropout_batch_bn(model, xl, n_pred, seed=seed, window_offset=s, distributed=True,
                                            global_n=n)[..., 0]

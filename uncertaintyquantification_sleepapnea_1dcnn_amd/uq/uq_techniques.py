@@ -70,13 +70,18 @@ def mc_dropout_predict(model, x_test_data, n_pred: int = 50, bn_mode: str = "bat
     if (D.active() if distributed is None else distributed):
         out = D.mc_dropout_predict_sharded(model, x_test_data, n_pred, bn_mode, seed)
     elif bn_mode == "running" and getattr(model, "uses_hip", lambda: False)():
-        # fused whole-network kernel (reference architecture) or the layer-wise HIP kernels (any spec)
+        # fused whole-network kernel (reference architecture) or the layer-wise HIP kernels (any spec);
+        # like model(x, training=True), every call draws fresh masks (pass ids advance per call)
         x = model._as_input(x_test_data).to(torch.bfloat16).contiguous()
-        out = model.hip_forward(x, n_pass=n_pred, dropout=True, seed=seed).unsqueeze(-1)
+        base = model._call_counter
+        out = model.hip_forward(x, n_pass=n_pred, dropout=True, seed=seed, pass_offset=base).unsqueeze(-1)
+        model._call_counter = base + n_pred
     elif bn_mode == "running":
         x = model._as_input(x_test_data)
-        out = torch.stack([torch.sigmoid(model.logits(x, dropout=True, bn_batch_stats=False, pass_id=t,
+        base = model._call_counter
+        out = torch.stack([torch.sigmoid(model.logits(x, dropout=True, bn_batch_stats=False, pass_id=base + t,
                                                       seed=seed)) for t in range(n_pred)])
+        model._call_counter = base + n_pred
     else:
         from ..ops import bn_batch
 
