@@ -69,13 +69,16 @@ def test_hip_train_step_matches_autograd(n):
         torch.testing.assert_close(st.views[name], v, atol=2e-3, rtol=2e-2)
 
 
-def test_batch_stats_mc_dropout_matches_reference():
+@pytest.mark.parametrize("n,max_samples", [(50, 1 << 20), (37, 80)])
+def test_batch_stats_mc_dropout_matches_reference(n, max_samples):
+    """Odd n: tiles straddle pass boundaries; max_samples=80: 2 chunks share block 1's output/moments."""
     _ext.require()
     dev = torch.device("cuda")
     m = AlarconCNN1D(seed=6, device=dev)
-    x = torch.randn(50, 60, 4, generator=torch.Generator().manual_seed(0)).to(dev)
+    x = torch.randn(n, 60, 4, generator=torch.Generator().manual_seed(0)).to(dev)
     snap = m.snapshot()
-    got = train_ops.forward_batch_stats(m, x, 3, pass_base=0, seed=m.seed, update_moving=True)
+    got = train_ops.forward_batch_stats(m, x, 3, pass_base=0, seed=m.seed, update_moving=True,
+                                        max_samples=max_samples)
     hip_stats = m.store.stats.clone()
     m.restore(snap)
     ref = []
@@ -85,6 +88,28 @@ def test_batch_stats_mc_dropout_matches_reference():
     ref = torch.stack(ref)
     torch.testing.assert_close(got, ref, atol=3e-2, rtol=3e-2)
     torch.testing.assert_close(hip_stats, m.store.stats, atol=2e-3, rtol=2e-2)
+
+
+def test_batch_bn_moments_fp64_at_bench_scale():
+    """BN batch moments over 16384 windows x 60 rows per channel (the reference's whole-test-set
+    batch, uq_techniques.py:22) vs fp64 moments of the very activations the kernels stored."""
+    _ext.require()
+    dev = torch.device("cuda")
+    m = AlarconCNN1D(seed=7, device=dev)
+    n = 16384
+    x = torch.randn(n, 60, 4, generator=torch.Generator().manual_seed(1)).to(dev)
+    train_ops.forward_batch_stats(m, x, 1, pass_base=0, seed=m.seed, update_moving=False, max_samples=n)
+    ws = m._mcd_ws
+    for l in range(6):
+        c = ws.ch[l + 1]
+        r = ws.R[l][train_ops.HALO: train_ops.HALO + train_ops.SR * n].view(n, train_ops.SR, c)[:, :60]
+        v = (r.view(torch.int16) & 0x7FFF).view(torch.bfloat16).double().reshape(-1, c)  # |R|: sign = dropout mask
+        mu_ref, var_ref = v.mean(0), v.var(0, unbiased=False)
+        st = ws.st[l].view(train_ops.STAT_SLOTS, ws.groups, 2, c)[:, 0].sum(0)
+        mu = st[0] / (n * 60)
+        var = st[1] / (n * 60) - mu * mu
+        assert ((mu - mu_ref).abs() / mu_ref.abs().clamp_min(1e-3)).max().item() < 1e-5, l
+        assert ((var - var_ref).abs() / var_ref.clamp_min(1e-6)).max().item() < 1e-5, l
 
 
 def test_hip_training_reduces_loss():

@@ -48,14 +48,14 @@ namespace train {
 struct Layer {
   const void* wf; const void* wd; const float* bias; const float* gamma; const float* beta;
   float* mmean; float* mvar; float* gw; float* gb; float* ggamma; float* gbeta;
-  void* R; void* dY; void* dZ; float* st; float* bst; unsigned thr; float dsc;
+  void* R; void* dY; void* dZ; double* st; float* bst; unsigned thr; float dsc;
 };
 struct Args {
   Layer L[6];
   const void* x; const float* y; const float* dense_w; const float* dense_b; float* g_dense_w; float* g_dense_b;
   float* logits; float* dlogit; float* loss_sum;
   int B; int n_win; int groups; unsigned pass_base; unsigned window_offset; unsigned long long seed; int dropout;
-  float inv_count; float inv_batch; float eps; float momentum; const unsigned* pass_dev;
+  float inv_count; float inv_batch; float eps; float momentum; const unsigned* pass_dev; int st_groups; int shared0;
 };
 }  // namespace train
 int train_args_size();
@@ -174,7 +174,7 @@ void bump_counters(at::Tensor& counters) {
 }
 
 // ctx: int64 CPU tensor of device pointers / scalars built once per workspace (ops/train_ops.py)
-constexpr int kCtxLayer = 18, kCtxLen = 6 * kCtxLayer + 21;
+constexpr int kCtxLayer = 18, kCtxLen = 6 * kCtxLayer + 23;
 
 float bits_to_float(int64_t v) {
   uint32_t u = static_cast<uint32_t>(v);
@@ -207,7 +207,7 @@ apneauq::train::Args args_from_ctx(const at::Tensor& ctx, int64_t pass_base) {
     L.gbeta = reinterpret_cast<float*>(q[10]);
     L.R = reinterpret_cast<void*>(q[11]);
     L.dY = reinterpret_cast<void*>(q[12]);
-    L.st = reinterpret_cast<float*>(q[13]);
+    L.st = reinterpret_cast<double*>(q[13]);
     L.bst = reinterpret_cast<float*>(q[14]);
     L.thr = static_cast<unsigned>(q[15]);
     L.dsc = bits_to_float(q[16]);
@@ -235,17 +235,28 @@ apneauq::train::Args args_from_ctx(const at::Tensor& ctx, int64_t pass_base) {
   A.eps = bits_to_float(g[18]);
   A.momentum = bits_to_float(g[19]);
   A.pass_dev = reinterpret_cast<const unsigned*>(g[20]);
+  A.st_groups = static_cast<int>(g[21]);
+  A.shared0 = static_cast<int>(g[22]);
+  TORCH_CHECK(A.st_groups >= A.groups, "train ctx: moment buffers hold fewer groups than requested");
   return A;
 }
 
-// op: 0 fwd(layer) | 1 head(flag=backward) | 2 dgrad(layer) | 3 wgrad(layer) | 4 finalize(layer=update_moving, flag=grads)
+// op: 0 fwd(layer; flag=1: the pass-shared block 1 of batch-BN MC Dropout, over the n_win windows)
+//     | 1 head(flag=backward) | 2 dgrad(layer) | 3 wgrad(layer) | 4 finalize(layer=update_moving, flag=grads)
 void train_call(const at::Tensor& ctx, int64_t op, int64_t layer, int64_t flag, int64_t pass_base, int64_t device) {
   const at::DeviceGuard guard(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(device)));
   auto A = args_from_ctx(ctx, pass_base);
   TORCH_CHECK(A.B > 0 && A.n_win > 0 && A.groups > 0, "train_call: bad sizes");
   hipStream_t s = cur_stream();
   switch (op) {
-    case 0: TORCH_CHECK(layer >= 0 && layer < 6); check(apneauq::train_launch_fwd(A, (int)layer, s), "train fwd"); break;
+    case 0:
+      TORCH_CHECK(layer >= 0 && layer < 6);
+      if (flag == 1) {
+        TORCH_CHECK(layer == 0 && A.shared0, "train fwd: flag 1 = shared block 1 (layer 0, shared0 ctx)");
+        A.B = A.n_win;  // one copy per window; stats group 0 (the buffers keep the ctx's group stride)
+      }
+      check(apneauq::train_launch_fwd(A, (int)layer, s), "train fwd");
+      break;
     case 1: check(apneauq::train_launch_head(A, (int)flag, s), "train head"); break;
     case 2: TORCH_CHECK(layer >= 1 && layer < 6); check(apneauq::train_launch_dgrad(A, (int)layer, s), "train dgrad"); break;
     case 3: TORCH_CHECK(layer >= 0 && layer < 6); check(apneauq::train_launch_wgrad(A, (int)layer, s), "train wgrad"); break;

@@ -10,11 +10,15 @@
 // tile = 2 samples = rows [128*tile, 128*tile + 136) — one contiguous copy including the conv halo.
 //
 // Per block l the buffers are R_l = relu(conv(A_{l-1}) + b) (pre-BN, bf16) and dY_l = dL/dBN-output
-// (bf16).  BN apply + dropout of block l are never materialised: the consumer of A_l (the next
-// forward, the wgrad of block l+1) recomputes  A_l = mask * (R_l * s + t) / (1-p)  while staging
-// into LDS, and the consumers of dZ_l (dgrad / wgrad of block l) recompute
+// (bf16).  R_l >= 0, so its sign bit is free: the producer stores the dropout mask of block l there
+// (sign set = dropped; |R_l| is the activation), hashing each element's mask exactly once.  BN apply
+// + dropout of block l are never materialised: the consumer of A_l (the next forward, the wgrad of
+// block l+1) recomputes  A_l = [sign clear] * (|R_l| * s + t) / (1-p)  while staging into LDS (no
+// hash), and the consumers of dZ_l (dgrad / wgrad of block l) recompute
 //   dZ_l = [R_l > 0] * gamma * rstd * (dY_l - mean(dY_l) - xhat * mean(dY_l * xhat))
-// from the per-channel sums accumulated by the producer's epilogue (fp32 atomics).  dgrad_l also
+// from the per-channel sums accumulated by the producer's epilogue (moments: fp32 per-workgroup
+// partials merged into fp64 slots, so batch statistics over ~10^6 rows per channel (MC Dropout with
+// the whole test set as one batch) keep ~1e-7 relative precision; backward sums: fp32).  dgrad_l also
 // writes its staged dZ_l rows to global memory, so wgrad_l (whose ci-blocked workgroups would each
 // recompute the whole dZ tile) stages it with a plain copy.
 //
@@ -55,7 +59,7 @@ struct Layer {
   __bf16* R;           // PL (rows, C) post-ReLU, pre-BN
   __bf16* dY;          // PL (rows, C) gradient wrt BN output (blocks 1..5)
   __bf16* dZ;          // PL (rows, C) gradient wrt the conv pre-activation, written by dgrad_l (l >= 1)
-  float* st;           // [groups][2][C] forward sums (sum r, sum r^2)
+  double* st;          // [slots][groups][2][C] forward moment sums (sum r, sum r^2), fp64
   float* bst;          // [2][C] backward sums (sum dY, sum dY * xhat)
   unsigned thr;        // dropout threshold (16-bit units) and 1/(1-p)
   float dsc;
@@ -84,12 +88,37 @@ struct Args {
   float eps;
   float momentum;
   const unsigned* pass_dev;  // optional device step counter added to pass_base (HIP-graph replays)
+  int st_groups;       // groups the moment buffers are allocated for (>= groups)
+  int shared0;         // batch-BN MC Dropout: block 1 (no dropout before it) is computed once for the
+                       // n_win windows (stats group 0, R_0 unencoded, indexed by window) and shared by
+                       // every pass; block 2's staging applies block 1's dropout from the hash
 };
 
 template <typename T>
 __device__ __forceinline__ T gld(const void* p) {
   return *(const __attribute__((address_space(1))) T*)(p);
 }
+
+// R_l's sign bit = block l's dropout mask (set: dropped); |R_l| is the post-ReLU activation
+__device__ __forceinline__ bool bf_dropped(__bf16 v) { return (__builtin_bit_cast(unsigned short, v) & 0x8000u) != 0; }
+__device__ __forceinline__ float bf_abs(__bf16 v) {
+  return __uint_as_float(((unsigned)__builtin_bit_cast(unsigned short, v) & 0x7FFFu) << 16);
+}
+
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// A = dropout(BN(R)) of one packed bf16 pair of R: |r| * s + t, or 0 where the sign bit is set
+// (dropped, or a pad / out-of-batch row, which the producer writes as -0.0).  7 VALU per pair:
+// 2 unpacks, one v_pk_fma_f32, one v_cvt_pk_bf16_f32, v_pk_ashrrev_i16 + not + and for the masks.
+__device__ __forceinline__ uint32_t decode_pair(uint32_t d, float s0, float t0, float s1, float t1) {
+  const float lo = __builtin_fmaf(__uint_as_float(d << 16), s0, t0);
+  const float hi = __builtin_fmaf(__uint_as_float(d & 0xFFFF0000u), s1, t1);
+  const bf16x2 p = {(__bf16)lo, (__bf16)hi};
+  const s16x2 sm = __builtin_bit_cast(s16x2, d) >> (s16x2){15, 15};
+  return __builtin_bit_cast(uint32_t, p) & ~__builtin_bit_cast(uint32_t, sm);
+}
+constexpr uint32_t kNegZero2 = 0x80008000u;  // a pair of -0.0: "dropped" = decodes to A = 0
 
 __device__ __forceinline__ int row_sample(int grow) { return (grow - kHalo) >> 6; }  // may be -1 / >= B
 __device__ __forceinline__ int row_time(int grow) { return (grow - kHalo) & 63; }
@@ -98,7 +127,8 @@ __device__ __forceinline__ int row_time(int grow) { return (grow - kHalo) & 63; 
 // so that the ~512 workgroups of a layer do not serialise on the same 2*C L2 atomic addresses;
 // readers add the slots.  Layout per layer: st[slot][group][2][C], bst[slot][2][C].
 // Probe hooks for timing the forward kernel's phases (always 0 in the library build; nonzero
-// values compute garbage): 4 = no copy-out, 8 = no conv MFMAs.
+// values compute garbage): 4 = no copy-out, 8 = no conv MFMAs, 16 = no input staging, 32 = no epilogue
+// moments.
 #ifndef APNEAUQ_FWD_ABL
 #define APNEAUQ_FWD_ABL 0
 #endif
@@ -110,12 +140,33 @@ __device__ __forceinline__ int row_time(int grow) { return (grow - kHalo) & 63; 
 #endif
 
 constexpr int kStatSlots = 16;
-__device__ __forceinline__ int st_stride(const Args& A, int Cc) { return A.groups * 2 * Cc; }
+// slot stride of the moment buffers: the ALLOCATED group count (a last MC-Dropout chunk may run fewer
+// groups while block 1's shared moments, written by the first chunk, keep their slots)
+__device__ __forceinline__ int st_stride(const Args& A, int Cc) { return A.st_groups * 2 * Cc; }
 __device__ __forceinline__ float slot_sum(const float* p, int stride) {
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < kStatSlots; ++i) s += p[i * stride];
   return s;
+}
+__device__ __forceinline__ double slot_sumd(const double* p, int stride) {
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < kStatSlots; ++i) s += p[i * stride];
+  return s;
+}
+// stats group holding block l's moments for pass group g (block 1 is shared by all passes in shared0 mode)
+__device__ __forceinline__ int stat_group(const Args& A, int l, int g) { return (l == 0 && A.shared0) ? 0 : g; }
+// biased batch moments of channel c of block l, stats group g (fp64 merge, fp32 results)
+__device__ __forceinline__ void bn_moments(const Args& A, int l, int g, int c, float& mu, float& var) {
+  const int Cc = C[l + 1];
+  const int ss = st_stride(A, Cc);
+  const int gg = stat_group(A, l, g);
+  const double s1 = slot_sumd(A.L[l].st + (gg * 2 + 0) * Cc + c, ss);
+  const double s2 = slot_sumd(A.L[l].st + (gg * 2 + 1) * Cc + c, ss);
+  const double m = s1 * (double)A.inv_count;
+  mu = (float)m;
+  var = (float)fmax(s2 * (double)A.inv_count - m * m, 0.0);
 }
 
 // Per-channel BN affine of block l for stats group g, into LDS: s[c], t[c], mean[c], rstd[c].
@@ -124,10 +175,8 @@ __device__ __forceinline__ void bn_affine_to_lds(const Args& A, int l, int g, fl
   const int Cc = C[l + 1];
   const Layer& Ly = A.L[l];
   for (int c = threadIdx.x; c < Cc; c += kThreads) {
-    const int ss = st_stride(A, Cc);
-    const float s1 = slot_sum(Ly.st + (g * 2 + 0) * Cc + c, ss), s2 = slot_sum(Ly.st + (g * 2 + 1) * Cc + c, ss);
-    const float mu = s1 * A.inv_count;
-    const float var = fmaxf(s2 * A.inv_count - mu * mu, 0.f);
+    float mu, var;
+    bn_moments(A, l, g, c, mu, var);
     const float rs = rsqrtf(var + A.eps);
     const float sc = Ly.gamma[c] * rs;
     s[c] = sc;
@@ -140,13 +189,11 @@ __device__ __forceinline__ void bn_affine_to_lds(const Args& A, int l, int g, fl
 // Per-channel batch mean and 1/sqrt(var + eps) of block l, stats group g, into LDS.
 __device__ __forceinline__ void bn_stats_to_lds(const Args& A, int l, int g, float* mean, float* rstd) {
   const int Cc = C[l + 1];
-  const Layer& Ly = A.L[l];
   for (int c = threadIdx.x; c < Cc; c += kThreads) {
-    const int ss = st_stride(A, Cc);
-    const float s1 = slot_sum(Ly.st + (g * 2 + 0) * Cc + c, ss), s2 = slot_sum(Ly.st + (g * 2 + 1) * Cc + c, ss);
-    const float mu = s1 * A.inv_count;
+    float mu, var;
+    bn_moments(A, l, g, c, mu, var);
     mean[c] = mu;
-    rstd[c] = rsqrtf(fmaxf(s2 * A.inv_count - mu * mu, 0.f) + A.eps);
+    rstd[c] = rsqrtf(var + A.eps);
   }
 }
 
@@ -204,10 +251,15 @@ __device__ __forceinline__ bf16x8 zero8() {
 // (plus the halo rows of the neighbours: pad rows, or rows whose outputs are discarded).
 //
 // Each thread owns one 8-channel chunk (cw = tid % NCW) for all its rows, so the BN affine of the
-// chunk (x 1/(1-rate) when dropping) and the two samples' dropout keys are loaded / derived once per
-// call instead of per 16-B item; the affine of the second stats group (a tile straddling an
-// MC-Dropout pass boundary, g1 = s/t + 256) is selected per row only when it differs.
-template <int l, int NR, int NCW, int UMAX = kStageU>
+// chunk (x 1/(1-rate) when dropping) is loaded once per call instead of per 16-B item; the affine of
+// the second stats group (a tile straddling an MC-Dropout pass boundary, g1 = s/t + 256) is selected
+// per row only when it differs.  The dropout mask is R_l's sign bit (set by the producer), so the
+// transform is  a = sign ? 0 : |r| * s + t  on the packed bf16 pairs.
+//
+// HASH_IN (batch-BN MC Dropout, block 2 reading the pass-shared block-1 output): R_0 holds one
+// unencoded copy per WINDOW; rows are fetched from the sample's window and block 1's dropout mask
+// is drawn from the counter hash here.
+template <int l, int NR, int NCW, int UMAX = kStageU, bool HASH_IN = false>
 __device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, int row0, int c0, const float* s,
                                           const float* t, int g0) {
   constexpr int Cc = C[l + 1];
@@ -235,14 +287,59 @@ __device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, i
     t1[j] = two ? t[256 + c + j] * dsc : t0[j];
   }
   unsigned key0 = 0u, key1 = 0u;
-  if (drop) {
-    key0 = layer_sample_key(A, l, min(smp0, A.B - 1));
-    key1 = layer_sample_key(A, l, min(smp0 + 1, A.B - 1));
+  const __bf16* src0 = nullptr;
+  const __bf16* src1 = nullptr;
+  if constexpr (HASH_IN) {
+    const int n0 = min(smp0, A.B - 1), n1 = min(smp0 + 1, A.B - 1);
+    if (drop) {
+      key0 = layer_sample_key(A, l, n0);
+      key1 = layer_sample_key(A, l, n1);
+    }
+    src0 = Ly.R + (long long)(kHalo + (n0 - g0 * A.n_win) * kSR) * Cc + c;
+    src1 = Ly.R + (long long)(kHalo + (n1 - g1 * A.n_win) * kSR) * Cc + c;
   }
   auto valid = [&](int grow) {
     const int n = row_sample(grow), tt = row_time(grow);
+    if constexpr (HASH_IN) return grow >= kHalo && (n == smp0 || n == smp0 + 1) && n < A.B && tt < kL;
     return !(grow < kHalo || n >= A.B || tt >= kL);
   };
+  if constexpr (!HASH_IN) {
+    // Every staged row exists in the padded buffer, and pad rows / rows past the batch / the
+    // buffer's halo rows hold -0.0, which decodes to 0 like a dropped element: no per-row checks.
+    auto run = [&](auto two_groups) {
+#pragma unroll
+      for (int b = 0; b < NK; b += U) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int r = rin + (b + u) * RP;
+          if (b + u < NK && active && r < NR) v[u] = gld<u32x4>(Ly.R + (long long)(row0 + r) * Cc + c);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int r = rin + (b + u) * RP;
+          if (b + u >= NK || !active || r >= NR) continue;
+          u32x4 o;
+          if constexpr (decltype(two_groups)::value) {  // rare: a tile straddling an MC-Dropout pass boundary
+            const bool hi = row_sample(row0 + r) != smp0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              o[q] = decode_pair(v[u][q], hi ? s1[2 * q] : s0[2 * q], hi ? t1[2 * q] : t0[2 * q],
+                                 hi ? s1[2 * q + 1] : s0[2 * q + 1], hi ? t1[2 * q + 1] : t0[2 * q + 1]);
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = decode_pair(v[u][q], s0[2 * q], t0[2 * q], s0[2 * q + 1], t0[2 * q + 1]);
+          }
+          *reinterpret_cast<u32x4*>(lds + r * ldsrs + cw * 16) = o;
+        }
+      }
+    };
+    if (two)
+      run(std::true_type{});
+    else
+      run(std::false_type{});
+    return;
+  }
 #pragma unroll
   for (int b = 0; b < NK; b += U) {
     bf16x8 v[U];
@@ -250,54 +347,55 @@ __device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, i
     for (int u = 0; u < U; ++u) {
       const int r = rin + (b + u) * RP;
       const int grow = row0 + r;
-      if (b + u < NK) v[u] = (active && r < NR && valid(grow)) ? gld<bf16x8>(Ly.R + (long long)grow * Cc + c) : zero8();
+      if (b + u < NK) {
+        const bool hi = row_sample(grow) != smp0;
+        v[u] = (active && r < NR && valid(grow)) ? gld<bf16x8>((hi ? src1 : src0) + (long long)row_time(grow) * Cc)
+                                                 : zero8();
+      }
     }
-    auto store = [&](auto two_groups) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int r = rin + (b + u) * RP;
-        if (b + u >= NK || !active || r >= NR) continue;
-        const int grow = row0 + r;
-        bf16x8 o = zero8();
-        if (valid(grow)) {
-          const int tt = row_time(grow);
-          const bool hi = row_sample(grow) != smp0;
+    for (int u = 0; u < U; ++u) {
+      const int r = rin + (b + u) * RP;
+      if (b + u >= NK || !active || r >= NR) continue;
+      const int grow = row0 + r;
+      bf16x8 o = zero8();
+      if (valid(grow)) {
+        const bool hi = row_sample(grow) != smp0;
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(&v[u]);
+        unsigned kb = 0xFFu;  // bit j = channel c + j kept
+        if (drop) {
           const unsigned key = hi ? key1 : key0;
+          const int tt = row_time(grow);
+          kb = 0u;
 #pragma unroll
           for (int j = 0; j < 8; j += 2) {
-            float a0, a1;
-            if constexpr (decltype(two_groups)::value) {
-              a0 = (float)v[u][j] * (hi ? s1[j] : s0[j]) + (hi ? t1[j] : t0[j]);
-              a1 = (float)v[u][j + 1] * (hi ? s1[j + 1] : s0[j + 1]) + (hi ? t1[j + 1] : t0[j + 1]);
-            } else {
-              a0 = (float)v[u][j] * s0[j] + t0[j];
-              a1 = (float)v[u][j + 1] * s0[j + 1] + t0[j + 1];
-            }
-            if (drop) {
-              const unsigned h = dropout_bits2(key, tt, c + j);
-              a0 = (h & 0xFFFFu) >= Ly.thr ? a0 : 0.f;
-              a1 = (h >> 16) >= Ly.thr ? a1 : 0.f;
-            }
-            o[j] = (__bf16)a0;
-            o[j + 1] = (__bf16)a1;
+            const unsigned h = dropout_bits2(key, tt, c + j);
+            kb |= ((h & 0xFFFFu) >= Ly.thr ? 1u : 0u) << j;
+            kb |= ((h >> 16) >= Ly.thr ? 1u : 0u) << (j + 1);
           }
         }
-        *reinterpret_cast<bf16x8*>(lds + r * ldsrs + cw * 16) = o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t d = w[q];
+          const float a0 = __builtin_fmaf(__uint_as_float(d << 16), hi ? s1[2 * q] : s0[2 * q], hi ? t1[2 * q] : t0[2 * q]);
+          const float a1 = __builtin_fmaf(__uint_as_float(d & 0xFFFF0000u), hi ? s1[2 * q + 1] : s0[2 * q + 1],
+                                          hi ? t1[2 * q + 1] : t0[2 * q + 1]);
+          o[2 * q] = (__bf16)(((kb >> (2 * q)) & 1u) ? a0 : 0.f);
+          o[2 * q + 1] = (__bf16)(((kb >> (2 * q + 1)) & 1u) ? a1 : 0.f);
+        }
       }
-    };
-    if (two)
-      store(std::true_type{});
-    else
-      store(std::false_type{});
+      *reinterpret_cast<bf16x8*>(lds + r * ldsrs + cw * 16) = o;
+    }
   }
 }
 
 // dZ_l rows into LDS (rows [row0, row0+NR), channels [c0, c0+NCW*8)); rows [own_lo, own_hi) are
 // also written to ``gout`` (dgrad materialises dZ_l for wgrad).
-//   l == 5: dY_6 = dlogit[n] * w[c] / 60 * mask6 * dsc6 (recomputed; never stored)
+//   l == 5: dY_6 = dlogit[n] * w[c] / 60 * mask6 * dsc6 (recomputed; never stored; mask6 = R_6's sign)
 // As in stage_act, each thread owns one 8-channel chunk, and the BN backward
 //   dz = relu'(r) * g*rstd * (dy - mean(dy) - xhat * mean(dy*xhat)),  xhat = (r - mean) * rstd
-// is folded per channel into dz = relu'(r) * (al * dy + be * r + ga), evaluated from registers.
+// is folded per channel into dz = relu'(r) * (al * dy + be * r + ga), evaluated from registers
+// (r = |R_l|: the sign bit carries block l's dropout mask).
 template <int l, int NR, int NCW>
 __device__ __forceinline__ void stage_dz(const Args& A, char* lds, int ldsrs, int row0, int c0,
                                          const float* gam_rstd, const float* mean, const float* rstd, const float* mdy,
@@ -324,17 +422,12 @@ __device__ __forceinline__ void stage_dz(const Args& A, char* lds, int ldsrs, in
   }
   // block 6: dY is recomputed from dlogit, the dense weights and the dropout mask of block 6
   float dw[8] = {}, dl0 = 0.f, dl1 = 0.f;
-  unsigned key0 = 0u, key1 = 0u;
   if constexpr (l == 5) {
     const float dsc = A.dropout ? Ly.dsc : 1.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) dw[j] = A.dense_w[c + j] * dsc;
     dl0 = A.dlogit[min(smp0, A.B - 1)] * (1.0f / kL);
     dl1 = A.dlogit[min(smp0 + 1, A.B - 1)] * (1.0f / kL);
-    if (A.dropout) {
-      key0 = layer_sample_key(A, 5, min(smp0, A.B - 1));
-      key1 = layer_sample_key(A, 5, min(smp0 + 1, A.B - 1));
-    }
   }
   auto valid = [&](int grow) {
     const int n = row_sample(grow), tt = row_time(grow);
@@ -362,28 +455,17 @@ __device__ __forceinline__ void stage_dz(const Args& A, char* lds, int ldsrs, in
       if (valid(grow)) {
         float dy[8];
         if constexpr (l == 5) {
-          const int tt = row_time(grow);
           const bool hi = row_sample(grow) != smp0;
           const float dl = hi ? dl1 : dl0;
-          const unsigned key = hi ? key1 : key0;
 #pragma unroll
-          for (int j = 0; j < 8; j += 2) {
-            float d0 = dl * dw[j], d1 = dl * dw[j + 1];
-            if (A.dropout) {
-              const unsigned h = dropout_bits2(key, tt, c + j);
-              d0 = (h & 0xFFFFu) >= Ly.thr ? d0 : 0.f;
-              d1 = (h >> 16) >= Ly.thr ? d1 : 0.f;
-            }
-            dy[j] = d0;
-            dy[j + 1] = d1;
-          }
+          for (int j = 0; j < 8; ++j) dy[j] = bf_dropped(q[u].a[j]) ? 0.f : dl * dw[j];
         } else {
 #pragma unroll
           for (int j = 0; j < 8; ++j) dy[j] = (float)q[u].b[j];
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float rr = (float)q[u].a[j];
+          const float rr = bf_abs(q[u].a[j]);
           const float dz = __builtin_fmaf(al[j], dy[j], __builtin_fmaf(be[j], rr, ga[j]));
           o[j] = (__bf16)(rr > 0.f ? dz : 0.f);
         }
@@ -473,6 +555,25 @@ struct Conv {
   }
 };
 
+__device__ __forceinline__ bf16x8 tr_frag(const char* lds, int ldsrs, int row_base, int col0) {
+  // fragment for a 16x16x32 operand whose K index is the LDS row: lane (m, h) gets rows
+  // row_base + 8h + [0..8) of column col0 + m.  Group h reads 4 rows x 16 cols per instruction.
+  const int lane = threadIdx.x & 63;
+  const int h = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const char* a0 = lds + (row_base + 8 * h + q) * ldsrs + (col0 + 4 * p) * 2;
+  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)a0);
+  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)(a0 + 4 * ldsrs));
+  bf16x8 r;
+  const __bf16* pl = reinterpret_cast<const __bf16*>(&lo);
+  const __bf16* ph = reinterpret_cast<const __bf16*>(&hi);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r[j] = pl[j];
+    r[4 + j] = ph[j];
+  }
+  return r;
+}
+
 // wave tilings (WM, WN) per output-channel count
 template <int COUT> struct Tiling;
 template <> struct Tiling<128> { static constexpr int WM = 1, WN = 4; };
@@ -508,10 +609,12 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
   const int wm = wave / T::WN, wn = wave % T::WN;
   const int m = lane & 15, h = lane >> 4;
   const Layer& Ly = A.L[l];
-  // Each workgroup owns a contiguous range of tiles (so the stats group changes rarely) and sums the
-  // per-tile channel moments in LDS (lstat, 2 waves per address at most); the global atomics are
-  // issued once per run of tiles of one stats group instead of once per tile (with ~10^5 tiles per
-  // call the per-tile atomics were ~20 % of the kernel).
+  // Each workgroup owns a contiguous range of tiles (so the stats group changes rarely).  The channel
+  // moments of a stored tile come from the matrix cores: per 16-channel tile ct, sum_rows r^2 is the
+  // diagonal of R_ct^T R_ct and sum_rows r is ones^T R_ct, 8 MFMAs over the 128 rows on operands read
+  // with ds_read_b64_tr_b16 (no per-element VALU: the layer kernels are VALU-issue bound).  The lanes
+  // holding a diagonal keep fp32 partials across the run of tiles of one stats group, merged (LDS
+  // atomics, then fp64 global slots) only when the group changes.
   const int tiles = (A.B + 1) / 2;
   const int tpw = (tiles + gridDim.x - 1) / gridDim.x;
   const int t_begin = blockIdx.x * tpw;
@@ -519,18 +622,44 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
   float* lstat = prm + 1024;  // [2][COUT]: sum r, sum r^2 of the current group run
   for (int c = threadIdx.x; c < 2 * COUT; c += kThreads) lstat[c] = 0.f;
   int gcur = -1;
-  float* st = Ly.st + (blockIdx.x % kStatSlots) * st_stride(A, COUT);
-  auto flush = [&]() {  // workgroup-uniform
+  double* st = Ly.st + (blockIdx.x % kStatSlots) * st_stride(A, COUT);
+  constexpr int CW = COUT / 8;             // 16-B chunks per output row
+  constexpr int RPo = kThreads / CW;       // rows per copy-out pass
+  constexpr int NPo = (kR + RPo - 1) / RPo;
+  const int ocw = threadIdx.x % CW, orin = threadIdx.x / CW;
+  const bool oact = orin < RPo;
+  constexpr int NCTo = COUT / 16, CPW = (NCTo + 3) / 4;  // moment channel tiles: ct = wave + 4j
+  const int sn = lane & 15;
+  const bool diag_lane = (lane >> 4) == (sn >> 2);        // holds D[sn][sn] of a 16x16 tile
+  float ps1[CPW], ps2[CPW];
+#pragma unroll
+  for (int j = 0; j < CPW; ++j) ps1[j] = ps2[j] = 0.f;
+  auto flush = [&]() {  // workgroup-uniform: fp32 run partials (<= ~10^4 rows / lane) merged in fp64
+    if (gcur >= 0 && diag_lane) {
+#pragma unroll
+      for (int j = 0; j < CPW; ++j) {
+        const int ct = wave + 4 * j;
+        if (ct < NCTo) {
+          atomicAdd(&lstat[ct * 16 + sn], ps1[j]);
+          atomicAdd(&lstat[COUT + ct * 16 + sn], ps2[j]);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < CPW; ++j) ps1[j] = ps2[j] = 0.f;
     __syncthreads();
     if (gcur >= 0) {
       for (int c = threadIdx.x; c < COUT; c += kThreads) {
-        atomicAdd(st + (gcur * 2 + 0) * COUT + c, lstat[c]);
-        atomicAdd(st + (gcur * 2 + 1) * COUT + c, lstat[COUT + c]);
+        atomicAdd(st + (gcur * 2 + 0) * COUT + c, (double)lstat[c]);
+        atomicAdd(st + (gcur * 2 + 1) * COUT + c, (double)lstat[COUT + c]);
         lstat[c] = lstat[COUT + c] = 0.f;
       }
     }
     __syncthreads();
   };
+  // this block's dropout mask goes into the sign bit of R_l (not for the pass-shared block 1)
+  const bool enc = A.dropout != 0 && !(l == 0 && A.shared0);
+  const bool hash_in = l == 1 && A.shared0;  // workgroup-uniform
   int gaff = -1;  // stats group whose BN affine (of block l-1) is in prm
   for (int tile = t_begin; tile < t_end; ++tile) {
     APNEAUQ_DASSERT(2 * tile < A.B + 1 && blockDim.x == kThreads);
@@ -538,7 +667,8 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
     const int smp0 = 2 * tile;
     const int g0 = min(smp0, A.B - 1) / A.n_win, g1 = min(smp0 + 1, A.B - 1) / A.n_win;
     __syncthreads();  // previous tile's copy-out has read the LDS tile
-    if constexpr (l == 0) {
+    if constexpr ((APNEAUQ_FWD_ABL & 16) != 0) {
+    } else if constexpr (l == 0) {
       staged_loop<kRows * 8 / 16>(
           [&](int i) -> bf16x8 { return gld<bf16x8>(A.x + (long long)row0 * 4 + i * 8); },
           [&](int i, const bf16x8& v) { reinterpret_cast<bf16x8*>(act)[i] = v; });
@@ -549,7 +679,12 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
         gaff = (g1 == g0) ? g0 : -1;
         __syncthreads();
       }
-      stage_act<l - 1, kRows, CIN / 8>(A, act, kRS, row0, 0, prm, prm + 512, g0);
+      // every row of the tile in flight at once: one memory round trip per tile (the staging was
+      // latency-bound at 8 loads per thread in flight)
+      if (hash_in)
+        stage_act<l - 1, kRows, CIN / 8, 32, true>(A, act, kRS, row0, 0, prm, prm + 512, g0);
+      else
+        stage_act<l - 1, kRows, CIN / 8, 32, false>(A, act, kRS, row0, 0, prm, prm + 512, g0);
     }
     __syncthreads();
     f32x4 acc[CV::CT][CV::RT];
@@ -562,40 +697,90 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
     CV::run(Ly.wf, act, IN_RS, acc);
 #endif
     __syncthreads();  // all waves done reading the staged input; reuse it for the output tile
-    // epilogue over the rows of sample slot `sel` (-1: both): bias + ReLU -> bf16 LDS tile, and the
-    // moments of the stored values into lstat (group gcur)
-    auto epi = [&](int sel) {
+
+    // epilogue: bias + ReLU -> bf16 LDS tile (rows outside the batch / pad rows: 0).  Only the row
+    // tiles holding t = 48..63 (pad rows on lanes m >= 12) and the batch's last tile need the select.
+    const bool last_tile = smp0 + 1 >= A.B;  // workgroup-uniform
 #pragma unroll
-      for (int c = 0; c < CV::CT; ++c) {
-        const int co0 = (wn * CV::CT + c) * 16 + 4 * h;
-        const f32x4 bias = gld<f32x4>(Ly.bias + co0);
-        f32x4 p1 = {0.f, 0.f, 0.f, 0.f}, p2 = {0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < CV::CT; ++c) {
+      const int co0 = (wn * CV::CT + c) * 16 + 4 * h;
+      const f32x4 bias = gld<f32x4>(Ly.bias + co0);
 #pragma unroll
-        for (int r = 0; r < CV::RT; ++r) {
-          const int row = wm * CV::RT * 16 + r * 16 + m;  // 0..127 within the tile
-          const int slot = row >> 6, tt = row & 63;
-          if (sel >= 0 && slot != sel) continue;
-          const bool valid = tt < kL && (smp0 + slot) < A.B;
-          f32x4 v;
+      for (int r = 0; r < CV::RT; ++r) {
+        const int rtg = wm * CV::RT + r;  // row tile in the tile (wave-uniform)
+        const int row = rtg * 16 + m;     // 0..127 within the tile
+        f32x4 v;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = valid ? fmaxf(acc[c][r][i] + bias[i], 0.f) : 0.f;
-          bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
-          *reinterpret_cast<bf16x4*>(act + row * kRS + co0 * 2) = o;
+        for (int i = 0; i < 4; ++i) v[i] = fmaxf(acc[c][r][i] + bias[i], 0.f);
+        if ((rtg & 3) == 3 || last_tile) {
+          const bool valid = (row & 63) < kL && (smp0 + (row >> 6)) < A.B;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float q = (float)o[i];  // moments of the values the consumers will normalise
-            p1[i] += q;
-            p2[i] += q * q;
+            v[i] = valid ? v[i] : 0.f;
+            asm volatile("" : "+v"(v[i]));  // keep the select in fp32 (no per-element cvt + v_perm repack)
           }
         }
+        bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+        *reinterpret_cast<bf16x4*>(act + row * kRS + co0 * 2) = o;
+      }
+    }
+    __syncthreads();
+    // channel moments of the stored tile (zero rows add nothing) on the matrix cores
+    auto moments = [&](int sel) {  // sel: sample slot (rows 64*sel .. +64 = 32-row chunks 2sel, 2sel+1), -1: both
+      if constexpr (!(APNEAUQ_FWD_ABL & 32)) {
+        bf16x8 ones;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float t1 = group16_sum(p1[i]), t2 = group16_sum(p2[i]);
-          if (m == 0) {
-            atomicAdd(&lstat[co0 + i], t1);
-            atomicAdd(&lstat[COUT + co0 + i], t2);
+        for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.f;
+        const int si = sn & 3;
+#pragma unroll
+        for (int j = 0; j < CPW; ++j) {
+          const int ct = wave + 4 * j;
+          if (ct >= NCTo) break;  // wave-uniform
+          f32x4 g = {0.f, 0.f, 0.f, 0.f}, sm = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kc = 0; kc < kR / 32; ++kc) {
+            if (sel >= 0 && (kc >> 1) != sel) continue;
+            const bf16x8 f = tr_frag(act, kRS, kc * 32, ct * 16);
+            g = mfma16(f, f, g);       // R^T R
+            sm = mfma16(ones, f, sm);  // ones^T R
+          }
+          const float dg = si == 0 ? g[0] : si == 1 ? g[1] : si == 2 ? g[2] : g[3];
+          const float s1v = si == 0 ? sm[0] : si == 1 ? sm[1] : si == 2 ? sm[2] : sm[3];
+          ps1[j] += s1v;
+          ps2[j] += dg;
+        }
+      }
+    };
+    // coalesced copy-out of the 128 tile rows (16 B per thread-iteration) with this block's dropout
+    // mask in the sign bits (drawn here, where no accumulators are live)
+    unsigned key[kSlots] = {0u, 0u};
+    if (enc) {
+      key[0] = layer_sample_key(A, l, min(smp0, A.B - 1));
+      key[1] = layer_sample_key(A, l, min(smp0 + 1, A.B - 1));
+    }
+    auto copy_out = [&]() {
+      // opaque row index (see staged_loop): keeps the NPo per-row addresses out of the tile loop
+      int rin = orin;
+      asm volatile("" : "+v"(rin));
+#pragma unroll
+      for (int k = 0; k < NPo; ++k) {
+        const int r = rin + k * RPo;
+        if (!oact || r >= kR) continue;
+        const int slot = r >> 6, tt = r & 63;
+        bf16x8 o = *reinterpret_cast<const bf16x8*>(act + r * kRS + ocw * 16);
+        uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
+        if (!(tt < kL && smp0 + slot < A.B)) {  // pad / out-of-batch rows: -0.0, decoded as A = 0
+#pragma unroll
+          for (int q = 0; q < 4; ++q) ow[q] = kNegZero2;
+        } else if (enc) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const unsigned hh = dropout_bits2(key[slot], tt, ocw * 8 + 2 * q);
+            ow[q] |= ((hh & 0xFFFFu) < Ly.thr ? 0x8000u : 0u) | ((hh >> 16) < Ly.thr ? 0x80000000u : 0u);
           }
         }
+        if constexpr (!(APNEAUQ_FWD_ABL & 4))
+          *reinterpret_cast<bf16x8*>(Ly.R + (long long)(row0 + kHalo + r) * COUT + ocw * 8) = o;
       }
     };
     if (g0 == g1) {
@@ -603,23 +788,16 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
         flush();
         gcur = g0;
       }
-      epi(-1);
-    } else {  // a tile straddling two stats groups (MC-Dropout pass boundary)
+      moments(-1);
+    } else {  // a tile straddling two stats groups (MC-Dropout pass boundary): moments per slot
       flush();
       gcur = g0;
-      epi(0);
+      moments(0);
       flush();
       gcur = g1;
-      epi(1);
+      moments(1);
     }
-    __syncthreads();
-    // coalesced copy-out of the 128 tile rows (16 B per thread-iteration)
-    constexpr int CW = COUT / 8;
-    for (int i = threadIdx.x; i < ((APNEAUQ_FWD_ABL & 4) ? 0 : kR * CW); i += kThreads) {
-      const int r = i / CW, cw = i - r * CW;
-      *reinterpret_cast<bf16x8*>(Ly.R + (long long)(row0 + kHalo + r) * COUT + cw * 8) =
-          *reinterpret_cast<const bf16x8*>(act + r * kRS + cw * 16);
-    }
+    copy_out();
   }
   flush();
 }
@@ -649,9 +827,8 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A, int backward) {
   for (int c = threadIdx.x; c < 3 * Cc + 2; c += kThreads) dw[c] = 0.f;
   auto params = [&](int g) {
     for (int c = threadIdx.x; c < Cc; c += kThreads) {
-      const int ss = st_stride(A, Cc);
-      const float m1 = slot_sum(Ly.st + (g * 2) * Cc + c, ss) * A.inv_count;
-      const float var = fmaxf(slot_sum(Ly.st + (g * 2 + 1) * Cc + c, ss) * A.inv_count - m1 * m1, 0.f);
+      float m1, var;
+      bn_moments(A, 5, g, c, m1, var);
       const float r = rsqrtf(var + A.eps);
       pmu[c] = m1;
       prs[c] = r;
@@ -675,9 +852,8 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A, int backward) {
     for (int j = 0; j < 8; ++j) {
       const int c = c0 + j;
       if (mixed && g != g_first) {
-        const int ss = st_stride(A, Cc);
-        const float m1 = slot_sum(Ly.st + (g * 2) * Cc + c, ss) * A.inv_count;
-        const float var = fmaxf(slot_sum(Ly.st + (g * 2 + 1) * Cc + c, ss) * A.inv_count - m1 * m1, 0.f);
+        float m1, var;
+        bn_moments(A, 5, g, c, m1, var);
         rs[j] = rsqrtf(var + A.eps);
         mu[j] = m1;
         sc[j] = Ly.gamma[c] * rs[j];
@@ -692,31 +868,18 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A, int backward) {
     }
   }
   bf16x8 v[NJ];
-  unsigned keep[NJ];  // bit j: channel c0 + j kept by dropout at row ph + 5 k
   float gap[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const float dsc6 = A.dropout ? Ly.dsc : 1.f;
   if (active) {
     const __bf16* base = Ly.R + (long long)(kHalo + n * kSR) * Cc + c0;
 #pragma unroll
     for (int k = 0; k < NJ; ++k) v[k] = gld<bf16x8>(base + (long long)(ph + NPH * k) * Cc);
-    const unsigned key = A.dropout ? layer_sample_key(A, 5, n) : 0u;
 #pragma unroll
     for (int k = 0; k < NJ; ++k) {
-      const int tt = ph + NPH * k;
-      unsigned kb = 0xFFu;
-      if (A.dropout) {
-        kb = 0u;
 #pragma unroll
-        for (int j = 0; j < 8; j += 2) {
-          const unsigned hh = dropout_bits2(key, tt, c0 + j);
-          kb |= ((hh & 0xFFFFu) >= Ly.thr ? 1u : 0u) << j;
-          kb |= ((hh >> 16) >= Ly.thr ? 1u : 0u) << (j + 1);
-        }
-      }
-      keep[k] = kb;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float a = (float)v[k][j] * sc[j] + sh[j];
-        gap[j] += ((kb >> j) & 1u) ? (A.dropout ? a * Ly.dsc : a) : 0.f;
+      for (int j = 0; j < 8; ++j) {  // block 6's dropout mask is R_6's sign bit
+        const float a = bf_abs(v[k][j]) * sc[j] + sh[j];
+        gap[j] += bf_dropped(v[k][j]) ? 0.f : a * dsc6;
       }
     }
   }
@@ -742,9 +905,8 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A, int backward) {
         for (int k = 0; k < NJ; ++k) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            float dy = dl * w[j] * (1.0f / kL);
-            if (A.dropout) dy = ((keep[k] >> j) & 1u) ? dy * Ly.dsc : 0.f;
-            const float xh = ((float)v[k][j] - mu[j]) * rs[j];
+            const float dy = bf_dropped(v[k][j]) ? 0.f : dl * w[j] * (1.0f / kL) * dsc6;
+            const float xh = (bf_abs(v[k][j]) - mu[j]) * rs[j];
             b0[j] += dy;
             b1[j] += dy * xh;
           }
@@ -823,11 +985,7 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
   const int wm = wave / T::WN, wn = wave % T::WN;
   const int m = lane & 15, h = lane >> 4;
   const Layer& Lp = A.L[l - 1];
-  unsigned key[kSlots] = {0u, 0u};
-  if (A.dropout) {
-    key[0] = layer_sample_key(A, l - 1, min(smp0, A.B - 1));
-    key[1] = layer_sample_key(A, l - 1, min(smp0 + 1, A.B - 1));
-  }
+  const float dscp = A.dropout ? Lp.dsc : 1.f;
 #pragma unroll
   for (int c = 0; c < CV::CT; ++c) {
     const int co0 = (wn * CV::CT + c) * 16 + 4 * h;
@@ -837,28 +995,23 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
       const int row = wm * CV::RT * 16 + r * 16 + m;
       const int slot = row >> 6, tt = row & 63;
       const bool valid = tt < kL && (smp0 + slot) < A.B;
+      // R_{l-1}: |R| for xhat, its sign bit = the dropout mask of block l-1
+#if (APNEAUQ_DG_ABL & 1)
+      bf16x4 rr = {(__bf16)acc[c][r][0], (__bf16)acc[c][r][1], (__bf16)acc[c][r][2], (__bf16)acc[c][r][3]};
+#else
+      bf16x4 rr = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
+      if (valid) rr = gld<bf16x4>(Lp.R + (long long)(row0 + kHalo + row) * COUT + co0);
+#endif
       f32x4 v = acc[c][r];
-      if (A.dropout) {
-        const unsigned k = slot ? key[1] : key[0];
-        const unsigned h01 = dropout_bits2(k, tt, co0), h23 = dropout_bits2(k, tt, co0 + 2);
-        v[0] = (h01 & 0xFFFFu) >= Lp.thr ? v[0] * Lp.dsc : 0.f;
-        v[1] = (h01 >> 16) >= Lp.thr ? v[1] * Lp.dsc : 0.f;
-        v[2] = (h23 & 0xFFFFu) >= Lp.thr ? v[2] * Lp.dsc : 0.f;
-        v[3] = (h23 >> 16) >= Lp.thr ? v[3] * Lp.dsc : 0.f;
-      }
-      if (!valid) v = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = (!valid || bf_dropped(rr[i])) ? 0.f : v[i] * dscp;
       bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
       *reinterpret_cast<bf16x4*>(act + row * kRS + co0 * 2) = o;
       if (valid) {
-#if (APNEAUQ_DG_ABL & 1)
-        const bf16x4 rr = o;
-#else
-        const bf16x4 rr = gld<bf16x4>(Lp.R + (long long)(row0 + kHalo + row) * COUT + co0);
-#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float q = (float)o[i];
-          const float xh = ((float)rr[i] - mean_prev[co0 + i]) * rstd_prev[co0 + i];
+          const float xh = (bf_abs(rr[i]) - mean_prev[co0 + i]) * rstd_prev[co0 + i];
           b0[i] += q;
           b1[i] += q * xh;
         }
@@ -897,24 +1050,6 @@ template <> struct WgCfg<3> { static constexpr int CIB = 32, COB = 96, WCO = 2, 
 template <> struct WgCfg<4> { static constexpr int CIB = 16, COB = 128, WCO = 4, WCI = 1, RTILES = 16, MINWG = 512, U = 8, MINB = 3; };
 template <> struct WgCfg<5> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = 512, U = 4, MINB = 2; };
 
-__device__ __forceinline__ bf16x8 tr_frag(const char* lds, int ldsrs, int row_base, int col0) {
-  // fragment for a 16x16x32 operand whose K index is the LDS row: lane (m, h) gets rows
-  // row_base + 8h + [0..8) of column col0 + m.  Group h reads 4 rows x 16 cols per instruction.
-  const int lane = threadIdx.x & 63;
-  const int h = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-  const char* a0 = lds + (row_base + 8 * h + q) * ldsrs + (col0 + 4 * p) * 2;
-  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)a0);
-  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)(a0 + 4 * ldsrs));
-  bf16x8 r;
-  const __bf16* pl = reinterpret_cast<const __bf16*>(&lo);
-  const __bf16* ph = reinterpret_cast<const __bf16*>(&hi);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    r[j] = pl[j];
-    r[4 + j] = ph[j];
-  }
-  return r;
-}
 
 template <int l>
 __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A) {
@@ -1089,9 +1224,8 @@ __global__ void bn_finalize_kernel(Args A, int update_moving, int grads) {
   for (int c = threadIdx.x; c < Cc; c += blockDim.x) {
     if (update_moving) {
       for (int g = 0; g < A.groups; ++g) {  // one Keras call (= one moving update) per group
-        const int ss = st_stride(A, Cc);
-        const float mu = slot_sum(Ly.st + (g * 2) * Cc + c, ss) * A.inv_count;
-        const float var = fmaxf(slot_sum(Ly.st + (g * 2 + 1) * Cc + c, ss) * A.inv_count - mu * mu, 0.f);
+        float mu, var;
+        bn_moments(A, l, g, c, mu, var);
         Ly.mmean[c] = Ly.mmean[c] * A.momentum + mu * (1.f - A.momentum);
         Ly.mvar[c] = Ly.mvar[c] * A.momentum + var * (1.f - A.momentum);
       }
