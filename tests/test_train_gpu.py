@@ -177,3 +177,29 @@ def test_fit_concurrent_on_streams_matches_sequential():
                                batch_size=512, verbose=0, epoch_backup=False)
         assert all(os.path.exists(p) for p in paths)
         assert len(load_ensemble_prefix(os.path.join(d, "m"), 3, device="cuda")) == 3
+
+
+def test_bf16_hip_training_matches_fp32_training(monkeypatch):
+    """bf16 HIP training tracks fp32 training: same data, seed and Keras loop (10 epochs,
+    batch 1024, validation_split=0.1 -> tail slice).  Every epoch's training loss agrees within 2 %
+    and the final val AUC within 0.01.  (Val LOSS is not compared: on the tail slice it is evaluated
+    with Keras moving-average BN statistics that lag the weights, and swings 0.1 <-> 1.1 from epoch to
+    epoch in BOTH backends -- tools/probes/parity_train.py, profiles/train_parity_r2.jsonl.)  The
+    windows are the synthetic apnea set with extra noise so the task is not saturated."""
+    _ext.require()
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.data.synthetic import synthetic_windows
+
+    x, y, _ = synthetic_windows(32768, seed=2025)
+    rs = np.random.RandomState(2025)
+    x = (x + rs.randn(*x.shape).astype(np.float32) * 1.6).astype(np.float32)
+    x = (x - x.mean(1, keepdims=True)) / (x.std(1, keepdims=True) + 1e-8)
+    res = {}
+    for backend in ("hip", "torch"):
+        monkeypatch.setenv("APNEAUQ_TRAIN_BACKEND", backend)
+        m = AlarconCNN1D(seed=2025, device="cuda")
+        res[backend] = m.fit(x, y.astype(np.float32), batch_size=1024, epochs=10, validation_split=0.1,
+                             verbose=0).history
+    hh, ht = res["hip"], res["torch"]
+    np.testing.assert_allclose(hh["loss"], ht["loss"], rtol=0.02)
+    assert 0.9 < ht["val_auc"][-1] < 0.9999, ht["val_auc"]
+    assert abs(hh["val_auc"][-1] - ht["val_auc"][-1]) < 0.01, (hh["val_auc"], ht["val_auc"])

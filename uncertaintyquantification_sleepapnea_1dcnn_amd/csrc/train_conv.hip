@@ -120,6 +120,15 @@ __device__ __forceinline__ uint32_t decode_pair(uint32_t d, float s0, float t0, 
 }
 constexpr uint32_t kNegZero2 = 0x80008000u;  // a pair of -0.0: "dropped" = decodes to A = 0
 
+// LDS tile addressing (SWZ 0: row-major; 1 / 2: XOR / row-permutation swizzles, kept for probes).
+// The transposed operand reads need no swizzle: see tr_frag.
+template <int SWZ>
+__device__ __forceinline__ int lds_off(int r, int b, int rs) {
+  if constexpr (SWZ == 1) return r * rs + (b ^ (((r >> 3) & 1) << 7));
+  if constexpr (SWZ == 2) return (r ^ (((r >> 3) & 1) << 2)) * rs + b;
+  return r * rs + b;
+}
+
 __device__ __forceinline__ int row_sample(int grow) { return (grow - kHalo) >> 6; }  // may be -1 / >= B
 __device__ __forceinline__ int row_time(int grow) { return (grow - kHalo) & 63; }
 
@@ -259,7 +268,7 @@ __device__ __forceinline__ bf16x8 zero8() {
 // HASH_IN (batch-BN MC Dropout, block 2 reading the pass-shared block-1 output): R_0 holds one
 // unencoded copy per WINDOW; rows are fetched from the sample's window and block 1's dropout mask
 // is drawn from the counter hash here.
-template <int l, int NR, int NCW, int UMAX = kStageU, bool HASH_IN = false>
+template <int l, int NR, int NCW, int UMAX = kStageU, bool HASH_IN = false, int SWZ = 0>
 __device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, int row0, int c0, const float* s,
                                           const float* t, int g0) {
   constexpr int Cc = C[l + 1];
@@ -330,7 +339,7 @@ __device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, i
 #pragma unroll
             for (int q = 0; q < 4; ++q) o[q] = decode_pair(v[u][q], s0[2 * q], t0[2 * q], s0[2 * q + 1], t0[2 * q + 1]);
           }
-          *reinterpret_cast<u32x4*>(lds + r * ldsrs + cw * 16) = o;
+          *reinterpret_cast<u32x4*>(lds + lds_off<SWZ>(r, cw * 16, ldsrs)) = o;
         }
       }
     };
@@ -384,7 +393,7 @@ __device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, i
           o[2 * q + 1] = (__bf16)(((kb >> (2 * q + 1)) & 1u) ? a1 : 0.f);
         }
       }
-      *reinterpret_cast<bf16x8*>(lds + r * ldsrs + cw * 16) = o;
+      *reinterpret_cast<bf16x8*>(lds + lds_off<SWZ>(r, cw * 16, ldsrs)) = o;
     }
   }
 }
@@ -396,7 +405,7 @@ __device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, i
 //   dz = relu'(r) * g*rstd * (dy - mean(dy) - xhat * mean(dy*xhat)),  xhat = (r - mean) * rstd
 // is folded per channel into dz = relu'(r) * (al * dy + be * r + ga), evaluated from registers
 // (r = |R_l|: the sign bit carries block l's dropout mask).
-template <int l, int NR, int NCW>
+template <int l, int NR, int NCW, int SWZ = 0>
 __device__ __forceinline__ void stage_dz(const Args& A, char* lds, int ldsrs, int row0, int c0,
                                          const float* gam_rstd, const float* mean, const float* rstd, const float* mdy,
                                          const float* mdyx, __bf16* gout = nullptr,
@@ -470,14 +479,14 @@ __device__ __forceinline__ void stage_dz(const Args& A, char* lds, int ldsrs, in
           o[j] = (__bf16)(rr > 0.f ? dz : 0.f);
         }
       }
-      *reinterpret_cast<bf16x8*>(lds + r * ldsrs + cw * 16) = o;
+      *reinterpret_cast<bf16x8*>(lds + lds_off<SWZ>(r, cw * 16, ldsrs)) = o;
       if (gout != nullptr && r >= own_lo && r < own_hi && !(APNEAUQ_DG_ABL & 2))
         *reinterpret_cast<bf16x8*>(gout + (long long)grow * Cc + c) = o;  // pad rows get their zeros too
     }
   }
 }
 
-template <int l, int NR, int NCW, int UMAX>
+template <int l, int NR, int NCW, int UMAX, int SWZ = 0>
 __device__ __forceinline__ void stage_dz_copy(const Args& A, char* lds, int ldsrs, int row0, int c0) {
   constexpr int Cc = C[l + 1];
   const Layer& Ly = A.L[l];
@@ -488,7 +497,7 @@ __device__ __forceinline__ void stage_dz_copy(const Args& A, char* lds, int ldsr
       },
       [&](int i, const bf16x8& o) {
         const int r = i / NCW, cw = i - r * NCW;
-        *reinterpret_cast<bf16x8*>(lds + r * ldsrs + cw * 16) = o;
+        *reinterpret_cast<bf16x8*>(lds + lds_off<SWZ>(r, cw * 16, ldsrs)) = o;
       });
 }
 
@@ -555,14 +564,22 @@ struct Conv {
   }
 };
 
+template <int SWZ = 0>
 __device__ __forceinline__ bf16x8 tr_frag(const char* lds, int ldsrs, int row_base, int col0) {
-  // fragment for a 16x16x32 operand whose K index is the LDS row: lane (m, h) gets rows
-  // row_base + 8h + [0..8) of column col0 + m.  Group h reads 4 rows x 16 cols per instruction.
+  // fragment for a 16x16x32 operand whose K index is the LDS row, 32 rows from row_base.  Lane
+  // group h (16 lanes) reads 4 rows x 16 cols per ds_read_b64_tr_b16; k-slot (h, j) of the fragment
+  // holds row row_base + 4h + j (j < 4, first read) or row_base + 16 + 4h + j - 4 (second read).
+  // Any k-permutation is exact as long as both operands use it, and this one makes each 32-lane
+  // bank group read 8 CONSECUTIVE rows: with a row stride that is an odd multiple of 32 B they fall
+  // on 8 distinct 8-bank groups, conflict-free for any row_base (the natural order, rows
+  // r0..r0+3 and r0+8..r0+11, is 2-way for every stride: 37-42 % conflict cycles in round 1).
   const int lane = threadIdx.x & 63;
   const int h = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-  const char* a0 = lds + (row_base + 8 * h + q) * ldsrs + (col0 + 4 * p) * 2;
+  const int ra = row_base + 4 * h + q;
+  const char* a0 = lds + lds_off<SWZ>(ra, (col0 + 4 * p) * 2, ldsrs);
+  const char* a1 = lds + lds_off<SWZ>(ra + 16, (col0 + 4 * p) * 2, ldsrs);
   const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)a0);
-  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)(a0 + 4 * ldsrs));
+  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)a1);
   bf16x8 r;
   const __bf16* pl = reinterpret_cast<const __bf16*>(&lo);
   const __bf16* ph = reinterpret_cast<const __bf16*>(&hi);
@@ -1043,6 +1060,8 @@ template <int l> struct WgCfg;
 // U: dZ staging loads in flight per thread; MINB: workgroups per CU the register budget targets
 // (batch-8192 probes, tools/probes/so_variants.sh: U 4 -> 8 saves 10-13 % on blocks 2, 3, 5; three
 // workgroups per CU save 17 % on block 4 and spill on block 6)
+// wgrad LDS tiles: the row stride is an odd multiple of 32 B (conflict-free tr_frag reads)
+__host__ __device__ constexpr int wg_rs(int width_bytes) { return (width_bytes / 32) % 2 ? width_bytes : width_bytes + 32; }
 template <> struct WgCfg<0> { static constexpr int CIB = 32, COB = 128, WCO = 4, WCI = 1, RTILES = 2, MINWG = 512, U = 4, MINB = 2; };  // im2col kk=32
 template <> struct WgCfg<1> { static constexpr int CIB = 32, COB = 192, WCO = 2, WCI = 2, RTILES = 8, MINWG = 256, U = 8, MINB = 2; };
 template <> struct WgCfg<2> { static constexpr int CIB = 32, COB = 224, WCO = 2, WCI = 2, RTILES = 8, MINWG = 256, U = 8, MINB = 2; };
@@ -1059,8 +1078,8 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A)
   constexpr int NTAP = FIRST ? 1 : K;           // block 1: taps folded into the im2col columns
   constexpr int NCO = W::COB / 16 / W::WCO;     // co tiles per wave
   constexpr int NCI = W::CIB / 16 / W::WCI;     // ci tiles per wave
-  constexpr int DZRS = W::COB * 2 + 16;         // LDS row strides (bytes)
-  constexpr int ARS = W::CIB * 2 + 16;
+  constexpr int DZRS = wg_rs(W::COB * 2);       // LDS row strides (bytes): odd multiples of 32 B
+  constexpr int ARS = wg_rs(FIRST ? 64 : W::CIB * 2);
   static_assert(W::WCO * W::WCI == 4, "4 waves");
   char* dz_lds = smem;                                   // 128 rows x COB
   char* a_lds = smem + kR * DZRS;                        // 136 rows x CIB (or 128 x 32 im2col)
@@ -1132,10 +1151,10 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A)
     const int row0 = kR * tile;
     __syncthreads();
     if constexpr (FIRST)  // no dgrad for block 1: dZ_1 is recomputed here (a single ci block)
-      stage_dz<l, kR, W::COB / 8>(A, dz_lds, DZRS, row0 + kHalo, co0, gr, mean, rstd, mdy, mdyx);
+      stage_dz<l, kR, W::COB / 8, 0>(A, dz_lds, DZRS, row0 + kHalo, co0, gr, mean, rstd, mdy, mdyx);
     else {
 #ifndef APNEAUQ_WG_NODZ  // probe: no dZ staging (wrong dW, timing only)
-      stage_dz_copy<l, kR, W::COB / 8, W::U>(A, dz_lds, DZRS, row0 + kHalo, co0);
+      stage_dz_copy<l, kR, W::COB / 8, W::U, 0>(A, dz_lds, DZRS, row0 + kHalo, co0);
 #endif
     }
     if constexpr (FIRST) {
@@ -1145,11 +1164,11 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A)
         const int tap = kk >> 2, ci = kk & 3;
         __bf16 v = (__bf16)0.f;
         if (tap < K) v = A.x[(long long)(row0 + kHalo + r + tap - PAD) * 4 + ci];
-        *reinterpret_cast<__bf16*>(a_lds + r * ARS + kk * 2) = v;
+        *reinterpret_cast<__bf16*>(a_lds + lds_off<0>(r, kk * 2, ARS)) = v;
       }
     } else {
 #ifndef APNEAUQ_WG_NOA  // probe: no A_{l-1} staging (wrong dW, timing only)
-      stage_act<l - 1, kRows, W::CIB / 8, 4>(A, a_lds, ARS, row0, ci0, sp, tp, 0);
+      stage_act<l - 1, kRows, W::CIB / 8, 4, false, 0>(A, a_lds, ARS, row0, ci0, sp, tp, 0);
 #endif
     }
     __syncthreads();
@@ -1157,7 +1176,7 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A)
     for (int ks = 0; ks < kR / 32; ++ks) {
       bf16x8 fb[NCO];
 #pragma unroll
-      for (int a = 0; a < NCO; ++a) fb[a] = tr_frag(dz_lds, DZRS, ks * 32, (wco * NCO + a) * 16);
+      for (int a = 0; a < NCO; ++a) fb[a] = tr_frag<0>(dz_lds, DZRS, ks * 32, (wco * NCO + a) * 16);
       if (bias_wave) {  // db[co] = sum_rows dZ[row][co]: one MFMA with an all-ones A fragment
 #pragma unroll
         for (int a = 0; a < NCO; ++a) accb[a] = mfma16(ones, fb[a], accb[a]);
@@ -1167,7 +1186,7 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A)
 #pragma unroll
         for (int b = 0; b < NCI; ++b) {
           const int arow = FIRST ? ks * 32 : kHalo + ks * 32 + k - PAD;
-          const bf16x8 fa = tr_frag(a_lds, ARS, arow, (wci * NCI + b) * 16);
+          const bf16x8 fa = tr_frag<0>(a_lds, ARS, arow, (wci * NCI + b) * 16);
 #ifndef APNEAUQ_WG_NOMFMA  // probe: staging only (wrong dW, timing only)
 #pragma unroll
           for (int a = 0; a < NCO; ++a) acc[k][b][a] = mfma16(fa, fb[a], acc[k][b][a]);
@@ -1276,8 +1295,11 @@ constexpr int lds_dgrad() { return train::kRows * train::kRS + 1792 * 4; }
 static_assert(2 * lds_dgrad() <= 160 * 1024, "dgrad must fit two workgroups per CU");
 template <int l>
 constexpr int lds_wgrad() {
-  return train::kR * (train::WgCfg<l>::COB * 2 + 16) + train::kRows * (train::WgCfg<l>::CIB * 2 + 16) + 1792 * 4;
+  return train::kR * train::wg_rs(train::WgCfg<l>::COB * 2) +
+         train::kRows * train::wg_rs(l == 0 ? 64 : train::WgCfg<l>::CIB * 2) + 1792 * 4;
 }
+static_assert(2 * lds_wgrad<1>() <= 160 * 1024 && 2 * lds_wgrad<2>() <= 160 * 1024 && 2 * lds_wgrad<4>() <= 160 * 1024,
+              "wgrad tiles must fit two workgroups per CU");
 
 int train_args_size() { return (int)sizeof(Args); }
 int train_layer_size() { return (int)sizeof(train::Layer); }
