@@ -37,10 +37,11 @@ def main():
                              text=True).stdout.splitlines()
     except OSError:
         dem = [x["name"] for x in rows]
-    print(f"{'kernel':70s} {'VGPR':>5s} {'AGPR':>5s} {'spill':>5s} {'occ':>4s} {'LDS':>6s}")
+    print(f"{'kernel':70s} {'VGPR':>5s} {'AGPR':>5s} {'spill':>5s} {'occ':>4s} {'LDS':>6s} {'scratch':>7s}")
     for x, d in zip(rows, dem):
         print(f"{d[:70]:70s} {x.get('VGPRs', '?'):>5s} {x.get('AGPRs', '?'):>5s} {x.get('VGPRs Spill', '?'):>5s} "
-              f"{x.get('Occupancy [waves/SIMD]', '?'):>4s} {x.get('LDS Size [bytes/block]', '?'):>6s}")
+              f"{x.get('Occupancy [waves/SIMD]', '?'):>4s} {x.get('LDS Size [bytes/block]', '?'):>6s} "
+              f"{x.get('ScratchSize [bytes/lane]', '?'):>7s}")
 
 
 if __name__ == "__main__":

@@ -44,6 +44,13 @@ hipError_t launch_metrics_update(const float* p, const float* y, long long n, co
                                  unsigned long long* counts, hipStream_t stream);
 hipError_t launch_generic_head(const void* y, const float* w, float b, int n, int L, int C, int out_logits, float* out,
                                hipStream_t stream);
+hipError_t launch_gt_wgrad(const void* x, long long x_rows, const void* dz, long long R, int cin, int cout, int k,
+                           float* gw, hipStream_t st);
+hipError_t launch_gt_head(const void* h, const float* w, const float* b, const float* y, float* prob, float* dlog,
+                          float* loss, float* gw, float* gb, int n, int L, int C, float inv_gb, hipStream_t st);
+int gt_pack_max_blocks();
+hipError_t launch_gt_pack(int nb, const float* const* w, void* const* fwd, void* const* dgr, const int* k,
+                          const int* cin, const int* cout, hipStream_t st);
 namespace train {
 struct Layer {
   const void* wf; const void* wd; const float* bias; const float* gamma; const float* beta;
@@ -445,6 +452,69 @@ void gt_bwd_finalize(const at::Tensor& bst, int64_t C, double inv_count, at::Ten
         "gt_bwd_finalize");
 }
 
+// Generic wgrad (csrc/generic_wgrad.hip): gw (k, cin, cout) fp32 += sum_R x[R + tap] dz[R]; gw pre-zeroed.
+void gt_wgrad(const at::Tensor& x, const at::Tensor& dz, int64_t R, int64_t cin, int64_t cout, int64_t k, at::Tensor& gw) {
+  need_rows(x, R + k - 1, cin, "gt_wgrad x");
+  need_rows(dz, R, cout, "gt_wgrad dz");
+  need_f32(gw, k * cin * cout, "gt_wgrad gw");
+  TORCH_CHECK(k >= 1 && k <= 15 && cin >= 1 && cout >= 1, "gt_wgrad: 1 <= k <= 15");
+  const at::DeviceGuard guard(x.device());
+  check(apneauq::launch_gt_wgrad(x.data_ptr(), x.numel() / cin, dz.data_ptr(), R, (int)cin, (int)cout, (int)k,
+                                 gw.data_ptr<float>(), cur_stream()),
+        "gt_wgrad");
+}
+
+// Generic head (csrc/generic_wgrad.hip): GAP + Dense + BCE + dlogit + dense grads, n samples.
+void gt_head(const at::Tensor& h, const at::Tensor& w, const at::Tensor& b, const at::Tensor& y, at::Tensor& prob,
+             at::Tensor& dlog, at::Tensor& loss, at::Tensor& gw, at::Tensor& gb, int64_t n, int64_t L, int64_t C,
+             double inv_gb) {
+  need_rows(h, n * L, C, "gt_head h");
+  need_f32(w, C, "gt_head w");
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&b, &loss, &gb}) need_f32(*t, 1, "gt_head scalar");
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&y, &prob, &dlog}) need_f32(*t, n, "gt_head per-sample");
+  need_f32(gw, C, "gt_head gw");
+  TORCH_CHECK(C >= 1 && C <= 4096 && L >= 1, "gt_head: bad shape");
+  const at::DeviceGuard guard(h.device());
+  check(apneauq::launch_gt_head(h.data_ptr(), w.data_ptr<float>(), b.data_ptr<float>(), y.data_ptr<float>(),
+                                prob.data_ptr<float>(), dlog.data_ptr<float>(), loss.data_ptr<float>(),
+                                gw.data_ptr<float>(), gb.data_ptr<float>(), (int)n, (int)L, (int)C, (float)inv_gb,
+                                cur_stream()),
+        "gt_head");
+}
+
+// All blocks' forward (+ dgrad) MFMA fragments in one launch (csrc/generic_wgrad.hip pack_kernel).
+void gt_pack(at::TensorList w, at::TensorList fwd, at::TensorList dgr, at::IntArrayRef k, at::IntArrayRef cin,
+             at::IntArrayRef cout) {
+  const int64_t nb = (int64_t)w.size();
+  TORCH_CHECK(nb >= 1 && nb <= apneauq::gt_pack_max_blocks() && (int64_t)fwd.size() == nb && (int64_t)dgr.size() == nb &&
+                  (int64_t)k.size() == nb && (int64_t)cin.size() == nb && (int64_t)cout.size() == nb,
+              "gt_pack: inconsistent block lists");
+  std::vector<const float*> wp(nb);
+  std::vector<void*> fp(nb), dp(nb);
+  std::vector<int> kk(nb), ci(nb), co(nb);
+  for (int64_t i = 0; i < nb; ++i) {
+    kk[i] = (int)k[i];
+    ci[i] = (int)cin[i];
+    co[i] = (int)cout[i];
+    TORCH_CHECK(w[i].is_cuda() && w[i].scalar_type() == at::kFloat && w[i].is_contiguous() &&
+                    w[i].numel() == k[i] * cin[i] * cout[i],
+                "gt_pack: w must be contiguous fp32 (k, cin, cout)");
+    const int64_t nf = ((k[i] * cin[i] + 31) / 32) * 512 * ((cout[i] + 15) / 16);
+    const int64_t nd = ((k[i] * cout[i] + 31) / 32) * 512 * ((cin[i] + 15) / 16);
+    TORCH_CHECK(fwd[i].scalar_type() == at::kBFloat16 && fwd[i].is_contiguous() && fwd[i].numel() == nf,
+                "gt_pack: forward fragment buffer has the wrong size");
+    TORCH_CHECK(dgr[i].numel() == 0 || (dgr[i].scalar_type() == at::kBFloat16 && dgr[i].is_contiguous() &&
+                                        dgr[i].numel() == nd),
+                "gt_pack: dgrad fragment buffer has the wrong size");
+    wp[i] = w[i].data_ptr<float>();
+    fp[i] = fwd[i].data_ptr();
+    dp[i] = dgr[i].numel() ? dgr[i].data_ptr() : nullptr;
+  }
+  const at::DeviceGuard guard(w[0].device());
+  check(apneauq::launch_gt_pack((int)nb, wp.data(), fp.data(), dp.data(), kk.data(), ci.data(), co.data(), cur_stream()),
+        "gt_pack");
+}
+
 at::Tensor generic_head(const at::Tensor& y, const at::Tensor& w, double b, bool out_logits) {
   TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kBFloat16 && y.is_contiguous() && y.dim() == 3, "generic_head: y must be (N, L, C) bf16");
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == y.size(2), "generic_head: w must be (C,) fp32");
@@ -511,6 +581,10 @@ TORCH_LIBRARY(apneauq, m) {
         "int C, bool pool, bool dropout, int thr, float inv_keep, int skey, int window_offset, Tensor(a!)? bst, "
         "Tensor? coef, Tensor? gamma, Tensor(b!)? dz, int dz_rs, int dz_off, Tensor(c!)? gbias) -> ()");
   m.def("gt_bwd_finalize(Tensor bst, int C, float inv_count, Tensor(a!) coef, Tensor(b!) ggamma, Tensor(c!) gbeta) -> ()");
+  m.def("gt_wgrad(Tensor x, Tensor dz, int R, int cin, int cout, int k, Tensor(a!) gw) -> ()");
+  m.def("gt_head(Tensor h, Tensor w, Tensor b, Tensor y, Tensor(a!) prob, Tensor(b!) dlog, Tensor(c!) loss, "
+        "Tensor(d!) gw, Tensor(e!) gb, int n, int L, int C, float inv_gb) -> ()");
+  m.def("gt_pack(Tensor[] w, Tensor(a!)[] fwd, Tensor(b!)[] dgr, int[] k, int[] cin, int[] cout) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
@@ -528,4 +602,7 @@ TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
   m.impl("gt_apply", &gt_apply);
   m.impl("gt_bwd", &gt_bwd);
   m.impl("gt_bwd_finalize", &gt_bwd_finalize);
+  m.impl("gt_wgrad", &gt_wgrad);
+  m.impl("gt_head", &gt_head);
+  m.impl("gt_pack", &gt_pack);
 }

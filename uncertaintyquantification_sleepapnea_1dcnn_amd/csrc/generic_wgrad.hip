@@ -1,0 +1,411 @@
+// Generic-spec training kernels that replace library GEMMs and torch ops on the generic hot path
+// (gfx950 / MI355X): any ModelSpec -- pooled blocks, the "30 s single-channel" ModelSpec(30, 1), other
+// filter / kernel sizes -- trains on the layer-wise kernels of generic_train.hip plus these:
+//
+//   wgrad_kernel  dW[tap][ci][co] = sum_R Xpad[R + tap][ci] * dZpad[R][co]   (split-K over rows)
+//                 on v_mfma_f32_16x16x32_bf16.  Both operands are row-major (rows x channels) bf16
+//                 tiles staged in LDS and read with the transposing ds_read_b64_tr_b16 (K = rows);
+//                 the row order inside a 32-row k-step makes every read conflict-free on strides
+//                 that are odd multiples of 32 B (train_conv.hip tr_frag).  A workgroup owns one
+//                 16-channel ci tile x 4*NCO co tiles and a contiguous range of 64-row chunks; every
+//                 tap's fragment is re-read from the same staged rows (shifted by the tap).  Few
+//                 input channels (Cin * k <= 32, the first block) use an im2col tile instead:
+//                 kk = tap * Cin + ci as the M dimension.  fp32 results are atomically added.
+//                 (Round 1 ran this as hipBLASLt strided-batched GEMMs.)
+//   head_kernel   GAP + Dense(C -> 1) + BCE on logits + dlogit + dense gradients, one wave/sample
+//                 (round 1: six torch ops).
+//   pack_kernel   fp32 (k, Cin, Cout) kernels of every block -> forward and dgrad (flipped,
+//                 transposed) MFMA A fragments, channels zero-padded to 16, in one launch
+//                 (round 1: torch pad / flip / permute / cast per block and step).
+//
+// Reference: models/train_deep_ensemble_cnns.py:30-71 (the pooled variants), cnn_baseline_train.py:
+// 100-102 (Adam, BCE) -- the Keras train step these kernels implement.
+#include "common.h"
+
+namespace apneauq {
+namespace gwgrad {
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+
+constexpr int kThreads = 256;
+constexpr int kChunk = 64;  // rows staged per step (two 32-row k-steps)
+
+__host__ __device__ constexpr int odd32(int bytes) { return ((bytes + 31) / 32) % 2 ? (bytes + 31) / 32 * 32 : (bytes + 31) / 32 * 32 + 32; }
+
+// fragment of a 16x16x32 operand whose K index is the LDS row (32 rows from row_base), 16 columns
+// from col0: k-slot order as train_conv.hip tr_frag (conflict-free on odd-32B strides)
+__device__ __forceinline__ bf16x8 tr_frag(const char* lds, int rs, int row_base, int col0) {
+  const int lane = threadIdx.x & 63;
+  const int h = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const char* a0 = lds + (row_base + 4 * h + q) * rs + (col0 + 4 * p) * 2;
+  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)a0);
+  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)(a0 + 16 * rs));
+  bf16x8 r;
+  const __bf16* pl = reinterpret_cast<const __bf16*>(&lo);
+  const __bf16* ph = reinterpret_cast<const __bf16*>(&hi);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r[j] = pl[j];
+    r[4 + j] = ph[j];
+  }
+  return r;
+}
+
+struct WgArgs {
+  const __bf16* x;   // Xpad rows (x_rows, cin)
+  const __bf16* dz;  // dZpad rows (R, cout)
+  float* gw;         // (k, cin, cout) fp32, accumulated
+  long long R;       // reduction rows (n * rs)
+  long long x_rows;  // rows of the x buffer (>= R + k - 1)
+  int cin, cout, k;
+  int n_ci, n_co;    // ci tiles (16) / co blocks (4 * NCO tiles) of the grid
+  int chunks_per_wg;
+};
+
+// IM2COL: M = kk = tap * cin + ci < 32 (two 16-row A tiles), one "tap".
+template <int NCO, int KMAX, bool IM2COL>
+__global__ __launch_bounds__(kThreads) void wgrad_kernel(WgArgs A) {
+  constexpr int COB = 64 * NCO;                        // co per workgroup
+  constexpr int XCOLS = IM2COL ? 32 : 16;              // staged A columns (ci, or kk)
+  constexpr int DZRS = odd32(COB * 2);
+  constexpr int XRS = odd32(XCOLS * 2);
+  constexpr int XROWS = kChunk + (IM2COL ? 0 : KMAX - 1) + 16;  // + slack: the last tr read of a tap
+  constexpr int NT = IM2COL ? 1 : KMAX;                // taps held in accumulators
+  constexpr int NM = IM2COL ? 2 : 1;                   // A tiles per tap
+  __shared__ __attribute__((aligned(16))) char dz_lds[kChunk * DZRS];
+  __shared__ __attribute__((aligned(16))) char x_lds[XROWS * XRS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // XCD-aware block order: the n_ci blocks sharing a chunk range run on one XCD (shared dZ rows in L2)
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xq = nwg / 8, xr = nwg % 8, xcd = bid % 8;
+  const int wg = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + bid / 8;
+  const int ci_t = wg % A.n_ci;
+  const int co_b = (wg / A.n_ci) % A.n_co;
+  const int rg = wg / (A.n_ci * A.n_co);
+  const int ci0 = ci_t * 16, co0 = co_b * COB;
+  const int k = A.k;
+  f32x4 acc[NT][NM][NCO];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int mi = 0; mi < NM; ++mi)
+#pragma unroll
+      for (int c = 0; c < NCO; ++c) acc[t][mi][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const long long chunks = (A.R + kChunk - 1) / kChunk;
+  const long long c_begin = (long long)rg * A.chunks_per_wg;
+  const long long c_end = c_begin + A.chunks_per_wg < chunks ? c_begin + A.chunks_per_wg : chunks;
+  for (long long ch = c_begin; ch < c_end; ++ch) {
+    const long long r0 = ch * kChunk;
+    __syncthreads();  // previous chunk's reads of the tiles are done
+    // dZ rows [r0, r0 + 64) x channels [co0, co0 + COB): 16-B pieces, zero past R / Cout
+    for (int i = threadIdx.x; i < kChunk * (COB / 8); i += kThreads) {
+      const int r = i / (COB / 8), cw = i - r * (COB / 8);
+      const int co = co0 + cw * 8;
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
+      if (r0 + r < A.R) {
+        const __bf16* src = A.dz + (r0 + r) * A.cout + co;
+        if ((A.cout & 7) == 0 && co + 8 <= A.cout) {
+          v = *(const gbf16x8*)(src);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (co + j < A.cout) v[j] = src[j];
+        }
+      }
+      *reinterpret_cast<bf16x8*>(dz_lds + r * DZRS + cw * 16) = v;
+    }
+    if constexpr (IM2COL) {
+      // im2col: column kk = tap * cin + ci of row r is Xpad[r0 + r + tap][ci]
+      for (int i = threadIdx.x; i < kChunk * 32; i += kThreads) {
+        const int r = i >> 5, kk = i & 31;
+        const int tap = kk / A.cin, ci = kk - tap * A.cin;
+        __bf16 v = (__bf16)0.f;
+        if (tap < k && r0 + r + tap < A.x_rows) v = A.x[(r0 + r + tap) * A.cin + ci];
+        *reinterpret_cast<__bf16*>(x_lds + r * XRS + kk * 2) = v;
+      }
+    } else {
+      // X rows [r0, r0 + 64 + k - 1) x channels [ci0, ci0 + 16)
+      const int xr_n = kChunk + k - 1;
+      for (int i = threadIdx.x; i < XROWS * 2; i += kThreads) {
+        const int r = i >> 1, half = i & 1;
+        const int ci = ci0 + half * 8;
+        bf16x8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
+        if (r < xr_n && r0 + r < A.x_rows) {
+          const __bf16* src = A.x + (r0 + r) * A.cin + ci;
+          if ((A.cin & 7) == 0 && ci + 8 <= A.cin) {
+            v = *(const gbf16x8*)(src);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              if (ci + j < A.cin) v[j] = src[j];
+          }
+        }
+        *reinterpret_cast<bf16x8*>(x_lds + r * XRS + half * 16) = v;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < kChunk / 32; ++ks) {
+      bf16x8 fb[NCO];
+#pragma unroll
+      for (int c = 0; c < NCO; ++c) fb[c] = tr_frag(dz_lds, DZRS, ks * 32, (wave * NCO + c) * 16);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        if (IM2COL || t < k) {  // uniform; t stays a compile-time index (acc in registers)
+#pragma unroll
+          for (int mi = 0; mi < NM; ++mi) {
+            const bf16x8 fa = tr_frag(x_lds, XRS, ks * 32 + (IM2COL ? 0 : t), mi * 16);
+#pragma unroll
+            for (int c = 0; c < NCO; ++c) acc[t][mi][c] = mfma16(fa, fb[c], acc[t][mi][c]);
+          }
+        }
+      }
+    }
+  }
+  // D[m][n]: lane holds rows m = 4h + i (ci or kk), column n = lane & 15 (co)
+  const int h = lane >> 4, nn = lane & 15;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    if (!IM2COL && t >= k) continue;
+#pragma unroll
+    for (int mi = 0; mi < NM; ++mi)
+#pragma unroll
+      for (int c = 0; c < NCO; ++c) {
+        const int co = co0 + (wave * NCO + c) * 16 + nn;
+        if (co >= A.cout) continue;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = mi * 16 + 4 * h + i;
+          int tap, ci;
+          if constexpr (IM2COL) {
+            tap = m / A.cin;
+            ci = m - tap * A.cin;
+            if (tap >= k) continue;
+          } else {
+            tap = t;
+            ci = ci0 + m;
+            if (ci >= A.cin) continue;
+          }
+          atomicAdd(A.gw + ((long long)tap * A.cin + ci) * A.cout + co, acc[t][mi][c][i]);
+        }
+      }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// head: GAP over time + Dense(C -> 1), BCE on logits, dlogit = (sigmoid - y) / global batch, dense
+// gradients.  One wave per sample, lanes over channels; workgroup-level sums, then one atomic per
+// channel / scalar per workgroup.
+// ---------------------------------------------------------------------------------------------
+struct HeadArgs {
+  const __bf16* h;   // (n, L, C)
+  const float* w;    // (C)
+  const float* b;    // (1)
+  const float* y;    // (n)
+  float* prob;       // (n)
+  float* dlog;       // (n)
+  float* loss;       // (1) summed BCE
+  float* gw;         // (C)
+  float* gb;         // (1)
+  int n, L, C;
+  float inv_gb;
+};
+
+__global__ __launch_bounds__(256) void head_kernel(HeadArgs A) {
+  extern __shared__ __attribute__((aligned(16))) float hsm[];  // [4 waves][C] gap, then 2 sums
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int s = blockIdx.x * 4 + wave;
+  float* gap = hsm + wave * A.C;
+  float part = 0.f;
+  if (s < A.n) {
+    const __bf16* base = A.h + (long long)s * A.L * A.C;
+    for (int c = lane; c < A.C; c += 64) {
+      float acc = 0.f;
+      for (int t = 0; t < A.L; ++t) acc += (float)base[(long long)t * A.C + c];
+      const float g = acc / (float)A.L;
+      gap[c] = g;
+      part += g * A.w[c];
+    }
+  }
+  const float z = wave_sum(part) + A.b[0];
+  float dl = 0.f;
+  if (s < A.n) {
+    const float yv = A.y[s];
+    const float p = 1.0f / (1.0f + __expf(-z));
+    dl = (p - yv) * A.inv_gb;
+    if (lane == 0) {
+      A.prob[s] = p;
+      A.dlog[s] = dl;
+      atomicAdd(A.loss, fmaxf(z, 0.f) - z * yv + log1pf(__expf(-fabsf(z))));
+    }
+  } else {
+    for (int c = lane; c < A.C; c += 64) gap[c] = 0.f;
+  }
+  float* dls = hsm + 4 * A.C;
+  if (lane == 0) dls[wave] = dl;
+  __syncthreads();
+  for (int c = threadIdx.x; c < A.C; c += 256) {
+    float g = 0.f;
+#pragma unroll
+    for (int w2 = 0; w2 < 4; ++w2) g += dls[w2] * hsm[w2 * A.C + c];
+    atomicAdd(A.gw + c, g);
+  }
+  if (threadIdx.x == 0) atomicAdd(A.gb, dls[0] + dls[1] + dls[2] + dls[3]);
+}
+
+// ---------------------------------------------------------------------------------------------
+// pack: per block, fp32 kernel (k, cin, cout) -> forward fragments (nstep, cout16/16, 64, 8) with
+// kk = tap*cin + ci, co = 16 ct + (lane & 15), and dgrad fragments of W'[tap'][co][ci] =
+// W[k-1-tap'][ci][co] (output channels ci padded to 16).  Zero outside the real ranges.
+// ---------------------------------------------------------------------------------------------
+constexpr int kMaxBlocks = 16;
+struct PackBlock {
+  const float* w;
+  __bf16* fwd;
+  __bf16* dgr;  // nullptr: no dgrad fragments (block 1)
+  int k, cin, cout;
+  long long nf, nd;  // elements of each fragment array
+};
+struct PackArgs {
+  PackBlock b[kMaxBlocks];
+  int nblocks;
+};
+
+__global__ void pack_kernel(PackArgs P) {
+  const PackBlock B = P.b[blockIdx.y];
+  const long long tot = B.nf + (B.dgr ? B.nd : 0);
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < tot; e += (long long)gridDim.x * blockDim.x) {
+    const bool is_f = e < B.nf;
+    const long long i = is_f ? e : e - B.nf;
+    const int ci_ = is_f ? B.cin : B.cout;   // GEMM K channels
+    const int co_ = is_f ? B.cout : B.cin;   // GEMM M channels (padded to 16)
+    const int j = (int)(i & 7), lane = (int)((i >> 3) & 63);
+    const long long fr = i >> 9;
+    const int nct = (co_ + 15) / 16;
+    const int ct = (int)(fr % nct), s = (int)(fr / nct);
+    const int co = 16 * ct + (lane & 15);
+    const int kk = 32 * s + 8 * (lane >> 4) + j;
+    float v = 0.f;
+    if (kk < ci_ * B.k && co < co_) {
+      const int tap = kk / ci_, ci = kk - tap * ci_;
+      v = is_f ? B.w[((long long)tap * B.cin + ci) * B.cout + co]
+               : B.w[((long long)(B.k - 1 - tap) * B.cin + co) * B.cout + ci];
+    }
+    (is_f ? B.fwd : B.dgr)[i] = (__bf16)v;
+  }
+}
+
+}  // namespace gwgrad
+
+// ------------------------------------------------------------------------------------------- host
+template <int NCO, int KMAX, bool IM2COL>
+static void wg_go(const gwgrad::WgArgs& A, int grid, hipStream_t st) {
+  hipLaunchKernelGGL((gwgrad::wgrad_kernel<NCO, KMAX, IM2COL>), dim3(grid), dim3(gwgrad::kThreads), 0, st, A);
+}
+
+template <int NCO>
+static hipError_t wg_dispatch(const gwgrad::WgArgs& A, int grid, bool im2col, hipStream_t st) {
+  if (im2col) {
+    wg_go<NCO, 1, true>(A, grid, st);
+  } else if (A.k <= 3) {
+    wg_go<NCO, 3, false>(A, grid, st);
+  } else if (A.k <= 5) {
+    wg_go<NCO, 5, false>(A, grid, st);
+  } else if (A.k <= 9) {
+    wg_go<NCO, 9, false>(A, grid, st);
+  } else if (A.k <= 15) {
+    wg_go<NCO, 15, false>(A, grid, st);
+  } else {
+    return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// gw must be zeroed by the caller (the step zeroes the whole flat gradient).
+hipError_t launch_gt_wgrad(const void* x, long long x_rows, const void* dz, long long R, int cin, int cout, int k,
+                           float* gw, hipStream_t st) {
+  if (R <= 0) return hipSuccess;
+  if (k < 1 || k > 15 || cin < 1 || cout < 1) return hipErrorInvalidValue;
+  if (x_rows < R + k - 1) return hipErrorInvalidValue;  // every tap's rows must exist
+  gwgrad::WgArgs A;
+  A.x = reinterpret_cast<const __bf16*>(x);
+  A.dz = reinterpret_cast<const __bf16*>(dz);
+  A.gw = gw;
+  A.R = R;
+  A.x_rows = x_rows;
+  A.cin = cin;
+  A.cout = cout;
+  A.k = k;
+  const bool im2col = cin * k <= 32;
+  // co tiles per wave: the fewest padded tile slots (4 waves x NCO per block), then the largest NCO; the
+  // accumulators (k x NCO tiles) are capped so a workgroup keeps >= 2 waves per SIMD
+  const int co_tiles = (cout + 15) / 16;
+  const int nmax = k <= 5 ? 4 : k <= 9 ? 3 : 2;
+  int nco = 1;
+  for (int c = 2; c <= nmax; ++c) {
+    const int slots_c = (co_tiles + 4 * c - 1) / (4 * c) * 4 * c, slots_b = (co_tiles + 4 * nco - 1) / (4 * nco) * 4 * nco;
+    if (slots_c <= slots_b) nco = c;
+  }
+  A.n_ci = im2col ? 1 : (cin + 15) / 16;
+  A.n_co = (co_tiles + 4 * nco - 1) / (4 * nco);
+  const long long chunks = (R + gwgrad::kChunk - 1) / gwgrad::kChunk;
+  // ~2048 workgroups (8 per CU over the 256 CUs), at least 4 chunks each (fewer output atomics)
+  const long long blocks = (long long)A.n_ci * A.n_co;
+  long long rg = 2048 / blocks;
+  if (rg < 1) rg = 1;
+  if (rg > (chunks + 3) / 4) rg = (chunks + 3) / 4;
+  if (rg < 1) rg = 1;
+  A.chunks_per_wg = (int)((chunks + rg - 1) / rg);
+  rg = (chunks + A.chunks_per_wg - 1) / A.chunks_per_wg;
+  const long long grid = blocks * rg;
+  if (grid > 0x7FFFFFFF) return hipErrorInvalidValue;
+  switch (nco) {
+    case 1: return wg_dispatch<1>(A, (int)grid, im2col, st);
+    case 2: return wg_dispatch<2>(A, (int)grid, im2col, st);
+    case 3: return wg_dispatch<3>(A, (int)grid, im2col, st);
+    default: return wg_dispatch<4>(A, (int)grid, im2col, st);
+  }
+}
+
+hipError_t launch_gt_head(const void* h, const float* w, const float* b, const float* y, float* prob, float* dlog,
+                          float* loss, float* gw, float* gb, int n, int L, int C, float inv_gb, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  gwgrad::HeadArgs A{reinterpret_cast<const __bf16*>(h), w, b, y, prob, dlog, loss, gw, gb, n, L, C, inv_gb};
+  const size_t lds = (4 * (size_t)C + 4) * sizeof(float);
+  hipLaunchKernelGGL(gwgrad::head_kernel, dim3((n + 3) / 4), dim3(256), lds, st, A);
+  return hipGetLastError();
+}
+
+int gt_pack_max_blocks() { return gwgrad::kMaxBlocks; }
+
+// blocks: nb descriptors (w, fwd, dgr-or-null, k, cin, cout)
+hipError_t launch_gt_pack(int nb, const float* const* w, void* const* fwd, void* const* dgr, const int* k,
+                          const int* cin, const int* cout, hipStream_t st) {
+  if (nb < 1 || nb > gwgrad::kMaxBlocks) return hipErrorInvalidValue;
+  gwgrad::PackArgs P;
+  P.nblocks = nb;
+  long long most = 0;
+  for (int i = 0; i < nb; ++i) {
+    auto& B = P.b[i];
+    B.w = w[i];
+    B.fwd = reinterpret_cast<__bf16*>(fwd[i]);
+    B.dgr = reinterpret_cast<__bf16*>(dgr[i]);
+    B.k = k[i];
+    B.cin = cin[i];
+    B.cout = cout[i];
+    B.nf = (long long)((k[i] * cin[i] + 31) / 32) * 512 * ((cout[i] + 15) / 16);
+    B.nd = (long long)((k[i] * cout[i] + 31) / 32) * 512 * ((cin[i] + 15) / 16);
+    const long long t = B.nf + (B.dgr ? B.nd : 0);
+    most = t > most ? t : most;
+  }
+  long long gx = (most + 255) / 256;
+  if (gx > 1024) gx = 1024;
+  hipLaunchKernelGGL(gwgrad::pack_kernel, dim3((unsigned)gx, nb), dim3(256), 0, st, P);
+  return hipGetLastError();
+}
+
+}  // namespace apneauq

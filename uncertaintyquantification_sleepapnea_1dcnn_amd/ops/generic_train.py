@@ -10,13 +10,15 @@ update) -> [pool] -> Dropout, BCE, Adam):
   per block, forward       ``gt_conv`` mode 1   z = relu(conv(h) + b) + BN moment slots (MFMA)
                            ``gt_bn_finalize``   scale / shift / mean / rstd + moving update
                            ``gt_apply``         BN + pool + dropout -> next input (zero-padded rows)
-  head                     GAP + Dense + BCE + dlogit + dense grads (a few fused torch ops)
+  head                     ``gt_head``: GAP + Dense + BCE + dlogit + dense grads, one launch
+  weights                  ``gt_pack``: every block's forward + dgrad MFMA fragments, one launch
   per block, backward      ``gt_bwd`` stats     sum(dy), sum(dy xhat) (dropout/pool routed back)
                            ``gt_bwd_finalize``  dgamma, dbeta, BN-backward coefficients
                            ``gt_bwd`` dz        dz (zero-padded rows) + bias gradient
                            ``gt_conv`` mode 2   dgrad = conv(dz, flipped W^T) (MFMA)
-                           wgrad                one strided-batched hipBLASLt GEMM over the k taps:
-                                                dW[tap] = Xpad[tap : tap + R]^T dZpad
+                           ``gt_wgrad``         dW[tap] = Xpad[tap : tap + R]^T dZpad: split-K MFMA
+                                                over the rows (csrc/generic_wgrad.hip; round 1
+                                                ran it as hipBLASLt strided-batched GEMMs)
   Adam                     one multi-tensor launch over the flat buffer (``csrc/adam.hip``)
 
 The zero-padded row layout (every sample's rows framed by k//2 zero rows, plus k//2 guard rows
@@ -44,7 +46,7 @@ SLOTS = 16  # == kStatSlots (csrc/generic_conv.hip, csrc/generic_train.hip)
 def supports(spec: ModelSpec) -> bool:
     """True if the generic HIP training kernels implement ``spec`` (the same shapes as the generic
     inference kernels).  On a GPU box a missing extension raises unless APNEAUQ_ALLOW_FALLBACK=1."""
-    if not generic.supports(spec):
+    if not generic.supports(spec) or any(b.kernel_size > 15 for b in spec.blocks):  # gt_wgrad: k <= 15
         return False
     if _ext.available():
         return True
@@ -88,6 +90,10 @@ class GenericTrainWorkspace:
             self.dbs_all = torch.zeros(sum(sizes) // 2, device=dev)
             self.dbs = [t.view(SLOTS, -1) for t in torch.split(self.dbs_all, [s // 2 for s in sizes])]
             self.coef = [torch.zeros(2 * self.ch[l + 1], device=dev) for l in range(nl)]
+            self.y = torch.zeros(B, device=dev)
+            self.prob = torch.zeros(B, device=dev)
+            self.dlog = torch.zeros(B, device=dev)
+            self.head_loss = torch.zeros(1, device=dev)
             store = model.store
             self.grad = torch.zeros_like(store.flat)
             self.gviews = {}
@@ -100,14 +106,25 @@ class GenericTrainWorkspace:
         self.xin[0][p: p + n * self.rs[0]].view(n, self.rs[0], self.ch[0])[:, p: p + self.L[0]].copy_(x)
 
     def pack(self, backward: bool):
-        """bf16 MFMA fragments of every conv kernel (forward; + dgrad orientation when training)."""
+        """bf16 MFMA fragments of every conv kernel (forward; + dgrad orientation when training), all
+        blocks in one HIP launch into buffers allocated once (the weights change every step)."""
         v = self.model.store.views
-        wf, wd = [], []
-        for l in range(len(self.ks)):
-            w = v[f"conv1d_{l + 1}/kernel"].float()
-            wf.append(_frag(w))
-            wd.append(_frag(w.flip(0).transpose(1, 2)) if backward and l > 0 else None)
-        return wf, wd
+        nl = len(self.ks)
+        if getattr(self, "_wf", None) is None:
+            dev = self.model.store.device
+            self._wf, self._wd = [], []
+            for l in range(nl):
+                k, cin, cout = self.ks[l], self.ch[l], self.ch[l + 1]
+                nf = ((k * cin + 31) // 32, (cout + 15) // 16, 64, 8)
+                nd = ((k * cout + 31) // 32, (cin + 15) // 16, 64, 8)
+                self._wf.append(torch.empty(nf, dtype=torch.bfloat16, device=dev))
+                self._wd.append(torch.empty(nd, dtype=torch.bfloat16, device=dev) if l > 0 else
+                                torch.empty(0, dtype=torch.bfloat16, device=dev))
+            self._none = torch.empty(0, dtype=torch.bfloat16, device=dev)
+        w = [v[f"conv1d_{l + 1}/kernel"] for l in range(nl)]
+        dgr = self._wd if backward else [self._none] * nl
+        _ext.ops().gt_pack(w, self._wf, dgr, list(self.ks), list(self.ch[:-1]), list(self.ch[1:]))
+        return self._wf, [d if d.numel() else None for d in dgr]
 
 
 def _frag(w: torch.Tensor) -> torch.Tensor:
@@ -173,17 +190,14 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, syn
     pass_id = TRAIN_PASS_BASE + model._train_step_counter
     seed = model.seed
     h = _forward(ws, n, gb, seed, pass_id, window_offset, True, True, sync, wf)
-    # head: GAP + Dense + BCE(logits), mean over the global batch
-    gap = h.float().mean(dim=1)
+    # head: GAP + Dense + BCE(logits) + dlogit + dense gradients (mean over the global batch), one launch
     wdense = v["output_layer/kernel"].reshape(-1)
-    logit = torch.addmv(v["output_layer/bias"], gap, wdense)
-    yv = y.reshape(-1).float()
-    lv = torch.nn.functional.binary_cross_entropy_with_logits(logit, yv, reduction="none")
-    prob = torch.sigmoid(logit)
-    dlog = ((prob - yv) / gb).contiguous()
     ws.grad.zero_()
-    torch.mv(gap.t(), dlog, out=g["output_layer/kernel"].view(-1))
-    g["output_layer/bias"].copy_(dlog.sum().reshape(1))
+    ws.head_loss.zero_()
+    ws.y[:n].copy_(y.reshape(-1))
+    o.gt_head(h, wdense, v["output_layer/bias"], ws.y, ws.prob, ws.dlog, ws.head_loss, g["output_layer/kernel"],
+              g["output_layer/bias"], n, ws.L[-1], ws.ch[-1], 1.0 / gb)
+    dlog, prob = ws.dlog, ws.prob[:n]
     ws.bst_all.zero_()
     ws.dbs_all.zero_()
     for l in range(nl - 1, -1, -1):
@@ -207,18 +221,8 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, syn
         torch.sum(ws.dbs[l], 0, out=g[f"conv1d_{i}/bias"])
         if l > 0:
             o.gt_conv(ws.dzp[l], wd[l], None, ws.dh[l], None, n, L, cout, cin, k, 2, ws.rs[l], p)
-        # wgrad: dW[tap] = Xpad[tap : tap + R]^T dZpad (R = n * rs rows), fp32 out of one batched GEMM
-        R = n * ws.rs[l]
-        if cin >= 16:
-            xs = ws.xin[l].as_strided((k, cin, R), (cin, 1, cin))
-            dzs = ws.dzp[l][:R].unsqueeze(0).expand(k, R, cout)
-            g[f"conv1d_{i}/kernel"].copy_(torch.bmm(xs, dzs, out_dtype=torch.float32))
-        else:
-            # few input channels (block 1): a (R, k * Cin) im2col is small, and one plain GEMM avoids
-            # the ~10 ms host-side solution search hipBLASLt runs for a lda < 16 strided batch
-            xcol = ws.xin[l].as_strided((R, k * cin), (cin, 1)).contiguous()
-            g[f"conv1d_{i}/kernel"].view(k * cin, cout).copy_(
-                torch.mm(xcol.t(), ws.dzp[l][:R], out_dtype=torch.float32))
+        # wgrad: dW[tap] = Xpad[tap : tap + R]^T dZpad (R = n * rs rows), split-K MFMA into the zeroed grad
+        o.gt_wgrad(ws.xin[l], ws.dzp[l], n * ws.rs[l], cin, cout, k, g[f"conv1d_{i}/kernel"])
     if sync is not None and sync_world > 1:  # the synced sums made dgamma / dbeta global already
         for i in range(1, nl + 1):
             g[f"batchnorm_{i}/gamma"].div_(sync_world)
@@ -227,7 +231,7 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, syn
     if grad_allreduce is not None:
         scale = grad_allreduce(ws.grad)
     model.optimizer.step(model.store.flat, ws.grad, grad_scale=scale)
-    return lv.detach().sum().double(), prob.detach()
+    return ws.head_loss.double().sum(), prob
 
 
 @torch.no_grad()
