@@ -39,8 +39,9 @@ def main():
         m = AlarconCNN1D(spec=spec, seed=1, device="cuda")
         x = torch.randn(a.batch, spec.input_length, spec.input_channels, device="cuda")
         y = (torch.rand(a.batch, device="cuda") > 0.5).float()
-        hip = _time(lambda: generic_train.train_step(m, x, y), a.iters)
-        r = {"hip_generic_ms": hip * 1e3, "hip_windows_per_s": a.batch / hip,
+        eager = _time(lambda: generic_train.train_step(m, x, y), a.iters)
+        hip = _time(lambda: generic_train.graph_train_step(m, x, y), a.iters)  # HIP-graph replay (the default path)
+        r = {"hip_generic_ms": hip * 1e3, "hip_generic_eager_ms": eager * 1e3, "hip_windows_per_s": a.batch / hip,
              "train_tflops_eff": 3 * 2 * spec.forward_macs() * a.batch / hip / 1e12}
         if not a.no_torch:
             os.environ["APNEAUQ_TRAIN_BACKEND"] = "torch"

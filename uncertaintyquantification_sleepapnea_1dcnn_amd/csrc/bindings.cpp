@@ -33,11 +33,12 @@ hipError_t launch_gt_bn_finalize(const float* st, int C, float inv_count, const 
                                  hipStream_t stream);
 hipError_t launch_gt_apply(const void* z, const float* bn, void* out, int n, int L, int C, int pool, int out_rs,
                            int out_off, int dropout, unsigned thr, float inv_keep, unsigned skey,
-                           unsigned window_offset, hipStream_t stream);
+                           unsigned window_offset, hipStream_t stream, const unsigned* skey_dev);
 hipError_t launch_gt_bwd(int dz_mode, const void* z, const float* bn, const void* dh, const float* dlog,
                          const float* w, float invL, int n, int L, int C, int pool, int dropout, unsigned thr,
                          float inv_keep, unsigned skey, unsigned window_offset, float* bst, const float* coef,
-                         const float* gamma, void* dz, int dz_rs, int dz_off, float* gbias, hipStream_t stream);
+                         const float* gamma, void* dz, int dz_rs, int dz_off, float* gbias, hipStream_t stream,
+                         const unsigned* skey_dev);
 hipError_t launch_gt_bwd_finalize(const float* bst, int C, float inv_count, float* coef, float* ggamma, float* gbeta,
                                   hipStream_t stream);
 hipError_t launch_metrics_update(const float* p, const float* y, long long n, const float* thr, int n_thr,
@@ -372,10 +373,18 @@ void gt_bn_finalize(const at::Tensor& st, int64_t C, double inv_count, const at:
         "gt_bn_finalize");
 }
 
+// optional device-resident dropout stream key (int32, one element): graph-replayed steps
+inline const unsigned* skey_dev_ptr(const c10::optional<at::Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kInt && t->numel() >= 1, "skey_dev: int32 GPU tensor");
+  return reinterpret_cast<const unsigned*>(t->data_ptr<int>());
+}
+
 void gt_apply(const at::Tensor& z, const at::Tensor& bn, at::Tensor& out, int64_t n, int64_t L, int64_t C, bool pool,
               int64_t out_rs, int64_t out_off, bool dropout, int64_t thr, double inv_keep, int64_t skey,
-              int64_t window_offset) {
+              int64_t window_offset, const c10::optional<at::Tensor>& skey_dev) {
   TORCH_CHECK(C % 4 == 0 && C <= 1024 && L >= 1, "gt_apply: bad shape");
+  const unsigned* kd = skey_dev_ptr(skey_dev);
   const int64_t lout = pool ? L / 2 : L;
   need_rows(z, n * L, C, "gt_apply z");
   need_f32(bn, 4 * C, "gt_apply bn");
@@ -384,7 +393,7 @@ void gt_apply(const at::Tensor& z, const at::Tensor& bn, at::Tensor& out, int64_
   const at::DeviceGuard guard(out.device());
   check(apneauq::launch_gt_apply(z.data_ptr(), bn.data_ptr<float>(), out.data_ptr(), (int)n, (int)L, (int)C, pool ? 1 : 0,
                                  (int)out_rs, (int)out_off, dropout ? 1 : 0, (unsigned)thr, (float)inv_keep,
-                                 (unsigned)skey, (unsigned)window_offset, cur_stream()),
+                                 (unsigned)skey, (unsigned)window_offset, cur_stream(), kd),
         "gt_apply");
 }
 
@@ -395,7 +404,7 @@ void gt_bwd(bool dz_mode, const at::Tensor& z, const at::Tensor& bn, const c10::
             int64_t C, bool pool, bool dropout, int64_t thr, double inv_keep, int64_t skey, int64_t window_offset,
             const c10::optional<at::Tensor>& bst, const c10::optional<at::Tensor>& coef,
             const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& dz, int64_t dz_rs, int64_t dz_off,
-            const c10::optional<at::Tensor>& gbias) {
+            const c10::optional<at::Tensor>& gbias, const c10::optional<at::Tensor>& skey_dev) {
   TORCH_CHECK(C % 4 == 0 && C <= 1024 && L >= 1, "gt_bwd: bad shape");
   const int64_t lout = pool ? L / 2 : L;
   need_rows(z, n * L, C, "gt_bwd z");
@@ -436,7 +445,7 @@ void gt_bwd(bool dz_mode, const at::Tensor& z, const at::Tensor& bn, const c10::
   check(apneauq::launch_gt_bwd(dz_mode ? 1 : 0, z.data_ptr(), bn.data_ptr<float>(), dhp, dlp, wp, (float)invL, (int)n,
                                (int)L, (int)C, pool ? 1 : 0, dropout ? 1 : 0, (unsigned)thr, (float)inv_keep,
                                (unsigned)skey, (unsigned)window_offset, bp, cp, gp, dzp, (int)dz_rs, (int)dz_off, gbp,
-                               cur_stream()),
+                               cur_stream(), skey_dev_ptr(skey_dev)),
         "gt_bwd");
 }
 
@@ -576,10 +585,10 @@ TORCH_LIBRARY(apneauq, m) {
   m.def("gt_bn_finalize(Tensor st, int C, float inv_count, Tensor gamma, Tensor beta, float eps, float momentum, "
         "Tensor(a!) mmean, Tensor(b!) mvar, bool update, Tensor(c!) bn) -> ()");
   m.def("gt_apply(Tensor z, Tensor bn, Tensor(a!) out, int n, int L, int C, bool pool, int out_rs, int out_off, "
-        "bool dropout, int thr, float inv_keep, int skey, int window_offset) -> ()");
+        "bool dropout, int thr, float inv_keep, int skey, int window_offset, Tensor? skey_dev=None) -> ()");
   m.def("gt_bwd(bool dz_mode, Tensor z, Tensor bn, Tensor? dh, Tensor? dlog, Tensor? w, float invL, int n, int L, "
         "int C, bool pool, bool dropout, int thr, float inv_keep, int skey, int window_offset, Tensor(a!)? bst, "
-        "Tensor? coef, Tensor? gamma, Tensor(b!)? dz, int dz_rs, int dz_off, Tensor(c!)? gbias) -> ()");
+        "Tensor? coef, Tensor? gamma, Tensor(b!)? dz, int dz_rs, int dz_off, Tensor(c!)? gbias, Tensor? skey_dev=None) -> ()");
   m.def("gt_bwd_finalize(Tensor bst, int C, float inv_count, Tensor(a!) coef, Tensor(b!) ggamma, Tensor(c!) gbeta) -> ()");
   m.def("gt_wgrad(Tensor x, Tensor dz, int R, int cin, int cout, int k, Tensor(a!) gw) -> ()");
   m.def("gt_head(Tensor h, Tensor w, Tensor b, Tensor y, Tensor(a!) prob, Tensor(b!) dlog, Tensor(c!) loss, "

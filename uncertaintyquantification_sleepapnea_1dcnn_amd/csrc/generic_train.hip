@@ -63,9 +63,11 @@ struct ApplyArgs {
   float inv_keep;
   unsigned skey;  // stream_key(seed, layer, pass)
   unsigned window_offset;
+  const unsigned* skey_dev;  // optional: the key read from device memory (HIP-graph replays)
 };
 
 __global__ __launch_bounds__(256) void apply_kernel(ApplyArgs A) {
+  if (A.skey_dev != nullptr) A.skey = *A.skey_dev;
   const int G = A.C >> 2;
   const long long total = (long long)A.n * A.lout * G;
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
@@ -109,6 +111,7 @@ struct BwdArgs {
   unsigned thr;
   float inv_keep;
   unsigned skey, window_offset;
+  const unsigned* skey_dev;  // optional: the key read from device memory (HIP-graph replays)
   float* bst;          // bwd_stats: (kSlots, 2, C) sums of dy, dy * xhat
   const float* coef;   // bwd_dz: (2, C) E[dy], E[dy xhat]
   const float* gamma;
@@ -171,6 +174,7 @@ __device__ __forceinline__ void block_reduce8(float* lds, float (&v)[8], int G, 
 template <bool DZ>
 __global__ __launch_bounds__(256) void bwd_kernel(BwdArgs A) {
   __shared__ float lds[8 * 256];
+  if (A.skey_dev != nullptr) A.skey = *A.skey_dev;
   const int G = A.C >> 2;
   const int rpb = 256 / G;
   const int cg = threadIdx.x % G, rl = threadIdx.x / G;
@@ -261,8 +265,9 @@ hipError_t launch_gt_bn_finalize(const float* st, int C, float inv_count, const 
 
 hipError_t launch_gt_apply(const void* z, const float* bn, void* out, int n, int L, int C, int pool, int out_rs,
                            int out_off, int dropout, unsigned thr, float inv_keep, unsigned skey,
-                           unsigned window_offset, hipStream_t stream) {
+                           unsigned window_offset, hipStream_t stream, const unsigned* skey_dev) {
   gtrain::ApplyArgs A;
+  A.skey_dev = skey_dev;
   A.z = reinterpret_cast<const __bf16*>(z);
   A.bn = bn;
   A.out = reinterpret_cast<__bf16*>(out);
@@ -287,8 +292,10 @@ hipError_t launch_gt_apply(const void* z, const float* bn, void* out, int n, int
 hipError_t launch_gt_bwd(int dz_mode, const void* z, const float* bn, const void* dh, const float* dlog,
                          const float* w, float invL, int n, int L, int C, int pool, int dropout, unsigned thr,
                          float inv_keep, unsigned skey, unsigned window_offset, float* bst, const float* coef,
-                         const float* gamma, void* dz, int dz_rs, int dz_off, float* gbias, hipStream_t stream) {
+                         const float* gamma, void* dz, int dz_rs, int dz_off, float* gbias, hipStream_t stream,
+                         const unsigned* skey_dev) {
   gtrain::BwdArgs A;
+  A.skey_dev = skey_dev;
   A.z = reinterpret_cast<const __bf16*>(z);
   A.bn = bn;
   A.dh = reinterpret_cast<const __bf16*>(dh);

@@ -94,60 +94,95 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(WgArgs A) {
   const long long chunks = (A.R + kChunk - 1) / kChunk;
   const long long c_begin = (long long)rg * A.chunks_per_wg;
   const long long c_end = c_begin + A.chunks_per_wg < chunks ? c_begin + A.chunks_per_wg : chunks;
-  for (long long ch = c_begin; ch < c_end; ++ch) {
-    const long long r0 = ch * kChunk;
-    __syncthreads();  // previous chunk's reads of the tiles are done
-    // dZ rows [r0, r0 + 64) x channels [co0, co0 + COB): 16-B pieces, zero past R / Cout
-    for (int i = threadIdx.x; i < kChunk * (COB / 8); i += kThreads) {
+  // Software pipeline: chunk ch+1's rows are loaded into registers (DZI + XI 16-B pieces per
+  // thread, IM2COL: 8 scalars) while chunk ch's MFMAs run; the staging otherwise paid one full
+  // memory round trip per 64-row chunk with only ~600 MFMA cycles per wave to cover it.
+  constexpr int DZI = kChunk * (COB / 8) / kThreads;      // 16-B dZ pieces per thread
+  constexpr int XI = (XROWS * 2 + kThreads - 1) / kThreads;  // 16-B X pieces per thread (non-im2col)
+  constexpr int XS = IM2COL ? kChunk * 32 / kThreads : 1;   // im2col scalars per thread
+  static_assert(kChunk * (COB / 8) % kThreads == 0, "dZ staging must tile the workgroup");
+  bf16x8 rdz[DZI];
+  bf16x8 rx[XI];
+  __bf16 rxs[XS];
+  auto load = [&](long long r0) {
+#pragma unroll
+    for (int u = 0; u < DZI; ++u) {
+      const int i = threadIdx.x + u * kThreads;
       const int r = i / (COB / 8), cw = i - r * (COB / 8);
       const int co = co0 + cw * 8;
-      bf16x8 v;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
+      for (int j = 0; j < 8; ++j) rdz[u][j] = (__bf16)0.f;
       if (r0 + r < A.R) {
         const __bf16* src = A.dz + (r0 + r) * A.cout + co;
         if ((A.cout & 7) == 0 && co + 8 <= A.cout) {
-          v = *(const gbf16x8*)(src);
+          rdz[u] = *(const gbf16x8*)(src);
         } else {
 #pragma unroll
           for (int j = 0; j < 8; ++j)
-            if (co + j < A.cout) v[j] = src[j];
+            if (co + j < A.cout) rdz[u][j] = src[j];
         }
       }
-      *reinterpret_cast<bf16x8*>(dz_lds + r * DZRS + cw * 16) = v;
     }
     if constexpr (IM2COL) {
       // im2col: column kk = tap * cin + ci of row r is Xpad[r0 + r + tap][ci]
-      for (int i = threadIdx.x; i < kChunk * 32; i += kThreads) {
+#pragma unroll
+      for (int u = 0; u < XS; ++u) {
+        const int i = threadIdx.x + u * kThreads;
         const int r = i >> 5, kk = i & 31;
         const int tap = kk / A.cin, ci = kk - tap * A.cin;
-        __bf16 v = (__bf16)0.f;
-        if (tap < k && r0 + r + tap < A.x_rows) v = A.x[(r0 + r + tap) * A.cin + ci];
-        *reinterpret_cast<__bf16*>(x_lds + r * XRS + kk * 2) = v;
+        rxs[u] = (__bf16)0.f;
+        if (tap < k && r0 + r + tap < A.x_rows) rxs[u] = A.x[(r0 + r + tap) * A.cin + ci];
       }
     } else {
       // X rows [r0, r0 + 64 + k - 1) x channels [ci0, ci0 + 16)
       const int xr_n = kChunk + k - 1;
-      for (int i = threadIdx.x; i < XROWS * 2; i += kThreads) {
+#pragma unroll
+      for (int u = 0; u < XI; ++u) {
+        const int i = threadIdx.x + u * kThreads;
         const int r = i >> 1, half = i & 1;
         const int ci = ci0 + half * 8;
-        bf16x8 v;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
-        if (r < xr_n && r0 + r < A.x_rows) {
+        for (int j = 0; j < 8; ++j) rx[u][j] = (__bf16)0.f;
+        if (i < XROWS * 2 && r < xr_n && r0 + r < A.x_rows) {
           const __bf16* src = A.x + (r0 + r) * A.cin + ci;
           if ((A.cin & 7) == 0 && ci + 8 <= A.cin) {
-            v = *(const gbf16x8*)(src);
+            rx[u] = *(const gbf16x8*)(src);
           } else {
 #pragma unroll
             for (int j = 0; j < 8; ++j)
-              if (ci + j < A.cin) v[j] = src[j];
+              if (ci + j < A.cin) rx[u][j] = src[j];
           }
         }
-        *reinterpret_cast<bf16x8*>(x_lds + r * XRS + half * 16) = v;
       }
     }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int u = 0; u < DZI; ++u) {
+      const int i = threadIdx.x + u * kThreads;
+      const int r = i / (COB / 8), cw = i - r * (COB / 8);
+      *reinterpret_cast<bf16x8*>(dz_lds + r * DZRS + cw * 16) = rdz[u];
+    }
+    if constexpr (IM2COL) {
+#pragma unroll
+      for (int u = 0; u < XS; ++u) {
+        const int i = threadIdx.x + u * kThreads;
+        *reinterpret_cast<__bf16*>(x_lds + (i >> 5) * XRS + (i & 31) * 2) = rxs[u];
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < XI; ++u) {
+        const int i = threadIdx.x + u * kThreads;
+        if (i < XROWS * 2) *reinterpret_cast<bf16x8*>(x_lds + (i >> 1) * XRS + (i & 1) * 16) = rx[u];
+      }
+    }
+  };
+  if (c_begin < c_end) load(c_begin * kChunk);
+  for (long long ch = c_begin; ch < c_end; ++ch) {
+    __syncthreads();  // previous chunk's reads of the tiles are done
+    store();
     __syncthreads();
+    if (ch + 1 < c_end) load((ch + 1) * kChunk);  // in flight under this chunk's MFMAs
 #pragma unroll
     for (int ks = 0; ks < kChunk / 32; ++ks) {
       bf16x8 fb[NCO];

@@ -143,9 +143,10 @@ def _get_ws(model, batch: int, with_backward: bool = True) -> GenericTrainWorksp
 
 
 def _forward(ws: GenericTrainWorkspace, n: int, global_n: int, seed: int, pass_id: int, window_offset: int,
-             dropout: bool, update_moving: bool, sync: Optional[Callable], wf) -> torch.Tensor:
+             dropout: bool, update_moving: bool, sync: Optional[Callable], wf, keys_dev=None) -> torch.Tensor:
     """Batch-statistics forward of ``n`` windows already loaded in ``ws.xin[0]``; returns the
-    last block's output (n, L_out, C) bf16."""
+    last block's output (n, L_out, C) bf16.  ``keys_dev`` (int32 (blocks,)) makes the kernels read
+    the dropout stream keys from device memory (HIP-graph replays)."""
     o = _ext.ops()
     spec, v = ws.model.spec, ws.model.store.views
     nl = len(spec.blocks)
@@ -167,7 +168,7 @@ def _forward(ws: GenericTrainWorkspace, n: int, global_n: int, seed: int, pass_i
         drop = bool(dropout and b.dropout > 0)
         o.gt_apply(ws.z[l], ws.bn[l], out, n, L, cout, bool(b.pool), out_rs, out_off, drop,
                    rng.dropout_threshold(b.dropout), _inv_keep(b.dropout), rng.stream_key(seed, l, pass_id),
-                   int(window_offset))
+                   int(window_offset), None if keys_dev is None else keys_dev[l:l + 1])
     return ws.hlast[: n * ws.L[-1]].view(n, ws.L[-1], ws.ch[-1])
 
 
@@ -175,21 +176,17 @@ def _inv_keep(rate: float) -> float:
     return 1.0 / (1.0 - rate) if rate < 1.0 else 0.0
 
 
-def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, sync: Optional[Callable] = None,
-               global_batch: Optional[int] = None, window_offset: int = 0, sync_world: int = 1):
-    """One Keras-semantics optimizer step on the generic HIP kernels; returns (loss_sum, probs)."""
+def _grads(model, ws: GenericTrainWorkspace, y: torch.Tensor, n: int, gb: int, pass_id: int, window_offset: int,
+           sync: Optional[Callable], keys_dev=None):
+    """Forward + head + backward of the ``n`` windows in ``ws.xin[0]`` into ``ws.grad`` (zeroed here).
+    Every launch is a HIP kernel of this package (no library GEMM, no host sync): capturable."""
     spec: ModelSpec = model.spec
-    n = int(x.shape[0])
-    gb = int(global_batch or n)
-    ws = _get_ws(model, n)
     o = _ext.ops()
     v, g = model.store.views, ws.gviews
     nl = len(spec.blocks)
-    ws.load_input(x)
-    wf, wd = ws.pack(backward=True)
-    pass_id = TRAIN_PASS_BASE + model._train_step_counter
     seed = model.seed
-    h = _forward(ws, n, gb, seed, pass_id, window_offset, True, True, sync, wf)
+    wf, wd = ws.pack(backward=True)
+    h = _forward(ws, n, gb, seed, pass_id, window_offset, True, True, sync, wf, keys_dev)
     # head: GAP + Dense + BCE(logits) + dlogit + dense gradients (mean over the global batch), one launch
     wdense = v["output_layer/kernel"].reshape(-1)
     ws.grad.zero_()
@@ -197,7 +194,7 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, syn
     ws.y[:n].copy_(y.reshape(-1))
     o.gt_head(h, wdense, v["output_layer/bias"], ws.y, ws.prob, ws.dlog, ws.head_loss, g["output_layer/kernel"],
               g["output_layer/bias"], n, ws.L[-1], ws.ch[-1], 1.0 / gb)
-    dlog, prob = ws.dlog, ws.prob[:n]
+    dlog = ws.dlog
     ws.bst_all.zero_()
     ws.dbs_all.zero_()
     for l in range(nl - 1, -1, -1):
@@ -205,33 +202,123 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, syn
         cin, cout, L, p, k = ws.ch[l], ws.ch[l + 1], ws.L[l], ws.pads[l], ws.ks[l]
         drop = b.dropout > 0
         thr, ik, skey = rng.dropout_threshold(b.dropout), _inv_keep(b.dropout), rng.stream_key(seed, l, pass_id)
+        kd = None if keys_dev is None else keys_dev[l:l + 1]
         if l == nl - 1:
             up = dict(dh=None, dlog=dlog, w=wdense, invL=1.0 / ws.L[-1])
         else:
             up = dict(dh=ws.dh[l + 1], dlog=None, w=None, invL=1.0)
         o.gt_bwd(False, ws.z[l], ws.bn[l], up["dh"], up["dlog"], up["w"], up["invL"], n, L, cout, bool(b.pool), drop,
-                 thr, ik, skey, int(window_offset), ws.bst[l], None, None, None, 0, 0, None)
+                 thr, ik, skey, int(window_offset), ws.bst[l], None, None, None, 0, 0, None, kd)
         if sync is not None:
             sync(ws.bst[l])
         o.gt_bwd_finalize(ws.bst[l], cout, 1.0 / (gb * L), ws.coef[l], g[f"batchnorm_{i}/gamma"],
                           g[f"batchnorm_{i}/beta"])
         o.gt_bwd(True, ws.z[l], ws.bn[l], up["dh"], up["dlog"], up["w"], up["invL"], n, L, cout, bool(b.pool), drop,
                  thr, ik, skey, int(window_offset), None, ws.coef[l], v[f"batchnorm_{i}/gamma"], ws.dzp[l], ws.rs[l], p,
-                 ws.dbs[l])
+                 ws.dbs[l], kd)
         torch.sum(ws.dbs[l], 0, out=g[f"conv1d_{i}/bias"])
         if l > 0:
             o.gt_conv(ws.dzp[l], wd[l], None, ws.dh[l], None, n, L, cout, cin, k, 2, ws.rs[l], p)
         # wgrad: dW[tap] = Xpad[tap : tap + R]^T dZpad (R = n * rs rows), split-K MFMA into the zeroed grad
         o.gt_wgrad(ws.xin[l], ws.dzp[l], n * ws.rs[l], cin, cout, k, g[f"conv1d_{i}/kernel"])
+
+
+def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, sync: Optional[Callable] = None,
+               global_batch: Optional[int] = None, window_offset: int = 0, sync_world: int = 1):
+    """One Keras-semantics optimizer step on the generic HIP kernels; returns (loss_sum, probs)."""
+    n = int(x.shape[0])
+    gb = int(global_batch or n)
+    ws = _get_ws(model, n)
+    ws.load_input(x)
+    _grads(model, ws, y, n, gb, TRAIN_PASS_BASE + model._train_step_counter, window_offset, sync)
+    g = ws.gviews
     if sync is not None and sync_world > 1:  # the synced sums made dgamma / dbeta global already
-        for i in range(1, nl + 1):
+        for i in range(1, len(model.spec.blocks) + 1):
             g[f"batchnorm_{i}/gamma"].div_(sync_world)
             g[f"batchnorm_{i}/beta"].div_(sync_world)
     scale = 1.0
     if grad_allreduce is not None:
         scale = grad_allreduce(ws.grad)
     model.optimizer.step(model.store.flat, ws.grad, grad_scale=scale)
-    return ws.head_loss.double().sum(), prob
+    return ws.head_loss.double().sum(), ws.prob[:n]
+
+
+class GraphedGenericStep:
+    """The whole generic-spec training step of one batch size captured once as a HIP graph.
+
+    Per step the generic path issues ~9 launches per block (conv, BN finalize, apply, two backward
+    passes, finalize, bias sum, dgrad, wgrad) plus head, packing and Adam: ~60 launches for six
+    blocks, ~1 ms of host dispatch at batch 1024.  The dropout stream keys of the step are written to
+    a device array before each replay (the kernels read them through ``skey_dev``) and Adam's
+    bias-correction step comes from a device counter, so a replay is exactly the eager step.
+    Single device only (data-parallel steps all-reduce through torch.distributed)."""
+
+    def __init__(self, model, batch: int):
+        self.model = model
+        self.batch = int(batch)
+        dev = model.store.device
+        spec = model.spec
+        self.ws = GenericTrainWorkspace(model, self.batch)
+        self.x_in = torch.zeros(self.batch, spec.input_length, spec.input_channels, device=dev)
+        self.y_in = torch.zeros(self.batch, device=dev)
+        self.keys = torch.zeros(len(spec.blocks), dtype=torch.int32, device=dev)
+        self.counters = torch.zeros(2, dtype=torch.int32, device=dev)  # [unused, Adam iterations]
+        model.optimizer._ensure(model.store.flat)
+        from . import train_ops
+
+        self.bound = train_ops.bound_key(model)
+        self._set_counters()
+        self.ws.pack(backward=True)  # allocates the fragment buffers outside the capture (no model change)
+        self.graph = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(self.graph, stream=side):
+                self._body()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self._iters_dev = int(model.optimizer.iterations)
+
+    def _set_counters(self):
+        self.counters.copy_(torch.tensor([0, int(self.model.optimizer.iterations)], dtype=torch.int32))
+
+    def _body(self):
+        ws, n, m = self.ws, self.batch, self.model
+        ws.load_input(self.x_in)
+        _grads(m, ws, self.y_in, n, n, TRAIN_PASS_BASE, 0, None, keys_dev=self.keys)
+        opt = m.optimizer
+        _ext.ops().adam_step(m.store.flat, ws.grad, opt.m, opt.v, opt.beta_1, opt.beta_2, opt.learning_rate,
+                             opt.epsilon, 1.0, self.counters)
+        _ext.ops().bump_counters(self.counters)
+
+    def __call__(self, x: torch.Tensor, y: torch.Tensor):
+        m = self.model
+        pass_id = TRAIN_PASS_BASE + m._train_step_counter
+        k = [rng.stream_key(m.seed, l, pass_id) for l in range(len(m.spec.blocks))]
+        self.keys.copy_(torch.tensor([v - (1 << 32) if v >= (1 << 31) else v for v in k], dtype=torch.int32))
+        if int(m.optimizer.iterations) != self._iters_dev:
+            self._set_counters()
+        self.x_in.copy_(x)
+        self.y_in.copy_(y.reshape(-1))
+        self.graph.replay()
+        m.optimizer.iterations += 1
+        self._iters_dev = int(m.optimizer.iterations)
+        return self.ws.head_loss.double().sum(), self.ws.prob[: self.batch]
+
+    _iters_dev = -1
+
+
+def graph_train_step(model, x: torch.Tensor, y: torch.Tensor):
+    """Replay (capturing on first use) the graphed generic step for this batch size."""
+    from . import train_ops
+
+    g = getattr(model, "_gtrain_graphs", None)
+    if g is None:
+        g = model._gtrain_graphs = {}
+    n = int(x.shape[0])
+    cur = g.get(n)
+    if cur is None or not train_ops._same_bound(cur.bound, train_ops.bound_key(model)):
+        g[n] = cur = GraphedGenericStep(model, n)
+    return cur(x, y)
 
 
 @torch.no_grad()

@@ -58,6 +58,8 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, dp_
             return generic_train.train_step(model, x, y, grad_allreduce=lambda g: (dp.all_reduce_(g), 1.0)[1],
                                             sync=dp.all_reduce_, global_batch=gn, window_offset=off,
                                             sync_world=dp.size)
+        if grad_allreduce is None and _use_graphs():
+            return generic_train.graph_train_step(model, x, y)
         return generic_train.train_step(model, x, y, grad_allreduce=grad_allreduce)
     if backend == "hip":
         from ..ops import train_ops
