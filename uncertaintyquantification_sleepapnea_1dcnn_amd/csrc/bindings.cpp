@@ -50,6 +50,7 @@ hipError_t launch_gt_wgrad(const void* x, long long x_rows, const void* dz, long
 hipError_t launch_gt_head(const void* h, const float* w, const float* b, const float* y, float* prob, float* dlog,
                           float* loss, float* gw, float* gb, int n, int L, int C, float inv_gb, hipStream_t st);
 int gt_pack_max_blocks();
+long long train_wgrad_part_floats(int B);
 hipError_t launch_gt_pack(int nb, const float* const* w, void* const* fwd, void* const* dgr, const int* k,
                           const int* cin, const int* cout, hipStream_t st);
 namespace train {
@@ -63,7 +64,7 @@ struct Args {
   const void* x; const float* y; const float* dense_w; const float* dense_b; float* g_dense_w; float* g_dense_b;
   float* logits; float* dlogit; float* loss_sum;
   int B; int n_win; int groups; unsigned pass_base; unsigned window_offset; unsigned long long seed; int dropout;
-  float inv_count; float inv_batch; float eps; float momentum; const unsigned* pass_dev; int st_groups; int shared0;
+  float inv_count; float inv_batch; float eps; float momentum; const unsigned* pass_dev; int st_groups; float* wpart; int shared0;
 };
 }  // namespace train
 int train_args_size();
@@ -182,7 +183,7 @@ void bump_counters(at::Tensor& counters) {
 }
 
 // ctx: int64 CPU tensor of device pointers / scalars built once per workspace (ops/train_ops.py)
-constexpr int kCtxLayer = 18, kCtxLen = 6 * kCtxLayer + 23;
+constexpr int kCtxLayer = 18, kCtxLen = 6 * kCtxLayer + 24;
 
 float bits_to_float(int64_t v) {
   uint32_t u = static_cast<uint32_t>(v);
@@ -245,6 +246,7 @@ apneauq::train::Args args_from_ctx(const at::Tensor& ctx, int64_t pass_base) {
   A.pass_dev = reinterpret_cast<const unsigned*>(g[20]);
   A.st_groups = static_cast<int>(g[21]);
   A.shared0 = static_cast<int>(g[22]);
+  A.wpart = reinterpret_cast<float*>(g[23]);
   TORCH_CHECK(A.st_groups >= A.groups, "train ctx: moment buffers hold fewer groups than requested");
   return A;
 }
@@ -272,6 +274,8 @@ void train_call(const at::Tensor& ctx, int64_t op, int64_t layer, int64_t flag, 
     default: TORCH_CHECK(false, "train_call: unknown op ", op);
   }
 }
+
+int64_t train_wgrad_part_size(int64_t B) { return apneauq::train_wgrad_part_floats((int)B); }
 
 void train_pack(const at::Tensor& w, int64_t k, int64_t cin, int64_t cout, at::Tensor& fwd, at::Tensor& dgr) {
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == k * cin * cout,
@@ -573,6 +577,7 @@ TORCH_LIBRARY(apneauq, m) {
   m.def("fused_layout() -> int[]", &fused_layout);
   m.def("train_call(Tensor ctx, int op, int layer, int flag, int pass_base, int device) -> ()", &train_call);
   m.def("train_pack(Tensor w, int k, int cin, int cout, Tensor(a!) fwd, Tensor(b!) dgr) -> ()");
+  m.def("train_wgrad_part_size(int B) -> int", &train_wgrad_part_size);
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, float b1, float b2, float alpha, float eps, "
         "float gscale, Tensor? counters=None) -> ()");
   m.def("bump_counters(Tensor(a!) counters) -> ()");

@@ -89,6 +89,7 @@ struct Args {
   float momentum;
   const unsigned* pass_dev;  // optional device step counter added to pass_base (HIP-graph replays)
   int st_groups;       // groups the moment buffers are allocated for (>= groups)
+  float* wpart;        // wgrad partials [row group][K*Cin*Cout + Cout] (nullptr: fp32 atomics)
   int shared0;         // batch-BN MC Dropout: block 1 (no dropout before it) is computed once for the
                        // n_win windows (stats group 0, R_0 unencoded, indexed by window) and shared by
                        // every pass; block 2's staging applies block 1's dropout from the hash
@@ -413,7 +414,7 @@ __device__ __forceinline__ void stage_dz(const Args& A, char* lds, int ldsrs, in
   constexpr int Cc = C[l + 1];
   constexpr int RP = kThreads / NCW;
   constexpr int NK = (NR + RP - 1) / RP;
-  constexpr int U = NK < kStageU / 2 ? NK : kStageU / 2;
+  constexpr int U = NK < kStageU ? NK : kStageU;  // R + dY payloads in flight per thread
   const Layer& Ly = A.L[l];
   int tid = threadIdx.x;
   asm volatile("" : "+v"(tid));
@@ -1200,6 +1201,7 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A)
   // lane (m, h) holds D[ci = 4h + i][co = m] of each tile: 16 consecutive co per row -> 64-B runs
   const int m = lane & 15, h = lane >> 4;
   const Layer& Ly = A.L[l];
+  float* part = A.wpart != nullptr ? A.wpart + (long long)rg * (K * CIN * COUT + COUT) : nullptr;
 #pragma unroll
   for (int k = 0; k < NTAP; ++k)
 #pragma unroll
@@ -1210,26 +1212,61 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int rowi = (wci * NCI + b) * 16 + 4 * h + i;  // ci (or kk for block 1)
-#ifdef APNEAUQ_WG_NOATOMIC  // probe: plain stores instead of atomics (wrong results, timing only)
+          int e;  // element of dW (k, Cin, Cout)
           if constexpr (FIRST) {
             const int tap = rowi >> 2, ci = rowi & 3;
-            if (tap < K) Ly.gw[(tap * CIN + ci) * COUT + co] = acc[k][b][a][i];
+            if (tap >= K) continue;
+            e = (tap * CIN + ci) * COUT + co;
           } else {
-            Ly.gw[(k * CIN + ci0 + rowi) * COUT + co] = acc[k][b][a][i];
+            e = (k * CIN + ci0 + rowi) * COUT + co;
           }
-#else
-          if constexpr (FIRST) {
-            const int tap = rowi >> 2, ci = rowi & 3;
-            if (tap < K) atomicAdd(Ly.gw + (tap * CIN + ci) * COUT + co, acc[k][b][a][i]);
-          } else {
-            atomicAdd(Ly.gw + (k * CIN + ci0 + rowi) * COUT + co, acc[k][b][a][i]);
-          }
-#endif
+          if (part != nullptr)
+            part[e] = acc[k][b][a][i];  // this row group's exclusive slot: summed in order by wgrad_reduce
+          else
+            atomicAdd(Ly.gw + e, acc[k][b][a][i]);
         }
       }
   if (bias_wave && h == 0) {  // row 0 of each ones^T dZ tile: lanes 0-15 hold its 16 column sums
 #pragma unroll
-    for (int a = 0; a < NCO; ++a) atomicAdd(Ly.gb + co0 + (wco * NCO + a) * 16 + m, accb[a][0]);
+    for (int a = 0; a < NCO; ++a) {
+      const int co = co0 + (wco * NCO + a) * 16 + m;
+      if (part != nullptr)
+        part[K * CIN * COUT + co] = accb[a][0];
+      else
+        atomicAdd(Ly.gb + co, accb[a][0]);
+    }
+  }
+}
+
+// dW, db = sum over the row groups of the wgrad partials, in row-group order: deterministic, and
+// cheaper than the ~K*Cin*Cout fp32 atomics per row group it replaces (25-35 us of a 70-80 us wgrad
+// at batch 1024, profiles/train_step_r2.md).
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int rgs, int kcc, int cout,
+                                                           float* __restrict__ gw, float* __restrict__ gb) {
+  // 4 consecutive elements per thread (16-B loads), 8 row groups in flight per step; partial sums
+  // combined in a fixed order, so the result is bitwise reproducible
+  const int S = kcc + cout;  // a multiple of 4 (Cout is)
+  const int S4 = S >> 2;
+  const f32x4* p4 = reinterpret_cast<const f32x4*>(part);
+  for (int e4 = blockIdx.x * 256 + threadIdx.x; e4 < S4; e4 += gridDim.x * 256) {
+    f32x4 acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int r = 0;
+    for (; r + 8 <= rgs; r += 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += p4[(long long)(r + j) * S4 + e4];
+    }
+    for (int j = 0; r < rgs; ++r, ++j) acc[j] += p4[(long long)r * S4 + e4];
+    f32x4 s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = 4 * e4 + i;
+      if (e < kcc)
+        gw[e] = s[i];
+      else
+        gb[e - kcc] = s[i];
+    }
   }
 }
 
@@ -1347,16 +1384,40 @@ hipError_t train_launch_dgrad(const Args& A, int l, hipStream_t st) {
 }
 
 template <int l>
+static int wg_rgs(int B) {
+  using W = train::WgCfg<l>;
+  const int nci = (l == 0) ? 1 : train::C[l] / W::CIB;
+  const int nco = train::C[l + 1] / W::COB;
+  const int tiles = (B + 1) / 2;
+  // RTILES row tiles per workgroup, but never fewer than ~MINWG workgroups while tiles remain
+  const int nblk = nci * nco;
+  const int rt = std::max(1, std::min(W::RTILES, (tiles * nblk + W::MINWG - 1) / W::MINWG));
+  return (tiles + rt - 1) / rt;
+}
+
+template <int l>
+static long long wg_part_floats(int B) {
+  return (long long)wg_rgs<l>(B) * (train::KS[l] * train::C[l] * train::C[l + 1] + train::C[l + 1]);
+}
+
+template <int l>
 static void wg_launch(const Args& A, hipStream_t st) {
   using W = train::WgCfg<l>;
   const int nci = (l == 0) ? 1 : train::C[l] / W::CIB;
   const int nco = train::C[l + 1] / W::COB;
-  const int tiles = (A.B + 1) / 2;
-  // RTILES row tiles per workgroup, but never fewer than ~MINWG workgroups while tiles remain
-  const int nblk = nci * nco;
-  const int rt = std::max(1, std::min(W::RTILES, (tiles * nblk + W::MINWG - 1) / W::MINWG));
-  const int rgs = (tiles + rt - 1) / rt;
+  const int rgs = wg_rgs<l>(A.B);
   hipLaunchKernelGGL(train::wgrad_kernel<l>, dim3(nci * nco * rgs), dim3(256), lds_wgrad<l>(), st, A);
+  if (A.wpart != nullptr) {
+    const int kcc = train::KS[l] * train::C[l] * train::C[l + 1];
+    const int blocks = std::min(2048, ((kcc + train::C[l + 1]) / 4 + 255) / 256);
+    hipLaunchKernelGGL(train::wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, A.wpart, rgs, kcc, train::C[l + 1],
+                       A.L[l].gw, A.L[l].gb);
+  }
+}
+
+long long train_wgrad_part_floats(int B) {
+  return std::max({wg_part_floats<0>(B), wg_part_floats<1>(B), wg_part_floats<2>(B), wg_part_floats<3>(B),
+                   wg_part_floats<4>(B), wg_part_floats<5>(B)});
 }
 
 hipError_t train_launch_wgrad(const Args& A, int l, hipStream_t st) {

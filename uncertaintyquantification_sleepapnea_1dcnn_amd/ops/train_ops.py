@@ -113,6 +113,10 @@ class TrainWorkspace:
             nd = ((ch[l + 1] * ks[l] + 31) // 32) * 32 * ch[l]
             self.wf.append(torch.zeros(nf, dtype=bf, device=dev))
             self.wd.append(torch.zeros(nd, dtype=bf, device=dev))
+        # wgrad partials (one slot per row group, summed in order by wgrad_reduce: deterministic and
+        # cheaper than fp32 atomics); shared by the six sequential wgrad launches
+        self.wpart = (torch.empty(int(_ext.ops().train_wgrad_part_size(self.B)), device=dev)
+                      if with_backward else None)
         self.y = torch.zeros(self.B, device=dev)
         self.logits = torch.zeros(self.B, device=dev)
         self.dlogit = torch.zeros(self.B, device=dev)
@@ -153,7 +157,8 @@ class TrainWorkspace:
                  self.loss.data_ptr(), n, n_win, groups, TRAIN_PASS_BASE, window_offset,
                  int(seed) & ((1 << 63) - 1), int(bool(dropout)), _fbits(inv_count), _fbits(inv_batch),
                  _fbits(spec.bn_epsilon), _fbits(spec.bn_momentum),
-                 self.counters.data_ptr() if device_counters else 0, self.groups, int(self.shared0)]
+                 self.counters.data_ptr() if device_counters else 0, self.groups, int(self.shared0),
+                 self.wpart.data_ptr() if self.wpart is not None else 0]
         self.ctx = torch.tensor(vals, dtype=torch.int64)
         self._ctx_key = key
         return self.ctx
