@@ -135,3 +135,46 @@ def test_uq_api_sharded_equals_single_process(bn_mode):
         np.testing.assert_allclose(r_mcd, mcd, atol=1e-5, rtol=1e-5)
         np.testing.assert_allclose(r_de, de, atol=1e-6, rtol=1e-6)
         torch.testing.assert_close(r_stats, m.store.stats, atol=1e-5, rtol=1e-5)  # same moving-average side effect
+
+
+def _boot_sharded(rank, world, parity):
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.uq import uq_techniques as U
+
+    rs = np.random.RandomState(5)
+    p = rs.rand(6, 41).astype(np.float32)
+    y = (rs.rand(41) > 0.6).astype(np.int64)
+    return U.bootstrap_metrics(p, y, 17, random_state=9, parity=parity, device="cpu")
+
+
+@pytest.mark.parametrize("parity", [True, False])
+def test_bootstrap_sharded_equals_single_process(parity):
+    """3 ranks each sum the bootstrap draws landing in their window shard (41 windows,
+    uneven) and all-reduce the (B, 8) raw sums; every rank gets the single-process replicates."""
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.uq import uq_techniques as U
+
+    res = run_ranks(_boot_sharded, 3, (parity,))
+    rs = np.random.RandomState(5)
+    p = rs.rand(6, 41).astype(np.float32)
+    y = (rs.rand(41) > 0.6).astype(np.int64)
+    ref = U.bootstrap_metrics(p, y, 17, random_state=9, parity=parity, device="cpu", distributed=False)
+    for r in res:
+        assert len(r) == 17
+        for a, b in zip(r, ref):
+            for k in b:
+                assert abs(a[k] - b[k]) <= 1e-6 * max(1.0, abs(b[k])), (k, a[k], b[k])
+
+
+def test_bootstrap_partial_sums_cover_all_draws():
+    """Partial sums over a split of the windows add up to the full-range sums, and finalize
+    reproduces ops.uq.bootstrap (hash draws)."""
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import uq as uq_ops
+
+    g = torch.Generator().manual_seed(0)
+    p = torch.rand(5, 37, generator=g)
+    y = (torch.rand(37, generator=g) > 0.5).long()
+    m = uq_ops.metrics(p)
+    parts = [uq_ops.bootstrap_partial(m[:, s:e], y[s:e], 9, 37, s, seed=3) for s, e in ((0, 10), (10, 30), (30, 37))]
+    tot = sum(parts)
+    assert torch.all(tot[:, 2] + tot[:, 4] == 37)
+    full = uq_ops.bootstrap(m, y, 9, seed=3)
+    torch.testing.assert_close(uq_ops.finalize_bootstrap_sums(tot, 37), full, atol=1e-6, rtol=1e-6)

@@ -94,3 +94,17 @@ def test_fused_bitwise_deterministic_and_pass_offset():
     assert torch.equal(tail, a[5:])
     c = F.fused_forward(x, blob, S, n_pass=8, dropout=True, seed=6)[0]
     assert not torch.equal(a, c)
+
+
+@pytest.mark.parametrize("limit", [1000, 250])
+def test_fused_chunked_launches_equal_one_launch(monkeypatch, limit):
+    """Calls with n_pass * N >= 2^31 samples are split into pass (and window) chunks; with the
+    per-launch limit lowered, the chunked result is bitwise that of one launch (global mask keys)."""
+    _ext.require()
+    ps = [_params(20 + m) for m in range(2)]
+    x = torch.randn(300, 60, 4, generator=torch.Generator().manual_seed(8)).to(torch.bfloat16).cuda()
+    blobs = torch.stack([F.pack_blob(S, p) for p in ps]).cuda()
+    full = F.fused_forward(x, blobs, S, n_pass=7, dropout=True, seed=11, pass_offset=3, window_offset=5)
+    monkeypatch.setattr(F, "_MAX_SAMPLES", limit)
+    chunked = F.fused_forward(x, blobs, S, n_pass=7, dropout=True, seed=11, pass_offset=3, window_offset=5)
+    assert chunked.shape == full.shape and torch.equal(chunked, full)

@@ -48,6 +48,27 @@ def test_bootstrap_kernel(parity):
         np.testing.assert_allclose(got[b], [ref[b][k] for k in M.AGG_KEYS], rtol=2e-4, atol=1e-7)
 
 
+@pytest.mark.parametrize("parity", [True, False])
+def test_bootstrap_partial_kernel_matches_eager(parity):
+    """Sharded bootstrap kernel: per-shard (B, 8) sums equal the eager sums, and the
+    summed shards finalize to the single-launch bootstrap."""
+    _ext.require()
+    rs = np.random.RandomState(2)
+    n, B = 3001, 16
+    p = torch.from_numpy(rs.rand(5, n).astype(np.float32)).cuda()
+    y = torch.from_numpy((rs.rand(n) > 0.6).astype(np.int32)).cuda()
+    mt = uq_ops.metrics(p)
+    idx = torch.from_numpy(M.parity_bootstrap_indices(n, B, 7).astype(np.int32)).cuda() if parity else None
+    tot = torch.zeros(B, 8, dtype=torch.float64, device="cuda")
+    for s, e in ((0, 1000), (1000, 1001), (1001, n)):
+        part = uq_ops.bootstrap_partial(mt[:, s:e].contiguous(), y[s:e], B, n, s, idx=idx, seed=7)
+        ref = uq_ops.bootstrap_partial_eager(mt[:, s:e].cpu(), y[s:e].cpu(), None if idx is None else idx.cpu(), 7, B, n, s)
+        torch.testing.assert_close(part.cpu(), ref, rtol=1e-9, atol=1e-9)
+        tot += part
+    full = uq_ops.bootstrap(mt, y, B, idx=idx, seed=7)
+    torch.testing.assert_close(uq_ops.finalize_bootstrap_sums(tot, n), full, rtol=1e-12, atol=1e-12)
+
+
 def test_adam_kernel_matches_eager():
     _ext.require()
     n = 851457

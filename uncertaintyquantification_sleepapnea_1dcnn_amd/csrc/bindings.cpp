@@ -21,6 +21,8 @@ void fused_layout(int* woffs, int* eoffs, int* dense_off);
 hipError_t launch_uq_reduce(const float* probs, int t_count, int n, float* out, hipStream_t stream);
 hipError_t launch_bootstrap(const float* metrics, const int* y, const int* idx, unsigned seed, int n, int n_boot,
                             double* out, hipStream_t stream);
+hipError_t launch_bootstrap_partial(const float* metrics, const int* y, const int* idx, unsigned seed, int n, int lo,
+                                    int n_loc, int n_boot, double* out, hipStream_t stream);
 hipError_t launch_adam(float* p, const float* g, float* m, float* v, long long n, float b1, float b2, float alpha,
                        float eps, float gscale, const int* step_dev, hipStream_t stream);
 hipError_t train_bump_counters(int* c, int n, hipStream_t st);
@@ -152,6 +154,33 @@ at::Tensor bootstrap(const at::Tensor& metrics, const at::Tensor& y, const c10::
   check(apneauq::launch_bootstrap(m.data_ptr<float>(), yy.data_ptr<int>(), ip, (unsigned)seed, (int)n, (int)n_boot,
                                   out.data_ptr<double>(), cur_stream()),
         "bootstrap");
+  return out;
+}
+
+// Sharded bootstrap: raw (B, 8) sums over the draws landing in this rank's windows
+// [lo, lo + n_loc) of n_global; summed over ranks by the caller, then turned into the 6 means.
+at::Tensor bootstrap_partial(const at::Tensor& metrics, const at::Tensor& y, const c10::optional<at::Tensor>& idx,
+                             int64_t seed, int64_t n_boot, int64_t n_global, int64_t lo) {
+  TORCH_CHECK(metrics.is_cuda() && metrics.scalar_type() == at::kFloat && metrics.dim() == 2 && metrics.size(0) == 7,
+              "bootstrap_partial: metrics must be the (7, n_loc) output of uq_reduce");
+  const int64_t n_loc = metrics.size(1);
+  TORCH_CHECK(lo >= 0 && lo + n_loc <= n_global && n_global < (int64_t(1) << 31), "bootstrap_partial: bad shard");
+  auto m = metrics.contiguous();
+  auto yy = y.to(at::kInt).contiguous();
+  TORCH_CHECK(yy.is_cuda() && yy.numel() == n_loc, "bootstrap_partial: y must be (n_loc,) on the GPU");
+  const int* ip = nullptr;
+  at::Tensor ii;
+  if (idx.has_value()) {
+    ii = idx->to(at::kInt).contiguous();
+    TORCH_CHECK(ii.is_cuda() && ii.dim() == 2 && ii.size(0) == n_boot && ii.size(1) == n_global,
+                "bootstrap_partial: idx must be (B, n_global) on the GPU");
+    ip = ii.data_ptr<int>();
+  }
+  const at::DeviceGuard guard(m.device());
+  auto out = at::empty({n_boot, 8}, m.options().dtype(at::kDouble));
+  check(apneauq::launch_bootstrap_partial(m.data_ptr<float>(), yy.data_ptr<int>(), ip, (unsigned)seed, (int)n_global,
+                                          (int)lo, (int)n_loc, (int)n_boot, out.data_ptr<double>(), cur_stream()),
+        "bootstrap_partial");
   return out;
 }
 
@@ -574,6 +603,7 @@ TORCH_LIBRARY(apneauq, m) {
         "bool dropout, bool out_logits, int[] thr, float[] dscale, int grid) -> Tensor");
   m.def("uq_reduce(Tensor probs) -> Tensor");
   m.def("bootstrap(Tensor metrics, Tensor y, Tensor? idx, int seed, int n_boot) -> Tensor");
+  m.def("bootstrap_partial(Tensor metrics, Tensor y, Tensor? idx, int seed, int n_boot, int n_global, int lo) -> Tensor");
   m.def("fused_layout() -> int[]", &fused_layout);
   m.def("train_call(Tensor ctx, int op, int layer, int flag, int pass_base, int device) -> ()", &train_call);
   m.def("train_pack(Tensor w, int k, int cin, int cout, Tensor(a!) fwd, Tensor(b!) dgr) -> ()");
@@ -605,6 +635,7 @@ TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
   m.impl("fused_forward", &fused_forward);
   m.impl("uq_reduce", &uq_reduce);
   m.impl("bootstrap", &bootstrap);
+  m.impl("bootstrap_partial", &bootstrap_partial);
   m.impl("adam_step", &adam_step);
   m.impl("bump_counters", &bump_counters);
   m.impl("train_pack", &train_pack);

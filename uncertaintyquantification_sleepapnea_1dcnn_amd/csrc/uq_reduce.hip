@@ -61,15 +61,20 @@ __global__ __launch_bounds__(256) void uq_reduce_kernel(const float* __restrict_
 // mean_total_pred_entropy, mean_expected_aleatoric_entropy, mean_mutual_info.
 constexpr int kBootThreads = 512;
 
+// PARTIAL (sharded windows): this rank holds the metrics of global windows [lo, lo + n_loc);
+// every draw is enumerated, only those landing in the shard are summed, and the 8 raw sums per
+// replicate go out for an all-reduce (ops/uq.py bootstrap_partial) instead of the 6 means.
+template <bool PARTIAL>
 __global__ __launch_bounds__(kBootThreads) void bootstrap_kernel(const float* __restrict__ metrics, const int* __restrict__ y,
                                                                  const int* __restrict__ idx, unsigned seed, int n,
-                                                                 double* __restrict__ out) {
+                                                                 int lo, int n_loc, double* __restrict__ out) {
   const int b = blockIdx.x;
   APNEAUQ_DASSERT(blockDim.x == kBootThreads && n > 0);
-  const float* var = metrics + kVar * (long long)n;
-  const float* ent = metrics + kEntNats * (long long)n;
-  const float* eent = metrics + kExpEnt * (long long)n;
-  const float* mi = metrics + kMI * (long long)n;
+  const int ld = PARTIAL ? n_loc : n;  // leading dimension of the metric rows
+  const float* var = metrics + kVar * (long long)ld;
+  const float* ent = metrics + kEntNats * (long long)ld;
+  const float* eent = metrics + kExpEnt * (long long)ld;
+  const float* mi = metrics + kMI * (long long)ld;
   double acc[7] = {0, 0, 0, 0, 0, 0, 0};  // sum var, sum var|0, cnt0, sum var|1, cnt1, sum H, sum EH  (+MI below)
   double smi = 0.0;
   const unsigned bkey = mix32(seed ^ mix32((unsigned)b * 0x9E3779B9u + 0x7F4A7C15u));
@@ -80,6 +85,10 @@ __global__ __launch_bounds__(kBootThreads) void bootstrap_kernel(const float* __
     } else {
       const unsigned hsh = mix32(bkey ^ mix32((unsigned)j));
       k = (int)(((unsigned long long)hsh * (unsigned long long)n) >> 32);
+    }
+    if constexpr (PARTIAL) {
+      k -= lo;
+      if (k < 0 || k >= n_loc) continue;
     }
     const float v = var[k];
     const int yy = y[k];
@@ -106,6 +115,10 @@ __global__ __launch_bounds__(kBootThreads) void bootstrap_kernel(const float* __
       t[q] = 0.0;
       for (int w = 0; w < kBootThreads / kWave; ++w) t[q] += red[q][w];
     }
+    if constexpr (PARTIAL) {
+      for (int q = 0; q < 8; ++q) out[b * 8 + q] = t[q];
+      return;
+    }
     out[b * 6 + 0] = t[0] / n;
     out[b * 6 + 1] = t[2] > 0 ? t[1] / t[2] : 0.0;
     out[b * 6 + 2] = t[4] > 0 ? t[3] / t[4] : 0.0;
@@ -124,7 +137,16 @@ hipError_t launch_uq_reduce(const float* probs, int t_count, int n, float* out, 
 hipError_t launch_bootstrap(const float* metrics, const int* y, const int* idx, unsigned seed, int n, int n_boot,
                             double* out, hipStream_t stream) {
   if (n_boot <= 0) return hipSuccess;
-  hipLaunchKernelGGL(bootstrap_kernel, dim3(n_boot), dim3(kBootThreads), 0, stream, metrics, y, idx, seed, n, out);
+  hipLaunchKernelGGL(bootstrap_kernel<false>, dim3(n_boot), dim3(kBootThreads), 0, stream, metrics, y, idx, seed, n, 0, n,
+                     out);
+  return hipGetLastError();
+}
+
+hipError_t launch_bootstrap_partial(const float* metrics, const int* y, const int* idx, unsigned seed, int n, int lo,
+                                    int n_loc, int n_boot, double* out, hipStream_t stream) {
+  if (n_boot <= 0) return hipSuccess;
+  hipLaunchKernelGGL(bootstrap_kernel<true>, dim3(n_boot), dim3(kBootThreads), 0, stream, metrics, y, idx, seed, n, lo,
+                     n_loc, out);
   return hipGetLastError();
 }
 

@@ -142,6 +142,9 @@ def pack_blob(spec: ModelSpec, p, bn_override: Optional[Sequence] = None) -> tor
     return blob
 
 
+_MAX_SAMPLES = 1 << 31  # samples per fused launch (32-bit sample index); tests lower it
+
+
 def dropout_tables(spec: ModelSpec):
     thr = [rng.dropout_threshold(b.dropout) for b in spec.blocks]
     dsc = [1.0 / (1.0 - b.dropout) if b.dropout < 1.0 else 0.0 for b in spec.blocks]
@@ -151,13 +154,30 @@ def dropout_tables(spec: ModelSpec):
 def fused_forward(x_bf16: torch.Tensor, blobs: torch.Tensor, spec: ModelSpec = DEFAULT_SPEC, *, n_pass: int = 1,
                   dropout: bool = False, seed: int = 0, window_offset: int = 0, pass_offset: int = 0,
                   logits: bool = False) -> torch.Tensor:
-    """Run the fused kernel: returns (members, n_pass, N) fp32 probabilities (or logits)."""
+    """Run the fused kernel: returns (members, n_pass, N) fp32 probabilities (or logits).
+
+    One launch indexes samples (pass, window) with 32-bit ints, so a call with
+    n_pass * N >= 2^31 samples is split into pass chunks (and window chunks if N alone is that
+    large); masks are keyed by the global (pass, window) ids, so the result is that of one launch."""
     o = _ext.ops()
     if blobs.dim() == 1:
         blobs = blobs.unsqueeze(0)
     thr, dsc = dropout_tables(spec)
-    return o.fused_forward(x_bf16, blobs, int(n_pass), int(window_offset), int(pass_offset), int(seed) & ((1 << 63) - 1),
-                           bool(dropout), bool(logits), thr, dsc, 0)
+    seed = int(seed) & ((1 << 63) - 1)
+    n_win = x_bf16.shape[0]
+    if n_pass * n_win < _MAX_SAMPLES:
+        return o.fused_forward(x_bf16, blobs, int(n_pass), int(window_offset), int(pass_offset), seed, bool(dropout),
+                               bool(logits), thr, dsc, 0)
+    out = torch.empty(blobs.shape[0], n_pass, n_win, dtype=torch.float32, device=x_bf16.device)
+    wc = min(n_win, _MAX_SAMPLES - 1)
+    pc = max(1, (_MAX_SAMPLES - 1) // wc)
+    for w0 in range(0, n_win, wc):
+        w1 = min(n_win, w0 + wc)
+        for p0 in range(0, n_pass, pc):
+            p1 = min(n_pass, p0 + pc)
+            out[:, p0:p1, w0:w1] = o.fused_forward(x_bf16[w0:w1], blobs, p1 - p0, int(window_offset) + w0,
+                                                   int(pass_offset) + p0, seed, bool(dropout), bool(logits), thr, dsc, 0)
+    return out
 
 
 # ------------------------------------------------------------------------------------------------

@@ -83,3 +83,47 @@ def bootstrap(m: torch.Tensor, y: torch.Tensor, n_boot: int, idx: Optional[torch
         return _ext.ops().bootstrap(m, y.to(m.device), None if idx is None else idx.to(m.device), int(seed) & 0xFFFFFFFF,
                                     int(n_boot))
     return bootstrap_eager(m, y, idx, seed, n_boot)
+
+
+def bootstrap_partial_eager(m_loc: torch.Tensor, y_loc: torch.Tensor, idx: Optional[torch.Tensor], seed: int,
+                            n_boot: int, n_global: int, lo: int) -> torch.Tensor:
+    """(B, 8) float64 raw sums over the draws that land in windows [lo, lo + n_loc): [sum var,
+    sum var|y=0, n0, sum var|y=1, n1, sum H, sum E[H], sum MI] (bootstrap_kernel<true>)."""
+    n_loc = m_loc.shape[1]
+    if idx is None:
+        idx = _hash_idx(n_global, n_boot, seed, m_loc.device)
+    k = idx.long() - lo
+    inside = (k >= 0) & (k < n_loc)
+    var, h, e, mi = (m_loc[r].double() for r in (VAR, ENT_NATS, EXP_ENT, MI))
+    yy = y_loc.long()
+    out = torch.zeros(n_boot, 8, dtype=torch.float64, device=m_loc.device)
+    for b in range(n_boot):
+        kk = k[b][inside[b]]
+        v, yb = var[kk], yy[kk]
+        c0, c1 = yb == 0, yb == 1
+        out[b] = torch.stack([v.sum(), v[c0].sum(), c0.sum().double(), v[c1].sum(), c1.sum().double(), h[kk].sum(),
+                              e[kk].sum(), mi[kk].sum()])
+    return out
+
+
+def bootstrap_partial(m_loc: torch.Tensor, y_loc: torch.Tensor, n_boot: int, n_global: int, lo: int,
+                      idx: Optional[torch.Tensor] = None, seed: int = 0) -> torch.Tensor:
+    """This shard's (B, 8) bootstrap sums (HIP kernel on the GPU); sum them over ranks, then
+    :func:`finalize_bootstrap_sums`."""
+    if m_loc.is_cuda:
+        return _ext.ops().bootstrap_partial(m_loc, y_loc.to(m_loc.device), None if idx is None else idx.to(m_loc.device),
+                                            int(seed) & 0xFFFFFFFF, int(n_boot), int(n_global), int(lo))
+    return bootstrap_partial_eager(m_loc, y_loc, idx, int(seed) & 0xFFFFFFFF, n_boot, n_global, lo)
+
+
+def finalize_bootstrap_sums(s: torch.Tensor, n_global: int) -> torch.Tensor:
+    """(B, 8) summed raw sums -> (B, 6) replicate means (order = metrics.AGG_KEYS)."""
+    s = s.double()
+    out = torch.zeros(s.shape[0], 6, dtype=torch.float64, device=s.device)
+    out[:, 0] = s[:, 0] / n_global
+    out[:, 1] = torch.where(s[:, 2] > 0, s[:, 1] / s[:, 2].clamp_min(1), torch.zeros_like(s[:, 1]))
+    out[:, 2] = torch.where(s[:, 4] > 0, s[:, 3] / s[:, 4].clamp_min(1), torch.zeros_like(s[:, 3]))
+    out[:, 3] = s[:, 5] / n_global
+    out[:, 4] = s[:, 6] / n_global
+    out[:, 5] = s[:, 7] / n_global
+    return out

@@ -12,6 +12,9 @@ the same calls shard the work:
   statistics are those of the whole test set, exactly as the single-batch reference computes them.
 * **Deep Ensemble** — member m runs on rank ``m % world`` (all windows; one fused launch for the
   rank's members).
+* **Bootstrap**  — each rank reduces the per-window metrics of its window shard and
+  sums the bootstrap draws that land in it; one all-reduce of the (B, 8) float64 raw sums gives
+  every rank the replicate means (:func:`bootstrap_sharded`).
 * Results are all-gathered so every rank returns the full (T|M, N, 1) array the
   reference API promises; the drivers then do host-side work on rank 0 only.
 """
@@ -116,3 +119,37 @@ def deep_ensembles_predict_sharded(ensemble_models: List, x_test_data) -> torch.
         n = np.asarray(x_test_data).shape[0] if not isinstance(x_test_data, torch.Tensor) else x_test_data.shape[0]
         loc = torch.zeros(0, n)
     return _gather_members(loc.float().to(dev), ids, M, world).unsqueeze(-1)
+
+
+@torch.no_grad()
+def bootstrap_sharded(predictions, y_true, n_boot: int, seed: int = 0, idx=None) -> torch.Tensor:
+    """(B, 6) float64 bootstrap replicate means on every rank (``uq_techniques.py:137-157``).
+
+    ``predictions`` is either the full (T, N) array (every rank slices its window shard) or this
+    rank's (T, n_local) shard of the contiguous split ``shard_range(N, rank, world)`` — pass
+    ``n_global`` via ``y_true`` being the full label vector in both cases.  ``idx`` (B, N)
+    parity indices or the device counter hash (``seed``) pick the draws; the result equals the
+    single-process ``ops.uq.bootstrap`` up to float64 summation order."""
+    from ..ops import uq as uq_ops
+
+    world, rank = dist.get_world_size(), dist.get_rank()
+    y = torch.as_tensor(np.asarray(y_true.cpu() if isinstance(y_true, torch.Tensor) else y_true)).reshape(-1)
+    n = y.numel()
+    s, e = pdist.shard_range(n, rank, world)
+    p = predictions if isinstance(predictions, torch.Tensor) else torch.as_tensor(np.asarray(predictions))
+    if p.dim() == 3 and p.shape[-1] == 1:
+        p = p[..., 0]
+    if p.dim() == 1:
+        p = p.reshape(1, -1)
+    if p.shape[1] == n and e - s != n:
+        p = p[:, s:e]
+    assert p.shape[1] == e - s, (p.shape, s, e)
+    dev = pdist.info().device if (torch.cuda.is_available() and dist.get_backend() != "gloo") else \
+        (p.device if p.is_cuda else torch.device("cpu"))
+    m = uq_ops.metrics(p.to(dev, torch.float32).contiguous())
+    ii = None if idx is None else torch.as_tensor(np.asarray(idx.cpu() if isinstance(idx, torch.Tensor) else idx)
+                                                  .astype(np.int32)).to(dev)
+    part = uq_ops.bootstrap_partial(m, y[s:e].to(dev, torch.int32), n_boot, n, s, idx=ii, seed=seed)
+    comm = part.to(_comm_device())
+    dist.all_reduce(comm)
+    return uq_ops.finalize_bootstrap_sums(comm, n)

@@ -173,12 +173,14 @@ def uq_evaluation_dist(uq_predictions, y_true) -> Dict[str, np.ndarray]:
 
 # ===================== Confidence Intervals =====================
 def bootstrap_metrics(uq_predictions, y_true, n_bootstrap: int = 100, random_state: Optional[int] = None,
-                      parity: bool = True, device: Optional[str] = None) -> Optional[List[Dict]]:
+                      parity: bool = True, device: Optional[str] = None,
+                      distributed: Optional[bool] = None) -> Optional[List[Dict]]:
     """B bootstrap replicates of the 6 aggregate UQ metrics.
 
     The per-window metrics are invariant under resampling, so each replicate is a gather + mean
     over the resampled windows (mathematically identical to the reference's full recomputation,
-    ``uq_techniques.py:137-157``).
+    ``uq_techniques.py:137-157``).  Under a multi-rank process group the windows are sharded and
+    the replicate sums all-reduced (``distributed.bootstrap_sharded``).
     """
     torch = _torch()
     p = uq_predictions
@@ -186,8 +188,14 @@ def bootstrap_metrics(uq_predictions, y_true, n_bootstrap: int = 100, random_sta
     y = np.asarray(y_true.cpu() if isinstance(y_true, torch.Tensor) else y_true)
     print(f"Starting bootstrap with {n_bootstrap} iterations...")
     use_dev = (device == "cuda") or (device is None and ((isinstance(p, torch.Tensor) and p.is_cuda) or _gpu_ok()))
+    from . import distributed as D
+
     try:
-        if use_dev:
+        if D.active() if distributed is None else distributed:
+            idx = M.parity_bootstrap_indices(n_samples, n_bootstrap, random_state) if parity else None
+            res = D.bootstrap_sharded(p, y, n_bootstrap, seed=0 if random_state is None else random_state, idx=idx)
+            out = [dict(zip(M.AGG_KEYS, (float(v) for v in row))) for row in res.cpu().numpy()]
+        elif use_dev:
             from ..ops import uq as uq_ops
 
             mt, _ = _device_windows(p)
