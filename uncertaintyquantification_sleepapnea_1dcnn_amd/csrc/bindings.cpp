@@ -59,7 +59,7 @@ namespace train {
 struct Layer {
   const void* wf; const void* wd; const float* bias; const float* gamma; const float* beta;
   float* mmean; float* mvar; float* gw; float* gb; float* ggamma; float* gbeta;
-  void* R; void* dY; void* dZ; double* st; float* bst; unsigned thr; float dsc;
+  void* R; void* dY; void* dZ; double* st; float* bst; unsigned thr; float dsc; float* aff;
 };
 struct Args {
   Layer L[6];
@@ -212,7 +212,7 @@ void bump_counters(at::Tensor& counters) {
 }
 
 // ctx: int64 CPU tensor of device pointers / scalars built once per workspace (ops/train_ops.py)
-constexpr int kCtxLayer = 18, kCtxLen = 6 * kCtxLayer + 24;
+constexpr int kCtxLayer = 19, kCtxLen = 6 * kCtxLayer + 24;
 
 float bits_to_float(int64_t v) {
   uint32_t u = static_cast<uint32_t>(v);
@@ -250,6 +250,7 @@ apneauq::train::Args args_from_ctx(const at::Tensor& ctx, int64_t pass_base) {
     L.thr = static_cast<unsigned>(q[15]);
     L.dsc = bits_to_float(q[16]);
     L.dZ = reinterpret_cast<void*>(q[17]);
+    L.aff = reinterpret_cast<float*>(q[18]);
   }
   const int64_t* g = c + 6 * kCtxLayer;
   A.x = reinterpret_cast<const void*>(g[0]);

@@ -59,6 +59,16 @@ __device__ __forceinline__ uint32_t dropout_bits2(uint32_t skey, uint32_t t, uin
   return mix32(skey ^ ((t << 9) | (c_even >> 1)));
 }
 
+// Dropout decisions of a dropout_bits2 pair as bf16 sign bits: bit 15 set iff the low 16-bit uniform
+// is < thr, bit 31 iff the high one is (thr2 = thr * 0x10001).  Three packed VALU ops:
+// sat(thr - u) is nonzero iff u < thr, and sat(that + 0x7FFF) then has its top bit set.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t drop_signs2(uint32_t h, uint32_t thr2) {
+  const u16x2 d = __builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, thr2), __builtin_bit_cast(u16x2, h));
+  const u16x2 t = __builtin_elementwise_add_sat(d, (u16x2){0x7FFF, 0x7FFF});
+  return __builtin_bit_cast(uint32_t, t) & 0x80008000u;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);

@@ -28,6 +28,7 @@
 // LDS read ds_read_b64_tr_b16 from row-major tiles; each workgroup sums 16 row tiles in registers
 // and adds its output block to the fp32 gradient with global atomics.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -63,6 +64,8 @@ struct Layer {
   float* bst;          // [2][C] backward sums (sum dY, sum dY * xhat)
   unsigned thr;        // dropout threshold (16-bit units) and 1/(1-p)
   float dsc;
+  float* aff;          // [groups][2][C] BN affine (s = gamma * rstd, t = beta - mean * s) of the batch
+                       // statistics, written by aff_kernel for the ping-pong forward's staging
 };
 
 struct Args {
@@ -142,6 +145,19 @@ __device__ __forceinline__ int row_time(int grow) { return (grow - kHalo) & 63; 
 #ifndef APNEAUQ_FWD_ABL
 #define APNEAUQ_FWD_ABL 0
 #endif
+// 1: the forward kernels load tile i+1's input while tile i's moments and copy-out run (0: probe)
+#ifndef APNEAUQ_FWD_PIPE
+#define APNEAUQ_FWD_PIPE 0
+#endif
+// s_setprio 1 around the forward conv MFMAs (the co-resident workgroup's staging / copy-out VALU
+// gets the leftover issue slots: -1.5 % per chunk); probe: an initial s_sleep offset (x 127*64
+// cycles) for the second half of the grid (phase offset between co-resident workgroups: no effect)
+#ifndef APNEAUQ_FWD_PRIO
+#define APNEAUQ_FWD_PRIO 1
+#endif
+#ifndef APNEAUQ_FWD_DELAY
+#define APNEAUQ_FWD_DELAY 0
+#endif
 // dgrad probe hooks (0 in the library build; nonzero values compute garbage): 1 = epilogue without
 // the R_{l-1} loads, 2 = stage_dz without the global dZ write, 4 = no dY copy-out, 8 = no MFMAs,
 // 16 = stage_dz without its global loads
@@ -161,7 +177,7 @@ __device__ __forceinline__ float slot_sum(const float* p, int stride) {
 }
 __device__ __forceinline__ double slot_sumd(const double* p, int stride) {
   double s = 0.0;
-#pragma unroll
+#pragma unroll 4  // partly unrolled: the forward kernels call this with their next tile's input in registers
   for (int i = 0; i < kStatSlots; ++i) s += p[i * stride];
   return s;
 }
@@ -266,10 +282,7 @@ __device__ __forceinline__ bf16x8 zero8() {
 // per row only when it differs.  The dropout mask is R_l's sign bit (set by the producer), so the
 // transform is  a = sign ? 0 : |r| * s + t  on the packed bf16 pairs.
 //
-// HASH_IN (batch-BN MC Dropout, block 2 reading the pass-shared block-1 output): R_0 holds one
-// unencoded copy per WINDOW; rows are fetched from the sample's window and block 1's dropout mask
-// is drawn from the counter hash here.
-template <int l, int NR, int NCW, int UMAX = kStageU, bool HASH_IN = false, int SWZ = 0>
+template <int l, int NR, int NCW, int UMAX = kStageU, int SWZ = 0>
 __device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, int row0, int c0, const float* s,
                                           const float* t, int g0) {
   constexpr int Cc = C[l + 1];
@@ -296,24 +309,7 @@ __device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, i
     s1[j] = two ? s[256 + c + j] * dsc : s0[j];
     t1[j] = two ? t[256 + c + j] * dsc : t0[j];
   }
-  unsigned key0 = 0u, key1 = 0u;
-  const __bf16* src0 = nullptr;
-  const __bf16* src1 = nullptr;
-  if constexpr (HASH_IN) {
-    const int n0 = min(smp0, A.B - 1), n1 = min(smp0 + 1, A.B - 1);
-    if (drop) {
-      key0 = layer_sample_key(A, l, n0);
-      key1 = layer_sample_key(A, l, n1);
-    }
-    src0 = Ly.R + (long long)(kHalo + (n0 - g0 * A.n_win) * kSR) * Cc + c;
-    src1 = Ly.R + (long long)(kHalo + (n1 - g1 * A.n_win) * kSR) * Cc + c;
-  }
-  auto valid = [&](int grow) {
-    const int n = row_sample(grow), tt = row_time(grow);
-    if constexpr (HASH_IN) return grow >= kHalo && (n == smp0 || n == smp0 + 1) && n < A.B && tt < kL;
-    return !(grow < kHalo || n >= A.B || tt >= kL);
-  };
-  if constexpr (!HASH_IN) {
+  {
     // Every staged row exists in the padded buffer, and pad rows / rows past the batch / the
     // buffer's halo rows hold -0.0, which decodes to 0 like a dropped element: no per-row checks.
     auto run = [&](auto two_groups) {
@@ -348,56 +344,124 @@ __device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, i
       run(std::true_type{});
     else
       run(std::false_type{});
-    return;
-  }
-#pragma unroll
-  for (int b = 0; b < NK; b += U) {
-    bf16x8 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int r = rin + (b + u) * RP;
-      const int grow = row0 + r;
-      if (b + u < NK) {
-        const bool hi = row_sample(grow) != smp0;
-        v[u] = (active && r < NR && valid(grow)) ? gld<bf16x8>((hi ? src1 : src0) + (long long)row_time(grow) * Cc)
-                                                 : zero8();
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int r = rin + (b + u) * RP;
-      if (b + u >= NK || !active || r >= NR) continue;
-      const int grow = row0 + r;
-      bf16x8 o = zero8();
-      if (valid(grow)) {
-        const bool hi = row_sample(grow) != smp0;
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(&v[u]);
-        unsigned kb = 0xFFu;  // bit j = channel c + j kept
-        if (drop) {
-          const unsigned key = hi ? key1 : key0;
-          const int tt = row_time(grow);
-          kb = 0u;
-#pragma unroll
-          for (int j = 0; j < 8; j += 2) {
-            const unsigned h = dropout_bits2(key, tt, c + j);
-            kb |= ((h & 0xFFFFu) >= Ly.thr ? 1u : 0u) << j;
-            kb |= ((h >> 16) >= Ly.thr ? 1u : 0u) << (j + 1);
-          }
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint32_t d = w[q];
-          const float a0 = __builtin_fmaf(__uint_as_float(d << 16), hi ? s1[2 * q] : s0[2 * q], hi ? t1[2 * q] : t0[2 * q]);
-          const float a1 = __builtin_fmaf(__uint_as_float(d & 0xFFFF0000u), hi ? s1[2 * q + 1] : s0[2 * q + 1],
-                                          hi ? t1[2 * q + 1] : t0[2 * q + 1]);
-          o[2 * q] = (__bf16)(((kb >> (2 * q)) & 1u) ? a0 : 0.f);
-          o[2 * q + 1] = (__bf16)(((kb >> (2 * q + 1)) & 1u) ? a1 : 0.f);
-        }
-      }
-      *reinterpret_cast<bf16x8*>(lds + lds_off<SWZ>(r, cw * 16, ldsrs)) = o;
-    }
   }
 }
+
+// The forward kernels' input staging split in two phases so that a tile's global loads overlap the
+// previous tile's moments and copy-out: load() issues every row load of a tile into registers (no
+// wait), store() decodes A = dropout(BN(R)) from them into LDS (same transform as stage_act, all
+// CIN channels, 136 rows).
+//
+// HASH_IN (batch-BN MC Dropout, block 2 reading the pass-shared block-1 output): R_0 holds one
+// unencoded copy per WINDOW.  Branch-free: every staged row maps to a row of R_0 -- rows of the
+// tile's two samples to their window's rows, all other rows (halo rows of the neighbours) to pad
+// row 60, which holds -0.0 and decodes to 0 -- and block 1's dropout mask is drawn here from the
+// counter hash on every row, as sign bits (pad rows stay -0.0 whatever it draws).
+template <int l, bool HASH_IN>  // HASH_IN: may run in hash_in mode (runtime flag, workgroup-uniform)
+struct ActStager {
+  static constexpr int Cc = C[l + 1];
+  static constexpr int NCW = Cc / 8;
+  static constexpr int RP = kThreads / NCW;  // rows per pass over the workgroup
+  static constexpr int NK = (kRows + RP - 1) / RP;
+  u32x4 v[NK];
+
+  __device__ __forceinline__ static int tid() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));  // opaque: keeps the per-row addresses out of the tile loop
+    return t;
+  }
+
+  // every v[u] is assigned on every path (zeros where unused), so v is dead between store() and the
+  // next load() -- in particular across the conv MFMAs
+  __device__ __forceinline__ void load(const Args& A, int row0, bool hash_in) {
+    const int t = tid(), cw = t % NCW, rin = t / NCW;
+#pragma unroll
+    for (int u = 0; u < NK; ++u) v[u] = u32x4{0u, 0u, 0u, 0u};
+    if (rin >= RP) return;
+    const __bf16* R = A.L[l].R + cw * 8;
+    if (HASH_IN && hash_in) {
+      const int smp0 = row0 >> 6;
+      const int n0 = min(smp0, A.B - 1), n1 = min(smp0 + 1, A.B - 1);
+      const int g0 = n0 / A.n_win, g1 = n1 / A.n_win;
+      const __bf16* src0 = R + (long long)(kHalo + (n0 - g0 * A.n_win) * kSR) * Cc;
+      const __bf16* src1 = R + (long long)(kHalo + (n1 - g1 * A.n_win) * kSR) * Cc;
+#pragma unroll
+      for (int u = 0; u < NK; ++u) {
+        const int r = rin + u * RP;
+        if (r >= kRows) continue;
+        const int grow = row0 + r;
+        const int n = row_sample(grow);
+        const bool own = grow >= kHalo && (n == smp0 || n == smp0 + 1);
+        v[u] = gld<u32x4>((n == smp0 + 1 ? src1 : src0) + (long long)(own ? row_time(grow) : kL) * Cc);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < NK; ++u) {
+        const int r = rin + u * RP;
+        if (r < kRows) v[u] = gld<u32x4>(R + (long long)(row0 + r) * Cc);
+      }
+    }
+  }
+
+  // s, t: the affine of stats group g0 (s + 256, t + 256: group g1 when the tile straddles two)
+  __device__ __forceinline__ void store(const Args& A, char* lds, int row0, const float* s, const float* t,
+                                        int g0, bool hash_in) const {
+    const int tt_ = tid(), cw = tt_ % NCW, rin = tt_ / NCW;
+    if (rin >= RP) return;
+    const Layer& Ly = A.L[l];
+    const int c = cw * 8;
+    const int smp0 = row0 >> 6;
+    const int g1 = min(smp0 + 1, A.B - 1) / A.n_win;
+    const bool two = g1 != g0;  // workgroup-uniform
+    const bool drop = A.dropout != 0;
+    const float dsc = drop ? Ly.dsc : 1.f;
+    float s0[8], t0[8], s1[8], t1[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s0[j] = s[c + j] * dsc;
+      t0[j] = t[c + j] * dsc;
+      s1[j] = two ? s[256 + c + j] * dsc : s0[j];
+      t1[j] = two ? t[256 + c + j] * dsc : t0[j];
+    }
+    unsigned key0 = 0u, key1 = 0u;
+    if (HASH_IN && hash_in) {
+      key0 = layer_sample_key(A, l, min(smp0, A.B - 1));
+      key1 = layer_sample_key(A, l, min(smp0 + 1, A.B - 1));
+    }
+    const uint32_t thr2 = drop ? Ly.thr * 0x10001u : 0u;  // thr 0: nothing dropped
+    auto run = [&](auto two_groups, auto hashed) {
+#pragma unroll
+      for (int u = 0; u < NK; ++u) {
+        const int r = rin + u * RP;
+        if (r >= kRows) continue;
+        const int grow = row0 + r;
+        const bool hi = row_sample(grow) == smp0 + 1;
+        u32x4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          uint32_t d = v[u][q];
+          if constexpr (decltype(hashed)::value) d |= drop_signs2(dropout_bits2(hi ? key1 : key0, row_time(grow), c + 2 * q), thr2);
+          if constexpr (decltype(two_groups)::value)  // rare: a tile straddling an MC-Dropout pass boundary
+            o[q] = decode_pair(d, hi ? s1[2 * q] : s0[2 * q], hi ? t1[2 * q] : t0[2 * q],
+                               hi ? s1[2 * q + 1] : s0[2 * q + 1], hi ? t1[2 * q + 1] : t0[2 * q + 1]);
+          else
+            o[q] = decode_pair(d, s0[2 * q], t0[2 * q], s0[2 * q + 1], t0[2 * q + 1]);
+        }
+        *reinterpret_cast<u32x4*>(lds + r * kRS + cw * 16) = o;
+      }
+    };
+    auto dispatch = [&](auto hashed) {
+      if (two)
+        run(std::true_type{}, hashed);
+      else
+        run(std::false_type{}, hashed);
+    };
+    if (HASH_IN && hash_in)
+      dispatch(std::integral_constant<bool, HASH_IN>{});
+    else
+      dispatch(std::false_type{});
+  }
+};
 
 // dZ_l rows into LDS (rows [row0, row0+NR), channels [c0, c0+NCW*8)); rows [own_lo, own_hi) are
 // also written to ``gout`` (dgrad materialises dZ_l for wgrad).
@@ -513,15 +577,24 @@ struct Conv {
   static_assert(NCT % WN == 0 && kRT % WM == 0 && WM * WN == 4, "wave tiling");
 
   __device__ __forceinline__ static void run(const gbf16x8* wfrag, const char* lds, int ldsrs, f32x4 (&acc)[CT][RT]) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int wm = wave / WN, wn = wave % WN;
-    const int m = lane & 15, h = lane >> 4;
-    const gbf16x8* wp = wfrag + (wn * CT) * 64 + lane;
-    const int row0 = wm * RT * 16 + m;
 #pragma unroll
     for (int c = 0; c < CT; ++c)
 #pragma unroll
       for (int r = 0; r < RT; ++r) acc[c][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+    steps<0, NSTEP>(wfrag, lds, ldsrs, acc);
+  }
+
+  // steps [S0, S1) accumulated into acc (S1 - S0 even unless S1 == NSTEP); the wave's place in its
+  // 4-wave team is (threadIdx.x >> 6) & 3, so 512-thread kernels run two teams
+  template <int S0, int S1>
+  __device__ __forceinline__ static void steps(const gbf16x8* wfrag, const char* lds, int ldsrs,
+                                               f32x4 (&acc)[CT][RT]) {
+    static_assert(S0 % 2 == 0 && (S1 == NSTEP || (S1 - S0) % 2 == 0) && S0 < S1, "step range");
+    const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3;
+    const int wm = wave / WN, wn = wave % WN;
+    const int m = lane & 15, h = lane >> 4;
+    const gbf16x8* wp = wfrag + (wn * CT) * 64 + lane;
+    const int row0 = wm * RT * 16 + m;
     const char* bbase = lds + (kHalo + row0 - PAD) * ldsrs + 16 * h;
     auto load_b = [&](int s, int r) -> bf16x8 {
       if constexpr (FIRST) {
@@ -551,17 +624,17 @@ struct Conv {
     };
     // unconditional (clamped) prefetch keeps hipcc's vmcnt accounting exact (see fused_forward.hip)
     bf16x8 a0[CT], a1[CT];
-    load_a(0, a0);
+    load_a(S0, a0);
 #pragma unroll 1
-    for (int s = 0; s + 1 < NSTEP; s += 2) {
+    for (int s = S0; s + 1 < S1; s += 2) {
       load_a(s + 1, a1);
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this step's MFMAs
       step(s, a0);
-      load_a(s + 2 < NSTEP ? s + 2 : s + 1, a0);
+      load_a(s + 2 < S1 ? s + 2 : s + 1, a0);
       __builtin_amdgcn_sched_barrier(0);
       step(s + 1, a1);
     }
-    if constexpr (NSTEP & 1) step(NSTEP - 1, a0);
+    if constexpr ((S1 - S0) & 1) step(S1 - 1, a0);
   }
 };
 
@@ -679,6 +752,14 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
   const bool enc = A.dropout != 0 && !(l == 0 && A.shared0);
   const bool hash_in = l == 1 && A.shared0;  // workgroup-uniform
   int gaff = -1;  // stats group whose BN affine (of block l-1) is in prm
+  // input staging, software-pipelined: tile i+1's rows are loaded into registers while tile i's
+  // moments and copy-out run, and decoded into LDS at the top of the next iteration
+  ActStager<(l > 0 ? l - 1 : 0), l == 1> stg;
+  if constexpr (APNEAUQ_FWD_DELAY > 0)
+    if (blockIdx.x >= gridDim.x / 2)
+      for (int i = 0; i < APNEAUQ_FWD_DELAY; ++i) __builtin_amdgcn_s_sleep(127);
+  if constexpr (l > 0 && !(APNEAUQ_FWD_ABL & 16) && APNEAUQ_FWD_PIPE)
+    if (t_begin < t_end) stg.load(A, kR * t_begin, hash_in);
   for (int tile = t_begin; tile < t_end; ++tile) {
     APNEAUQ_DASSERT(2 * tile < A.B + 1 && blockDim.x == kThreads);
     const int row0 = kR * tile;                        // first staged row (global PL index)
@@ -697,12 +778,8 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
         gaff = (g1 == g0) ? g0 : -1;
         __syncthreads();
       }
-      // every row of the tile in flight at once: one memory round trip per tile (the staging was
-      // latency-bound at 8 loads per thread in flight)
-      if (hash_in)
-        stage_act<l - 1, kRows, CIN / 8, 32, true>(A, act, kRS, row0, 0, prm, prm + 512, g0);
-      else
-        stage_act<l - 1, kRows, CIN / 8, 32, false>(A, act, kRS, row0, 0, prm, prm + 512, g0);
+      if constexpr (!APNEAUQ_FWD_PIPE) stg.load(A, row0, hash_in);
+      stg.store(A, act, row0, prm, prm + 512, g0, hash_in);
     }
     __syncthreads();
     f32x4 acc[CV::CT][CV::RT];
@@ -712,7 +789,9 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
 #pragma unroll
       for (int r = 0; r < CV::RT; ++r) acc[c][r] = f32x4{(float)act[threadIdx.x], 0.f, 0.f, (float)r};
 #else
+    if constexpr (APNEAUQ_FWD_PRIO) __builtin_amdgcn_s_setprio(1);
     CV::run(Ly.wf, act, IN_RS, acc);
+    if constexpr (APNEAUQ_FWD_PRIO) __builtin_amdgcn_s_setprio(0);
 #endif
     __syncthreads();  // all waves done reading the staged input; reuse it for the output tile
 
@@ -776,11 +855,12 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
       key[0] = layer_sample_key(A, l, min(smp0, A.B - 1));
       key[1] = layer_sample_key(A, l, min(smp0 + 1, A.B - 1));
     }
+    const uint32_t thr2 = Ly.thr * 0x10001u;
     auto copy_out = [&]() {
       // opaque row index (see staged_loop): keeps the NPo per-row addresses out of the tile loop
       int rin = orin;
       asm volatile("" : "+v"(rin));
-#pragma unroll
+#pragma unroll 2
       for (int k = 0; k < NPo; ++k) {
         const int r = rin + k * RPo;
         if (!oact || r >= kR) continue;
@@ -792,15 +872,14 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
           for (int q = 0; q < 4; ++q) ow[q] = kNegZero2;
         } else if (enc) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const unsigned hh = dropout_bits2(key[slot], tt, ocw * 8 + 2 * q);
-            ow[q] |= ((hh & 0xFFFFu) < Ly.thr ? 0x8000u : 0u) | ((hh >> 16) < Ly.thr ? 0x80000000u : 0u);
-          }
+          for (int q = 0; q < 4; ++q) ow[q] |= drop_signs2(dropout_bits2(key[slot], tt, ocw * 8 + 2 * q), thr2);
         }
         if constexpr (!(APNEAUQ_FWD_ABL & 4))
           *reinterpret_cast<bf16x8*>(Ly.R + (long long)(row0 + kHalo + r) * COUT + ocw * 8) = o;
       }
     };
+    if constexpr (l > 0 && !(APNEAUQ_FWD_ABL & 16) && APNEAUQ_FWD_PIPE)
+      if (tile + 1 < t_end) stg.load(A, row0 + kR, hash_in);  // next tile's input, in flight from here
     if (g0 == g1) {
       if (g0 != gcur) {
         flush();
@@ -817,6 +896,313 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
     }
     copy_out();
   }
+  flush();
+}
+
+// ------------------------------------------------------------------------------------------------
+// BN affine of block l for every stats group, for the ping-pong forward's staging (one small launch
+// before each layer instead of ~256 workgroups re-summing the fp64 slots).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void aff_kernel(Args A, int l) {
+  const int g = blockIdx.x;
+  const int Cc = C[l + 1];
+  const Layer& Ly = A.L[l];
+  for (int c = threadIdx.x; c < Cc; c += blockDim.x) {
+    float mu, var;
+    bn_moments(A, l, g, c, mu, var);
+    const float sc = Ly.gamma[c] * rsqrtf(var + A.eps);
+    Ly.aff[(g * 2 + 0) * Cc + c] = sc;
+    Ly.aff[(g * 2 + 1) * Cc + c] = Ly.beta[c] - mu * sc;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Ping-pong forward of block l >= 1 for large batches (batch-BN MC Dropout runs T x N samples through
+// every layer).  One 512-thread workgroup per CU = two 4-wave teams, each with its own LDS tile
+// buffer and its own 2-sample tiles (team h takes tiles t_begin + 2i + h).  A team's tile goes
+// through four phases -- S: stage A_{l-1} = dropout(BN(R_{l-1})) into LDS; C1, C2: the two halves of
+// the implicit-GEMM MFMA steps; E: bias + ReLU epilogue into LDS, channel moments on the matrix
+// cores, coalesced copy-out of R_l with the dropout mask in the sign bits -- and the teams run two
+// phases apart, separated by workgroup barriers:
+//     segment   4i    4i+1   4i+2   4i+3
+//     team 0    S      C1     C2     E
+//     team 1    C2     E      S      C1
+// (each team runs its own copy of the loop; s_barrier counts arrivals, not code locations)
+// so on every SIMD (one wave of each team) a conv half always runs beside the other team's memory /
+// VALU phase.  With the single-team kernel both co-resident workgroups spent their staging and
+// copy-out with idle matrix cores.  E is wave-local (each wave stores, reduces and copies out only
+// its own accumulator block), so no barrier is needed inside a phase.  Moment partials stay per
+// lane (fp32) until the stats group changes and then go to the fp64 slots with global atomics.
+// ------------------------------------------------------------------------------------------------
+template <int l> struct PP {
+  static constexpr int CIN = C[l], COUT = C[l + 1];
+  static constexpr int IN_RS = CIN * 2 + 32, OUT_RS = COUT * 2 + 32;  // odd multiples of 32 B
+  static constexpr int BUF = (kRows * IN_RS > kR * OUT_RS) ? kRows * IN_RS : kR * OUT_RS;
+  static constexpr int LDS = 2 * BUF;
+  static_assert(LDS <= 160 * 1024, "ping-pong tiles exceed the LDS");
+};
+
+template <int l>
+__global__ __launch_bounds__(512, 1) void fwd_pp_kernel(Args A) {
+  static_assert(l >= 1, "block 1 reads the input: fwd_kernel<0>");
+  using P = PP<l>;
+  constexpr int CIN = P::CIN, COUT = P::COUT, lr = l - 1;
+  using T = Tiling<COUT>;
+  using CV = Conv<CIN, COUT, KS[l], T::WM, T::WN, false>;
+  constexpr int NS1 = (CV::NSTEP / 2) & ~1;
+  constexpr int CRin = C[l];  // channels of R_{l-1}
+  constexpr int NCW = CRin / 8, RP = kThreads / NCW, NK = (kRows + RP - 1) / RP;
+  const int team = threadIdx.x >> 8;  // wave-uniform
+  const int ht = threadIdx.x & 255;
+  const int lane = threadIdx.x & 63, hw = (threadIdx.x >> 6) & 3;
+  const int wm = hw / T::WN, wn = hw % T::WN;
+  const int m = lane & 15, h = lane >> 4;
+  char* buf = smem + team * P::BUF;
+  const Layer& Ly = A.L[l];
+  const Layer& Lr = A.L[lr];
+  const int tiles = (A.B + 1) / 2;
+  const int tpw = (tiles + gridDim.x - 1) / gridDim.x;
+  const int t_begin = blockIdx.x * tpw;
+  const int n_t = max(0, min(tiles, t_begin + tpw) - t_begin);
+  const int n_team = (n_t + 1 - team) / 2;
+  const int nseg = 4 * ((n_t + 1) / 2) + 2;
+  const bool hash_in = l == 1 && A.shared0;  // block 2 reads the pass-shared block-1 output
+  const bool drop = A.dropout != 0;
+  const bool enc = drop;  // blocks >= 2 always encode their dropout mask
+  const uint32_t thr_in = (hash_in && drop) ? Lr.thr * 0x10001u : 0u;
+  const uint32_t thr_out = Ly.thr * 0x10001u;
+  const float dsc_in = drop ? Lr.dsc : 1.f;
+  // moments: per-lane partials of this wave's channel tiles (diag lanes hold D[sn][sn])
+  const int sn = lane & 15, si = sn & 3;
+  const bool diag_lane = (lane >> 4) == (sn >> 2);
+  float ps1[CV::CT], ps2[CV::CT];
+#pragma unroll
+  for (int j = 0; j < CV::CT; ++j) ps1[j] = ps2[j] = 0.f;
+  int gcur = -1;
+  double* st = Ly.st + ((blockIdx.x * 2 + team) % kStatSlots) * st_stride(A, COUT);
+  auto flush = [&]() __attribute__((always_inline)) {  // wave-local: fp32 lane partials into the fp64 slots
+    if (gcur >= 0 && diag_lane) {
+#pragma unroll
+      for (int j = 0; j < CV::CT; ++j) {
+        const int c = (wn * CV::CT + j) * 16 + sn;
+        atomicAdd(st + (gcur * 2 + 0) * COUT + c, (double)ps1[j]);
+        atomicAdd(st + (gcur * 2 + 1) * COUT + c, (double)ps2[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < CV::CT; ++j) ps1[j] = ps2[j] = 0.f;
+  };
+  // ---- S: stage A_{l-1} rows [row0, row0 + 136) into buf (all CIN channels), PPU rows per thread
+  // in flight (the phase runs beside the other team's conv half, which covers the second round trip)
+  constexpr int PPB = 1, PPU = NK;  // every row of the tile in flight: one round trip
+  auto stage = [&](int tile) __attribute__((always_inline)) {
+    const int row0 = kR * tile, smp0 = 2 * tile;
+    int t_ = ht;
+    asm volatile("" : "+v"(t_));  // opaque: keeps per-row addresses out of the segment loop
+    const int cw = t_ % NCW, rin = t_ / NCW;
+    if (rin >= RP) return;
+    const int c = cw * 8;
+    const int n0 = min(smp0, A.B - 1), n1 = min(smp0 + 1, A.B - 1);
+    const int g0 = n0 / A.n_win, g1 = n1 / A.n_win;
+    const __bf16* src0 = Lr.R + c;
+    const __bf16* src1 = src0;
+    if (hash_in) {  // R_0: one unencoded copy per window
+      src0 += (long long)(kHalo + (n0 - g0 * A.n_win) * kSR) * CRin;
+      src1 += (long long)(kHalo + (n1 - g1 * A.n_win) * kSR) * CRin;
+    }
+    // BN affine of the tile's stats group(s) (x 1/(1-rate)), from aff_kernel; the second group's
+    // only in the rare tile that straddles an MC-Dropout pass boundary
+    auto affine = [&](int g, float (&sv)[8], float (&tv)[8]) {
+      const float* a = Lr.aff + (long long)(stat_group(A, lr, g) * 2) * CRin + c;
+#pragma unroll
+      for (int j = 0; j < 8; j += 4) {
+        const f32x4 sa = gld<f32x4>(a + j), ta = gld<f32x4>(a + CRin + j);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          sv[j + q] = sa[q] * dsc_in;
+          tv[j + q] = ta[q] * dsc_in;
+        }
+      }
+    };
+    float s0[8], t0[8];
+    affine(g0, s0, t0);
+    const unsigned key0 = hash_in ? layer_sample_key(A, lr, n0) : 0u;
+    const unsigned key1 = hash_in ? layer_sample_key(A, lr, n1) : 0u;
+    auto run = [&](auto two_groups, auto hashed) {
+      constexpr bool HSH = decltype(hashed)::value;
+      float s1[8], t1[8];
+      if constexpr (decltype(two_groups)::value) affine(g1, s1, t1);
+#pragma unroll
+      for (int b = 0; b < NK; b += PPU) {
+        u32x4 v[PPU];
+#pragma unroll
+        for (int u = 0; u < PPU; ++u) {
+          if (b + u >= NK) continue;
+          const int grow = row0 + min(rin + (b + u) * RP, kRows - 1);
+          if constexpr (HSH) {  // non-own rows (neighbours' halo rows) -> pad row 60 (-0.0)
+            const int n = row_sample(grow);
+            const bool own = grow >= kHalo && (n == smp0 || n == smp0 + 1);
+            v[u] = gld<u32x4>((n == smp0 + 1 ? src1 : src0) + (long long)(own ? row_time(grow) : kL) * CRin);
+          } else {
+            v[u] = gld<u32x4>(src0 + (long long)grow * CRin);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < PPU; ++u) {
+          const int r = rin + (b + u) * RP;
+          if (b + u >= NK || r >= kRows) continue;
+          const int grow = row0 + r;
+          const bool hi = row_sample(grow) == smp0 + 1;
+          u32x4 o;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            uint32_t d = v[u][q];
+            if constexpr (HSH) d |= drop_signs2(dropout_bits2(hi ? key1 : key0, row_time(grow), c + 2 * q), thr_in);
+            if constexpr (decltype(two_groups)::value)
+              o[q] = decode_pair(d, hi ? s1[2 * q] : s0[2 * q], hi ? t1[2 * q] : t0[2 * q],
+                                 hi ? s1[2 * q + 1] : s0[2 * q + 1], hi ? t1[2 * q + 1] : t0[2 * q + 1]);
+            else
+              o[q] = decode_pair(d, s0[2 * q], t0[2 * q], s0[2 * q + 1], t0[2 * q + 1]);
+          }
+          *reinterpret_cast<u32x4*>(buf + r * P::IN_RS + cw * 16) = o;
+        }
+      }
+    };
+    auto dispatch = [&](auto hashed) {
+      if (g1 != g0)
+        run(std::true_type{}, hashed);
+      else
+        run(std::false_type{}, hashed);
+    };
+    if (l == 1 && hash_in)
+      dispatch(std::integral_constant<bool, l == 1>{});
+    else
+      dispatch(std::false_type{});
+  };
+
+  // ---- E: epilogue, moments and copy-out of this wave's accumulator block (wave-local)
+  auto finish = [&](int tile, const f32x4 (&acc)[CV::CT][CV::RT]) __attribute__((always_inline)) {
+    // opaque lane index: every lane-derived LDS / global address of this phase is recomputed here
+    // instead of being hoisted out of the segment loop (and held across the other phases)
+    int lane_ = lane;
+    asm volatile("" : "+v"(lane_));
+    const int m = lane_ & 15, h = lane_ >> 4;
+    const int row0 = kR * tile, smp0 = 2 * tile;
+    const bool last_tile = smp0 + 1 >= A.B;
+#pragma unroll
+    for (int c = 0; c < CV::CT; ++c) {
+      const int co0 = (wn * CV::CT + c) * 16 + 4 * h;
+      const f32x4 bias = gld<f32x4>(Ly.bias + co0);
+#pragma unroll
+      for (int r = 0; r < CV::RT; ++r) {
+        const int rtg = wm * CV::RT + r;
+        const int row = rtg * 16 + m;
+        f32x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = fmaxf(acc[c][r][i] + bias[i], 0.f);
+        if ((rtg & 3) == 3 || last_tile) {
+          const bool valid = (row & 63) < kL && (smp0 + (row >> 6)) < A.B;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            v[i] = valid ? v[i] : 0.f;
+            asm volatile("" : "+v"(v[i]));
+          }
+        }
+        bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+        *reinterpret_cast<bf16x4*>(buf + row * P::OUT_RS + co0 * 2) = o;
+      }
+    }
+    // the wave reads back what its other lanes wrote: LDS is in order within a wave, keep the
+    // compiler from hoisting the reads above the stores
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // channel moments over the wave's rows, per stats group (slot 0 / slot 1 rows of a tile that
+    // straddles an MC-Dropout pass boundary)
+    const int g0 = min(smp0, A.B - 1) / A.n_win, g1 = min(smp0 + 1, A.B - 1) / A.n_win;
+    bf16x8 ones;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.f;
+    constexpr int KC = CV::RT / 2;  // 32-row chunks of the wave's rows
+#pragma unroll
+    for (int kq = 0; kq < KC; ++kq) {
+      const int kc = wm * KC + kq;
+      const int g = (kc >> 1) ? g1 : g0;  // rows 64.. belong to the tile's second sample
+      if (g != gcur) {  // wave-uniform
+        flush();
+        gcur = g;
+      }
+#pragma unroll
+      for (int j = 0; j < CV::CT; ++j) {
+        const int ct = wn * CV::CT + j;
+        const bf16x8 f = tr_frag(buf, P::OUT_RS, kc * 32, ct * 16);
+        f32x4 gg = mfma16(f, f, f32x4{0.f, 0.f, 0.f, 0.f});
+        f32x4 sm = mfma16(ones, f, f32x4{0.f, 0.f, 0.f, 0.f});
+        const int si_ = lane_ & 3;
+        ps2[j] += si_ == 0 ? gg[0] : si_ == 1 ? gg[1] : si_ == 2 ? gg[2] : gg[3];
+        ps1[j] += si_ == 0 ? sm[0] : si_ == 1 ? sm[1] : si_ == 2 ? sm[2] : sm[3];
+      }
+    }
+    // copy-out of the wave's block: RT*16 rows x CT*16 channels, 16 B per item
+    unsigned key[kSlots] = {0u, 0u};
+    if (enc) {
+      key[0] = layer_sample_key(A, l, min(smp0, A.B - 1));
+      key[1] = layer_sample_key(A, l, min(smp0 + 1, A.B - 1));
+    }
+    constexpr int CPR = CV::CT * 2, NIT = CV::RT * 16 * CPR / 64;
+    static_assert(CV::RT * 16 * CPR % 64 == 0, "copy-out items per wave");
+    int li = lane_;
+    asm volatile("" : "+v"(li));
+#pragma unroll 2
+    for (int k = 0; k < NIT; ++k) {
+      const int i = li + 64 * k;
+      const int r = wm * CV::RT * 16 + i / CPR;
+      const int ch = (wn * CV::CT * 16) / 8 + i % CPR;
+      const int slot = r >> 6, tt = r & 63;
+      bf16x8 o = *reinterpret_cast<const bf16x8*>(buf + r * P::OUT_RS + ch * 16);
+      uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
+      if (!(tt < kL && smp0 + slot < A.B)) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ow[q] = kNegZero2;
+      } else if (enc) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ow[q] |= drop_signs2(dropout_bits2(key[slot], tt, ch * 8 + 2 * q), thr_out);
+      }
+      *reinterpret_cast<bf16x8*>(Ly.R + (long long)(row0 + kHalo + r) * COUT + ch * 8) = o;
+    }
+  };
+
+  // Each team runs its own copy of the loop (team 1 two barriers later), so a team's accumulators
+  // are dead during its staging phase and the staging keeps every row load in flight.  Both copies
+  // execute the same number of workgroup barriers (nseg).
+  auto team_loop = [&](auto team_c) {
+    constexpr int tm = decltype(team_c)::value;
+    int seg = 0;
+    for (; seg < 2 * tm; ++seg) __syncthreads();
+#pragma unroll 1
+    for (int i = 0; i < n_team; ++i, seg += 4) {
+      const int tile = t_begin + 2 * i + tm;
+      if constexpr (!(APNEAUQ_FWD_ABL & 16)) stage(tile);
+      __syncthreads();
+      f32x4 acc[CV::CT][CV::RT];
+#pragma unroll
+      for (int c = 0; c < CV::CT; ++c)
+#pragma unroll
+        for (int r = 0; r < CV::RT; ++r)
+          acc[c][r] = f32x4{0.f, 0.f, (APNEAUQ_FWD_ABL & 8) ? (float)buf[ht] : 0.f, 0.f};  // probe: opaque
+      if constexpr (!(APNEAUQ_FWD_ABL & 8)) CV::template steps<0, NS1>(Ly.wf, buf, P::IN_RS, acc);
+      __syncthreads();
+      if constexpr (!(APNEAUQ_FWD_ABL & 8)) CV::template steps<NS1, CV::NSTEP>(Ly.wf, buf, P::IN_RS, acc);
+      __syncthreads();
+      if constexpr (!(APNEAUQ_FWD_ABL & 32)) finish(tile, acc);
+      __syncthreads();
+    }
+#pragma unroll 1
+    for (; seg < nseg; ++seg) __syncthreads();
+  };
+  if (team == 0)
+    team_loop(std::integral_constant<int, 0>{});
+  else
+    team_loop(std::integral_constant<int, 1>{});
   flush();
 }
 
@@ -1169,7 +1555,7 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A)
       }
     } else {
 #ifndef APNEAUQ_WG_NOA  // probe: no A_{l-1} staging (wrong dW, timing only)
-      stage_act<l - 1, kRows, W::CIB / 8, 4, false, 0>(A, a_lds, ARS, row0, ci0, sp, tp, 0);
+      stage_act<l - 1, kRows, W::CIB / 8, 4, 0>(A, a_lds, ARS, row0, ci0, sp, tp, 0);
 #endif
     }
     __syncthreads();
@@ -1350,9 +1736,49 @@ hipError_t train_bump_counters(int* c, int n, hipStream_t st) {
   return hipGetLastError();
 }
 
+static int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+// APNEAUQ_FWD_PP=1: batches of at least kPPMinTilesPerCU 2-sample tiles per CU take the ping-pong
+// forward.  Opt-in: it measured 8 % SLOWER than the single-team kernel (profiles/batch_bn_fwd_r2.md:
+// the texture/L1 return path, loaded mostly by the per-tile weight fragments, is the limiter, and
+// overlapping staging with MFMA does not relieve it).  Kept, tested against the default path.
+constexpr int kPPMinTilesPerCU = 8;
+static bool pp_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("APNEAUQ_FWD_PP");
+    on = (e != nullptr && e[0] == '1') ? 1 : 0;
+  }
+  return on == 1;
+}
+
 hipError_t train_launch_fwd(const Args& A, int l, hipStream_t st) {
+  const int all_tiles = (A.B + 1) / 2;
+  const int ncu = cu_count();
+  if (l >= 1 && A.L[l - 1].aff != nullptr && all_tiles >= kPPMinTilesPerCU * ncu && pp_enabled()) {
+    hipLaunchKernelGGL(train::aff_kernel, dim3(A.groups), dim3(256), 0, st, A, l - 1);
+    const int grid = ncu;  // one two-team workgroup per CU, contiguous tile ranges
+    switch (l) {
+      case 1: hipLaunchKernelGGL(train::fwd_pp_kernel<1>, dim3(grid), dim3(512), train::PP<1>::LDS, st, A); break;
+      case 2: hipLaunchKernelGGL(train::fwd_pp_kernel<2>, dim3(grid), dim3(512), train::PP<2>::LDS, st, A); break;
+      case 3: hipLaunchKernelGGL(train::fwd_pp_kernel<3>, dim3(grid), dim3(512), train::PP<3>::LDS, st, A); break;
+      case 4: hipLaunchKernelGGL(train::fwd_pp_kernel<4>, dim3(grid), dim3(512), train::PP<4>::LDS, st, A); break;
+      case 5: hipLaunchKernelGGL(train::fwd_pp_kernel<5>, dim3(grid), dim3(512), train::PP<5>::LDS, st, A); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   // persistent forward: at most 4 workgroups per CU-slot pair, each over a contiguous tile range
-  const int tiles = std::min((A.B + 1) / 2, 256 * 8);
+  const int tiles = std::min(all_tiles, 256 * 8);
   switch (l) {
     case 0: hipLaunchKernelGGL(train::fwd_kernel<0>, dim3(tiles), dim3(256), lds_fwd(), st, A); break;
     case 1: hipLaunchKernelGGL(train::fwd_kernel<1>, dim3(tiles), dim3(256), lds_fwd(), st, A); break;

@@ -269,13 +269,9 @@ class GraphedGenericStep:
         self.bound = train_ops.bound_key(model)
         self._set_counters()
         self.ws.pack(backward=True)  # allocates the fragment buffers outside the capture (no model change)
-        self.graph = torch.cuda.CUDAGraph()
-        side = torch.cuda.Stream(device=dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):
-            with torch.cuda.graph(self.graph, stream=side):
-                self._body()
-        torch.cuda.current_stream(dev).wait_stream(side)
+        from .train_ops import capture_graph
+
+        self.graph = capture_graph(self._body, dev)
         self._iters_dev = int(model.optimizer.iterations)
 
     def _set_counters(self):

@@ -99,6 +99,13 @@ class TrainWorkspace:
         self.st_all = torch.zeros(sum(S * self.groups * 2 * ch[l + 1] for l in range(6)), dtype=torch.float64,
                                   device=dev)
         self.bst_all = torch.zeros(sum(S * 2 * ch[l + 1] for l in range(6)), device=dev)
+        # per-group BN affine of every layer, written by aff_kernel for the ping-pong forward
+        self.aff_all = torch.zeros(sum(self.groups * 2 * ch[l + 1] for l in range(6)), device=dev)
+        self.aff = []
+        o3 = 0
+        for l in range(6):
+            self.aff.append(self.aff_all[o3: o3 + self.groups * 2 * ch[l + 1]])
+            o3 += self.groups * 2 * ch[l + 1]
         self.st, self.bst = [], []
         o1 = o2 = 0
         for l in range(6):
@@ -150,7 +157,8 @@ class TrainWorkspace:
                      g[f"conv1d_{i}/kernel"].data_ptr(), g[f"conv1d_{i}/bias"].data_ptr(),
                      g[f"batchnorm_{i}/gamma"].data_ptr(), g[f"batchnorm_{i}/beta"].data_ptr(),
                      self.R[l].data_ptr(), self.dY[l].data_ptr(), self.st[l].data_ptr(), self.bst[l].data_ptr(),
-                     rng.dropout_threshold(p), _fbits(1.0 / (1.0 - p) if p < 1 else 0.0), self.dZ[l].data_ptr()]
+                     rng.dropout_threshold(p), _fbits(1.0 / (1.0 - p) if p < 1 else 0.0), self.dZ[l].data_ptr(),
+                     self.aff[l].data_ptr()]
         vals += [self.x.data_ptr(), self.y.data_ptr(), v["output_layer/kernel"].data_ptr(),
                  v["output_layer/bias"].data_ptr(), g["output_layer/kernel"].data_ptr(),
                  g["output_layer/bias"].data_ptr(), self.logits.data_ptr(), self.dlogit.data_ptr(),
@@ -231,6 +239,33 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, syn
     return ws.loss.double().sum(), torch.sigmoid(ws.logits[:n])
 
 
+def capture_graph(body, dev):
+    """Capture ``body()`` (HIP launches only) as a graph on a side stream.
+
+    Two hazards handled here: a garbage collection during the capture can destroy an OLD graph,
+    which HIP refuses while a stream is capturing (abort); and the first replay of a freshly
+    instantiated graph was seen reading stale step inputs about once in 40 captures unless the
+    device is synchronised after the capture (tools/probes/generic_step1_keys.py)."""
+    import gc
+
+    graph = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    was = gc.isenabled()
+    gc.collect()
+    gc.disable()
+    try:
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(graph, stream=side):
+                body()
+    finally:
+        if was:
+            gc.enable()
+    torch.cuda.current_stream(dev).wait_stream(side)
+    torch.cuda.synchronize(dev)
+    return graph
+
+
 def bound_key(model):
     """What a captured training graph bakes in: buffer identities and the optimizer's scalars
     (learning rate / betas / epsilon are kernel arguments of the captured Adam launch)."""
@@ -269,13 +304,9 @@ class GraphedTrainStep:
         # tensor objects (a restored optimizer state or a moved model triggers a re-capture)
         self.bound = bound_key(model)
         self._sync_counters()
-        self.graph = torch.cuda.CUDAGraph()
-        side = torch.cuda.Stream(device=dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):
-            with torch.cuda.graph(self.graph, stream=side):
-                self.loss_out, self.probs_out = self._body()
-        torch.cuda.current_stream(dev).wait_stream(side)
+        outs = []
+        self.graph = capture_graph(lambda: outs.extend(self._body()), dev)
+        self.loss_out, self.probs_out = outs
 
     def _state(self):
         return (int(self.model._train_step_counter), int(self.model.optimizer.iterations))
