@@ -53,20 +53,21 @@ hipError_t launch_gt_head(const void* h, const float* w, const float* b, const f
                           float* loss, float* gw, float* gb, int n, int L, int C, float inv_gb, hipStream_t st);
 int gt_pack_max_blocks();
 long long train_wgrad_part_floats(int B);
+int train_det_floats(int B);
 hipError_t launch_gt_pack(int nb, const float* const* w, void* const* fwd, void* const* dgr, const int* k,
                           const int* cin, const int* cout, hipStream_t st);
 namespace train {
 struct Layer {
   const void* wf; const void* wd; const float* bias; const float* gamma; const float* beta;
   float* mmean; float* mvar; float* gw; float* gb; float* ggamma; float* gbeta;
-  void* R; void* dY; void* dZ; double* st; float* bst; unsigned thr; float dsc; float* aff;
+  void* R; void* dY; void* dZ; double* st; double* bst; unsigned thr; float dsc; float* aff;
 };
 struct Args {
   Layer L[6];
   const void* x; const float* y; const float* dense_w; const float* dense_b; float* g_dense_w; float* g_dense_b;
   float* logits; float* dlogit; float* loss_sum;
   int B; int n_win; int groups; unsigned pass_base; unsigned window_offset; unsigned long long seed; int dropout;
-  float inv_count; float inv_batch; float eps; float momentum; const unsigned* pass_dev; int st_groups; float* wpart; int shared0;
+  float inv_count; float inv_batch; float eps; float momentum; const unsigned* pass_dev; int st_groups; float* wpart; float* det; int shared0;
 };
 }  // namespace train
 int train_args_size();
@@ -212,7 +213,7 @@ void bump_counters(at::Tensor& counters) {
 }
 
 // ctx: int64 CPU tensor of device pointers / scalars built once per workspace (ops/train_ops.py)
-constexpr int kCtxLayer = 19, kCtxLen = 6 * kCtxLayer + 24;
+constexpr int kCtxLayer = 19, kCtxLen = 6 * kCtxLayer + 25;
 
 float bits_to_float(int64_t v) {
   uint32_t u = static_cast<uint32_t>(v);
@@ -246,7 +247,7 @@ apneauq::train::Args args_from_ctx(const at::Tensor& ctx, int64_t pass_base) {
     L.R = reinterpret_cast<void*>(q[11]);
     L.dY = reinterpret_cast<void*>(q[12]);
     L.st = reinterpret_cast<double*>(q[13]);
-    L.bst = reinterpret_cast<float*>(q[14]);
+    L.bst = reinterpret_cast<double*>(q[14]);
     L.thr = static_cast<unsigned>(q[15]);
     L.dsc = bits_to_float(q[16]);
     L.dZ = reinterpret_cast<void*>(q[17]);
@@ -277,6 +278,7 @@ apneauq::train::Args args_from_ctx(const at::Tensor& ctx, int64_t pass_base) {
   A.st_groups = static_cast<int>(g[21]);
   A.shared0 = static_cast<int>(g[22]);
   A.wpart = reinterpret_cast<float*>(g[23]);
+  A.det = reinterpret_cast<float*>(g[24]);
   TORCH_CHECK(A.st_groups >= A.groups, "train ctx: moment buffers hold fewer groups than requested");
   return A;
 }
@@ -306,6 +308,7 @@ void train_call(const at::Tensor& ctx, int64_t op, int64_t layer, int64_t flag, 
 }
 
 int64_t train_wgrad_part_size(int64_t B) { return apneauq::train_wgrad_part_floats((int)B); }
+int64_t train_det_size(int64_t B) { return apneauq::train_det_floats((int)B); }
 
 void train_pack(const at::Tensor& w, int64_t k, int64_t cin, int64_t cout, at::Tensor& fwd, at::Tensor& dgr) {
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == k * cin * cout,
@@ -609,6 +612,7 @@ TORCH_LIBRARY(apneauq, m) {
   m.def("train_call(Tensor ctx, int op, int layer, int flag, int pass_base, int device) -> ()", &train_call);
   m.def("train_pack(Tensor w, int k, int cin, int cout, Tensor(a!) fwd, Tensor(b!) dgr) -> ()");
   m.def("train_wgrad_part_size(int B) -> int", &train_wgrad_part_size);
+  m.def("train_det_size(int B) -> int", &train_det_size);
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, float b1, float b2, float alpha, float eps, "
         "float gscale, Tensor? counters=None) -> ()");
   m.def("bump_counters(Tensor(a!) counters) -> ()");

@@ -61,7 +61,9 @@ struct Layer {
   __bf16* dY;          // PL (rows, C) gradient wrt BN output (blocks 1..5)
   __bf16* dZ;          // PL (rows, C) gradient wrt the conv pre-activation, written by dgrad_l (l >= 1)
   double* st;          // [slots][groups][2][C] forward moment sums (sum r, sum r^2), fp64
-  float* bst;          // [2][C] backward sums (sum dY, sum dY * xhat)
+  double* bst;         // [slots][2][C] backward sums (sum dY, sum dY * xhat), fp64: partial sums of
+                       // data-parallel ranks then add exactly (a 2-rank step computes the 1-rank
+                       // BN-backward coefficients bit for bit in deterministic mode)
   unsigned thr;        // dropout threshold (16-bit units) and 1/(1-p)
   float dsc;
   float* aff;          // [groups][2][C] BN affine (s = gamma * rstd, t = beta - mean * s) of the batch
@@ -93,6 +95,10 @@ struct Args {
   const unsigned* pass_dev;  // optional device step counter added to pass_base (HIP-graph replays)
   int st_groups;       // groups the moment buffers are allocated for (>= groups)
   float* wpart;        // wgrad partials [row group][K*Cin*Cout + Cout] (nullptr: fp32 atomics)
+  float* det;          // deterministic mode (training, one stats group): per-workgroup / per-sample
+                       // partial sums of the BN moments, head and dgrad statistics go here with
+                       // plain stores and det_reduce_kernel adds them in a fixed order (nullptr:
+                       // atomics, whose summation order varies run to run)
   int shared0;         // batch-BN MC Dropout: block 1 (no dropout before it) is computed once for the
                        // n_win windows (stats group 0, R_0 unencoded, indexed by window) and shared by
                        // every pass; block 2's staging applies block 1's dropout from the hash
@@ -166,6 +172,7 @@ __device__ __forceinline__ int row_time(int grow) { return (grow - kHalo) & 63; 
 #endif
 
 constexpr int kStatSlots = 16;
+constexpr int kHeadRec = 2 + 3 * 96;  // deterministic head record per sample: loss, dlogit, dW, sum dY, sum dY xhat
 // slot stride of the moment buffers: the ALLOCATED group count (a last MC-Dropout chunk may run fewer
 // groups while block 1's shared moments, written by the first chunk, keep their slots)
 __device__ __forceinline__ int st_stride(const Args& A, int Cc) { return A.st_groups * 2 * Cc; }
@@ -677,11 +684,11 @@ extern __shared__ __attribute__((aligned(16))) char smem[];
 
 // Reduce per-lane partial sums over the 16 rows of a lane group and add them to a global
 // per-channel accumulator (fp32 atomics; one per channel per wave row-group).
-__device__ __forceinline__ void atomic_channel_sums(float* dst, int co0, const f32x4& a, bool leader) {
+__device__ __forceinline__ void atomic_channel_sums(double* dst, int co0, const f32x4& a, bool leader) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const float v = group16_sum(a[i]);
-    if (leader) atomicAdd(dst + co0 + i, v);
+    if (leader) atomicAdd(dst + co0 + i, (double)v);
   }
 }
 
@@ -739,7 +746,7 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
 #pragma unroll
     for (int j = 0; j < CPW; ++j) ps1[j] = ps2[j] = 0.f;
     __syncthreads();
-    if (gcur >= 0) {
+    if (gcur >= 0 && A.det == nullptr) {
       for (int c = threadIdx.x; c < COUT; c += kThreads) {
         atomicAdd(st + (gcur * 2 + 0) * COUT + c, (double)lstat[c]);
         atomicAdd(st + (gcur * 2 + 1) * COUT + c, (double)lstat[COUT + c]);
@@ -897,6 +904,10 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
     copy_out();
   }
   flush();
+  if (A.det != nullptr) {  // deterministic mode (one stats group): this workgroup's moment partials
+    float* dp = A.det + (long long)blockIdx.x * 2 * COUT;
+    for (int c = threadIdx.x; c < 2 * COUT; c += kThreads) dp[c] = lstat[c];
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1297,11 +1308,17 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A, int backward) {
       const float pz = 1.0f / (1.0f + __expf(-z));
       const float yv = A.y[n];
       const float dl = (pz - yv) * A.inv_batch;
+      float* rec = A.det != nullptr ? A.det + (long long)n * kHeadRec : nullptr;  // deterministic mode
       if (lane == 0) {
         const float loss = fmaxf(z, 0.f) - z * yv + log1pf(__expf(-fabsf(z)));  // BCE on logits
-        atomicAdd(&red[0], loss);
         A.dlogit[n] = dl;
-        atomicAdd(&red[1], dl);
+        if (rec != nullptr) {
+          rec[0] = loss;
+          rec[1] = dl;
+        } else {
+          atomicAdd(&red[0], loss);
+          atomicAdd(&red[1], dl);
+        }
       }
       if (active) {
         float b0[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, b1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -1315,14 +1332,35 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A, int backward) {
             b1[j] += dy * xh;
           }
         }
+        if (rec != nullptr) {
+          // the sample's sums over its 5 row-phase lanes (lanes cw + 12 ph), in a fixed order
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          atomicAdd(&dw[c0 + j], dl * gap[j] * (1.0f / kL));
-          atomicAdd(&bsum0[c0 + j], b0[j]);
-          atomicAdd(&bsum1[c0 + j], b1[j]);
+          for (int j = 0; j < 8; ++j) {
+            float sdw = 0.f, sb0 = 0.f, sb1 = 0.f;
+            const float pdw = dl * gap[j] * (1.0f / kL);
+#pragma unroll
+            for (int q = 0; q < NPH; ++q) {
+              sdw += __shfl(pdw, cw + NCW * q, kWave);
+              sb0 += __shfl(b0[j], cw + NCW * q, kWave);
+              sb1 += __shfl(b1[j], cw + NCW * q, kWave);
+            }
+            if (ph == 0) {
+              rec[2 + c0 + j] = sdw;
+              rec[2 + Cc + c0 + j] = sb0;
+              rec[2 + 2 * Cc + c0 + j] = sb1;
+            }
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            atomicAdd(&dw[c0 + j], dl * gap[j] * (1.0f / kL));
+            atomicAdd(&bsum0[c0 + j], b0[j]);
+            atomicAdd(&bsum1[c0 + j], b1[j]);
+          }
         }
       }
     }
+    if (A.det != nullptr) return;  // det_reduce_kernel sums the per-sample records
     __syncthreads();
     for (int c = threadIdx.x; c < Cc; c += kThreads) {
       if (c == 0) {
@@ -1330,9 +1368,9 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A, int backward) {
         atomicAdd(A.g_dense_b, red[1]);
       }
       atomicAdd(A.g_dense_w + c, dw[c]);
-      float* bst = Ly.bst + (blockIdx.x % kStatSlots) * 2 * Cc;
-      atomicAdd(bst + c, bsum0[c]);
-      atomicAdd(bst + Cc + c, bsum1[c]);
+      double* bst = Ly.bst + (blockIdx.x % kStatSlots) * 2 * Cc;
+      atomicAdd(bst + c, (double)bsum0[c]);
+      atomicAdd(bst + Cc + c, (double)bsum1[c]);
     }
   }
 }
@@ -1367,8 +1405,8 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
     __syncthreads();
     for (int c = threadIdx.x; c < CIN; c += kThreads) {
       gr[c] = Ly.gamma[c] * rstd[c];
-      mdy[c] = slot_sum(Ly.bst + c, 2 * CIN) * A.inv_count;
-      mdyx[c] = slot_sum(Ly.bst + CIN + c, 2 * CIN) * A.inv_count;
+      mdy[c] = (float)(slot_sumd(Ly.bst + c, 2 * CIN) * (double)A.inv_count);
+      mdyx[c] = (float)(slot_sumd(Ly.bst + CIN + c, 2 * CIN) * (double)A.inv_count);
     }
     bn_stats_to_lds(A, l - 1, 0, mean_prev, rstd_prev);
   }
@@ -1421,9 +1459,21 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
         }
       }
     }
-    float* bst = Lp.bst + (blockIdx.x % kStatSlots) * 2 * COUT;
-    atomic_channel_sums(bst, co0, b0, m == 0);
-    atomic_channel_sums(bst + COUT, co0, b1, m == 0);
+    if (A.det != nullptr) {  // deterministic mode: this wave's row-block partial, reduced in order later
+      float* dp = A.det + (long long)(tile * T::WM + wm) * 2 * COUT;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float s0 = group16_sum(b0[i]), s1 = group16_sum(b1[i]);
+        if (m == 0) {
+          dp[co0 + i] = s0;
+          dp[COUT + co0 + i] = s1;
+        }
+      }
+    } else {
+      double* bst = Lp.bst + (blockIdx.x % kStatSlots) * 2 * COUT;
+      atomic_channel_sums(bst, co0, b0, m == 0);
+      atomic_channel_sums(bst + COUT, co0, b1, m == 0);
+    }
   }
   __syncthreads();
   constexpr int CW = COUT / 8;
@@ -1501,8 +1551,8 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A)
     __syncthreads();
     for (int c = threadIdx.x; c < COUT; c += kThreads) {
       gr[c] = Ly.gamma[c] * rstd[c];
-      mdy[c] = slot_sum(Ly.bst + c, 2 * COUT) * A.inv_count;
-      mdyx[c] = slot_sum(Ly.bst + COUT + c, 2 * COUT) * A.inv_count;
+      mdy[c] = (float)(slot_sumd(Ly.bst + c, 2 * COUT) * (double)A.inv_count);
+      mdyx[c] = (float)(slot_sumd(Ly.bst + COUT + c, 2 * COUT) * (double)A.inv_count);
     }
     if constexpr (!FIRST) bn_affine_to_lds(A, l - 1, 0, sp, tp, nullptr, nullptr);
   }
@@ -1659,6 +1709,43 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 // ------------------------------------------------------------------------------------------------
 // BN finalize: moving averages (Keras momentum update on batch moments) and dgamma / dbeta.
 // ------------------------------------------------------------------------------------------------
+// Deterministic mode: column sums of an (n, w) row-major fp32 partial table in a fixed order (fp64
+// accumulation), scattered to up to four destination segments (consecutive column ranges; fp64 or
+// fp32 stores).  One thread per column; the rows are read coalesced across threads.
+struct DetSeg {
+  void* ptr;
+  int cols;
+  int f64;
+};
+struct DetDst {
+  DetSeg seg[4];
+};
+
+__global__ __launch_bounds__(256) void det_reduce_kernel(const float* __restrict__ part, int n, int w, DetDst d) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= w) return;
+  double acc = 0.0;
+  int i = 0;
+  for (; i + 4 <= n; i += 4) {  // fixed association: ((r0 + r1) + (r2 + r3)) per group of four rows
+    const double a = (double)part[(long long)i * w + c] + (double)part[(long long)(i + 1) * w + c];
+    const double b = (double)part[(long long)(i + 2) * w + c] + (double)part[(long long)(i + 3) * w + c];
+    acc += a + b;
+  }
+  for (; i < n; ++i) acc += (double)part[(long long)i * w + c];
+  int k = c;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (k < d.seg[q].cols) {
+      if (d.seg[q].f64)
+        reinterpret_cast<double*>(d.seg[q].ptr)[k] = acc;
+      else
+        reinterpret_cast<float*>(d.seg[q].ptr)[k] = (float)acc;
+      return;
+    }
+    k -= d.seg[q].cols;
+  }
+}
+
 __global__ void bn_finalize_kernel(Args A, int update_moving, int grads) {
   const int l = blockIdx.x;
   const Layer& Ly = A.L[l];
@@ -1673,8 +1760,8 @@ __global__ void bn_finalize_kernel(Args A, int update_moving, int grads) {
       }
     }
     if (grads) {
-      Ly.gbeta[c] = slot_sum(Ly.bst + c, 2 * Cc);
-      Ly.ggamma[c] = slot_sum(Ly.bst + Cc + c, 2 * Cc);
+      Ly.gbeta[c] = (float)slot_sumd(Ly.bst + c, 2 * Cc);
+      Ly.ggamma[c] = (float)slot_sumd(Ly.bst + Cc + c, 2 * Cc);
     }
   }
 }
@@ -1761,9 +1848,48 @@ static bool pp_enabled() {
   return on == 1;
 }
 
+static hipError_t det_reduce(const float* part, int n, int w, train::DetDst d, hipStream_t st) {
+  hipLaunchKernelGGL(train::det_reduce_kernel, dim3((w + 255) / 256), dim3(256), 0, st, part, n, w, d);
+  return hipGetLastError();
+}
+
+static train::DetDst det_dst(void* p0, int c0, int f0, void* p1 = nullptr, int c1 = 0, void* p2 = nullptr, int c2 = 0,
+                             void* p3 = nullptr, int c3 = 0, int f3 = 0) {
+  train::DetDst d;
+  d.seg[0] = {p0, c0, f0};
+  d.seg[1] = {p1, c1, 0};
+  d.seg[2] = {p2, c2, 0};
+  d.seg[3] = {p3, c3, f3};
+  return d;
+}
+
+// floats of the deterministic-mode partial table for a batch of B samples (fwd / head / dgrad reuse it)
+static int fwd_grid(int B) { return std::min((B + 1) / 2, 256 * 8); }
+int train_det_floats(int B) {
+  const int tiles = (B + 1) / 2;
+  return std::max({fwd_grid(B) * 2 * 256, B * train::kHeadRec, tiles * 2 * 2 * 256});
+}
+
 hipError_t train_launch_fwd(const Args& A, int l, hipStream_t st) {
   const int all_tiles = (A.B + 1) / 2;
   const int ncu = cu_count();
+  if (A.det != nullptr) {  // deterministic training: single-team kernel, ordered moment reduction
+    if (A.groups != 1 || A.shared0) return hipErrorInvalidValue;
+    const int grid = fwd_grid(A.B);
+    switch (l) {
+      case 0: hipLaunchKernelGGL(train::fwd_kernel<0>, dim3(grid), dim3(256), lds_fwd(), st, A); break;
+      case 1: hipLaunchKernelGGL(train::fwd_kernel<1>, dim3(grid), dim3(256), lds_fwd(), st, A); break;
+      case 2: hipLaunchKernelGGL(train::fwd_kernel<2>, dim3(grid), dim3(256), lds_fwd(), st, A); break;
+      case 3: hipLaunchKernelGGL(train::fwd_kernel<3>, dim3(grid), dim3(256), lds_fwd(), st, A); break;
+      case 4: hipLaunchKernelGGL(train::fwd_kernel<4>, dim3(grid), dim3(256), lds_fwd(), st, A); break;
+      case 5: hipLaunchKernelGGL(train::fwd_kernel<5>, dim3(grid), dim3(256), lds_fwd(), st, A); break;
+      default: return hipErrorInvalidValue;
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int cc = train::C[l + 1];
+    return det_reduce(A.det, grid, 2 * cc, det_dst(A.L[l].st, 2 * cc, 1), st);
+  }
   if (l >= 1 && A.L[l - 1].aff != nullptr && all_tiles >= kPPMinTilesPerCU * ncu && pp_enabled()) {
     hipLaunchKernelGGL(train::aff_kernel, dim3(A.groups), dim3(256), 0, st, A, l - 1);
     const int grid = ncu;  // one two-team workgroup per CU, contiguous tile ranges
@@ -1778,7 +1904,7 @@ hipError_t train_launch_fwd(const Args& A, int l, hipStream_t st) {
     return hipGetLastError();
   }
   // persistent forward: at most 4 workgroups per CU-slot pair, each over a contiguous tile range
-  const int tiles = std::min(all_tiles, 256 * 8);
+  const int tiles = fwd_grid(A.B);
   switch (l) {
     case 0: hipLaunchKernelGGL(train::fwd_kernel<0>, dim3(tiles), dim3(256), lds_fwd(), st, A); break;
     case 1: hipLaunchKernelGGL(train::fwd_kernel<1>, dim3(tiles), dim3(256), lds_fwd(), st, A); break;
@@ -1793,7 +1919,11 @@ hipError_t train_launch_fwd(const Args& A, int l, hipStream_t st) {
 
 hipError_t train_launch_head(const Args& A, int backward, hipStream_t st) {
   hipLaunchKernelGGL(train::head_kernel, dim3((A.B + 3) / 4), dim3(256), (8 * train::C[6] + 2) * 4, st, A, backward);
-  return hipGetLastError();
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !backward || A.det == nullptr) return e;
+  constexpr int cc = train::C[6];  // per-sample records: loss, dlogit, dW, sum dY, sum dY xhat
+  return det_reduce(A.det, A.B, train::kHeadRec,
+                    det_dst(A.loss_sum, 1, 0, A.g_dense_b, 1, A.g_dense_w, cc, A.L[5].bst, 2 * cc, 1), st);
 }
 
 hipError_t train_launch_dgrad(const Args& A, int l, hipStream_t st) {
@@ -1806,7 +1936,13 @@ hipError_t train_launch_dgrad(const Args& A, int l, hipStream_t st) {
     case 5: hipLaunchKernelGGL(train::dgrad_kernel<5>, dim3(tiles), dim3(256), lds_dgrad(), st, A); break;
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess || A.det == nullptr) return e;
+  static constexpr int wm[6] = {0, train::Tiling<train::C[1]>::WM, train::Tiling<train::C[2]>::WM,
+                                train::Tiling<train::C[3]>::WM, train::Tiling<train::C[4]>::WM,
+                                train::Tiling<train::C[5]>::WM};
+  const int cc = train::C[l];  // block l's backward sums (of BN l-1's output) per (tile, wave row block)
+  return det_reduce(A.det, tiles * wm[l], 2 * cc, det_dst(A.L[l - 1].bst, 2 * cc, 1), st);
 }
 
 template <int l>

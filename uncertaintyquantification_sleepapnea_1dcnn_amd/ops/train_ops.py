@@ -19,6 +19,7 @@ batch statistics over the whole test set (the reference's ``model(x, training=Tr
 """
 from __future__ import annotations
 
+import os
 import struct
 from typing import Callable, List, Optional
 
@@ -66,7 +67,7 @@ class TrainWorkspace:
     """Device buffers + pointer context for one model and one (max) batch size."""
 
     def __init__(self, model, batch: int, groups: int = 1, n_win: Optional[int] = None, with_backward: bool = True,
-                 shared0: bool = False):
+                 shared0: bool = False, deterministic: bool = False):
         spec = model.spec
         store = model.store
         dev = store.device
@@ -94,11 +95,11 @@ class TrainWorkspace:
         self.dZ = [torch.zeros(rows, ch[l + 1], dtype=bf, device=dev) if (with_backward and l >= 1)
                    else torch.zeros(16, dtype=bf, device=dev) for l in range(6)]
         # BN moment sums: STAT_SLOTS interleaved copies per layer (kernels add into slot wg % S and
-        # readers sum the slots; train_conv.hip kStatSlots) -> st[S][groups][2][C] (fp64), bst[S][2][C]
+        # readers sum the slots; train_conv.hip kStatSlots) -> st[S][groups][2][C], bst[S][2][C] (fp64)
         S = STAT_SLOTS
         self.st_all = torch.zeros(sum(S * self.groups * 2 * ch[l + 1] for l in range(6)), dtype=torch.float64,
                                   device=dev)
-        self.bst_all = torch.zeros(sum(S * 2 * ch[l + 1] for l in range(6)), device=dev)
+        self.bst_all = torch.zeros(sum(S * 2 * ch[l + 1] for l in range(6)), dtype=torch.float64, device=dev)
         # per-group BN affine of every layer, written by aff_kernel for the ping-pong forward
         self.aff_all = torch.zeros(sum(self.groups * 2 * ch[l + 1] for l in range(6)), device=dev)
         self.aff = []
@@ -124,6 +125,10 @@ class TrainWorkspace:
         # cheaper than fp32 atomics); shared by the six sequential wgrad launches
         self.wpart = (torch.empty(int(_ext.ops().train_wgrad_part_size(self.B)), device=dev)
                       if with_backward else None)
+        # deterministic mode: per-workgroup / per-sample partials of the BN moments, head and dgrad
+        # sums, added in a fixed order by det_reduce_kernel instead of atomics (training only)
+        self.deterministic = bool(deterministic) and with_backward and self.groups == 1 and not self.shared0
+        self.det = (torch.empty(int(_ext.ops().train_det_size(self.B)), device=dev) if self.deterministic else None)
         self.y = torch.zeros(self.B, device=dev)
         self.logits = torch.zeros(self.B, device=dev)
         self.dlogit = torch.zeros(self.B, device=dev)
@@ -166,7 +171,8 @@ class TrainWorkspace:
                  int(seed) & ((1 << 63) - 1), int(bool(dropout)), _fbits(inv_count), _fbits(inv_batch),
                  _fbits(spec.bn_epsilon), _fbits(spec.bn_momentum),
                  self.counters.data_ptr() if device_counters else 0, self.groups, int(self.shared0),
-                 self.wpart.data_ptr() if self.wpart is not None else 0]
+                 self.wpart.data_ptr() if self.wpart is not None else 0,
+                 self.det.data_ptr() if self.det is not None else 0]
         self.ctx = torch.tensor(vals, dtype=torch.int64)
         self._ctx_key = key
         return self.ctx
@@ -182,10 +188,21 @@ def _call(ctx, op, layer=0, flag=0, pass_base=-1, device=0):
     _ext.ops().train_call(ctx, op, layer, flag, pass_base, device)
 
 
+# Deterministic training: every reduction of the HIP training step in a fixed order, so
+# two runs give bitwise-identical weights.  APNEAUQ_DETERMINISTIC=1 or set_deterministic(True);
+# costs a few small reduce launches per step.
+DETERMINISTIC = os.environ.get("APNEAUQ_DETERMINISTIC", "0") not in ("", "0")
+
+
+def set_deterministic(flag: bool = True) -> None:
+    global DETERMINISTIC
+    DETERMINISTIC = bool(flag)
+
+
 def _get_ws(model, batch: int) -> TrainWorkspace:
     ws = getattr(model, "_train_ws", None)
-    if ws is None or ws.B < batch or ws.groups != 1:
-        ws = TrainWorkspace(model, batch)
+    if ws is None or ws.B < batch or ws.groups != 1 or ws.deterministic != DETERMINISTIC:
+        ws = TrainWorkspace(model, batch, deterministic=DETERMINISTIC)
         model._train_ws = ws
     return ws
 
@@ -235,7 +252,8 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, syn
     scale = 1.0
     if grad_allreduce is not None:
         scale = grad_allreduce(ws.grad)
-    model.optimizer.step(model.store.flat, ws.grad, grad_scale=scale)
+    # device-side bias correction, as the captured step computes it (eager == graph bitwise)
+    model.optimizer.step(model.store.flat, ws.grad, grad_scale=scale, counters=ws.counters)
     return ws.loss.double().sum(), torch.sigmoid(ws.logits[:n])
 
 
@@ -294,7 +312,8 @@ class GraphedTrainStep:
         self.model = model
         self.batch = int(batch)
         dev = model.store.device
-        self.ws = TrainWorkspace(model, self.batch)
+        self.ws = TrainWorkspace(model, self.batch, deterministic=DETERMINISTIC)
+        self.deterministic = DETERMINISTIC
         self.x_in = torch.zeros(self.batch, 60, self.ws.ch[0], device=dev)
         self.y_in = torch.zeros(self.batch, device=dev)
         n = self.batch
@@ -360,7 +379,7 @@ def graph_train_step(model, x: torch.Tensor, y: torch.Tensor):
     n = int(x.shape[0])
     opt = model.optimizer
     cur = g.get(n)
-    if cur is None or not _same_bound(cur.bound, bound_key(model)):
+    if cur is None or not _same_bound(cur.bound, bound_key(model)) or cur.deterministic != DETERMINISTIC:
         g[n] = cur = GraphedTrainStep(model, n)
     return cur(x, y)
 

@@ -40,12 +40,20 @@ class Adam:
         return self.learning_rate * math.sqrt(1.0 - self.beta_2 ** t) / (1.0 - self.beta_1 ** t)
 
     @torch.no_grad()
-    def step(self, flat: torch.Tensor, grad: torch.Tensor, grad_scale: float = 1.0) -> None:
+    def step(self, flat: torch.Tensor, grad: torch.Tensor, grad_scale: float = 1.0, counters=None) -> None:
+        """``counters`` (int32 GPU tensor [.., iterations]): the bias correction is computed on the
+        device from the iteration counter -- the arithmetic of a captured (HIP-graph) step, so eager
+        and graphed steps give bitwise-identical weights."""
         self._ensure(flat)
         a = self.alpha()
         if flat.is_cuda and _ext.available():
-            _ext.ops().adam_step(flat, grad.contiguous(), self.m, self.v, self.beta_1, self.beta_2, a, self.epsilon,
-                                 float(grad_scale))
+            if counters is not None:
+                counters[1].fill_(self.iterations)
+                _ext.ops().adam_step(flat, grad.contiguous(), self.m, self.v, self.beta_1, self.beta_2,
+                                     self.learning_rate, self.epsilon, float(grad_scale), counters)
+            else:
+                _ext.ops().adam_step(flat, grad.contiguous(), self.m, self.v, self.beta_1, self.beta_2, a,
+                                     self.epsilon, float(grad_scale))
         else:
             g = grad * grad_scale if grad_scale != 1.0 else grad
             self.m.add_((g - self.m) * (1 - self.beta_1))

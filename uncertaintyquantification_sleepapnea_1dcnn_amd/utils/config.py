@@ -46,6 +46,8 @@ class RunConfig:
     input_channels: int = 4
     pool: bool = False              # opt-in MaxPool1D per block
     dtype: str = "bf16"             # compute dtype of the HIP kernels (fp32 accumulation)
+    deterministic: bool = False     # fixed-order reductions in the HIP training step (bitwise-reproducible
+                                    # weights; ops/train_ops.set_deterministic, env APNEAUQ_DETERMINISTIC)
     # ---- distribution
     world_size: int = 1
     backend: str = "auto"           # "nccl" (RCCL) on GPUs, "gloo" on CPU
