@@ -71,6 +71,10 @@ struct Args {
 };
 }  // namespace train
 int train_args_size();
+int train_read_stamps(void* dst, long long bytes);
+hipError_t launch_standardize(const double* x, double* out, long long n_win, int L, int C, double eps, hipStream_t stream);
+hipError_t launch_knn(const double* X, int n, int D, long long* out, int k, hipStream_t stream);
+int knn_lds_bytes(int D, int K);
 int train_layer_size();
 hipError_t train_launch_fwd(const train::Args& A, int l, hipStream_t st);
 hipError_t train_launch_head(const train::Args& A, int backward, hipStream_t st);
@@ -309,6 +313,11 @@ void train_call(const at::Tensor& ctx, int64_t op, int64_t layer, int64_t flag, 
 
 int64_t train_wgrad_part_size(int64_t B) { return apneauq::train_wgrad_part_floats((int)B); }
 int64_t train_det_size(int64_t B) { return apneauq::train_det_floats((int)B); }
+// probe builds only: forward phase stamps into a CPU uint8 tensor (returns -1 in the library build)
+int64_t train_stamps(const at::Tensor& out) {
+  TORCH_CHECK(out.device().is_cpu() && out.scalar_type() == at::kByte && out.is_contiguous(), "train_stamps: CPU uint8");
+  return apneauq::train_read_stamps(out.data_ptr(), out.numel());
+}
 
 void train_pack(const at::Tensor& w, int64_t k, int64_t cin, int64_t cout, at::Tensor& fwd, at::Tensor& dgr) {
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == k * cin * cout,
@@ -588,6 +597,33 @@ void metrics_update(const at::Tensor& p, const at::Tensor& y, const at::Tensor& 
         "metrics_update");
 }
 
+// K14 (csrc/prep.hip): per-window z-score of an (N, L, C) float64 tensor; exact fp64 k-NN of SMOTE
+at::Tensor prep_standardize(const at::Tensor& x, double eps) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kDouble && x.dim() == 3, "prep_standardize: (N, L, C) float64 GPU tensor");
+  auto xc = x.contiguous();
+  TORCH_CHECK(xc.size(1) * xc.size(2) * 8 <= 64 * 1024 && xc.size(2) <= 256, "prep_standardize: window too large");
+  const at::DeviceGuard guard(xc.device());
+  auto out = at::empty_like(xc);
+  check(apneauq::launch_standardize(xc.data_ptr<double>(), out.data_ptr<double>(), xc.size(0), (int)xc.size(1),
+                                    (int)xc.size(2), eps, cur_stream()),
+        "prep_standardize");
+  return out;
+}
+
+at::Tensor prep_knn(const at::Tensor& X, int64_t k) {
+  TORCH_CHECK(X.is_cuda() && X.scalar_type() == at::kDouble && X.dim() == 2, "prep_knn: (n, D) float64 GPU tensor");
+  TORCH_CHECK(k >= 1 && k <= 16, "prep_knn: 1 <= k <= 16");
+  TORCH_CHECK(X.size(0) < (int64_t(1) << 31), "prep_knn: too many rows");
+  auto xc = X.contiguous();
+  TORCH_CHECK(apneauq::knn_lds_bytes((int)xc.size(1), k <= 8 ? 8 : 16) <= 160 * 1024, "prep_knn: rows too wide for LDS");
+  const at::DeviceGuard guard(xc.device());
+  auto out = at::empty({xc.size(0), k}, xc.options().dtype(at::kLong));
+  check(apneauq::launch_knn(xc.data_ptr<double>(), (int)xc.size(0), (int)xc.size(1),
+                            reinterpret_cast<long long*>(out.data_ptr<int64_t>()), (int)k, cur_stream()),
+        "prep_knn");
+  return out;
+}
+
 std::vector<int64_t> fused_layout() {
   int w[6], e[6], d;
   apneauq::fused_layout(w, e, &d);
@@ -613,6 +649,9 @@ TORCH_LIBRARY(apneauq, m) {
   m.def("train_pack(Tensor w, int k, int cin, int cout, Tensor(a!) fwd, Tensor(b!) dgr) -> ()");
   m.def("train_wgrad_part_size(int B) -> int", &train_wgrad_part_size);
   m.def("train_det_size(int B) -> int", &train_det_size);
+  m.def("train_stamps(Tensor out) -> int", &train_stamps);
+  m.def("prep_standardize(Tensor x, float eps) -> Tensor");
+  m.def("prep_knn(Tensor X, int k) -> Tensor");
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, float b1, float b2, float alpha, float eps, "
         "float gscale, Tensor? counters=None) -> ()");
   m.def("bump_counters(Tensor(a!) counters) -> ()");
@@ -655,4 +694,6 @@ TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
   m.impl("gt_wgrad", &gt_wgrad);
   m.impl("gt_head", &gt_head);
   m.impl("gt_pack", &gt_pack);
+  m.impl("prep_standardize", &prep_standardize);
+  m.impl("prep_knn", &prep_knn);
 }

@@ -147,7 +147,9 @@ __device__ __forceinline__ int row_time(int grow) { return (grow - kHalo) & 63; 
 // readers add the slots.  Layout per layer: st[slot][group][2][C], bst[slot][2][C].
 // Probe hooks for timing the forward kernel's phases (always 0 in the library build; nonzero
 // values compute garbage): 4 = no copy-out, 8 = no conv MFMAs, 16 = no input staging, 32 = no epilogue
-// moments.
+// moments, 64 = no dropout hashing (copy-out / hash-in staging), 128 = every weight-fragment load reads
+// k-step 0 (L1-resident: the conv without its L2 weight stream), 256 = staging reads an L2-resident
+// 16-tile window instead of its own rows (decode kept), 512 = one workgroup per CU (LDS request doubled).
 #ifndef APNEAUQ_FWD_ABL
 #define APNEAUQ_FWD_ABL 0
 #endif
@@ -169,6 +171,22 @@ __device__ __forceinline__ int row_time(int grow) { return (grow - kHalo) & 63; 
 // 16 = stage_dz without its global loads
 #ifndef APNEAUQ_DG_ABL
 #define APNEAUQ_DG_ABL 0
+#endif
+
+// Phase stamps of the forward kernel (probe builds with -DAPNEAUQ_FWD_STAMPS only): s_memtime at the
+// phase boundaries of the first kFstT tiles of the first kFstWG workgroups (wave 0, lane 0), plus
+// the workgroup's XCC and CU ids; read back with train_read_stamps (tools/probes/fwd_stamps.py).
+constexpr int kFstWG = 1024, kFstT = 16, kFstN = 6;
+#ifdef APNEAUQ_FWD_STAMPS
+__device__ unsigned long long g_fst[kFstWG][kFstT][kFstN];
+__device__ unsigned g_fst_cu[kFstWG][2];
+#define APNEAUQ_FST(i, k)                                                                      \
+  do {                                                                                         \
+    if (l == APNEAUQ_FWD_STAMPS && blockIdx.x < kFstWG && (k) < kFstT && threadIdx.x == 0)    \
+      g_fst[blockIdx.x][(k)][(i)] = __builtin_amdgcn_s_memtime();                              \
+  } while (0)
+#else
+#define APNEAUQ_FST(i, k) ((void)0)
 #endif
 
 constexpr int kStatSlots = 16;
@@ -278,6 +296,18 @@ __device__ __forceinline__ bf16x8 zero8() {
   return o;
 }
 
+// 8 consecutive per-channel floats of an LDS table (c0 a multiple of 8) times a scale: two 16-B LDS
+// reads issued together (element-wise reads were 8 dependent round trips per table per tile)
+__device__ __forceinline__ void lds_row8(const float* tab, int c0, float scale, float (&o)[8]) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(tab + c0);
+  const f32x4 b = *reinterpret_cast<const f32x4*>(tab + c0 + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o[j] = a[j] * scale;
+    o[4 + j] = b[j] * scale;
+  }
+}
+
 // Stage A_l (= dropout(BN(R_l))) rows [row0, row0 + NR) x channels [c0, c0 + NCW*8) of global
 // PL buffer into LDS (row stride ldsrs bytes).  Pad rows and rows outside the batch become 0.
 // row0 is a tile start (a multiple of 128), so the rows hold samples smp0 = row0/64 and smp0 + 1
@@ -309,12 +339,17 @@ __device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, i
   const bool drop = A.dropout != 0;
   const float dsc = drop ? Ly.dsc : 1.f;
   float s0[8], t0[8], s1[8], t1[8];
+  lds_row8(s, c, dsc, s0);
+  lds_row8(t, c, dsc, t0);
+  if (two) {  // workgroup-uniform; the tables of callers with one stats group end at s + 256
+    lds_row8(s, 256 + c, dsc, s1);
+    lds_row8(t, 256 + c, dsc, t1);
+  } else {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    s0[j] = s[c + j] * dsc;
-    t0[j] = t[c + j] * dsc;
-    s1[j] = two ? s[256 + c + j] * dsc : s0[j];
-    t1[j] = two ? t[256 + c + j] * dsc : t0[j];
+    for (int j = 0; j < 8; ++j) {
+      s1[j] = s0[j];
+      t1[j] = t0[j];
+    }
   }
   {
     // Every staged row exists in the padded buffer, and pad rows / rows past the batch / the
@@ -405,7 +440,7 @@ struct ActStager {
 #pragma unroll
       for (int u = 0; u < NK; ++u) {
         const int r = rin + u * RP;
-        if (r < kRows) v[u] = gld<u32x4>(R + (long long)(row0 + r) * Cc);
+        if (r < kRows) v[u] = gld<u32x4>(R + (long long)(((APNEAUQ_FWD_ABL & 256) ? (row0 & 2047) : row0) + r) * Cc);
       }
     }
   }
@@ -423,13 +458,10 @@ struct ActStager {
     const bool drop = A.dropout != 0;
     const float dsc = drop ? Ly.dsc : 1.f;
     float s0[8], t0[8], s1[8], t1[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      s0[j] = s[c + j] * dsc;
-      t0[j] = t[c + j] * dsc;
-      s1[j] = two ? s[256 + c + j] * dsc : s0[j];
-      t1[j] = two ? t[256 + c + j] * dsc : t0[j];
-    }
+    lds_row8(s, c, dsc, s0);
+    lds_row8(t, c, dsc, t0);
+    lds_row8(s, 256 + c, dsc, s1);  // second group (used only when two): unconditional, read together
+    lds_row8(t, 256 + c, dsc, t1);
     unsigned key0 = 0u, key1 = 0u;
     if (HASH_IN && hash_in) {
       key0 = layer_sample_key(A, l, min(smp0, A.B - 1));
@@ -463,7 +495,7 @@ struct ActStager {
       else
         run(std::false_type{}, hashed);
     };
-    if (HASH_IN && hash_in)
+    if (HASH_IN && hash_in && !(APNEAUQ_FWD_ABL & 64))
       dispatch(std::integral_constant<bool, HASH_IN>{});
     else
       dispatch(std::false_type{});
@@ -583,20 +615,21 @@ struct Conv {
   static constexpr int PAD = (K - 1) / 2;
   static_assert(NCT % WN == 0 && kRT % WM == 0 && WM * WN == 4, "wave tiling");
 
+  template <int PD = 1>
   __device__ __forceinline__ static void run(const gbf16x8* wfrag, const char* lds, int ldsrs, f32x4 (&acc)[CT][RT]) {
 #pragma unroll
     for (int c = 0; c < CT; ++c)
 #pragma unroll
       for (int r = 0; r < RT; ++r) acc[c][r] = f32x4{0.f, 0.f, 0.f, 0.f};
-    steps<0, NSTEP>(wfrag, lds, ldsrs, acc);
+    steps<0, NSTEP, PD>(wfrag, lds, ldsrs, acc);
   }
 
-  // steps [S0, S1) accumulated into acc (S1 - S0 even unless S1 == NSTEP); the wave's place in its
-  // 4-wave team is (threadIdx.x >> 6) & 3, so 512-thread kernels run two teams
-  template <int S0, int S1>
+  // steps [S0, S1) accumulated into acc; the wave's place in its 4-wave team is (threadIdx.x >> 6) & 3,
+  // so 512-thread kernels run two teams.  PD = weight-fragment prefetch depth (k-steps in flight).
+  template <int S0, int S1, int PD = 1>
   __device__ __forceinline__ static void steps(const gbf16x8* wfrag, const char* lds, int ldsrs,
                                                f32x4 (&acc)[CT][RT]) {
-    static_assert(S0 % 2 == 0 && (S1 == NSTEP || (S1 - S0) % 2 == 0) && S0 < S1, "step range");
+    static_assert(S0 < S1 && PD >= 1, "step range");
     const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3;
     const int wm = wave / WN, wn = wave % WN;
     const int m = lane & 15, h = lane >> 4;
@@ -619,29 +652,52 @@ struct Conv {
     };
     auto load_a = [&](int s, bf16x8 (&a)[CT]) {
 #pragma unroll
-      for (int c = 0; c < CT; ++c) a[c] = wp[(s * NCT + c) * 64];
+      for (int c = 0; c < CT; ++c) a[c] = wp[((APNEAUQ_FWD_ABL & 128) ? 0 : s * NCT + c) * 64];
     };
-    auto step = [&](int s, const bf16x8 (&a)[CT]) {
+    // Weight fragments (A, from L2) run through a ring of PD + 1 stages: step s + PD's loads are issued
+    // before step s's MFMAs (the fused kernel's scheme; see FwdPD for the measured depths).
+    // B fragments (activations, LDS) run through a ring of NB registers over the (step, row tile)
+    // sequence: the read of fragment i + NB is issued right after the CT MFMAs of fragment i, so
+    // NB - 1 LDS reads stay in flight.
+    constexpr int NSA = PD + 1;
+    constexpr int NB = RT < 4 ? RT : 4;
+    static_assert(RT % NB == 0, "B ring phase restarts at every step");
+    constexpr int DSN = FIRST ? 2 : 1;  // LDS reads per B fragment
+    bf16x8 bq[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) bq[i] = load_b(S0, i);
+    // step s at position j of its group (group base sb = s - j); tail: no refills past S1
+    auto step = [&](int s, const bf16x8 (&a)[CT], int j, bool tail) {
 #pragma unroll
       for (int r = 0; r < RT; ++r) {
-        const bf16x8 b = load_b(s, r);
+        const int i = j * RT + r;
+        const bf16x8 b = bq[i % NB];
 #pragma unroll
         for (int c = 0; c < CT; ++c) acc[c][r] = mfma16(a[c], b, acc[c][r]);
+        const int nx = i + NB;               // ring successor within the group
+        const int sn = s - j + nx / RT;       // its step
+        if (!tail || sn < S1) bq[i % NB] = load_b(sn < S1 ? sn : S1 - 1, nx % RT);  // clamped: unconditional
+        __builtin_amdgcn_sched_group_barrier(0x008, CT, 0);   // the fragment's MFMAs ...
+        __builtin_amdgcn_sched_group_barrier(0x100, DSN, 0);  // ... then its successor's read
       }
     };
     // unconditional (clamped) prefetch keeps hipcc's vmcnt accounting exact (see fused_forward.hip)
-    bf16x8 a0[CT], a1[CT];
-    load_a(S0, a0);
+    bf16x8 a[NSA][CT];
+#pragma unroll
+    for (int j = 0; j < PD; ++j) load_a(S0 + j < S1 ? S0 + j : S1 - 1, a[j]);
+    constexpr int NFULL = (S1 - S0) / NSA * NSA;
 #pragma unroll 1
-    for (int s = S0; s + 1 < S1; s += 2) {
-      load_a(s + 1, a1);
-      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this step's MFMAs
-      step(s, a0);
-      load_a(s + 2 < S1 ? s + 2 : s + 1, a0);
-      __builtin_amdgcn_sched_barrier(0);
-      step(s + 1, a1);
+    for (int s0 = S0; s0 < S0 + NFULL; s0 += NSA) {
+#pragma unroll
+      for (int j = 0; j < NSA; ++j) {
+        const int s = s0 + j;
+        load_a(s + PD < S1 ? s + PD : S1 - 1, a[(j + PD) % NSA]);
+        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this step's MFMAs
+        step(s, a[j], j, false);
+      }
     }
-    if constexpr ((S1 - S0) & 1) step(S1 - 1, a0);
+#pragma unroll
+    for (int j = 0; j < (S1 - S0) - NFULL; ++j) step(S0 + NFULL + j, a[j], j, true);
   }
 };
 
@@ -671,6 +727,17 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* lds, int ldsrs, int row_ba
   }
   return r;
 }
+
+// Weight-fragment prefetch depth of the forward conv of block l (k-steps in flight).  Measured on a
+// 16-pass x 16384-window batch-BN chunk (tools/probes/so_chunk.sh): depth 1 everywhere 29.8 ms, depth 2
+// 30.0, per-layer (1,3,2,3,2,3) 30.4, depth 4 38.7 (spills) -- the conv is not bound by the L2 round
+// trip of its weight fragments (profiles/batch_bn_fwd_r2.md).  APNEAUQ_FWD_PD overrides (probes).
+template <int l> struct FwdPD { static constexpr int v = 1; };
+#ifdef APNEAUQ_FWD_PD
+#define APNEAUQ_FWD_PDV(l) APNEAUQ_FWD_PD
+#else
+#define APNEAUQ_FWD_PDV(l) (FwdPD<l>::v)
+#endif
 
 // wave tilings (WM, WN) per output-channel count
 template <int COUT> struct Tiling;
@@ -756,7 +823,7 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
     __syncthreads();
   };
   // this block's dropout mask goes into the sign bit of R_l (not for the pass-shared block 1)
-  const bool enc = A.dropout != 0 && !(l == 0 && A.shared0);
+  const bool enc = A.dropout != 0 && !(l == 0 && A.shared0) && !(APNEAUQ_FWD_ABL & 64);
   const bool hash_in = l == 1 && A.shared0;  // workgroup-uniform
   int gaff = -1;  // stats group whose BN affine (of block l-1) is in prm
   // input staging, software-pipelined: tile i+1's rows are loaded into registers while tile i's
@@ -767,8 +834,16 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
       for (int i = 0; i < APNEAUQ_FWD_DELAY; ++i) __builtin_amdgcn_s_sleep(127);
   if constexpr (l > 0 && !(APNEAUQ_FWD_ABL & 16) && APNEAUQ_FWD_PIPE)
     if (t_begin < t_end) stg.load(A, kR * t_begin, hash_in);
+#ifdef APNEAUQ_FWD_STAMPS
+  if (l == APNEAUQ_FWD_STAMPS && blockIdx.x < kFstWG && threadIdx.x == 0) {
+    g_fst_cu[blockIdx.x][0] = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID
+    g_fst_cu[blockIdx.x][1] = __smid();
+  }
+#endif
   for (int tile = t_begin; tile < t_end; ++tile) {
     APNEAUQ_DASSERT(2 * tile < A.B + 1 && blockDim.x == kThreads);
+    const int kst = tile - t_begin;
+    APNEAUQ_FST(0, kst);
     const int row0 = kR * tile;                        // first staged row (global PL index)
     const int smp0 = 2 * tile;
     const int g0 = min(smp0, A.B - 1) / A.n_win, g1 = min(smp0 + 1, A.B - 1) / A.n_win;
@@ -789,6 +864,7 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
       stg.store(A, act, row0, prm, prm + 512, g0, hash_in);
     }
     __syncthreads();
+    APNEAUQ_FST(1, kst);
     f32x4 acc[CV::CT][CV::RT];
 #if (APNEAUQ_FWD_ABL & 8)
 #pragma unroll
@@ -797,10 +873,15 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
       for (int r = 0; r < CV::RT; ++r) acc[c][r] = f32x4{(float)act[threadIdx.x], 0.f, 0.f, (float)r};
 #else
     if constexpr (APNEAUQ_FWD_PRIO) __builtin_amdgcn_s_setprio(1);
-    CV::run(Ly.wf, act, IN_RS, acc);
+    CV::template run<APNEAUQ_FWD_PDV(l)>(Ly.wf, act, IN_RS, acc);
     if constexpr (APNEAUQ_FWD_PRIO) __builtin_amdgcn_s_setprio(0);
 #endif
+#ifdef APNEAUQ_FWD_STAMPS
+    if (threadIdx.x == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
+    APNEAUQ_FST(2, kst);
     __syncthreads();  // all waves done reading the staged input; reuse it for the output tile
+    APNEAUQ_FST(3, kst);
 
     // epilogue: bias + ReLU -> bf16 LDS tile (rows outside the batch / pad rows: 0).  Only the row
     // tiles holding t = 48..63 (pad rows on lanes m >= 12) and the batch's last tile need the select.
@@ -829,6 +910,7 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
       }
     }
     __syncthreads();
+    APNEAUQ_FST(4, kst);
     // channel moments of the stored tile (zero rows add nothing) on the matrix cores
     auto moments = [&](int sel) {  // sel: sample slot (rows 64*sel .. +64 = 32-row chunks 2sel, 2sel+1), -1: both
       if constexpr (!(APNEAUQ_FWD_ABL & 32)) {
@@ -902,6 +984,7 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
       moments(1);
     }
     copy_out();
+    APNEAUQ_FST(5, kst);
   }
   flush();
   if (A.det != nullptr) {  // deterministic mode (one stats group): this workgroup's moment partials
@@ -1800,7 +1883,9 @@ __global__ void pack_kernel(const float* __restrict__ w, int k, int cin, int cou
 // ------------------------------------------------------------------------------------------------ host
 using train::Args;
 
-constexpr int lds_fwd() { return train::kRows * train::kRS + (1024 + 2 * 256) * 4; }  // tile + affine + lstat
+constexpr int lds_fwd() {  // tile + affine + lstat (probe 512: twice that, one workgroup per CU)
+  return (train::kRows * train::kRS + (1024 + 2 * 256) * 4) * ((APNEAUQ_FWD_ABL & 512) ? 2 : 1);
+}
 constexpr int lds_dgrad() { return train::kRows * train::kRS + 1792 * 4; }
 static_assert(2 * lds_dgrad() <= 160 * 1024, "dgrad must fit two workgroups per CU");
 template <int l>
@@ -1812,6 +1897,21 @@ static_assert(2 * lds_wgrad<1>() <= 160 * 1024 && 2 * lds_wgrad<2>() <= 160 * 10
               "wgrad tiles must fit two workgroups per CU");
 
 int train_args_size() { return (int)sizeof(Args); }
+
+// probe builds (-DAPNEAUQ_FWD_STAMPS): copy the forward phase stamps out; -1 in the library build
+int train_read_stamps(void* dst, long long bytes) {
+#ifdef APNEAUQ_FWD_STAMPS
+  const size_t n1 = sizeof(unsigned) * train::kFstWG * 2, n2 = sizeof(unsigned long long) * train::kFstWG * train::kFstT * train::kFstN;
+  if (bytes < (long long)(n1 + n2)) return -2;
+  if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(train::g_fst_cu), n1) != hipSuccess) return -3;
+  if (hipMemcpyFromSymbol((char*)dst + n1, HIP_SYMBOL(train::g_fst), n2) != hipSuccess) return -3;
+  return 0;
+#else
+  (void)dst;
+  (void)bytes;
+  return -1;
+#endif
+}
 int train_layer_size() { return (int)sizeof(train::Layer); }
 
 __global__ void bump_counters_kernel(int* c, int n) {

@@ -12,8 +12,10 @@ Algorithms and random streams follow imbalanced-learn 0.12 as used by
 * RUS: one ``RandomState(seed)``; for every non-minority class (ascending label order)
   ``choice(n_class, n_minority, replace=False)``; minority kept whole; output grouped by class.
 
-The k-NN search is the hot spot (O(n_class^2 * 240)); on a GPU it runs as chunked distance GEMMs
-(``||a||^2 + ||b||^2 - 2 a.b``, exact fp32 re-ranking of the candidates) + ``topk`` on the device.
+The k-NN search is the hot spot (O(n_class^2 * 240)); on a GPU it runs in the HIP kernel
+``csrc/prep.hip:knn_kernel``: exact fp64 squared distances, per-thread register top-k,
+(distance, index) order, self excluded.  ``device="torch"`` keeps the chunked distance-GEMM + ``topk``
+formulation (CPU float64 or any torch device) as a reference path.
 """
 from __future__ import annotations
 
@@ -53,17 +55,33 @@ def _knn_torch(X: np.ndarray, k: int, device: str, chunk: int = 8192) -> np.ndar
     return out
 
 
+def _knn_hip(X: np.ndarray, k: int) -> np.ndarray:
+    import torch
+
+    from ..ops import _ext
+
+    _ext.require()
+    A = torch.as_tensor(np.ascontiguousarray(X, dtype=np.float64)).to("cuda")
+    return torch.ops.apneauq.prep_knn(A, int(k)).cpu().numpy()
+
+
 def knn_indices(X: np.ndarray, k: int = 5, device: Optional[str] = None) -> np.ndarray:
+    """k nearest neighbours of every row of X among the other rows, (distance, index) order.
+
+    device: None (HIP kernel when a GPU is present, else scikit-learn), "hip", "sklearn", or a torch
+    device string for the distance-GEMM reference path ("cpu", "cuda", or "torch" = the GPU)."""
     if device is None:
         try:
             import torch
 
-            device = "cuda" if torch.cuda.is_available() else "sklearn"
+            device = "hip" if torch.cuda.is_available() else "sklearn"
         except Exception:
             device = "sklearn"
     if device == "sklearn" or X.shape[0] <= k + 1:
         return _knn_numpy(X, k)
-    return _knn_torch(X, k, device)
+    if device == "hip" or (device == "cuda" and k <= 16 and X.shape[1] <= 320):
+        return _knn_hip(X, k)
+    return _knn_torch(X, k, "cuda" if device == "torch" else device)
 
 
 class SMOTE:

@@ -65,6 +65,11 @@ def standardize_per_window(data_3d, epsilon: float = 1e-8, device: Optional[str]
         import torch
 
         x = torch.as_tensor(np.asarray(data_3d, np.float64), device=device)
+        if x.is_cuda and x.dim() == 3 and x.shape[1] * x.shape[2] * 8 <= 65536 and x.shape[2] <= 256:
+            from ..ops import _ext
+
+            _ext.require()  # K14: csrc/prep.hip standardize_kernel (fp64, LDS-staged windows)
+            return torch.ops.apneauq.prep_standardize(x, float(epsilon)).cpu().numpy()
         mean = x.mean(dim=1, keepdim=True)
         std = x.std(dim=1, keepdim=True, unbiased=False)
         return ((x - mean) / (std + epsilon)).cpu().numpy()
