@@ -615,18 +615,18 @@ struct Conv {
   static constexpr int PAD = (K - 1) / 2;
   static_assert(NCT % WN == 0 && kRT % WM == 0 && WM * WN == 4, "wave tiling");
 
-  template <int PD = 1>
+  template <int PD = 1, bool RING = true>
   __device__ __forceinline__ static void run(const gbf16x8* wfrag, const char* lds, int ldsrs, f32x4 (&acc)[CT][RT]) {
 #pragma unroll
     for (int c = 0; c < CT; ++c)
 #pragma unroll
       for (int r = 0; r < RT; ++r) acc[c][r] = f32x4{0.f, 0.f, 0.f, 0.f};
-    steps<0, NSTEP, PD>(wfrag, lds, ldsrs, acc);
+    steps<0, NSTEP, PD, RING>(wfrag, lds, ldsrs, acc);
   }
 
   // steps [S0, S1) accumulated into acc; the wave's place in its 4-wave team is (threadIdx.x >> 6) & 3,
   // so 512-thread kernels run two teams.  PD = weight-fragment prefetch depth (k-steps in flight).
-  template <int S0, int S1, int PD = 1>
+  template <int S0, int S1, int PD = 1, bool RING = true>
   __device__ __forceinline__ static void steps(const gbf16x8* wfrag, const char* lds, int ldsrs,
                                                f32x4 (&acc)[CT][RT]) {
     static_assert(S0 < S1 && PD >= 1, "step range");
@@ -658,16 +658,28 @@ struct Conv {
     // before step s's MFMAs (the fused kernel's scheme; see FwdPD for the measured depths).
     // B fragments (activations, LDS) run through a ring of NB registers over the (step, row tile)
     // sequence: the read of fragment i + NB is issued right after the CT MFMAs of fragment i, so
-    // NB - 1 LDS reads stay in flight.
+    // NB - 1 LDS reads stay in flight.  RING = false reads each B fragment just in time (dgrad: one
+    // tile per workgroup, two workgroups per CU, measured 5-17 % faster per layer without the ring).
     constexpr int NSA = PD + 1;
     constexpr int NB = RT < 4 ? RT : 4;
     static_assert(RT % NB == 0, "B ring phase restarts at every step");
     constexpr int DSN = FIRST ? 2 : 1;  // LDS reads per B fragment
     bf16x8 bq[NB];
+    if constexpr (RING) {
 #pragma unroll
-    for (int i = 0; i < NB; ++i) bq[i] = load_b(S0, i);
+      for (int i = 0; i < NB; ++i) bq[i] = load_b(S0, i);
+    }
     // step s at position j of its group (group base sb = s - j); tail: no refills past S1
     auto step = [&](int s, const bf16x8 (&a)[CT], int j, bool tail) {
+      if constexpr (!RING) {
+#pragma unroll
+        for (int r = 0; r < RT; ++r) {
+          const bf16x8 b = load_b(s, r);
+#pragma unroll
+          for (int c = 0; c < CT; ++c) acc[c][r] = mfma16(a[c], b, acc[c][r]);
+        }
+        return;
+      }
 #pragma unroll
       for (int r = 0; r < RT; ++r) {
         const int i = j * RT + r;
@@ -733,6 +745,9 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* lds, int ldsrs, int row_ba
 // 30.0, per-layer (1,3,2,3,2,3) 30.4, depth 4 38.7 (spills) -- the conv is not bound by the L2 round
 // trip of its weight fragments (profiles/batch_bn_fwd_r2.md).  APNEAUQ_FWD_PD overrides (probes).
 template <int l> struct FwdPD { static constexpr int v = 1; };
+#ifndef APNEAUQ_FWD_RING  // B-fragment register ring in the forward conv (probe: 0 = just-in-time reads)
+#define APNEAUQ_FWD_RING 1
+#endif
 #ifdef APNEAUQ_FWD_PD
 #define APNEAUQ_FWD_PDV(l) APNEAUQ_FWD_PD
 #else
@@ -873,7 +888,7 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
       for (int r = 0; r < CV::RT; ++r) acc[c][r] = f32x4{(float)act[threadIdx.x], 0.f, 0.f, (float)r};
 #else
     if constexpr (APNEAUQ_FWD_PRIO) __builtin_amdgcn_s_setprio(1);
-    CV::template run<APNEAUQ_FWD_PDV(l)>(Ly.wf, act, IN_RS, acc);
+    CV::template run<APNEAUQ_FWD_PDV(l), APNEAUQ_FWD_RING != 0>(Ly.wf, act, IN_RS, acc);
     if constexpr (APNEAUQ_FWD_PRIO) __builtin_amdgcn_s_setprio(0);
 #endif
 #ifdef APNEAUQ_FWD_STAMPS
@@ -1503,7 +1518,7 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
 #pragma unroll
     for (int r = 0; r < CV::RT; ++r) acc[c][r] = f32x4{(float)act[threadIdx.x], 0.f, 0.f, (float)r};
 #else
-  CV::run(A.L[l].wd, act, kRS, acc);
+  CV::template run<1, false>(A.L[l].wd, act, kRS, acc);
 #endif
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
