@@ -384,6 +384,17 @@ def graph_train_step(model, x: torch.Tensor, y: torch.Tensor):
     return cur(x, y)
 
 
+def _sync_slots(sync: Callable, st: torch.Tensor, used: int) -> None:
+    """SyncBN of one layer's moment buffer: add the STAT_SLOTS interleaved slots locally (fp64), then
+    all-reduce the first ``used`` doubles of one slot (16x fewer bytes on the wire than the raw buffer)
+    and leave the global sums in slot 0, zeros in the others (the kernels add all slots)."""
+    v = st.view(STAT_SLOTS, -1)
+    tot = v[:, :used].sum(0)
+    sync(tot)
+    v[:, :used].zero_()
+    v[0, :used].copy_(tot)
+
+
 @torch.no_grad()
 def forward_batch_stats(model, x: torch.Tensor, n_pass: int, pass_base: int, seed: int, update_moving: bool = True,
                         sync: Optional[Callable] = None, window_offset: int = 0, global_n: Optional[int] = None,
@@ -424,13 +435,13 @@ def forward_batch_stats(model, x: torch.Tensor, n_pass: int, pass_base: int, see
             ws.st_all.zero_()
             _call(ctx, 0, 0, 1, pass_base + t0, dev)  # block 1 once, over the n windows
             if sync is not None:
-                sync(ws.st[0])
+                _sync_slots(sync, ws.st[0], 2 * ws.ch[1])  # stats group 0 only
         else:
             ws.st_all[ws.st[0].numel():].zero_()  # block-1 moments stay (they are pass-independent)
         for l in range(1, 6):
             _call(ctx, 0, l, 0, pass_base + t0, dev)
             if sync is not None:
-                sync(ws.st[l])
+                _sync_slots(sync, ws.st[l], tc * 2 * ws.ch[l + 1])  # the chunk's tc stats groups
         _call(ctx, 1, 0, 0, pass_base + t0, dev)
         if update_moving:
             _call(ctx, 4, 1, 0, pass_base + t0, dev)
