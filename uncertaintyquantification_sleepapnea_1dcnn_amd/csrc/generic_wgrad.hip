@@ -20,6 +20,8 @@
 //
 // Reference: models/train_deep_ensemble_cnns.py:30-71 (the pooled variants), cnn_baseline_train.py:
 // 100-102 (Adam, BCE) -- the Keras train step these kernels implement.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace apneauq {
@@ -388,11 +390,19 @@ hipError_t launch_gt_wgrad(const void* x, long long x_rows, const void* dz, long
   A.n_ci = im2col ? 1 : (cin + 15) / 16;
   A.n_co = (co_tiles + 4 * nco - 1) / (4 * nco);
   const long long chunks = (R + gwgrad::kChunk - 1) / gwgrad::kChunk;
-  // ~2048 workgroups (8 per CU over the 256 CUs), at least 4 chunks each (fewer output atomics)
+  // ~2048 workgroups (8 per CU over the 256 CUs), but at least minc chunks each: every workgroup ends
+  // with k * 16 * 64 * NCO fp32 atomics, and the chip adds ~1.3 TB/s of atomic bytes, so at 4 chunks
+  // per workgroup the k = 9 blocks of ModelSpec(30, 1) spent ~100 us of a ~106 us wgrad on them.
+  // APNEAUQ_GWG_MINC overrides (probes).
+  static const int minc_env = [] {
+    const char* e = getenv("APNEAUQ_GWG_MINC");
+    return e ? atoi(e) : 0;
+  }();
+  const long long minc = minc_env > 0 ? minc_env : (k <= 3 ? 4 : 2 * k);
   const long long blocks = (long long)A.n_ci * A.n_co;
   long long rg = 2048 / blocks;
   if (rg < 1) rg = 1;
-  if (rg > (chunks + 3) / 4) rg = (chunks + 3) / 4;
+  if (rg > (chunks + minc - 1) / minc) rg = (chunks + minc - 1) / minc;
   if (rg < 1) rg = 1;
   A.chunks_per_wg = (int)((chunks + rg - 1) / rg);
   rg = (chunks + A.chunks_per_wg - 1) / A.chunks_per_wg;
