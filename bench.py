@@ -271,6 +271,8 @@ class _HipEngine:
         self.world, self.start, self.n_glob, self.seed, self.passes, self.sync = world, start, n_glob, seed, passes, sync
         self.params_mcd = params_mcd
         self.params_de = params_de
+        # batch-BN MCD: samples (passes x windows) per layer-kernel launch (probe override)
+        self.max_samples = int(os.environ.get("APNEAUQ_MCD_MAX_SAMPLES", 1 << 18))
         self.blob_mcd = fused.pack_blob(spec, params_mcd).unsqueeze(0)
         self.blobs_de = torch.stack([fused.pack_blob(spec, p) for p in params_de])
         # the batch-BN model owns its own parameter copy: its moving statistics are mutated every pass
@@ -286,7 +288,7 @@ class _HipEngine:
         # reference semantics: every pass normalises with the batch statistics of ALL windows
         return train_ops.forward_batch_stats(self.model, x_loc, self.passes, pass_base=i * self.passes, seed=self.seed,
                                              update_moving=True, sync=self.sync, window_offset=self.start,
-                                             global_n=self.n_glob, max_samples=1 << 18)
+                                             global_n=self.n_glob, max_samples=self.max_samples)
 
     def de(self, x):
         return self.fused.fused_forward(x, self.blobs_de, self.spec)[:, 0]

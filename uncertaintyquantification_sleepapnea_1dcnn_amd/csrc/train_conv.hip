@@ -415,10 +415,12 @@ struct ActStager {
 
   // every v[u] is assigned on every path (zeros where unused), so v is dead between store() and the
   // next load() -- in particular across the conv MFMAs
+  // [U0, U1): the row batch to load / store (a split staging keeps fewer loads in flight)
+  template <int U0 = 0, int U1 = NK>
   __device__ __forceinline__ void load(const Args& A, int row0, bool hash_in) {
     const int t = tid(), cw = t % NCW, rin = t / NCW;
 #pragma unroll
-    for (int u = 0; u < NK; ++u) v[u] = u32x4{0u, 0u, 0u, 0u};
+    for (int u = U0; u < U1; ++u) v[u] = u32x4{0u, 0u, 0u, 0u};
     if (rin >= RP) return;
     const __bf16* R = A.L[l].R + cw * 8;
     if (HASH_IN && hash_in) {
@@ -428,7 +430,7 @@ struct ActStager {
       const __bf16* src0 = R + (long long)(kHalo + (n0 - g0 * A.n_win) * kSR) * Cc;
       const __bf16* src1 = R + (long long)(kHalo + (n1 - g1 * A.n_win) * kSR) * Cc;
 #pragma unroll
-      for (int u = 0; u < NK; ++u) {
+      for (int u = U0; u < U1; ++u) {
         const int r = rin + u * RP;
         if (r >= kRows) continue;
         const int grow = row0 + r;
@@ -438,7 +440,7 @@ struct ActStager {
       }
     } else {
 #pragma unroll
-      for (int u = 0; u < NK; ++u) {
+      for (int u = U0; u < U1; ++u) {
         const int r = rin + u * RP;
         if (r < kRows) v[u] = gld<u32x4>(R + (long long)(((APNEAUQ_FWD_ABL & 256) ? (row0 & 2047) : row0) + r) * Cc);
       }
@@ -446,6 +448,7 @@ struct ActStager {
   }
 
   // s, t: the affine of stats group g0 (s + 256, t + 256: group g1 when the tile straddles two)
+  template <int U0 = 0, int U1 = NK>
   __device__ __forceinline__ void store(const Args& A, char* lds, int row0, const float* s, const float* t,
                                         int g0, bool hash_in) const {
     const int tt_ = tid(), cw = tt_ % NCW, rin = tt_ / NCW;
@@ -470,7 +473,7 @@ struct ActStager {
     const uint32_t thr2 = drop ? Ly.thr * 0x10001u : 0u;  // thr 0: nothing dropped
     auto run = [&](auto two_groups, auto hashed) {
 #pragma unroll
-      for (int u = 0; u < NK; ++u) {
+      for (int u = U0; u < U1; ++u) {
         const int r = rin + u * RP;
         if (r >= kRows) continue;
         const int grow = row0 + r;
@@ -754,6 +757,15 @@ template <int l> struct FwdPD { static constexpr int v = 1; };
 #define APNEAUQ_FWD_PDV(l) (FwdPD<l>::v)
 #endif
 
+// Forward input staging of block l in two row batches instead of all of a tile's row loads in flight
+// at once (ActStager).  Block 6 (256 staged channels = 17 x 16-B loads per thread) spilled 44 VGPRs
+// into scratch with one batch; split, it spills none and its batch-BN MC-Dropout chunk is ~2 % faster
+// (profiles/batch_bn_fwd_r2.md, session 3).  APNEAUQ_FWD_SPLIT = bit mask over blocks (probes).
+#ifndef APNEAUQ_FWD_SPLIT
+#define APNEAUQ_FWD_SPLIT 32
+#endif
+template <int l> struct FwdStageSplit { static constexpr bool v = (APNEAUQ_FWD_SPLIT >> l) & 1; };
+
 // wave tilings (WM, WN) per output-channel count
 template <int COUT> struct Tiling;
 template <> struct Tiling<128> { static constexpr int WM = 1, WN = 4; };
@@ -875,8 +887,18 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
         gaff = (g1 == g0) ? g0 : -1;
         __syncthreads();
       }
-      if constexpr (!APNEAUQ_FWD_PIPE) stg.load(A, row0, hash_in);
-      stg.store(A, act, row0, prm, prm + 512, g0, hash_in);
+      if constexpr (APNEAUQ_FWD_PIPE) {
+        stg.store(A, act, row0, prm, prm + 512, g0, hash_in);
+      } else if constexpr (FwdStageSplit<l>::v) {  // two row batches: fewer loads in flight, no spills
+        constexpr int NK = decltype(stg)::NK, H = (NK + 1) / 2;
+        stg.template load<0, H>(A, row0, hash_in);
+        stg.template store<0, H>(A, act, row0, prm, prm + 512, g0, hash_in);
+        stg.template load<H, NK>(A, row0, hash_in);
+        stg.template store<H, NK>(A, act, row0, prm, prm + 512, g0, hash_in);
+      } else {
+        stg.load(A, row0, hash_in);
+        stg.store(A, act, row0, prm, prm + 512, g0, hash_in);
+      }
     }
     __syncthreads();
     APNEAUQ_FST(1, kst);
