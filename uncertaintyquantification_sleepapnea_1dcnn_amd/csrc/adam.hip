@@ -60,4 +60,42 @@ hipError_t launch_adam(float* p, const float* g, float* m, float* v, long long n
   return hipGetLastError();
 }
 
+// Zero up to kZeroMax buffers in ONE launch (the training step clears its moment / gradient / loss
+// accumulators: four fill kernels, ~5 us per graph node each, became one).  Buffer y = blockIdx.y;
+// sizes in 4-byte words, 16-B stores where the buffer allows.
+constexpr int kZeroMax = 8;
+struct ZeroArgs {
+  uint32_t* p[kZeroMax];
+  long long words[kZeroMax];
+};
+
+__global__ __launch_bounds__(256) void zero_kernel(ZeroArgs Z) {
+  uint32_t* p = Z.p[blockIdx.y];
+  const long long n = Z.words[blockIdx.y];
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long t0 = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const bool vec = (reinterpret_cast<uintptr_t>(p) & 15) == 0;  // block-uniform
+  const long long n4 = vec ? n >> 2 : 0;
+  for (long long i = t0; i < n4; i += stride) reinterpret_cast<uint4*>(p)[i] = uint4{0u, 0u, 0u, 0u};
+  for (long long i = (n4 << 2) + t0; i < n; i += stride) p[i] = 0u;
+}
+
+int zero_max_buffers() { return kZeroMax; }
+
+hipError_t launch_zero(int nb, void* const* ptrs, const long long* words, hipStream_t stream) {
+  if (nb <= 0) return hipSuccess;
+  if (nb > kZeroMax) return hipErrorInvalidValue;
+  ZeroArgs Z = {};
+  long long mx = 0;
+  for (int i = 0; i < nb; ++i) {
+    Z.p[i] = reinterpret_cast<uint32_t*>(ptrs[i]);
+    Z.words[i] = words[i];
+    mx = words[i] > mx ? words[i] : mx;
+  }
+  long long blocks = ((mx >> 2) + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 512 ? 512 : blocks);
+  hipLaunchKernelGGL(zero_kernel, dim3((unsigned)blocks, (unsigned)nb), dim3(256), 0, stream, Z);
+  return hipGetLastError();
+}
+
 }  // namespace apneauq

@@ -23,6 +23,8 @@ hipError_t launch_bootstrap(const float* metrics, const int* y, const int* idx, 
                             double* out, hipStream_t stream);
 hipError_t launch_bootstrap_partial(const float* metrics, const int* y, const int* idx, unsigned seed, int n, int lo,
                                     int n_loc, int n_boot, double* out, hipStream_t stream);
+int zero_max_buffers();
+hipError_t launch_zero(int nb, void* const* ptrs, const long long* words, hipStream_t stream);
 hipError_t launch_adam(float* p, const float* g, float* m, float* v, long long n, float b1, float b2, float alpha,
                        float eps, float gscale, const int* step_dev, hipStream_t stream);
 hipError_t train_bump_counters(int* c, int n, hipStream_t st);
@@ -207,6 +209,24 @@ void adam_step(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
                              p.numel(), (float)b1, (float)b2, (float)alpha, (float)eps, (float)gscale, step_dev,
                              cur_stream()),
         "adam_step");
+}
+
+// Zero several GPU buffers (4-byte multiples) in one launch.
+void zero_buffers(at::TensorList ts) {
+  const int nb = (int)ts.size();
+  TORCH_CHECK(nb >= 1 && nb <= apneauq::zero_max_buffers(), "zero_buffers: 1..", apneauq::zero_max_buffers(), " tensors");
+  std::vector<void*> p(nb);
+  std::vector<long long> w(nb);
+  for (int i = 0; i < nb; ++i) {
+    TORCH_CHECK(ts[i].is_cuda() && ts[i].is_contiguous() && ts[i].device() == ts[0].device() &&
+                    (ts[i].numel() * ts[i].element_size()) % 4 == 0 &&
+                    reinterpret_cast<uintptr_t>(ts[i].data_ptr()) % 4 == 0,
+                "zero_buffers: contiguous GPU tensors of whole 4-byte words on one device required");
+    p[i] = ts[i].data_ptr();
+    w[i] = (long long)(ts[i].numel() * ts[i].element_size() / 4);
+  }
+  const at::DeviceGuard guard(ts[0].device());
+  check(apneauq::launch_zero(nb, p.data(), w.data(), cur_stream()), "zero_buffers");
 }
 
 void bump_counters(at::Tensor& counters) {
@@ -655,6 +675,7 @@ TORCH_LIBRARY(apneauq, m) {
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, float b1, float b2, float alpha, float eps, "
         "float gscale, Tensor? counters=None) -> ()");
   m.def("bump_counters(Tensor(a!) counters) -> ()");
+  m.def("zero_buffers(Tensor(a!)[] ts) -> ()");
   m.def("generic_conv(Tensor x, Tensor wfrag, Tensor epi, int cout, int ksize, bool pool, bool dropout, int thr, "
         "int layer, int n_win, int pass_offset, int window_offset, int seed) -> Tensor");
   m.def("generic_head(Tensor y, Tensor w, float b, bool logits) -> Tensor");
@@ -682,6 +703,7 @@ TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
   m.impl("bootstrap_partial", &bootstrap_partial);
   m.impl("adam_step", &adam_step);
   m.impl("bump_counters", &bump_counters);
+  m.impl("zero_buffers", &zero_buffers);
   m.impl("train_pack", &train_pack);
   m.impl("generic_conv", &generic_conv);
   m.impl("generic_head", &generic_head);

@@ -1794,35 +1794,48 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A)
   }
 }
 
-// dW, db = sum over the row groups of the wgrad partials, in row-group order: deterministic, and
-// cheaper than the ~K*Cin*Cout fp32 atomics per row group it replaces (25-35 us of a 70-80 us wgrad
-// at batch 1024, profiles/train_step_r2.md).
+// dW, db = sum over the row groups of the wgrad partials in a fixed order: deterministic, and cheaper
+// than the ~K*Cin*Cout fp32 atomics per row group it replaces (25-35 us of a 70-80 us wgrad at batch
+// 1024, profiles/train_step_r2.md).  A workgroup covers 256/J float4 columns with J threads per column:
+// thread j sums row groups j, j + J, ... (8 loads in flight), then the J partials are added in j order
+// through LDS.  J > 1 when the row groups outnumber the columns' parallelism (block 1: 512 row groups
+// of 928 float4 columns took 26 us with one thread per column).
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int rgs, int kcc, int cout,
-                                                           float* __restrict__ gw, float* __restrict__ gb) {
-  // 4 consecutive elements per thread (16-B loads), 8 row groups in flight per step; partial sums
-  // combined in a fixed order, so the result is bitwise reproducible
+                                                           float* __restrict__ gw, float* __restrict__ gb, int J) {
+  __shared__ f32x4 red[256];
   const int S = kcc + cout;  // a multiple of 4 (Cout is)
   const int S4 = S >> 2;
+  const int ncol = 256 / J;
+  const int cl = threadIdx.x % ncol, j = threadIdx.x / ncol;
   const f32x4* p4 = reinterpret_cast<const f32x4*>(part);
-  for (int e4 = blockIdx.x * 256 + threadIdx.x; e4 < S4; e4 += gridDim.x * 256) {
+  for (int base = blockIdx.x * ncol; base < S4; base += gridDim.x * ncol) {  // workgroup-uniform
+    const int e4 = base + cl;
     f32x4 acc[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    int r = 0;
-    for (; r + 8 <= rgs; r += 8) {
+    for (int q = 0; q < 8; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (e4 < S4) {
+      int r = j;
+      for (; r + 7 * J < rgs; r += 8 * J) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += p4[(long long)(r + j) * S4 + e4];
+        for (int q = 0; q < 8; ++q) acc[q] += p4[(long long)(r + q * J) * S4 + e4];
+      }
+      for (int q = 0; r < rgs; r += J, ++q) acc[q] += p4[(long long)r * S4 + e4];
     }
-    for (int j = 0; r < rgs; ++r, ++j) acc[j] += p4[(long long)r * S4 + e4];
-    f32x4 s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    red[threadIdx.x] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    __syncthreads();
+    if (j == 0 && e4 < S4) {
+      f32x4 s = red[cl];
+      for (int q = 1; q < J; ++q) s += red[q * ncol + cl];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = 4 * e4 + i;
-      if (e < kcc)
-        gw[e] = s[i];
-      else
-        gb[e - kcc] = s[i];
+      for (int i = 0; i < 4; ++i) {
+        const int e = 4 * e4 + i;
+        if (e < kcc)
+          gw[e] = s[i];
+        else
+          gb[e - kcc] = s[i];
+      }
     }
+    __syncthreads();
   }
 }
 
@@ -2108,9 +2121,13 @@ static void wg_launch(const Args& A, hipStream_t st) {
   hipLaunchKernelGGL(train::wgrad_kernel<l>, dim3(nci * nco * rgs), dim3(256), lds_wgrad<l>(), st, A);
   if (A.wpart != nullptr) {
     const int kcc = train::KS[l] * train::C[l] * train::C[l + 1];
-    const int blocks = std::min(2048, ((kcc + train::C[l + 1]) / 4 + 255) / 256);
+    const int s4 = (kcc + train::C[l + 1]) / 4;
+    // threads per column: enough columns x row-group splits to fill ~1024 workgroups' worth of lanes
+    int J = 1;
+    while (J < 16 && rgs >= 16 * J && (long long)s4 * J < 256LL * 1024) J *= 2;
+    const int blocks = std::min(2048, (s4 * J + 255) / 256);
     hipLaunchKernelGGL(train::wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, A.wpart, rgs, kcc, train::C[l + 1],
-                       A.L[l].gw, A.L[l].gb);
+                       A.L[l].gw, A.L[l].gb, J);
   }
 }
 

@@ -178,10 +178,18 @@ class TrainWorkspace:
         return self.ctx
 
     def pack(self) -> None:
-        o = _ext.ops()
+        """bf16 MFMA fragments of all six conv kernels (forward + dgrad orientation) in ONE launch
+        (csrc/generic_wgrad.hip pack_kernel: the same fragment layout as train_conv.hip's per-layer
+        pack for channel counts that are multiples of 16; block 1 has no dgrad)."""
         v = self.model.store.views
-        for l in range(6):
-            o.train_pack(v[f"conv1d_{l + 1}/kernel"], self.ks[l], self.ch[l], self.ch[l + 1], self.wf[l], self.wd[l])
+        if not hasattr(self, "_no_dgr"):
+            self._no_dgr = torch.empty(0, dtype=torch.bfloat16, device=self.wf[0].device)
+        _ext.ops().gt_pack([v[f"conv1d_{l + 1}/kernel"] for l in range(6)], self.wf,
+                           [self._no_dgr] + self.wd[1:], self.ks, self.ch[:6], self.ch[1:])
+
+    def zero_accumulators(self) -> None:
+        """BN moment / backward sums, the flat gradient and the loss: one launch."""
+        _ext.ops().zero_buffers([self.st_all, self.bst_all, self.grad, self.loss])
 
 
 def _call(ctx, op, layer=0, flag=0, pass_base=-1, device=0):
@@ -225,10 +233,7 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, syn
     if n < ws.B:  # a partial last batch: clear rows of samples beyond n (stale data from a larger batch)
         ws.x[HALO + SR * n:].zero_()
     ws.y[:n].copy_(y.reshape(-1))
-    ws.st_all.zero_()
-    ws.bst_all.zero_()
-    ws.grad.zero_()
-    ws.loss.zero_()
+    ws.zero_accumulators()
     ws.pack()
     pb = TRAIN_PASS_BASE + model._train_step_counter
     for l in range(6):
@@ -314,9 +319,11 @@ class GraphedTrainStep:
         dev = model.store.device
         self.ws = TrainWorkspace(model, self.batch, deterministic=DETERMINISTIC)
         self.deterministic = DETERMINISTIC
-        self.x_in = torch.zeros(self.batch, 60, self.ws.ch[0], device=dev)
-        self.y_in = torch.zeros(self.batch, device=dev)
         n = self.batch
+        # the step's inputs are copied straight into the workspace's padded-row buffers (views; the
+        # pad rows stay zero), outside the graph: no copy nodes inside it
+        self.x_in = self.ws.x[HALO: HALO + SR * n].view(n, SR, self.ws.ch[0])[:, :60]
+        self.y_in = self.ws.y[:n]
         self.ctx = self.ws.build_ctx(n, n, 1, 0, model.seed, True, 1.0 / (n * 60), 1.0 / n, device_counters=True)
         model.optimizer._ensure(model.store.flat)
         # the graph bakes these buffers' addresses: a replay is only valid while they are the same
@@ -338,12 +345,7 @@ class GraphedTrainStep:
     def _body(self):
         ws, n, o = self.ws, self.batch, _ext.ops()
         dev = self.x_in.device.index or 0
-        ws.x[HALO: HALO + SR * n].view(n, SR, ws.ch[0])[:, :60].copy_(self.x_in)
-        ws.y[:n].copy_(self.y_in)
-        ws.st_all.zero_()
-        ws.bst_all.zero_()
-        ws.grad.zero_()
-        ws.loss.zero_()
+        ws.zero_accumulators()
         ws.pack()
         for l in range(6):
             _call(self.ctx, 0, l, 0, TRAIN_PASS_BASE, dev)
@@ -357,7 +359,8 @@ class GraphedTrainStep:
         o.adam_step(self.model.store.flat, ws.grad, opt.m, opt.v, opt.beta_1, opt.beta_2, opt.learning_rate,
                     opt.epsilon, 1.0, ws.counters)
         o.bump_counters(ws.counters)
-        return ws.loss.double().sum(), torch.sigmoid(ws.logits[:n])
+        # the loss sum as a 0-d view of the kernels' fp32 accumulator (no cast / reduce nodes)
+        return ws.loss.view(()), torch.sigmoid(ws.logits[:n])
 
     def __call__(self, x: torch.Tensor, y: torch.Tensor):
         """One step; returns (loss_sum, probs) views of static buffers (valid until the next replay)."""
