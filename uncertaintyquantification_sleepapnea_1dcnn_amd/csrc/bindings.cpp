@@ -69,7 +69,7 @@ struct Args {
   const void* x; const float* y; const float* dense_w; const float* dense_b; float* g_dense_w; float* g_dense_b;
   float* logits; float* dlogit; float* loss_sum;
   int B; int n_win; int groups; unsigned pass_base; unsigned window_offset; unsigned long long seed; int dropout;
-  float inv_count; float inv_batch; float eps; float momentum; const unsigned* pass_dev; int st_groups; float* wpart; float* det; int shared0;
+  float inv_count; float inv_batch; float eps; float momentum; const unsigned* pass_dev; int st_groups; float* wpart; float* det; int shared0; float* tab;
 };
 }  // namespace train
 int train_args_size();
@@ -83,6 +83,7 @@ hipError_t train_launch_head(const train::Args& A, int backward, hipStream_t st)
 hipError_t train_launch_dgrad(const train::Args& A, int l, hipStream_t st);
 hipError_t train_launch_wgrad(const train::Args& A, int l, hipStream_t st);
 hipError_t train_launch_finalize(const train::Args& A, int update_moving, int grads, hipStream_t st);
+hipError_t train_launch_tab(const apneauq::train::Args& A, int mode, int l, hipStream_t st);
 hipError_t train_launch_pack(const float* w, int k, int cin, int cout, void* fwd, void* dgr, hipStream_t st);
 }  // namespace apneauq
 
@@ -237,7 +238,7 @@ void bump_counters(at::Tensor& counters) {
 }
 
 // ctx: int64 CPU tensor of device pointers / scalars built once per workspace (ops/train_ops.py)
-constexpr int kCtxLayer = 19, kCtxLen = 6 * kCtxLayer + 25;
+constexpr int kCtxLayer = 19, kCtxLen = 6 * kCtxLayer + 26;
 
 float bits_to_float(int64_t v) {
   uint32_t u = static_cast<uint32_t>(v);
@@ -303,12 +304,16 @@ apneauq::train::Args args_from_ctx(const at::Tensor& ctx, int64_t pass_base) {
   A.shared0 = static_cast<int>(g[22]);
   A.wpart = reinterpret_cast<float*>(g[23]);
   A.det = reinterpret_cast<float*>(g[24]);
+  A.tab = reinterpret_cast<float*>(g[25]);
+  TORCH_CHECK(A.tab == nullptr || (A.det == nullptr && A.groups == 1),
+              "train ctx: the parameter table needs one stats group and no deterministic partials");
   TORCH_CHECK(A.st_groups >= A.groups, "train ctx: moment buffers hold fewer groups than requested");
   return A;
 }
 
 // op: 0 fwd(layer; flag=1: the pass-shared block 1 of batch-BN MC Dropout, over the n_win windows)
 //     | 1 head(flag=backward) | 2 dgrad(layer) | 3 wgrad(layer) | 4 finalize(layer=update_moving, flag=grads)
+//     | 5 parameter table (flag 0: forward rows of every block, 1: backward rows of block ``layer``)
 void train_call(const at::Tensor& ctx, int64_t op, int64_t layer, int64_t flag, int64_t pass_base, int64_t device) {
   const at::DeviceGuard guard(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(device)));
   auto A = args_from_ctx(ctx, pass_base);
@@ -327,6 +332,7 @@ void train_call(const at::Tensor& ctx, int64_t op, int64_t layer, int64_t flag, 
     case 2: TORCH_CHECK(layer >= 1 && layer < 6); check(apneauq::train_launch_dgrad(A, (int)layer, s), "train dgrad"); break;
     case 3: TORCH_CHECK(layer >= 0 && layer < 6); check(apneauq::train_launch_wgrad(A, (int)layer, s), "train wgrad"); break;
     case 4: check(apneauq::train_launch_finalize(A, (int)layer, (int)flag, s), "train finalize"); break;
+    case 5: check(apneauq::train_launch_tab(A, (int)flag, (int)layer, s), "train param table"); break;
     default: TORCH_CHECK(false, "train_call: unknown op ", op);
   }
 }

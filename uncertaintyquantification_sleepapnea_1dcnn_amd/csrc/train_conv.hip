@@ -102,6 +102,11 @@ struct Args {
   int shared0;         // batch-BN MC Dropout: block 1 (no dropout before it) is computed once for the
                        // n_win windows (stats group 0, R_0 unencoded, indexed by window) and shared by
                        // every pass; block 2's staging applies block 1's dropout from the hash
+  float* tab;          // single-device training: per-layer BN parameter table [6][kTabRows][256] fp32
+                       // (mean, rstd, gamma*rstd, beta - mean*gamma*rstd, mean dY, mean dY*xhat), written
+                       // once per step by tab_kernel; the ~512 workgroups of each backward kernel read a
+                       // few KB instead of each re-summing 16 fp64 slots per channel from the device-
+                       // coherent moment buffers (~100 MB per dgrad launch).  nullptr: slot sums
 };
 
 template <typename T>
@@ -200,10 +205,16 @@ __device__ __forceinline__ float slot_sum(const float* p, int stride) {
   for (int i = 0; i < kStatSlots; ++i) s += p[i * stride];
   return s;
 }
+// All kStatSlots loads are issued before the first add: the training kernels run one tile per
+// workgroup at batch 1024, so their per-channel prologue (2-6 of these sums per channel) is exposed
+// latency -- 4 dependent round trips per sum cost dgrad 6-9 us (session-3 probe APNEAUQ_DG_ABL=32).
 __device__ __forceinline__ double slot_sumd(const double* p, int stride) {
+  double v[kStatSlots];
+#pragma unroll
+  for (int i = 0; i < kStatSlots; ++i) v[i] = p[i * stride];
   double s = 0.0;
-#pragma unroll 4  // partly unrolled: the forward kernels call this with their next tile's input in registers
-  for (int i = 0; i < kStatSlots; ++i) s += p[i * stride];
+#pragma unroll
+  for (int i = 0; i < kStatSlots; ++i) s += v[i];
   return s;
 }
 // stats group holding block l's moments for pass group g (block 1 is shared by all passes in shared0 mode)
@@ -246,6 +257,35 @@ __device__ __forceinline__ void bn_stats_to_lds(const Args& A, int l, int g, flo
     mean[c] = mu;
     rstd[c] = rsqrtf(var + A.eps);
   }
+}
+
+// Parameter table (Args::tab): rows of T[l][kTabRows][256]
+constexpr int kTabRows = 6, kTabMean = 0, kTabRstd = 1, kTabS = 2, kTabT = 3, kTabMdy = 4, kTabMdyx = 5;
+__device__ __forceinline__ const float* tab_row(const Args& A, int l, int row) {
+  return A.tab + (l * kTabRows + row) * 256;
+}
+
+// Forward rows of T[l] (stats group 0) from the fp64 slots (tab_kernel).
+__device__ __forceinline__ void tab_write_fwd(const Args& A, int l) {
+  const int Cc = C[l + 1], c = threadIdx.x;
+  if (c >= Cc) return;
+  float mu, var;
+  bn_moments(A, l, 0, c, mu, var);
+  const float rs = rsqrtf(var + A.eps), sc = A.L[l].gamma[c] * rs;
+  float* t = A.tab + l * kTabRows * 256;
+  t[kTabMean * 256 + c] = mu;
+  t[kTabRstd * 256 + c] = rs;
+  t[kTabS * 256 + c] = sc;
+  t[kTabT * 256 + c] = A.L[l].beta[c] - mu * sc;
+}
+
+// Backward rows of T[l] (mean dY, mean dY*xhat) from bst[l] (tab_kernel).
+__device__ __forceinline__ void tab_write_bwd(const Args& A, int l) {
+  const int Cc = C[l + 1], c = threadIdx.x;
+  if (c >= Cc) return;
+  float* t = A.tab + l * kTabRows * 256;
+  t[kTabMdy * 256 + c] = (float)(slot_sumd(A.L[l].bst + c, 2 * Cc) * (double)A.inv_count);
+  t[kTabMdyx * 256 + c] = (float)(slot_sumd(A.L[l].bst + Cc + c, 2 * Cc) * (double)A.inv_count);
 }
 
 __device__ __forceinline__ unsigned layer_sample_key(const Args& A, int l, int sample) {
@@ -1047,6 +1087,17 @@ __global__ __launch_bounds__(256) void aff_kernel(Args A, int l) {
   }
 }
 
+// Parameter table (Args::tab) of single-device training: mode 0 = the forward rows of every block
+// (one workgroup per block, launched after the six forward kernels; read by the head, dgrad and wgrad),
+// mode 1 = the backward rows of block l (not on the default step: the backward kernels sum bst[l]
+// themselves, 2 x 16 slots per channel, which measured cheaper than one more graph node per block).
+__global__ __launch_bounds__(256) void tab_kernel(Args A, int mode, int l) {
+  if (mode == 0)
+    tab_write_fwd(A, blockIdx.x);
+  else
+    tab_write_bwd(A, l);
+}
+
 // ------------------------------------------------------------------------------------------------
 // Ping-pong forward of block l >= 1 for large batches (batch-BN MC Dropout runs T x N samples through
 // every layer).  One 512-thread workgroup per CU = two 4-wave teams, each with its own LDS tile
@@ -1361,6 +1412,16 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A, int backward) {
   const int g_last = min(blockIdx.x * 4 + 3, A.B - 1) / A.n_win;
   for (int c = threadIdx.x; c < 3 * Cc + 2; c += kThreads) dw[c] = 0.f;
   auto params = [&](int g) {
+    if (A.tab != nullptr) {  // single-device training (one group): the forward rows of T[5]
+      for (int c = threadIdx.x; c < Cc; c += kThreads) {
+        pmu[c] = tab_row(A, 5, kTabMean)[c];
+        prs[c] = tab_row(A, 5, kTabRstd)[c];
+        psc[c] = tab_row(A, 5, kTabS)[c];
+        psh[c] = tab_row(A, 5, kTabT)[c];
+        pw[c] = A.dense_w[c];
+      }
+      return;
+    }
     for (int c = threadIdx.x; c < Cc; c += kThreads) {
       float m1, var;
       bn_moments(A, 5, g, c, m1, var);
@@ -1519,16 +1580,44 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
   APNEAUQ_DASSERT(2 * tile < A.B + 1 && blockDim.x == kThreads);
   const int row0 = kR * tile;
   const int smp0 = 2 * tile;
-  {
-    const Layer& Ly = A.L[l];
-    bn_affine_to_lds(A, l, 0, gr, mdy, mean, rstd);  // mdy temporarily holds the shift (unused)
-    __syncthreads();
-    for (int c = threadIdx.x; c < CIN; c += kThreads) {
-      gr[c] = Ly.gamma[c] * rstd[c];
-      mdy[c] = (float)(slot_sumd(Ly.bst + c, 2 * CIN) * (double)A.inv_count);
-      mdyx[c] = (float)(slot_sumd(Ly.bst + CIN + c, 2 * CIN) * (double)A.inv_count);
+  if constexpr ((APNEAUQ_DG_ABL & 32) != 0) {  // probe: constant parameters (no prologue loads)
+    for (int c = threadIdx.x; c < 256; c += kThreads) gr[c] = mean[c] = rstd[c] = mdy[c] = mdyx[c] = mean_prev[c] = rstd_prev[c] = 0.5f;
+  } else if (A.tab != nullptr) {  // single-device training: forward rows of T[l], T[l-1]; backward sums
+    const int c = threadIdx.x, ci = c < CIN ? c : 0;
+    const double b0 = slot_sumd(A.L[l].bst + ci, 2 * CIN), b1 = slot_sumd(A.L[l].bst + CIN + ci, 2 * CIN);
+    if (c < CIN) {
+      gr[c] = tab_row(A, l, kTabS)[c];
+      mean[c] = tab_row(A, l, kTabMean)[c];
+      rstd[c] = tab_row(A, l, kTabRstd)[c];
+      mdy[c] = (float)(b0 * (double)A.inv_count);
+      mdyx[c] = (float)(b1 * (double)A.inv_count);
     }
-    bn_stats_to_lds(A, l - 1, 0, mean_prev, rstd_prev);
+    if (c < COUT) {
+      mean_prev[c] = tab_row(A, l - 1, kTabMean)[c];
+      rstd_prev[c] = tab_row(A, l - 1, kTabRstd)[c];
+    }
+  } else {
+    // one channel per thread (CIN, COUT <= 256 = kThreads): block l's moments and backward sums and
+    // block l-1's moments, all 96 slot loads independent (clamped indices, stores predicated)
+    static_assert(CIN <= kThreads && COUT <= kThreads, "one channel per thread");
+    const Layer& Ly = A.L[l];
+    const int c = threadIdx.x, ci = c < CIN ? c : 0, cp = c < COUT ? c : 0;
+    float mu, var, mup, varp;
+    bn_moments(A, l, 0, ci, mu, var);
+    const double b0 = slot_sumd(Ly.bst + ci, 2 * CIN), b1 = slot_sumd(Ly.bst + CIN + ci, 2 * CIN);
+    bn_moments(A, l - 1, 0, cp, mup, varp);
+    if (c < CIN) {
+      const float rs = rsqrtf(var + A.eps);
+      mean[c] = mu;
+      rstd[c] = rs;
+      gr[c] = Ly.gamma[c] * rs;
+      mdy[c] = (float)(b0 * (double)A.inv_count);
+      mdyx[c] = (float)(b1 * (double)A.inv_count);
+    }
+    if (c < COUT) {
+      mean_prev[c] = mup;
+      rstd_prev[c] = rsqrtf(varp + A.eps);
+    }
   }
   __syncthreads();
   stage_dz<l, kRows, CIN / 8>(A, act, kRS, row0, 0, gr, mean, rstd, mdy, mdyx, A.L[l].dZ, kHalo, kHalo + kR);
@@ -1665,16 +1754,46 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A)
 #else
   const bool do_bias = (ci0 == 0);
 #endif
-  {
-    const Layer& Ly = A.L[l];
-    bn_affine_to_lds(A, l, 0, gr, mdy, mean, rstd);
-    __syncthreads();
-    for (int c = threadIdx.x; c < COUT; c += kThreads) {
-      gr[c] = Ly.gamma[c] * rstd[c];
-      mdy[c] = (float)(slot_sumd(Ly.bst + c, 2 * COUT) * (double)A.inv_count);
-      mdyx[c] = (float)(slot_sumd(Ly.bst + COUT + c, 2 * COUT) * (double)A.inv_count);
+  if (A.tab != nullptr) {  // single-device training: forward rows of T[l], T[l-1]; backward sums
+    const int c = threadIdx.x, co = c < COUT ? c : 0;
+    const double b0 = slot_sumd(A.L[l].bst + co, 2 * COUT), b1 = slot_sumd(A.L[l].bst + COUT + co, 2 * COUT);
+    if (c < COUT) {
+      gr[c] = tab_row(A, l, kTabS)[c];
+      mean[c] = tab_row(A, l, kTabMean)[c];
+      rstd[c] = tab_row(A, l, kTabRstd)[c];
+      mdy[c] = (float)(b0 * (double)A.inv_count);
+      mdyx[c] = (float)(b1 * (double)A.inv_count);
     }
-    if constexpr (!FIRST) bn_affine_to_lds(A, l - 1, 0, sp, tp, nullptr, nullptr);
+    if constexpr (!FIRST) {
+      if (c < CIN) {
+        sp[c] = tab_row(A, l - 1, kTabS)[c];
+        tp[c] = tab_row(A, l - 1, kTabT)[c];
+      }
+    }
+  } else {
+    // one channel per thread, every slot load independent (see dgrad_kernel's prologue)
+    static_assert(COUT <= kThreads && CIN <= kThreads, "one channel per thread");
+    const Layer& Ly = A.L[l];
+    const int c = threadIdx.x, co = c < COUT ? c : 0, cp = c < CIN ? c : 0;
+    float mu, var, mup = 0.f, varp = 0.f;
+    bn_moments(A, l, 0, co, mu, var);
+    const double b0 = slot_sumd(Ly.bst + co, 2 * COUT), b1 = slot_sumd(Ly.bst + COUT + co, 2 * COUT);
+    if constexpr (!FIRST) bn_moments(A, l - 1, 0, cp, mup, varp);
+    if (c < COUT) {
+      const float rs = rsqrtf(var + A.eps);
+      mean[c] = mu;
+      rstd[c] = rs;
+      gr[c] = Ly.gamma[c] * rs;
+      mdy[c] = (float)(b0 * (double)A.inv_count);
+      mdyx[c] = (float)(b1 * (double)A.inv_count);
+    }
+    if constexpr (!FIRST) {
+      if (c < CIN) {
+        const float sc = A.L[l - 1].gamma[c] * rsqrtf(varp + A.eps);
+        sp[c] = sc;
+        tp[c] = A.L[l - 1].beta[c] - mup * sc;
+      }
+    }
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -2064,6 +2183,13 @@ hipError_t train_launch_fwd(const Args& A, int l, hipStream_t st) {
     case 5: hipLaunchKernelGGL(train::fwd_kernel<5>, dim3(tiles), dim3(256), lds_fwd(), st, A); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+hipError_t train_launch_tab(const Args& A, int mode, int l, hipStream_t st) {
+  if (A.tab == nullptr) return hipSuccess;  // no table (multi-rank / deterministic / MC-Dropout ctx)
+  if (l < 0 || l >= 6) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(train::tab_kernel, dim3(mode == 0 ? 6 : 1), dim3(256), 0, st, A, mode, l);
   return hipGetLastError();
 }
 

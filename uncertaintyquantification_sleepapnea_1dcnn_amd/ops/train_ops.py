@@ -129,6 +129,9 @@ class TrainWorkspace:
         # sums, added in a fixed order by det_reduce_kernel instead of atomics (training only)
         self.deterministic = bool(deterministic) and with_backward and self.groups == 1 and not self.shared0
         self.det = (torch.empty(int(_ext.ops().train_det_size(self.B)), device=dev) if self.deterministic else None)
+        # single-device training: per-layer BN parameter table, written once per step after the
+        # forward kernels (train_conv.hip Args::tab / tab_kernel)
+        self.tab = torch.zeros(6 * 6 * 256, device=dev) if with_backward else None
         self.y = torch.zeros(self.B, device=dev)
         self.logits = torch.zeros(self.B, device=dev)
         self.dlogit = torch.zeros(self.B, device=dev)
@@ -147,8 +150,12 @@ class TrainWorkspace:
         self.counters = torch.zeros(2, dtype=torch.int32, device=dev)
 
     def build_ctx(self, n: int, n_win: int, groups: int, window_offset: int, seed: int, dropout: bool,
-                  inv_count: float, inv_batch: float, device_counters: bool = False):
-        key = (n, n_win, groups, window_offset, seed, dropout, inv_count, inv_batch, device_counters)
+                  inv_count: float, inv_batch: float, device_counters: bool = False, table: bool = False):
+        """``table``: the kernels exchange BN parameters through ``self.tab`` (single device, one stats
+        group, atomic mode only -- synchronised / deterministic moments are only final after the
+        kernel that produces them)."""
+        table = bool(table) and self.tab is not None and groups == 1 and self.det is None
+        key = (n, n_win, groups, window_offset, seed, dropout, inv_count, inv_batch, device_counters, table)
         if key == self._ctx_key:
             return self.ctx
         spec, v, g = self.model.spec, self.model.store.views, self.gviews
@@ -172,7 +179,8 @@ class TrainWorkspace:
                  _fbits(spec.bn_epsilon), _fbits(spec.bn_momentum),
                  self.counters.data_ptr() if device_counters else 0, self.groups, int(self.shared0),
                  self.wpart.data_ptr() if self.wpart is not None else 0,
-                 self.det.data_ptr() if self.det is not None else 0]
+                 self.det.data_ptr() if self.det is not None else 0,
+                 self.tab.data_ptr() if table else 0]
         self.ctx = torch.tensor(vals, dtype=torch.int64)
         self._ctx_key = key
         return self.ctx
@@ -226,7 +234,7 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, syn
     n = x.shape[0]
     ws = _get_ws(model, n)
     gb = global_batch or n
-    ctx = ws.build_ctx(n, n, 1, window_offset, model.seed, True, 1.0 / (gb * 60), 1.0 / gb)
+    ctx = ws.build_ctx(n, n, 1, window_offset, model.seed, True, 1.0 / (gb * 60), 1.0 / gb, table=sync is None)
     dev = x.device.index or 0
     # inputs in padded-row layout (pad rows stay zero)
     ws.x[HALO: HALO + SR * n].view(n, SR, ws.ch[0])[:, :60].copy_(x)
@@ -240,6 +248,7 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, syn
         _call(ctx, 0, l, 0, pb, dev)
         if sync is not None:
             sync(ws.st[l])
+    _call(ctx, 5, 0, 0, pb, dev)  # BN parameter table (forward rows; a no-op without a table)
     _call(ctx, 1, 0, 1, pb, dev)
     if sync is not None:
         sync(ws.bst[5])
@@ -324,7 +333,8 @@ class GraphedTrainStep:
         # pad rows stay zero), outside the graph: no copy nodes inside it
         self.x_in = self.ws.x[HALO: HALO + SR * n].view(n, SR, self.ws.ch[0])[:, :60]
         self.y_in = self.ws.y[:n]
-        self.ctx = self.ws.build_ctx(n, n, 1, 0, model.seed, True, 1.0 / (n * 60), 1.0 / n, device_counters=True)
+        self.ctx = self.ws.build_ctx(n, n, 1, 0, model.seed, True, 1.0 / (n * 60), 1.0 / n, device_counters=True,
+                                     table=True)
         model.optimizer._ensure(model.store.flat)
         # the graph bakes these buffers' addresses: a replay is only valid while they are the same
         # tensor objects (a restored optimizer state or a moved model triggers a re-capture)
@@ -349,6 +359,7 @@ class GraphedTrainStep:
         ws.pack()
         for l in range(6):
             _call(self.ctx, 0, l, 0, TRAIN_PASS_BASE, dev)
+        _call(self.ctx, 5, 0, 0, TRAIN_PASS_BASE, dev)  # BN parameter table (forward rows)
         _call(self.ctx, 1, 0, 1, TRAIN_PASS_BASE, dev)
         for l in range(5, 0, -1):
             _call(self.ctx, 2, l, 0, TRAIN_PASS_BASE, dev)
