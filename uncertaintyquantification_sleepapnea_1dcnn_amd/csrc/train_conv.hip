@@ -1560,6 +1560,12 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A, int backward) {
 // dgrad of block l (l >= 1): dA_{l-1} = conv^T(dZ_l, W_l);  epilogue -> dY_{l-1} = dA * mask_{l-1}
 // plus the backward sums of block l-1.
 // ------------------------------------------------------------------------------------------------
+// dgrad: prefetch the epilogue's R_{l-1} loads ahead of the conv (APNEAUQ_DG_PRE = bit mask over l)
+#ifndef APNEAUQ_DG_PRE
+#define APNEAUQ_DG_PRE 30
+#endif
+template <int l> struct DgPre { static constexpr bool v = (APNEAUQ_DG_PRE >> l) & 1; };
+
 template <int l>
 __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
   constexpr int CIN = C[l + 1], COUT = C[l];  // conv^T: input = dZ_l channels, output = block l-1 channels
@@ -1622,6 +1628,26 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
   __syncthreads();
   stage_dz<l, kRows, CIN / 8>(A, act, kRS, row0, 0, gr, mean, rstd, mdy, mdyx, A.L[l].dZ, kHalo, kHalo + kR);
   __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / T::WN, wn = wave % T::WN;
+  const int m = lane & 15, h = lane >> 4;
+  const Layer& Lp = A.L[l - 1];
+  // R_{l-1} at this lane's epilogue elements (|R| for xhat, sign = block l-1's dropout mask), loaded
+  // before the conv so the MFMAs cover their latency (DgPre: where the registers allow)
+  constexpr bool PRE = DgPre<l>::v && !(APNEAUQ_DG_ABL & 1);
+  bf16x4 rpre[PRE ? CV::CT : 1][PRE ? CV::RT : 1];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int c = 0; c < CV::CT; ++c)
+#pragma unroll
+      for (int r = 0; r < CV::RT; ++r) {
+        const int row = wm * CV::RT * 16 + r * 16 + m;
+        const bool valid = (row & 63) < kL && (smp0 + (row >> 6)) < A.B;
+        const int co0 = (wn * CV::CT + c) * 16 + 4 * h;
+        rpre[c][r] = valid ? gld<bf16x4>(Lp.R + (long long)(row0 + kHalo + row) * COUT + co0)
+                           : bf16x4{(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
+      }
+  }
   f32x4 acc[CV::CT][CV::RT];
 #if (APNEAUQ_DG_ABL & 8)
 #pragma unroll
@@ -1632,10 +1658,6 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
   CV::template run<1, false>(A.L[l].wd, act, kRS, acc);
 #endif
   __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave / T::WN, wn = wave % T::WN;
-  const int m = lane & 15, h = lane >> 4;
-  const Layer& Lp = A.L[l - 1];
   const float dscp = A.dropout ? Lp.dsc : 1.f;
 #pragma unroll
   for (int c = 0; c < CV::CT; ++c) {
@@ -1651,7 +1673,10 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
       bf16x4 rr = {(__bf16)acc[c][r][0], (__bf16)acc[c][r][1], (__bf16)acc[c][r][2], (__bf16)acc[c][r][3]};
 #else
       bf16x4 rr = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
-      if (valid) rr = gld<bf16x4>(Lp.R + (long long)(row0 + kHalo + row) * COUT + co0);
+      if constexpr (PRE)
+        rr = rpre[c][r];
+      else if (valid)
+        rr = gld<bf16x4>(Lp.R + (long long)(row0 + kHalo + row) * COUT + co0);
 #endif
       f32x4 v = acc[c][r];
 #pragma unroll
