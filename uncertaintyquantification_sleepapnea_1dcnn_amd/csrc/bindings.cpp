@@ -305,8 +305,9 @@ apneauq::train::Args args_from_ctx(const at::Tensor& ctx, int64_t pass_base) {
   A.wpart = reinterpret_cast<float*>(g[23]);
   A.det = reinterpret_cast<float*>(g[24]);
   A.tab = reinterpret_cast<float*>(g[25]);
-  TORCH_CHECK(A.tab == nullptr || (A.det == nullptr && A.groups == 1),
-              "train ctx: the parameter table needs one stats group and no deterministic partials");
+  TORCH_CHECK(A.tab == nullptr || (A.det == nullptr && A.groups == 1 && A.wpart != nullptr),
+              "train ctx: the parameter table needs one stats group, no deterministic partials and wgrad partials "
+              "(wgrad_reduce writes its backward rows)");
   TORCH_CHECK(A.st_groups >= A.groups, "train ctx: moment buffers hold fewer groups than requested");
   return A;
 }

@@ -1588,15 +1588,19 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
   const int smp0 = 2 * tile;
   if constexpr ((APNEAUQ_DG_ABL & 32) != 0) {  // probe: constant parameters (no prologue loads)
     for (int c = threadIdx.x; c < 256; c += kThreads) gr[c] = mean[c] = rstd[c] = mdy[c] = mdyx[c] = mean_prev[c] = rstd_prev[c] = 0.5f;
-  } else if (A.tab != nullptr) {  // single-device training: forward rows of T[l], T[l-1]; backward sums
-    const int c = threadIdx.x, ci = c < CIN ? c : 0;
-    const double b0 = slot_sumd(A.L[l].bst + ci, 2 * CIN), b1 = slot_sumd(A.L[l].bst + CIN + ci, 2 * CIN);
+  } else if (A.tab != nullptr) {  // single-device training: T[l] (block 6: backward sums), T[l-1]
+    const int c = threadIdx.x;
     if (c < CIN) {
       gr[c] = tab_row(A, l, kTabS)[c];
       mean[c] = tab_row(A, l, kTabMean)[c];
       rstd[c] = tab_row(A, l, kTabRstd)[c];
-      mdy[c] = (float)(b0 * (double)A.inv_count);
-      mdyx[c] = (float)(b1 * (double)A.inv_count);
+      if constexpr (l == 5) {  // block 6's backward sums come from the head, no table job in between
+        mdy[c] = (float)(slot_sumd(A.L[l].bst + c, 2 * CIN) * (double)A.inv_count);
+        mdyx[c] = (float)(slot_sumd(A.L[l].bst + CIN + c, 2 * CIN) * (double)A.inv_count);
+      } else {
+        mdy[c] = tab_row(A, l, kTabMdy)[c];
+        mdyx[c] = tab_row(A, l, kTabMdyx)[c];
+      }
     }
     if (c < COUT) {
       mean_prev[c] = tab_row(A, l - 1, kTabMean)[c];
@@ -1779,15 +1783,19 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A)
 #else
   const bool do_bias = (ci0 == 0);
 #endif
-  if (A.tab != nullptr) {  // single-device training: forward rows of T[l], T[l-1]; backward sums
-    const int c = threadIdx.x, co = c < COUT ? c : 0;
-    const double b0 = slot_sumd(A.L[l].bst + co, 2 * COUT), b1 = slot_sumd(A.L[l].bst + COUT + co, 2 * COUT);
+  if (A.tab != nullptr) {  // single-device training: T[l] (block 6: backward sums), T[l-1]
+    const int c = threadIdx.x;
     if (c < COUT) {
       gr[c] = tab_row(A, l, kTabS)[c];
       mean[c] = tab_row(A, l, kTabMean)[c];
       rstd[c] = tab_row(A, l, kTabRstd)[c];
-      mdy[c] = (float)(b0 * (double)A.inv_count);
-      mdyx[c] = (float)(b1 * (double)A.inv_count);
+      if constexpr (l == 5) {
+        mdy[c] = (float)(slot_sumd(A.L[l].bst + c, 2 * COUT) * (double)A.inv_count);
+        mdyx[c] = (float)(slot_sumd(A.L[l].bst + COUT + c, 2 * COUT) * (double)A.inv_count);
+      } else {
+        mdy[c] = tab_row(A, l, kTabMdy)[c];
+        mdyx[c] = tab_row(A, l, kTabMdyx)[c];
+      }
     }
     if constexpr (!FIRST) {
       if (c < CIN) {
@@ -1944,9 +1952,25 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A)
 // thread j sums row groups j, j + J, ... (8 loads in flight), then the J partials are added in j order
 // through LDS.  J > 1 when the row groups outnumber the columns' parallelism (block 1: 512 row groups
 // of 928 float4 columns took 26 us with one thread per column).
+struct TabBwd {  // backward rows of one block's parameter table entry (wgrad_reduce's side job)
+  const double* bst;  // [kStatSlots][2][cc]
+  float* mdy;
+  float* mdyx;
+  int cc;
+  float inv_count;
+};
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int rgs, int kcc, int cout,
-                                                           float* __restrict__ gw, float* __restrict__ gb, int J) {
+                                                           float* __restrict__ gw, float* __restrict__ gb, int J,
+                                                           TabBwd tb) {
   __shared__ f32x4 red[256];
+  if (blockIdx.y == 1) {  // the table's backward rows of the block the NEXT dgrad / wgrad read
+    const int c = threadIdx.x;
+    if (blockIdx.x == 0 && c < tb.cc) {
+      tb.mdy[c] = (float)(slot_sumd(tb.bst + c, 2 * tb.cc) * (double)tb.inv_count);
+      tb.mdyx[c] = (float)(slot_sumd(tb.bst + tb.cc + c, 2 * tb.cc) * (double)tb.inv_count);
+    }
+    return;
+  }
   const int S = kcc + cout;  // a multiple of 4 (Cout is)
   const int S4 = S >> 2;
   const int ncol = 256 / J;
@@ -2277,8 +2301,19 @@ static void wg_launch(const Args& A, hipStream_t st) {
     int J = 1;
     while (J < 16 && rgs >= 16 * J && (long long)s4 * J < 256LL * 1024) J *= 2;
     const int blocks = std::min(2048, (s4 * J + 255) / 256);
-    hipLaunchKernelGGL(train::wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, A.wpart, rgs, kcc, train::C[l + 1],
-                       A.L[l].gw, A.L[l].gb, J);
+    // side job: block l-1's backward rows of the parameter table (bst[l-1] is complete after dgrad<l>,
+    // which ran before this wgrad) for dgrad<l-1> / wgrad<l-1>
+    train::TabBwd tb = {};
+    const bool side = A.tab != nullptr && l >= 1;
+    if (side) {
+      tb.bst = A.L[l - 1].bst;
+      tb.cc = train::C[l];
+      tb.mdy = A.tab + ((l - 1) * train::kTabRows + train::kTabMdy) * 256;
+      tb.mdyx = A.tab + ((l - 1) * train::kTabRows + train::kTabMdyx) * 256;
+      tb.inv_count = A.inv_count;
+    }
+    hipLaunchKernelGGL(train::wgrad_reduce_kernel, dim3(blocks, side ? 2 : 1), dim3(256), 0, st, A.wpart, rgs, kcc,
+                       train::C[l + 1], A.L[l].gw, A.L[l].gb, J, tb);
   }
 }
 
