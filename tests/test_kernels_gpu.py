@@ -105,3 +105,22 @@ def test_metrics_kernel_matches_bucketize():
     np.testing.assert_array_equal(auc_d.neg_hist, auc_h.neg_hist)
     assert acc_d.result() == acc_h.result()
     assert abs(auc_d.result() - auc_h.result()) < 1e-12
+
+
+def test_zero_buffers_one_launch():
+    """ops zero_buffers: several buffers of mixed dtypes / sizes (not multiples of 16 B, unaligned
+    views) cleared by one launch; neighbouring memory untouched."""
+    import torch
+
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import _ext
+
+    _ext.require()
+    dev = torch.device("cuda")
+    a = torch.full((1001,), 3.0, dtype=torch.float64, device=dev)
+    b = torch.full((7,), 2.0, device=dev)
+    big = torch.full((1 << 20,), 1.0, device=dev)
+    c = big[1: 1 + 777777]  # 4-B aligned, not 16-B aligned
+    _ext.ops().zero_buffers([a, b, c])
+    torch.cuda.synchronize()
+    assert a.abs().sum().item() == 0 and b.abs().sum().item() == 0 and c.abs().sum().item() == 0
+    assert big[0].item() == 1.0 and big[1 + 777777:].eq(1.0).all().item()
