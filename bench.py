@@ -271,8 +271,22 @@ class _HipEngine:
         self.world, self.start, self.n_glob, self.seed, self.passes, self.sync = world, start, n_glob, seed, passes, sync
         self.params_mcd = params_mcd
         self.params_de = params_de
-        # batch-BN MCD: samples (passes x windows) per layer-kernel launch (probe override)
-        self.max_samples = int(os.environ.get("APNEAUQ_MCD_MAX_SAMPLES", 1 << 18))
+        # batch-BN MCD: samples (passes x windows) per layer-kernel launch.  All T passes in ONE chunk when
+        # the activations fit (T x N x 64 rows x 864 bf16 channels of R_2..R_6: ~90 GB at T=50, N=16384 --
+        # sized for 288 GB of HBM3E; fewer launch tails than 4 chunks of 2^18 samples, ~1 %), halved
+        # until they fit in half of the free device memory.  APNEAUQ_MCD_MAX_SAMPLES overrides (probes).
+        env = os.environ.get("APNEAUQ_MCD_MAX_SAMPLES")
+        if env:
+            self.max_samples = int(env)
+        else:
+            import torch
+
+            free = torch.cuda.mem_get_info(params_mcd["conv1d_1/kernel"].device)[0]
+            per_sample = 64 * sum(b.filters for b in spec.blocks[1:]) * 2
+            ms = 1 << 20
+            while ms > (1 << 16) and ms * per_sample > 0.5 * free:
+                ms >>= 1
+            self.max_samples = ms
         self.blob_mcd = fused.pack_blob(spec, params_mcd).unsqueeze(0)
         self.blobs_de = torch.stack([fused.pack_blob(spec, p) for p in params_de])
         # the batch-BN model owns its own parameter copy: its moving statistics are mutated every pass
