@@ -286,6 +286,12 @@ class _HipEngine:
             ms = 1 << 20
             while ms > (1 << 16) and ms * per_sample > 0.5 * free:
                 ms >>= 1
+            if world > 1:  # every rank must chunk the passes identically (one SyncBN all-reduce per chunk)
+                import torch.distributed as dist
+
+                t = torch.tensor([ms], dtype=torch.int64, device=params_mcd["conv1d_1/kernel"].device)
+                dist.all_reduce(t, op=dist.ReduceOp.MIN)
+                ms = int(t.item())
             self.max_samples = ms
         self.blob_mcd = fused.pack_blob(spec, params_mcd).unsqueeze(0)
         self.blobs_de = torch.stack([fused.pack_blob(spec, p) for p in params_de])

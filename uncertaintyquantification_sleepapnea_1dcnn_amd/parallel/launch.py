@@ -102,5 +102,8 @@ def check_world(expected: int, world: int, device_count: Optional[int] = None, d
         sys.stderr.write(f"apneauq: --gpus {expected} but WORLD_SIZE={world}; refusing to run\n")
         raise SystemExit(3)
     if device_type == "cuda" and device_count is not None and device_count < world:
+        if os.environ.get("APNEAUQ_REHEARSE_SHARED_GPU") == "1":  # multi-rank rehearsal on one card (gloo)
+            sys.stderr.write(f"apneauq: REHEARSAL: {world} ranks share {device_count} GPU(s); not a measurement\n")
+            return
         sys.stderr.write(f"apneauq: {world} ranks but only {device_count} visible GPU(s); refusing to share devices\n")
         raise SystemExit(3)
