@@ -154,7 +154,8 @@ __device__ __forceinline__ int row_time(int grow) { return (grow - kHalo) & 63; 
 // values compute garbage): 4 = no copy-out, 8 = no conv MFMAs, 16 = no input staging, 32 = no epilogue
 // moments, 64 = no dropout hashing (copy-out / hash-in staging), 128 = every weight-fragment load reads
 // k-step 0 (L1-resident: the conv without its L2 weight stream), 256 = staging reads an L2-resident
-// 16-tile window instead of its own rows (decode kept), 512 = one workgroup per CU (LDS request doubled).
+// 16-tile window instead of its own rows (decode kept), 512 = one workgroup per CU (LDS request doubled),
+// 1024 = constant BN affine (no slot sums in the prologue: 1-2 us per training launch, session 3).
 #ifndef APNEAUQ_FWD_ABL
 #define APNEAUQ_FWD_ABL 0
 #endif
@@ -921,7 +922,11 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
           [&](int i) -> bf16x8 { return gld<bf16x8>(A.x + (long long)row0 * 4 + i * 8); },
           [&](int i, const bf16x8& v) { reinterpret_cast<bf16x8*>(act)[i] = v; });
     } else {
-      if (g0 != gaff || g1 != g0) {  // (re)load the affine of block l-1 for this tile's group(s)
+      if ((APNEAUQ_FWD_ABL & 1024) && gaff < 0) {  // probe: constant affine (no slot loads)
+        for (int c = threadIdx.x; c < 1024; c += kThreads) prm[c] = 0.5f;
+        gaff = g0;
+        __syncthreads();
+      } else if (g0 != gaff || g1 != g0) {  // (re)load the affine of block l-1 for this tile's group(s)
         bn_affine_to_lds(A, l - 1, g0, prm, prm + 512, nullptr, nullptr);
         if (g1 != g0) bn_affine_to_lds(A, l - 1, g1, prm + 256, prm + 768, nullptr, nullptr);
         gaff = (g1 == g0) ? g0 : -1;
