@@ -2187,7 +2187,14 @@ static train::DetDst det_dst(void* p0, int c0, int f0, void* p1 = nullptr, int c
 }
 
 // floats of the deterministic-mode partial table for a batch of B samples (fwd / head / dgrad reuse it)
-static int fwd_grid(int B) { return std::min((B + 1) / 2, 256 * 8); }
+// Persistent forward: workgroups per CU (2 are resident at a time), each over a contiguous tile range.
+// Batch-BN MC Dropout (409,600 tiles per layer launch) measured 8 / 16 / 32 / 64 per CU: MCD phase
+// 91.9 / 91.1-91.4 / 91.0-91.4 / 90.5-90.9 ms (tools/probes/so_bench1.sh, one box): shorter ranges
+// balance the launch tail.  Batches of <= 16384 tiles (training) get one tile per workgroup anyway.
+#ifndef APNEAUQ_FWD_WG_PER_CU
+#define APNEAUQ_FWD_WG_PER_CU 64
+#endif
+static int fwd_grid(int B) { return std::min((B + 1) / 2, 256 * APNEAUQ_FWD_WG_PER_CU); }
 int train_det_floats(int B) {
   const int tiles = (B + 1) / 2;
   return std::max({fwd_grid(B) * 2 * 256, B * train::kHeadRec, tiles * 2 * 2 * 256});
