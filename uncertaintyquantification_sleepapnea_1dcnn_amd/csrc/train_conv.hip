@@ -757,6 +757,83 @@ struct Conv {
   }
 };
 
+// Pair-split implicit-GEMM conv tile (4 waves, every wave over all 8 row tiles): the NCT = 2 * PT
+// channel tiles go to two wave pairs, pair p owning tiles [p PT, p PT + PT) with PT odd; wave q of a
+// pair takes CT = (PT - 1) / 2 full tiles and the pair's middle tile for its own sample slot (row
+// tiles 4q .. 4q + 3).  Every wave issues the same MFMA count, and a weight fragment is loaded by one
+// wave (full tiles) or two (middle tiles) instead of by both wave rows of the WM = 2 tiling the
+// 96- and 224-channel layers use otherwise; the price is 8 instead of 4 B-fragment LDS reads per
+// k-step.  (The fused inference kernel measured this split slower for 96 channels, being bound by
+// LDS there; the batch-BN layer kernels are bound by the vector-memory return path.)
+template <int CIN, int COUT, int K>
+struct ConvHalf {
+  static constexpr int NSTEP = (CIN * K + 31) / 32;
+  static constexpr int NCT = COUT / 16, PT = NCT / 2, CT = (PT - 1) / 2, RT = kRT, HR = kRT / 2;
+  static constexpr int PAD = (K - 1) / 2;
+  static_assert(NCT % 2 == 0 && PT % 2 == 1 && CIN % 32 == 0, "pair split tiling");
+
+  // first full tile / middle tile of wave (p, q)
+  __device__ __forceinline__ static int full0(int wave) { return (wave >> 1) * PT + ((wave & 1) ? CT + 1 : 0); }
+  __device__ __forceinline__ static int mid(int wave) { return (wave >> 1) * PT + CT; }
+
+  template <int Q>
+  __device__ __forceinline__ static void run_q(const gbf16x8* wfrag, const char* lds, int ldsrs, f32x4 (&acc)[CT][RT],
+                                               f32x4 (&acch)[HR]) {
+    const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3;
+    const int m = lane & 15, h = lane >> 4;
+    const gbf16x8* wp = wfrag + full0(wave) * 64 + lane;
+    const gbf16x8* wph = wfrag + mid(wave) * 64 + lane;
+    const char* bbase = lds + (kHalo + m - PAD) * ldsrs + 16 * h;
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+#pragma unroll
+      for (int r = 0; r < RT; ++r) acc[c][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < HR; ++r) acch[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto load_b = [&](int s, int r) -> bf16x8 {
+      constexpr int CB = CIN / 32;
+      const int tap = s / CB, cb = s - tap * CB;
+      const int soff = __builtin_amdgcn_readfirstlane(tap * ldsrs + cb * 64);
+      return *reinterpret_cast<const bf16x8*>(bbase + soff + r * 16 * ldsrs);
+    };
+    bf16x8 a[2][CT], ah[2];
+    auto load_a = [&](int s, int st) {
+#pragma unroll
+      for (int c = 0; c < CT; ++c) a[st][c] = wp[(s * NCT + c) * 64];
+      ah[st] = wph[s * NCT * 64];
+    };
+    auto step = [&](int s, int st) {
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        const bf16x8 b = load_b(s, r);
+#pragma unroll
+        for (int c = 0; c < CT; ++c) acc[c][r] = mfma16(a[st][c], b, acc[c][r]);
+        if ((r >> 2) == Q) acch[r & 3] = mfma16(ah[st], b, acch[r & 3]);  // unrolled: compile-time
+      }
+    };
+    load_a(0, 0);
+    constexpr int NFULL = NSTEP / 2 * 2;
+#pragma unroll 1
+    for (int s0 = 0; s0 < NFULL; s0 += 2) {
+      load_a(s0 + 1, 1);  // s0 + 1 < NFULL <= NSTEP
+      __builtin_amdgcn_sched_barrier(0);
+      step(s0, 0);
+      load_a(s0 + 2 < NSTEP ? s0 + 2 : NSTEP - 1, 0);  // clamped, unconditional
+      __builtin_amdgcn_sched_barrier(0);
+      step(s0 + 1, 1);
+    }
+    if constexpr (NSTEP % 2) step(NSTEP - 1, 0);
+  }
+
+  __device__ __forceinline__ static void run(const gbf16x8* wfrag, const char* lds, int ldsrs, f32x4 (&acc)[CT][RT],
+                                             f32x4 (&acch)[HR]) {
+    if ((threadIdx.x >> 6) & 1)  // wave-uniform
+      run_q<1>(wfrag, lds, ldsrs, acc, acch);
+    else
+      run_q<0>(wfrag, lds, ldsrs, acc, acch);
+  }
+};
+
 template <int SWZ = 0>
 __device__ __forceinline__ bf16x8 tr_frag(const char* lds, int ldsrs, int row_base, int col0) {
   // fragment for a 16x16x32 operand whose K index is the LDS row, 32 rows from row_base.  Lane
@@ -806,6 +883,15 @@ template <int l> struct FwdPD { static constexpr int v = 1; };
 #define APNEAUQ_FWD_SPLIT 32
 #endif
 template <int l> struct FwdStageSplit { static constexpr bool v = (APNEAUQ_FWD_SPLIT >> l) & 1; };
+// Forward conv of block l on the pair-split tiling (ConvHalf; 96- and 224-channel outputs, l >= 1).
+// APNEAUQ_FWD_HALF = bit mask over blocks; off: batch-BN MCD phase 90.5-90.8 ms with the WM = 2
+// tilings, 90.6-90.8 with block 3 (224 ch) split, 92.0-92.4 / 93.0 with block 6 / block 4 (96 ch)
+// split (tools/probes/half_check.sh, one box): the extra B-fragment LDS reads cost more than the
+// weight loads they save.  Tested for correctness against the reference (same probe).
+#ifndef APNEAUQ_FWD_HALF
+#define APNEAUQ_FWD_HALF 0
+#endif
+template <int l> struct FwdHalf { static constexpr bool v = l >= 1 && ((APNEAUQ_FWD_HALF >> l) & 1); };
 
 // wave tilings (WM, WN) per output-channel count
 template <int COUT> struct Tiling;
@@ -947,6 +1033,48 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
     }
     __syncthreads();
     APNEAUQ_FST(1, kst);
+    // epilogue of one 16 x 16 accumulator tile: bias + ReLU -> bf16 LDS tile (rows outside the batch /
+    // pad rows: 0).  Only the row tiles holding t = 48..63 (pad rows on lanes m >= 12) and the batch's
+    // last tile need the select.
+    const bool last_tile = smp0 + 1 >= A.B;  // workgroup-uniform
+    auto epi = [&](const f32x4& a4, int co0, int rtg, const f32x4& bias) {
+      const int row = rtg * 16 + m;  // 0..127 within the tile (rtg wave-uniform)
+      f32x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = fmaxf(a4[i] + bias[i], 0.f);
+      if ((rtg & 3) == 3 || last_tile) {
+        const bool valid = (row & 63) < kL && (smp0 + (row >> 6)) < A.B;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[i] = valid ? v[i] : 0.f;
+          asm volatile("" : "+v"(v[i]));  // keep the select in fp32 (no per-element cvt + v_perm repack)
+        }
+      }
+      bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+      *reinterpret_cast<bf16x4*>(act + row * kRS + co0 * 2) = o;
+    };
+    if constexpr (FwdHalf<l>::v) {  // pair-split tiling (ConvHalf)
+      using CH = ConvHalf<CIN, COUT, KS[l]>;
+      f32x4 acc[CH::CT][CH::RT], acch[CH::HR];
+      if constexpr (APNEAUQ_FWD_PRIO) __builtin_amdgcn_s_setprio(1);
+      CH::run(Ly.wf, act, IN_RS, acc, acch);
+      if constexpr (APNEAUQ_FWD_PRIO) __builtin_amdgcn_s_setprio(0);
+      APNEAUQ_FST(2, kst);
+      __syncthreads();  // all waves done reading the staged input; reuse it for the output tile
+      APNEAUQ_FST(3, kst);
+      const int f0 = CH::full0(wave), q = wave & 1;
+#pragma unroll
+      for (int c = 0; c < CH::CT; ++c) {
+        const int co0 = (f0 + c) * 16 + 4 * h;
+        const f32x4 bias = gld<f32x4>(Ly.bias + co0);
+#pragma unroll
+        for (int r = 0; r < CH::RT; ++r) epi(acc[c][r], co0, r, bias);
+      }
+      const int coh = CH::mid(wave) * 16 + 4 * h;
+      const f32x4 biash = gld<f32x4>(Ly.bias + coh);
+#pragma unroll
+      for (int r = 0; r < CH::HR; ++r) epi(acch[r], coh, q * CH::HR + r, biash);
+    } else {
     f32x4 acc[CV::CT][CV::RT];
 #if (APNEAUQ_FWD_ABL & 8)
 #pragma unroll
@@ -964,32 +1092,13 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
     APNEAUQ_FST(2, kst);
     __syncthreads();  // all waves done reading the staged input; reuse it for the output tile
     APNEAUQ_FST(3, kst);
-
-    // epilogue: bias + ReLU -> bf16 LDS tile (rows outside the batch / pad rows: 0).  Only the row
-    // tiles holding t = 48..63 (pad rows on lanes m >= 12) and the batch's last tile need the select.
-    const bool last_tile = smp0 + 1 >= A.B;  // workgroup-uniform
 #pragma unroll
     for (int c = 0; c < CV::CT; ++c) {
       const int co0 = (wn * CV::CT + c) * 16 + 4 * h;
       const f32x4 bias = gld<f32x4>(Ly.bias + co0);
 #pragma unroll
-      for (int r = 0; r < CV::RT; ++r) {
-        const int rtg = wm * CV::RT + r;  // row tile in the tile (wave-uniform)
-        const int row = rtg * 16 + m;     // 0..127 within the tile
-        f32x4 v;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = fmaxf(acc[c][r][i] + bias[i], 0.f);
-        if ((rtg & 3) == 3 || last_tile) {
-          const bool valid = (row & 63) < kL && (smp0 + (row >> 6)) < A.B;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            v[i] = valid ? v[i] : 0.f;
-            asm volatile("" : "+v"(v[i]));  // keep the select in fp32 (no per-element cvt + v_perm repack)
-          }
-        }
-        bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
-        *reinterpret_cast<bf16x4*>(act + row * kRS + co0 * 2) = o;
-      }
+      for (int r = 0; r < CV::RT; ++r) epi(acc[c][r], co0, wm * CV::RT + r, bias);
+    }
     }
     __syncthreads();
     APNEAUQ_FST(4, kst);
