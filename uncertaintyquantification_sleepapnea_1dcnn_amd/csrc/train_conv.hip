@@ -160,6 +160,9 @@ __device__ __forceinline__ int row_time(int grow) { return (grow - kHalo) & 63; 
 #define APNEAUQ_FWD_ABL 0
 #endif
 // 1: the forward kernels load tile i+1's input while tile i's moments and copy-out run (0: probe)
+#ifndef APNEAUQ_FWD_SKIPPAD
+#define APNEAUQ_FWD_SKIPPAD 1
+#endif
 #ifndef APNEAUQ_FWD_PIPE
 #define APNEAUQ_FWD_PIPE 0
 #endif
@@ -944,7 +947,10 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
   double* st = Ly.st + (blockIdx.x % kStatSlots) * st_stride(A, COUT);
   constexpr int CW = COUT / 8;             // 16-B chunks per output row
   constexpr int RPo = kThreads / CW;       // rows per copy-out pass
-  constexpr int NPo = (kR + RPo - 1) / RPo;
+  // copy-out rows: the tile's 2 x 60 valid time steps only (APNEAUQ_FWD_SKIPPAD; the R buffers are
+  // allocated filled with -0.0 and their pad rows are never written), else all 128 rows
+  constexpr int kOutRows = APNEAUQ_FWD_SKIPPAD ? kSlots * kL : kR;
+  constexpr int NPo = (kOutRows + RPo - 1) / RPo;
   const int ocw = threadIdx.x % CW, orin = threadIdx.x / CW;
   const bool oact = orin < RPo;
   constexpr int NCTo = COUT / 16, CPW = (NCTo + 3) / 4;  // moment channel tiles: ct = wave + 4j
@@ -1142,9 +1148,17 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
       asm volatile("" : "+v"(rin));
 #pragma unroll 2
       for (int k = 0; k < NPo; ++k) {
-        const int r = rin + k * RPo;
-        if (!oact || r >= kR) continue;
-        const int slot = r >> 6, tt = r & 63;
+        const int rc = rin + k * RPo;
+        if (!oact || rc >= kOutRows) continue;
+        int slot, tt;
+        if constexpr (APNEAUQ_FWD_SKIPPAD) {
+          slot = rc >= kL;
+          tt = rc - kL * slot;
+        } else {
+          slot = rc >> 6;
+          tt = rc & 63;
+        }
+        const int r = slot * kSR + tt;
         bf16x8 o = *reinterpret_cast<const bf16x8*>(act + r * kRS + ocw * 16);
         uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
         if (!(tt < kL && smp0 + slot < A.B)) {  // pad / out-of-batch rows: -0.0, decoded as A = 0

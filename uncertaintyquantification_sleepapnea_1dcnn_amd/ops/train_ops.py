@@ -83,12 +83,11 @@ class TrainWorkspace:
         ks = [b.kernel_size for b in spec.blocks]
         bf = torch.bfloat16
         self.x = torch.zeros(rows0, ch[0], dtype=bf, device=dev)
-        self.R = [torch.zeros(rows0 if l == 0 else rows, ch[l + 1], dtype=bf, device=dev) for l in range(6)]
-        # the halo rows before the first / after the last tile are never written by the kernels: -0.0
-        # there decodes to A = 0 like every pad row (train_conv.hip decode_pair)
-        for r in self.R:
-            r[:HALO].fill_(-0.0)
-            r[-HALO:].fill_(-0.0)
+        # -0.0 everywhere: the halo rows before the first / after the last tile and the 4 pad rows of
+        # every sample are never written by the kernels (train_conv.hip APNEAUQ_FWD_SKIPPAD), and -0.0
+        # decodes to A = 0 (decode_pair) like a dropped element
+        self.R = [torch.empty(rows0 if l == 0 else rows, ch[l + 1], dtype=bf, device=dev).fill_(-0.0)
+                  for l in range(6)]
         self.dY = [torch.zeros(rows, ch[l + 1], dtype=bf, device=dev) if (with_backward and l < 5)
                    else torch.zeros(16, dtype=bf, device=dev) for l in range(6)]
         # dZ_l materialised by dgrad_l for wgrad_l (block 1 has no dgrad)
