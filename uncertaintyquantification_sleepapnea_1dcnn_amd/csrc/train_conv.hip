@@ -160,6 +160,9 @@ __device__ __forceinline__ int row_time(int grow) { return (grow - kHalo) & 63; 
 #define APNEAUQ_FWD_ABL 0
 #endif
 // 1: the forward kernels load tile i+1's input while tile i's moments and copy-out run (0: probe)
+#ifndef APNEAUQ_FWD_STAGEPAD
+#define APNEAUQ_FWD_STAGEPAD 1
+#endif
 #ifndef APNEAUQ_FWD_SKIPPAD
 #define APNEAUQ_FWD_SKIPPAD 1
 #endif
@@ -443,13 +446,28 @@ __device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, i
 // tile's two samples to their window's rows, all other rows (halo rows of the neighbours) to pad
 // row 60, which holds -0.0 and decodes to 0 -- and block 1's dropout mask is drawn here from the
 // counter hash on every row, as sign bits (pad rows stay -0.0 whatever it draws).
+//
+// APNEAUQ_FWD_STAGEPAD (default): only the tile's 2 x 60 valid rows are loaded; the 16 halo / pad rows
+// of the LDS tile (0-3, 64-67, 128-135) are written as zeros instead (no global load, no decode).
 template <int l, bool HASH_IN>  // HASH_IN: may run in hash_in mode (runtime flag, workgroup-uniform)
 struct ActStager {
   static constexpr int Cc = C[l + 1];
   static constexpr int NCW = Cc / 8;
   static constexpr int RP = kThreads / NCW;  // rows per pass over the workgroup
-  static constexpr int NK = (kRows + RP - 1) / RP;
+  static constexpr bool CMP = APNEAUQ_FWD_STAGEPAD != 0;
+  static constexpr int NR = CMP ? kSlots * kL : kRows;  // rows loaded from memory
+  static constexpr int NK = (NR + RP - 1) / RP;
   u32x4 v[NK];
+
+  // LDS row of loaded row rc (compact: the slot's time step, skipping halo and pad rows)
+  __device__ __forceinline__ static int lds_row(int rc) {
+    if constexpr (CMP) {
+      const int slot = rc >= kL;
+      return kHalo + slot * kSR + (rc - kL * slot);
+    } else {
+      return rc;
+    }
+  }
 
   __device__ __forceinline__ static int tid() {
     int t = threadIdx.x;
@@ -475,18 +493,24 @@ struct ActStager {
       const __bf16* src1 = R + (long long)(kHalo + (n1 - g1 * A.n_win) * kSR) * Cc;
 #pragma unroll
       for (int u = U0; u < U1; ++u) {
-        const int r = rin + u * RP;
-        if (r >= kRows) continue;
-        const int grow = row0 + r;
-        const int n = row_sample(grow);
-        const bool own = grow >= kHalo && (n == smp0 || n == smp0 + 1);
-        v[u] = gld<u32x4>((n == smp0 + 1 ? src1 : src0) + (long long)(own ? row_time(grow) : kL) * Cc);
+        const int rc = rin + u * RP;
+        if (rc >= NR) continue;
+        if constexpr (CMP) {
+          const int slot = rc >= kL;
+          v[u] = gld<u32x4>((slot ? src1 : src0) + (long long)(rc - kL * slot) * Cc);
+        } else {
+          const int grow = row0 + rc;
+          const int n = row_sample(grow);
+          const bool own = grow >= kHalo && (n == smp0 || n == smp0 + 1);
+          v[u] = gld<u32x4>((n == smp0 + 1 ? src1 : src0) + (long long)(own ? row_time(grow) : kL) * Cc);
+        }
       }
     } else {
 #pragma unroll
       for (int u = U0; u < U1; ++u) {
-        const int r = rin + u * RP;
-        if (r < kRows) v[u] = gld<u32x4>(R + (long long)(((APNEAUQ_FWD_ABL & 256) ? (row0 & 2047) : row0) + r) * Cc);
+        const int rc = rin + u * RP;
+        if (rc < NR)
+          v[u] = gld<u32x4>(R + (long long)(((APNEAUQ_FWD_ABL & 256) ? (row0 & 2047) : row0) + lds_row(rc)) * Cc);
       }
     }
   }
@@ -496,6 +520,13 @@ struct ActStager {
   __device__ __forceinline__ void store(const Args& A, char* lds, int row0, const float* s, const float* t,
                                         int g0, bool hash_in) const {
     const int tt_ = tid(), cw = tt_ % NCW, rin = tt_ / NCW;
+    if constexpr (CMP) {
+      if (U0 == 0)  // the 16 halo / pad rows of the LDS tile: zeros (0-3, 64-67, 128-135)
+        for (int i = tt_; i < 16 * NCW; i += kThreads) {
+          const int pi = i / NCW, pr = pi < 4 ? pi : (pi < 8 ? kL + pi : 2 * kL + pi);
+          *reinterpret_cast<u32x4*>(lds + pr * kRS + (i - pi * NCW) * 16) = u32x4{0u, 0u, 0u, 0u};
+        }
+    }
     if (rin >= RP) return;
     const Layer& Ly = A.L[l];
     const int c = cw * 8;
@@ -518,15 +549,17 @@ struct ActStager {
     auto run = [&](auto two_groups, auto hashed) {
 #pragma unroll
       for (int u = U0; u < U1; ++u) {
-        const int r = rin + u * RP;
-        if (r >= kRows) continue;
+        const int rc = rin + u * RP;
+        if (rc >= NR) continue;
+        const int r = lds_row(rc);
         const int grow = row0 + r;
-        const bool hi = row_sample(grow) == smp0 + 1;
+        const bool hi = CMP ? rc >= kL : row_sample(grow) == smp0 + 1;
+        const int tstep = CMP ? rc - kL * (rc >= kL) : row_time(grow);
         u32x4 o;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           uint32_t d = v[u][q];
-          if constexpr (decltype(hashed)::value) d |= drop_signs2(dropout_bits2(hi ? key1 : key0, row_time(grow), c + 2 * q), thr2);
+          if constexpr (decltype(hashed)::value) d |= drop_signs2(dropout_bits2(hi ? key1 : key0, tstep, c + 2 * q), thr2);
           if constexpr (decltype(two_groups)::value)  // rare: a tile straddling an MC-Dropout pass boundary
             o[q] = decode_pair(d, hi ? s1[2 * q] : s0[2 * q], hi ? t1[2 * q] : t0[2 * q],
                                hi ? s1[2 * q + 1] : s0[2 * q + 1], hi ? t1[2 * q + 1] : t0[2 * q + 1]);
@@ -883,7 +916,7 @@ template <int l> struct FwdPD { static constexpr int v = 1; };
 // into scratch with one batch; split, it spills none and its batch-BN MC-Dropout chunk is ~2 % faster
 // (profiles/batch_bn_fwd_r2.md, session 3).  APNEAUQ_FWD_SPLIT = bit mask over blocks (probes).
 #ifndef APNEAUQ_FWD_SPLIT
-#define APNEAUQ_FWD_SPLIT 32
+#define APNEAUQ_FWD_SPLIT 36  // blocks 3 and 6 (block 3 spilled 22 VGPRs with the compact staging)
 #endif
 template <int l> struct FwdStageSplit { static constexpr bool v = (APNEAUQ_FWD_SPLIT >> l) & 1; };
 // Forward conv of block l on the pair-split tiling (ConvHalf; 96- and 224-channel outputs, l >= 1).
