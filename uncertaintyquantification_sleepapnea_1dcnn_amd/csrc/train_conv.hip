@@ -40,7 +40,10 @@ namespace train {
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 
 constexpr int kL = 60, kSR = 64, kSlots = 2, kR = 128, kRT = 8, kHalo = 4, kRows = 136;
-constexpr int kRS = 256 * 2 + 32;  // LDS row stride (bytes) of staged activations
+#ifndef APNEAUQ_KRS  // LDS row stride (bytes) of the staged activation tiles (probes vary it)
+#define APNEAUQ_KRS (256 * 2 + 32)
+#endif
+constexpr int kRS = APNEAUQ_KRS;
 constexpr int kThreads = 256;
 constexpr int C[7] = {4, 128, 192, 224, 96, 256, 96};
 constexpr int KS[6] = {7, 5, 3, 7, 9, 9};
