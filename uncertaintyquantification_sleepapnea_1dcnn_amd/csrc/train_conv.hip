@@ -1901,11 +1901,25 @@ template <int l> struct WgCfg;
 // workgroups per CU save 17 % on block 4 and spill on block 6)
 // wgrad LDS tiles: the row stride is an odd multiple of 32 B (conflict-free tr_frag reads)
 __host__ __device__ constexpr int wg_rs(int width_bytes) { return (width_bytes / 32) % 2 ? width_bytes : width_bytes + 32; }
+// minimum wgrad workgroup counts of blocks 2-5 (probe overrides; batch-1024 step measured with
+// tools/probes/train_variants.sh: block 5 512 -> 768 took the step 0.795 -> 0.786 ms)
+#ifndef APNEAUQ_WG1_MINWG
+#define APNEAUQ_WG1_MINWG 256
+#endif
+#ifndef APNEAUQ_WG2_MINWG
+#define APNEAUQ_WG2_MINWG 256
+#endif
+#ifndef APNEAUQ_WG3_MINWG
+#define APNEAUQ_WG3_MINWG 512
+#endif
+#ifndef APNEAUQ_WG4_MINWG
+#define APNEAUQ_WG4_MINWG 768
+#endif
 template <> struct WgCfg<0> { static constexpr int CIB = 32, COB = 128, WCO = 4, WCI = 1, RTILES = 2, MINWG = 512, U = 4, MINB = 2; };  // im2col kk=32
-template <> struct WgCfg<1> { static constexpr int CIB = 32, COB = 192, WCO = 2, WCI = 2, RTILES = 8, MINWG = 256, U = 8, MINB = 2; };
-template <> struct WgCfg<2> { static constexpr int CIB = 32, COB = 224, WCO = 2, WCI = 2, RTILES = 8, MINWG = 256, U = 8, MINB = 2; };
-template <> struct WgCfg<3> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = 512, U = 8, MINB = 3; };
-template <> struct WgCfg<4> { static constexpr int CIB = 16, COB = 128, WCO = 4, WCI = 1, RTILES = 16, MINWG = 512, U = 8, MINB = 3; };
+template <> struct WgCfg<1> { static constexpr int CIB = 32, COB = 192, WCO = 2, WCI = 2, RTILES = 8, MINWG = APNEAUQ_WG1_MINWG, U = 8, MINB = 2; };
+template <> struct WgCfg<2> { static constexpr int CIB = 32, COB = 224, WCO = 2, WCI = 2, RTILES = 8, MINWG = APNEAUQ_WG2_MINWG, U = 8, MINB = 2; };
+template <> struct WgCfg<3> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = APNEAUQ_WG3_MINWG, U = 8, MINB = 3; };
+template <> struct WgCfg<4> { static constexpr int CIB = 16, COB = 128, WCO = 4, WCI = 1, RTILES = 16, MINWG = APNEAUQ_WG4_MINWG, U = 8, MINB = 3; };
 template <> struct WgCfg<5> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = 512, U = 4, MINB = 2; };
 
 
