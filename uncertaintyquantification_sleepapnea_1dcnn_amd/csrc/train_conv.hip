@@ -369,12 +369,25 @@ __device__ __forceinline__ void lds_row8(const float* tab, int c0, float scale, 
 // per row only when it differs.  The dropout mask is R_l's sign bit (set by the producer), so the
 // transform is  a = sign ? 0 : |r| * s + t  on the packed bf16 pairs.
 //
-template <int l, int NR, int NCW, int UMAX = kStageU, int SWZ = 0>
+//
+// CMP (NR = kRows only): load just the tile's 2 x 60 valid rows; the caller keeps the 16 halo / pad
+// rows of the LDS tile (0-3, 64-67, 128-135) at zero.
+template <int l, int NR, int NCW, int UMAX = kStageU, int SWZ = 0, bool CMP = false>
 __device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, int row0, int c0, const float* s,
                                           const float* t, int g0) {
+  static_assert(!CMP || NR == kRows, "compact staging covers a whole 136-row tile");
   constexpr int Cc = C[l + 1];
   constexpr int RP = kThreads / NCW;  // rows per pass over the workgroup
-  constexpr int NK = (NR + RP - 1) / RP;
+  constexpr int NRL = CMP ? kSlots * kL : NR;  // rows loaded
+  constexpr int NK = (NRL + RP - 1) / RP;
+  auto lrow = [](int rc) {  // LDS / tile row of loaded row rc
+    if constexpr (CMP) {
+      const int slot = rc >= kL;
+      return kHalo + slot * kSR + (rc - kL * slot);
+    } else {
+      return rc;
+    }
+  };
   constexpr int U = NK < UMAX ? NK : UMAX;
   const Layer& Ly = A.L[l];
   // opaque thread index (see staged_loop): keeps the per-row addresses out of enclosing tile loops
@@ -410,13 +423,14 @@ __device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, i
         u32x4 v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const int r = rin + (b + u) * RP;
-          if (b + u < NK && active && r < NR) v[u] = gld<u32x4>(Ly.R + (long long)(row0 + r) * Cc + c);
+          const int rc = rin + (b + u) * RP;
+          if (b + u < NK && active && rc < NRL) v[u] = gld<u32x4>(Ly.R + (long long)(row0 + lrow(rc)) * Cc + c);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const int r = rin + (b + u) * RP;
-          if (b + u >= NK || !active || r >= NR) continue;
+          const int rc = rin + (b + u) * RP;
+          if (b + u >= NK || !active || rc >= NRL) continue;
+          const int r = lrow(rc);
           u32x4 o;
           if constexpr (decltype(two_groups)::value) {  // rare: a tile straddling an MC-Dropout pass boundary
             const bool hi = row_sample(row0 + r) != smp0;
@@ -673,18 +687,30 @@ __device__ __forceinline__ void stage_dz(const Args& A, char* lds, int ldsrs, in
   }
 }
 
-template <int l, int NR, int NCW, int UMAX, int SWZ = 0>
+// CMP (NR = kR only): copy just the 2 x 60 valid rows of the tile; its 8 pad rows (60-63, 124-127)
+// stay at the zeros the caller wrote once (dZ is 0 there).
+template <int l, int NR, int NCW, int UMAX, int SWZ = 0, bool CMP = false>
 __device__ __forceinline__ void stage_dz_copy(const Args& A, char* lds, int ldsrs, int row0, int c0) {
+  static_assert(!CMP || NR == kR, "compact copy covers a whole 128-row tile");
   constexpr int Cc = C[l + 1];
+  constexpr int NRL = CMP ? kSlots * kL : NR;
   const Layer& Ly = A.L[l];
-  staged_loop<NR * NCW, UMAX>(
+  auto lrow = [](int rc) {
+    if constexpr (CMP) {
+      const int slot = rc >= kL;
+      return slot * kSR + (rc - kL * slot);
+    } else {
+      return rc;
+    }
+  };
+  staged_loop<NRL * NCW, UMAX>(
       [&](int i) -> bf16x8 {
-        const int r = i / NCW, cw = i - r * NCW;
-        return gld<bf16x8>(Ly.dZ + (long long)(row0 + r) * Cc + c0 + cw * 8);
+        const int rc = i / NCW, cw = i - rc * NCW;
+        return gld<bf16x8>(Ly.dZ + (long long)(row0 + lrow(rc)) * Cc + c0 + cw * 8);
       },
       [&](int i, const bf16x8& o) {
-        const int r = i / NCW, cw = i - r * NCW;
-        *reinterpret_cast<bf16x8*>(lds + lds_off<SWZ>(r, cw * 16, ldsrs)) = o;
+        const int rc = i / NCW, cw = i - rc * NCW;
+        *reinterpret_cast<bf16x8*>(lds + lds_off<SWZ>(lrow(rc), cw * 16, ldsrs)) = o;
       });
 }
 
@@ -1903,6 +1929,9 @@ template <int l> struct WgCfg;
 __host__ __device__ constexpr int wg_rs(int width_bytes) { return (width_bytes / 32) % 2 ? width_bytes : width_bytes + 32; }
 // minimum wgrad workgroup counts of blocks 2-5 (probe overrides; batch-1024 step measured with
 // tools/probes/train_variants.sh: block 5 512 -> 768 took the step 0.795 -> 0.786 ms)
+#ifndef APNEAUQ_WG_CMP  // wgrad stages only the tiles' valid rows (pad rows zeroed once per workgroup)
+#define APNEAUQ_WG_CMP 0  // measured slower at batch 1024: 0.778-0.785 vs 0.769-0.771 ms (session 3)
+#endif
 #ifndef APNEAUQ_WG1_MINWG
 #define APNEAUQ_WG1_MINWG 256
 #endif
@@ -1928,6 +1957,7 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A)
   using W = WgCfg<l>;
   constexpr int CIN = C[l], COUT = C[l + 1], K = KS[l], PAD = (K - 1) / 2;
   constexpr bool FIRST = (l == 0);
+  constexpr bool WG_CMP = !FIRST && APNEAUQ_WG_CMP;  // compact dZ / A staging (valid rows only)
   constexpr int NTAP = FIRST ? 1 : K;           // block 1: taps folded into the im2col columns
   constexpr int NCO = W::COB / 16 / W::WCO;     // co tiles per wave
   constexpr int NCI = W::CIB / 16 / W::WCI;     // ci tiles per wave
@@ -2032,6 +2062,19 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A)
   // sizes the grid for >= ~512 workgroups)
   const int rgs = gridDim.x / (nci_blk * nco_blk);
   const int rt = (ntiles + rgs - 1) / rgs;
+  // compact staging (blocks 2-6): the tiles' halo / pad rows are never staged and read as zeros, so
+  // they are zeroed once here (dZ rows 60-63 / 124-127, A rows 0-3 / 64-67 / 128-135)
+  if constexpr (WG_CMP) {
+    constexpr int DW = W::COB / 8, AW = W::CIB / 8;
+    for (int i = threadIdx.x; i < 8 * DW; i += kThreads) {
+      const int pi = i / DW, pr = pi < 4 ? kL + pi : kSR + kL + (pi - 4);
+      *reinterpret_cast<u32x4*>(dz_lds + lds_off<0>(pr, (i - pi * DW) * 16, DZRS)) = u32x4{0u, 0u, 0u, 0u};
+    }
+    for (int i = threadIdx.x; i < 16 * AW; i += kThreads) {
+      const int pi = i / AW, pr = pi < 4 ? pi : (pi < 8 ? kL + pi : 2 * kL + pi);
+      *reinterpret_cast<u32x4*>(a_lds + lds_off<0>(pr, (i - pi * AW) * 16, ARS)) = u32x4{0u, 0u, 0u, 0u};
+    }
+  }
   for (int it = 0; it < rt; ++it) {
     const int tile = rg * rt + it;
     if (tile >= ntiles) break;
@@ -2041,7 +2084,7 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A)
       stage_dz<l, kR, W::COB / 8, 0>(A, dz_lds, DZRS, row0 + kHalo, co0, gr, mean, rstd, mdy, mdyx);
     else {
 #ifndef APNEAUQ_WG_NODZ  // probe: no dZ staging (wrong dW, timing only)
-      stage_dz_copy<l, kR, W::COB / 8, W::U, 0>(A, dz_lds, DZRS, row0 + kHalo, co0);
+      stage_dz_copy<l, kR, W::COB / 8, W::U, 0, WG_CMP>(A, dz_lds, DZRS, row0 + kHalo, co0);
 #endif
     }
     if constexpr (FIRST) {
@@ -2055,7 +2098,7 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A)
       }
     } else {
 #ifndef APNEAUQ_WG_NOA  // probe: no A_{l-1} staging (wrong dW, timing only)
-      stage_act<l - 1, kRows, W::CIB / 8, 4, 0>(A, a_lds, ARS, row0, ci0, sp, tp, 0);
+      stage_act<l - 1, kRows, W::CIB / 8, 4, 0, WG_CMP>(A, a_lds, ARS, row0, ci0, sp, tp, 0);
 #endif
     }
     __syncthreads();
