@@ -1,14 +1,14 @@
 """Busy vs idle time of the GPU over a rocprofv3 kernel trace (csv): per-kernel sums, the union of
 kernel intervals and the gaps between consecutive dispatches (launch / graph-node overhead).
 
-    python tools/probes/gap_report.py <kernel_trace.csv> [name-substring-that-starts-a-step]
+    python tools/probes/gap_report.py <kernel_trace.csv>
 """
 import csv
 import sys
 from collections import defaultdict
 
 
-def main(path, mark=None):
+def main(path):
     rows = list(csv.DictReader(open(path)))
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
     # keep the last half of the trace (steady state)
@@ -37,4 +37,4 @@ def main(path, mark=None):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
+    main(sys.argv[1])
