@@ -1928,12 +1928,13 @@ template <int l> struct WgCfg;
 // wgrad LDS tiles: the row stride is an odd multiple of 32 B (conflict-free tr_frag reads)
 __host__ __device__ constexpr int wg_rs(int width_bytes) { return (width_bytes / 32) % 2 ? width_bytes : width_bytes + 32; }
 // minimum wgrad workgroup counts of blocks 2-5 (probe overrides; batch-1024 step measured with
-// tools/probes/train_variants.sh: block 5 512 -> 768 took the step 0.795 -> 0.786 ms)
+// tools/probes/train_variants.sh: block 5 512 -> 768 took the step 0.795 -> 0.786 ms, block 2
+// 256 -> 512 0.766-0.775 -> 0.758-0.768 ms over three interleaved rounds)
 #ifndef APNEAUQ_WG_CMP  // wgrad stages only the tiles' valid rows (pad rows zeroed once per workgroup)
 #define APNEAUQ_WG_CMP 0  // measured slower at batch 1024: 0.778-0.785 vs 0.769-0.771 ms (session 3)
 #endif
 #ifndef APNEAUQ_WG1_MINWG
-#define APNEAUQ_WG1_MINWG 256
+#define APNEAUQ_WG1_MINWG 512
 #endif
 #ifndef APNEAUQ_WG2_MINWG
 #define APNEAUQ_WG2_MINWG 256
