@@ -1933,6 +1933,12 @@ __host__ __device__ constexpr int wg_rs(int width_bytes) { return (width_bytes /
 #ifndef APNEAUQ_WG_CMP  // wgrad stages only the tiles' valid rows (pad rows zeroed once per workgroup)
 #define APNEAUQ_WG_CMP 0  // measured slower at batch 1024: 0.778-0.785 vs 0.769-0.771 ms (session 3)
 #endif
+#ifndef APNEAUQ_WG0_MINWG
+#define APNEAUQ_WG0_MINWG 512
+#endif
+#ifndef APNEAUQ_WG5_MINWG
+#define APNEAUQ_WG5_MINWG 512
+#endif
 #ifndef APNEAUQ_WG1_MINWG
 #define APNEAUQ_WG1_MINWG 512
 #endif
@@ -1945,12 +1951,12 @@ __host__ __device__ constexpr int wg_rs(int width_bytes) { return (width_bytes /
 #ifndef APNEAUQ_WG4_MINWG
 #define APNEAUQ_WG4_MINWG 768
 #endif
-template <> struct WgCfg<0> { static constexpr int CIB = 32, COB = 128, WCO = 4, WCI = 1, RTILES = 2, MINWG = 512, U = 4, MINB = 2; };  // im2col kk=32
+template <> struct WgCfg<0> { static constexpr int CIB = 32, COB = 128, WCO = 4, WCI = 1, RTILES = 2, MINWG = APNEAUQ_WG0_MINWG, U = 4, MINB = 2; };  // im2col kk=32
 template <> struct WgCfg<1> { static constexpr int CIB = 32, COB = 192, WCO = 2, WCI = 2, RTILES = 8, MINWG = APNEAUQ_WG1_MINWG, U = 8, MINB = 2; };
 template <> struct WgCfg<2> { static constexpr int CIB = 32, COB = 224, WCO = 2, WCI = 2, RTILES = 8, MINWG = APNEAUQ_WG2_MINWG, U = 8, MINB = 2; };
 template <> struct WgCfg<3> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = APNEAUQ_WG3_MINWG, U = 8, MINB = 3; };
 template <> struct WgCfg<4> { static constexpr int CIB = 16, COB = 128, WCO = 4, WCI = 1, RTILES = 16, MINWG = APNEAUQ_WG4_MINWG, U = 8, MINB = 3; };
-template <> struct WgCfg<5> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = 512, U = 4, MINB = 2; };
+template <> struct WgCfg<5> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = APNEAUQ_WG5_MINWG, U = 4, MINB = 2; };
 
 
 template <int l>
