@@ -69,7 +69,7 @@ struct Args {
   const void* x; const float* y; const float* dense_w; const float* dense_b; float* g_dense_w; float* g_dense_b;
   float* logits; float* dlogit; float* loss_sum;
   int B; int n_win; int groups; unsigned pass_base; unsigned window_offset; unsigned long long seed; int dropout;
-  float inv_count; float inv_batch; float eps; float momentum; const unsigned* pass_dev; int st_groups; float* wpart; float* det; int shared0; float* tab;
+  float inv_count; float inv_batch; float eps; float momentum; const unsigned* pass_dev; int st_groups; float* wpart; float* det; int shared0; float* tab; float* hpart;
 };
 }  // namespace train
 int train_args_size();
@@ -238,7 +238,7 @@ void bump_counters(at::Tensor& counters) {
 }
 
 // ctx: int64 CPU tensor of device pointers / scalars built once per workspace (ops/train_ops.py)
-constexpr int kCtxLayer = 19, kCtxLen = 6 * kCtxLayer + 26;
+constexpr int kCtxLayer = 19, kCtxLen = 6 * kCtxLayer + 27;
 
 float bits_to_float(int64_t v) {
   uint32_t u = static_cast<uint32_t>(v);
@@ -305,6 +305,8 @@ apneauq::train::Args args_from_ctx(const at::Tensor& ctx, int64_t pass_base) {
   A.wpart = reinterpret_cast<float*>(g[23]);
   A.det = reinterpret_cast<float*>(g[24]);
   A.tab = reinterpret_cast<float*>(g[25]);
+  A.hpart = reinterpret_cast<float*>(g[26]);
+  TORCH_CHECK(A.hpart == nullptr || A.det == nullptr, "train ctx: head slots are for the atomic mode");
   TORCH_CHECK(A.tab == nullptr || (A.det == nullptr && A.groups == 1 && A.wpart != nullptr),
               "train ctx: the parameter table needs one stats group, no deterministic partials and wgrad partials "
               "(wgrad_reduce writes its backward rows)");

@@ -110,6 +110,10 @@ struct Args {
                        // once per step by tab_kernel; the ~512 workgroups of each backward kernel read a
                        // few KB instead of each re-summing 16 fp64 slots per channel from the device-
                        // coherent moment buffers (~100 MB per dgrad launch).  nullptr: slot sums
+  float* hpart;        // training head: per-workgroup dense-weight / loss / dense-bias sums go to
+                       // [kStatSlots][96 + 2] fp32 slots (workgroup % kStatSlots) that bn_finalize adds
+                       // in slot order, instead of 256 workgroups' atomics on the same 98 addresses
+                       // (nullptr: direct atomics)
 };
 
 template <typename T>
@@ -1733,12 +1737,24 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A, int backward) {
     }
     if (A.det != nullptr) return;  // det_reduce_kernel sums the per-sample records
     __syncthreads();
+#ifdef APNEAUQ_HEAD_NOATOMIC  // probe: no per-workgroup global atomics (wrong gradients, timing only)
+    return;
+#endif
+    float* hp = A.hpart != nullptr ? A.hpart + (blockIdx.x % kStatSlots) * (Cc + 2) : nullptr;
     for (int c = threadIdx.x; c < Cc; c += kThreads) {
-      if (c == 0) {
-        atomicAdd(A.loss_sum, red[0]);
-        atomicAdd(A.g_dense_b, red[1]);
+      if (hp != nullptr) {  // slotted: summed by bn_finalize_kernel
+        if (c == 0) {
+          atomicAdd(hp + Cc, red[0]);
+          atomicAdd(hp + Cc + 1, red[1]);
+        }
+        atomicAdd(hp + c, dw[c]);
+      } else {
+        if (c == 0) {
+          atomicAdd(A.loss_sum, red[0]);
+          atomicAdd(A.g_dense_b, red[1]);
+        }
+        atomicAdd(A.g_dense_w + c, dw[c]);
       }
-      atomicAdd(A.g_dense_w + c, dw[c]);
       double* bst = Ly.bst + (blockIdx.x % kStatSlots) * 2 * Cc;
       atomicAdd(bst + c, (double)bsum0[c]);
       atomicAdd(bst + Cc + c, (double)bsum1[c]);
@@ -2291,6 +2307,18 @@ __global__ void bn_finalize_kernel(Args A, int update_moving, int grads) {
     if (grads) {
       Ly.gbeta[c] = (float)slot_sumd(Ly.bst + c, 2 * Cc);
       Ly.ggamma[c] = (float)slot_sumd(Ly.bst + Cc + c, 2 * Cc);
+    }
+  }
+  if (grads && l == 5 && A.hpart != nullptr) {  // the head's slotted sums, in slot order
+    for (int c = threadIdx.x; c < Cc + 2; c += blockDim.x) {
+      float v = 0.f;
+      for (int sl = 0; sl < kStatSlots; ++sl) v += A.hpart[sl * (Cc + 2) + c];
+      if (c < Cc)
+        A.g_dense_w[c] = v;
+      else if (c == Cc)
+        *A.loss_sum = v;
+      else
+        *A.g_dense_b = v;
     }
   }
 }

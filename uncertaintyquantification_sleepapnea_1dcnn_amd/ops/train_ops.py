@@ -131,6 +131,8 @@ class TrainWorkspace:
         # single-device training: per-layer BN parameter table, written once per step after the
         # forward kernels (train_conv.hip Args::tab / tab_kernel)
         self.tab = torch.zeros(6 * 6 * 256, device=dev) if with_backward else None
+        # training head: slotted dense-weight / loss / dense-bias sums (train_conv.hip Args::hpart)
+        self.hpart = torch.zeros(STAT_SLOTS * (ch[6] + 2), device=dev) if with_backward else None
         self.y = torch.zeros(self.B, device=dev)
         self.logits = torch.zeros(self.B, device=dev)
         self.dlogit = torch.zeros(self.B, device=dev)
@@ -179,7 +181,8 @@ class TrainWorkspace:
                  self.counters.data_ptr() if device_counters else 0, self.groups, int(self.shared0),
                  self.wpart.data_ptr() if self.wpart is not None else 0,
                  self.det.data_ptr() if self.det is not None else 0,
-                 self.tab.data_ptr() if table else 0]
+                 self.tab.data_ptr() if table else 0,
+                 self.hpart.data_ptr() if (self.hpart is not None and self.det is None) else 0]
         self.ctx = torch.tensor(vals, dtype=torch.int64)
         self._ctx_key = key
         return self.ctx
@@ -196,7 +199,8 @@ class TrainWorkspace:
 
     def zero_accumulators(self) -> None:
         """BN moment / backward sums, the flat gradient and the loss: one launch."""
-        _ext.ops().zero_buffers([self.st_all, self.bst_all, self.grad, self.loss])
+        bufs = [self.st_all, self.bst_all, self.grad, self.loss]
+        _ext.ops().zero_buffers(bufs + ([self.hpart] if self.hpart is not None else []))
 
 
 def _call(ctx, op, layer=0, flag=0, pass_base=-1, device=0):
