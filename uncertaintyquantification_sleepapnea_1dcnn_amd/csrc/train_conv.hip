@@ -2440,7 +2440,8 @@ static train::DetDst det_dst(void* p0, int c0, int f0, void* p1 = nullptr, int c
 // floats of the deterministic-mode partial table for a batch of B samples (fwd / head / dgrad reuse it)
 // Persistent forward: workgroups per CU (2 are resident at a time), each over a contiguous tile range.
 // Batch-BN MC Dropout (409,600 tiles per layer launch) measured 8 / 16 / 32 / 64 per CU: MCD phase
-// 91.9 / 91.1-91.4 / 91.0-91.4 / 90.5-90.9 ms (tools/probes/so_bench1.sh, one box): shorter ranges
+// 91.9 / 91.1-91.4 / 91.0-91.4 / 90.5-90.9 ms (tools/probes/so_bench1.sh, one box), and 64 / 128 / 256
+// on another: 90.8-90.9 / 91.2-91.8 / 91.9-92.1 ms: shorter ranges
 // balance the launch tail.  Batches of <= 16384 tiles (training) get one tile per workgroup anyway.
 #ifndef APNEAUQ_FWD_WG_PER_CU
 #define APNEAUQ_FWD_WG_PER_CU 64
