@@ -170,6 +170,9 @@ __device__ __forceinline__ int row_time(int grow) { return (grow - kHalo) & 63; 
 #ifndef APNEAUQ_FWD_STAGEPAD
 #define APNEAUQ_FWD_STAGEPAD 1
 #endif
+#ifndef APNEAUQ_FWD_NB
+#define APNEAUQ_FWD_NB 4
+#endif
 #ifndef APNEAUQ_FWD_SKIPPAD
 #define APNEAUQ_FWD_SKIPPAD 1
 #endif
@@ -774,7 +777,7 @@ struct Conv {
     // NB - 1 LDS reads stay in flight.  RING = false reads each B fragment just in time (dgrad: one
     // tile per workgroup, two workgroups per CU, measured 5-17 % faster per layer without the ring).
     constexpr int NSA = PD + 1;
-    constexpr int NB = RT < 4 ? RT : 4;
+    constexpr int NB = RT < APNEAUQ_FWD_NB ? RT : APNEAUQ_FWD_NB;  // B-fragment ring depth (probe macro)
     static_assert(RT % NB == 0, "B ring phase restarts at every step");
     constexpr int DSN = FIRST ? 2 : 1;  // LDS reads per B fragment
     bf16x8 bq[NB];
