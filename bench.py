@@ -10,23 +10,25 @@ complete UQ inference of both methods the reference evaluates
   1. MC Dropout, T=50 stochastic passes with the reference's semantics (``uq_techniques.py:22``,
      ``model(x, training=True)``): every pass normalises each BatchNorm with the batch statistics
      of the WHOLE window set (all ranks: SyncBN all-reduce per layer) and updates the moving
-     averages; layer-synchronous HIP kernels (``csrc/train_conv.hip``), counter-based dropout
-     masks keyed by the global window index; then the per-window mean / variance / entropy /
-     expected entropy / MI reduction (HIP ``uq_reduce``);
-  2. Deep Ensemble, M=8 members (inference BN, no dropout; ``uq_techniques.py:29``), fused
-     whole-network HIP kernel, member-parallel over the GPUs with an RCCL all_to_all of member
-     probabilities over xGMI, then the same reduction;
+     averages; counter-based dropout masks keyed by the global window index; then the per-window
+     mean / variance / entropy / expected entropy / MI reduction (HIP ``uq_reduce``);
+  2. Deep Ensemble, M=8 members (inference BN, no dropout; ``uq_techniques.py:29``), member-parallel
+     over the GPUs with an RCCL all_to_all of member probabilities over xGMI, then the same reduction;
   3. the 6 aggregate UQ scalars of each method, all-reduced over ranks.
 
-``value`` = windows fully UQ-evaluated (both methods) per second over ALL GPUs, for the
-reference-semantics MCD (``--bn-mode batch``, the default).  The same run also times standard MC
-Dropout (BN on running statistics, the fused whole-network kernel) and reports it under
-``extra.running_bn``, and an fp32 deviation block: the bf16 HIP paths against the fp32 PyTorch
-reference model (``models/reference.py``) on a fixed window subset.
+Precision (``--precision``, default ``fp32``): the reference computes in fp32 (Keras defaults, no
+mixed-precision policy), so the headline runs the fp32-faithful engine (``ops/x3.py``,
+``csrc/x3_layers.hip``): every conv product is three fp16 MFMAs over a hi/lo split of both operands
+with fp32 accumulation (22-bit operands, ~fp32 GEMM rounding), block 1 / BN / dropout / head in fp32.
+``extra.fp32_deviation`` measures it against the fp32 PyTorch reference (``models/reference.py``) on a
+fixed window subset.  The bf16 engine of rounds 1-2 is timed in the same run under ``extra.bf16``
+(``--precision bf16`` makes it the headline, labelled ``dtype: bf16``).
 
-Model: the reference Alarcón 1D-CNN (853,441 params, 60 x 4 windows), random-init weights with
-non-trivial BN statistics, synthetic standardised windows.  Timing: W untimed warmup steps, then K
-steps bracketed by barrier + synchronize; the max over ranks is reported.
+``value`` = windows fully UQ-evaluated (both methods) per second over ALL GPUs.  Model: the
+reference Alarcon 1D-CNN (853,441 params, 60 x 4 windows), random-init weights with non-trivial BN
+statistics, synthetic standardised windows.  Timing: W untimed warmup steps, then K steps bracketed by
+barrier + synchronize; the max over ranks is reported.  On the GPU a process group is formed even for
+one rank (RCCL, world size 1), so the N=1 point runs the same code path as N=8.
 
 ``--device cpu`` is a dry run of the same launcher / collectives / metrics on gloo with the fp32
 reference model (CPU tests); its numbers are not performance claims.
@@ -62,11 +64,13 @@ def parse(argv=None):
     ap.add_argument("--passes", type=int, default=50, help="MC Dropout passes T")
     ap.add_argument("--members", type=int, default=8, help="Deep Ensemble members M")
     ap.add_argument("--seed", type=int, default=2025)
+    ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
+                    help="headline engine: fp32-faithful (fp16x3 MFMA, the reference's precision; default) or bf16")
     ap.add_argument("--bn-mode", choices=["batch", "running"], default="batch",
                     help="MC-Dropout BatchNorm of the headline: per-pass batch statistics over the whole window set "
                          "(the reference's model(x, training=True); default) or running statistics (standard MC "
-                         "Dropout, fused kernel)")
-    ap.add_argument("--no-secondary", action="store_true", help="skip the other BN mode's timing")
+                         "Dropout)")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the bf16 engine's timing (extra.bf16)")
     ap.add_argument("--no-deviation", action="store_true", help="skip the fp32 deviation block")
     ap.add_argument("--deviation-windows", type=int, default=1024)
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
@@ -86,6 +90,8 @@ def main(argv=None):
     if a.device == "cpu":
         os.environ.setdefault("APNEAUQ_DIST_BACKEND", "gloo")
         os.environ["CUDA_VISIBLE_DEVICES"] = ""
+    else:
+        os.environ.setdefault("APNEAUQ_FORCE_PG", "1")  # RCCL group even at world size 1 (same path as N=8)
     run(a)
 
 
@@ -112,12 +118,11 @@ def run(a):
     n_loc = a.windows
     n_glob = n_loc * world
 
-    # ---- resident data: the whole synthetic window set lives in HBM on every rank
+    # ---- resident data: the whole synthetic window set lives in HBM on every rank (fp32, as Keras feeds it)
     g = torch.Generator(device="cpu").manual_seed(a.seed)
     x32_glob = torch.randn(n_glob, 60, 4, generator=g)
     y_glob = (torch.rand(n_glob, generator=g) < 0.3).to(torch.int32)
-    xdt = torch.float32 if cpu else torch.bfloat16
-    x_glob = x32_glob.to(xdt).to(dev)
+    x_glob = x32_glob.to(dev)
     y_glob = y_glob.to(dev)
     start, stop = pdist.shard_range(n_glob, rank, world)
     x_loc = x_glob[start:stop].contiguous()
@@ -128,14 +133,16 @@ def run(a):
     mem_ids = (list(range(rank * (a.members // world), (rank + 1) * (a.members // world)))
                if member_parallel else list(range(a.members)))
     params_de = [{k: v.to(dev) for k, v in R.synthetic_params(SPEC, a.seed + 100 + m).items()} for m in mem_ids]
-    sync = (lambda t: torch.distributed.all_reduce(t)) if world > 1 else None
+    use_pg = torch.distributed.is_available() and torch.distributed.is_initialized()
+    sync = (lambda t: torch.distributed.all_reduce(t)) if (use_pg and not cpu) or world > 1 else None
 
-    if cpu:
-        engine = _CpuEngine(R, SPEC, params_mcd, params_de, world, start, n_glob, a.seed, a.passes)
-    else:
-        engine = _HipEngine(R, SPEC, params_mcd, params_de, world, start, n_glob, a.seed, a.passes, sync)
+    def make(precision):
+        if cpu:
+            return _CpuEngine(R, SPEC, params_mcd, params_de, world, start, n_glob, a.seed, a.passes)
+        cls = _X3Engine if precision == "fp32" else _Bf16Engine
+        return cls(R, SPEC, params_mcd, params_de, world, start, n_glob, a.seed, a.passes, sync)
 
-    def timed(mode: str, steps: int, warmup: int, step_base: int):
+    def timed(engine, mode: str, steps: int, warmup: int, step_base: int):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if not cpu else None
         phase = [0.0, 0.0]
 
@@ -185,30 +192,37 @@ def run(a):
         elapsed = pdist.all_reduce_max(time.perf_counter() - t0)
         return elapsed, sums, phase
 
-    elapsed, sums, phase = timed(a.bn_mode, a.steps, a.warmup, 0)
+    head_prec = "fp32" if cpu else a.precision
+    engine = make(head_prec)
+    elapsed, sums, phase = timed(engine, a.bn_mode, a.steps, a.warmup, 0)
     agg_mcd = pinf.finalize_aggregates(sums[0])
     agg_de = pinf.finalize_aggregates(sums[1])
     ms = elapsed * 1e3 / a.steps
     value = n_glob * a.steps / elapsed
 
+    deviation = None
+    if not cpu and not a.no_deviation:
+        deviation = engine.deviation(x_glob[: a.deviation_windows], y_glob[: a.deviation_windows])
+
     secondary = None
-    if not a.no_secondary:
-        other = "running" if a.bn_mode == "batch" else "batch"
+    if not cpu and not a.no_secondary:
+        other = "bf16" if head_prec == "fp32" else "fp32"
+        del engine
+        torch.cuda.empty_cache()
+        eng2 = make(other)
         k2 = max(1, min(a.steps, 10))
-        e2, s2, ph2 = timed(other, k2, 1, 10_000)
+        e2, s2, ph2 = timed(eng2, a.bn_mode, k2, 1, 10_000)
         secondary = {
-            "bn_mode_mcd": other,
+            "precision": other,
             "value": round(n_glob * k2 / e2, 1),
             "ms_per_step": round(e2 * 1e3 / k2, 3),
             "steps": k2,
             "mcd_phase_ms": round(ph2[0] / k2, 3),
-            "mcd_windows_per_s_per_gpu": round(n_loc / (ph2[0] / k2 / 1e3), 1) if ph2[0] else None,
+            "de_phase_ms": round(ph2[1] / k2, 3),
             "mcd_mean_entropy": round(pinf.finalize_aggregates(s2[0])["mean_total_pred_entropy"], 6),
         }
-
-    deviation = None
-    if not cpu and not a.no_deviation:
-        deviation = engine.deviation(x32_glob[: a.deviation_windows].to(dev), y_glob[: a.deviation_windows])
+        if not a.no_deviation:
+            secondary["fp32_deviation"] = eng2.deviation(x_glob[: a.deviation_windows], y_glob[: a.deviation_windows])
 
     macs = SPEC.forward_macs()
     devices = pdist.gather_device_ids()  # collective: every rank
@@ -223,10 +237,13 @@ def run(a):
             "ms_per_step": round(ms, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": None if (BASELINE is None or cpu) else round(value / BASELINE, 3),
+            "vs_baseline": None if (BASELINE is None or cpu or head_prec != "fp32") else round(value / BASELINE, 3),
             "vs_baseline_basis": BASELINE_BASIS if a.bn_mode == "batch" else
             BASELINE_BASIS + " (NOTE: headline run in bn_mode=running; semantics differ)",
-            "dtype": "fp32" if cpu else "bf16",
+            "dtype": "fp32" if head_prec == "fp32" else "bf16",
+            "compute": ("fp32-faithful: conv products as 3 fp16 MFMAs over hi/lo splits of both operands, fp32 "
+                        "accumulate; block 1, BN (fp64 moments), dropout, GAP, Dense, sigmoid in fp32") if head_prec == "fp32"
+            else "bf16 MFMA operands, fp32 accumulate",
             "data": "synthetic (random standardized 60x4 windows, random-init weights)",
             "config": {
                 "model": "Alarcon 1D-CNN (6x[Conv1D-ReLU-BN-Dropout]+GAP+Dense, 853,441 params), input (60, 4)",
@@ -250,16 +267,91 @@ def run(a):
                 "effective_tflops_per_gpu": round(n_loc * (a.passes + a.members) * 2 * macs / (ms / 1e3) / 1e12, 1),
                 "mcd_mean_entropy": round(agg_mcd["mean_total_pred_entropy"], 6),
                 "de_mean_mutual_info": round(agg_de["mean_mutual_info"], 6),
-                ("running_bn" if a.bn_mode == "batch" else "batch_bn"): secondary,
                 "fp32_deviation": deviation,
+                ("bf16" if head_prec == "fp32" else "fp32"): secondary,
             },
         }
         print(json.dumps(out), flush=True)
     pdist.shutdown()
 
 
-class _HipEngine:
-    """bf16 HIP kernels: batch-BN MCD on the layer-wise kernels, running-BN MCD and DE fused."""
+def _mcd_deviation(R, spec, params, x32, y, T, seed, base, run_hip, uq_ops, pinf):
+    """max / mean |dp| and aggregate deltas of one engine's batch-BN and running-BN MC Dropout against
+    the fp32 reference forward on the same weights, masks and inputs."""
+    import torch
+
+    n = x32.shape[0]
+    ids = torch.arange(n, device=x32.device)
+    agg = {}
+    for mode in ("batch", "running"):
+        ph = run_hip(mode)
+        pr = torch.stack([R.forward(spec, params, x32, dropout=True, bn_batch_stats=(mode == "batch"), seed=seed,
+                                    pass_id=base + t, sample_ids=ids).reshape(-1) for t in range(T)])
+        ah = pinf.finalize_aggregates(pinf.aggregate_sums(uq_ops.metrics(ph), y))
+        ar = pinf.finalize_aggregates(pinf.aggregate_sums(uq_ops.metrics_eager(pr), y))
+        agg[mode] = {
+            "max_abs_dp": float((ph - pr).abs().max()),
+            "mean_abs_dp": float((ph - pr).abs().mean()),
+            "aggregates_hip": {k: round(v, 6) for k, v in ah.items()},
+            "aggregates_delta": {k: float(f"{ah[k] - ar[k]:.3e}") for k in ah},
+        }
+    return agg
+
+
+class _X3Engine:
+    """fp32-faithful engine (ops/x3.py): batch-BN MCD and DE on the fp16x3 layer kernels."""
+
+    def __init__(self, R, spec, params_mcd, params_de, world, start, n_glob, seed, passes, sync):
+        from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import x3
+
+        self.x3, self.R, self.spec = x3, R, spec
+        self.world, self.start, self.n_glob, self.seed, self.passes, self.sync = world, start, n_glob, seed, passes, sync
+        self.params_mcd, self.params_de = params_mcd, params_de
+        # the MCD model owns its own parameter copy: its moving statistics are mutated every pass
+        self.m_mcd = x3.X3Model(spec, [{k: v.clone() for k, v in params_mcd.items()}])
+        self.m_de = x3.X3Model(spec, params_de)
+
+    def mcd(self, mode, x_loc, i):
+        if mode == "running":
+            return self.x3.forward_running(self.m_mcd, x_loc, n_pass=self.passes, dropout=True, seed=self.seed,
+                                           pass_offset=i * self.passes, window_offset=self.start)[0]
+        return self.x3.mcd_batch(self.m_mcd, x_loc, self.passes, seed=self.seed, pass_base=i * self.passes,
+                                 window_offset=self.start, update_moving=True, sync=self.sync, global_n=self.n_glob)
+
+    def de(self, x):
+        return self.x3.forward_running(self.m_de, x)[:, 0]
+
+    def deviation(self, x32, y):
+        import torch
+
+        from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import uq as uq_ops
+        from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel import inference as pinf
+
+        x3, R, spec = self.x3, self.R, self.spec
+        out = {"windows": x32.shape[0], "engine": "fp32-faithful (fp16x3)",
+               "reference": "models/reference.py forward in fp32 (same weights, masks, fp32 input)"}
+        with torch.no_grad():
+            de = x3.X3Model(spec, self.params_de[:1])
+            p_hip = x3.forward_running(de, x32)[0, 0]
+            p_ref = R.forward(spec, self.params_de[0], x32, training=False).reshape(-1)
+            out["de_member_max_abs_dp"] = float((p_hip - p_ref).abs().max())
+            T, seed, base = self.passes, self.seed + 555, 777
+            mm = x3.X3Model(spec, [{k: v.clone() for k, v in self.params_mcd.items()}])
+
+            def run_hip(mode):
+                if mode == "batch":
+                    return x3.mcd_batch(mm, x32, T, seed=seed, pass_base=base, update_moving=False)
+                return x3.forward_running(mm, x32, n_pass=T, dropout=True, seed=seed, pass_offset=base)[0]
+
+            agg = _mcd_deviation(R, spec, self.params_mcd, x32, y, T, seed, base, run_hip, uq_ops, pinf)
+            out["mcd_T"] = T
+            out["mcd_batch_bn"] = agg["batch"]
+            out["mcd_running_bn"] = agg["running"]
+        return out
+
+
+class _Bf16Engine:
+    """bf16 HIP kernels of rounds 1-2: batch-BN MCD on the layer-wise kernels, running-BN MCD and DE fused."""
 
     def __init__(self, R, spec, params_mcd, params_de, world, start, n_glob, seed, passes, sync):
         import torch
@@ -271,17 +363,14 @@ class _HipEngine:
         self.world, self.start, self.n_glob, self.seed, self.passes, self.sync = world, start, n_glob, seed, passes, sync
         self.params_mcd = params_mcd
         self.params_de = params_de
-        # batch-BN MCD: samples (passes x windows) per layer-kernel launch.  All T passes in ONE chunk when
-        # the activations fit (T x N x 64 rows x 864 bf16 channels of R_2..R_6: ~90 GB at T=50, N=16384 --
-        # sized for 288 GB of HBM3E; fewer launch tails than 4 chunks of 2^18 samples, ~1 %), halved
-        # until they fit in half of the free device memory.  APNEAUQ_MCD_MAX_SAMPLES overrides (probes).
+        # batch-BN MCD: samples (passes x windows) per layer-kernel launch, all T passes in one chunk when
+        # the bf16 activations fit in half of the free HBM (halved until they do)
         env = os.environ.get("APNEAUQ_MCD_MAX_SAMPLES")
+        dev = params_mcd["conv1d_1/kernel"].device
         if env:
             self.max_samples = int(env)
         else:
-            import torch
-
-            free = torch.cuda.mem_get_info(params_mcd["conv1d_1/kernel"].device)[0]
+            free = torch.cuda.mem_get_info(dev)[0]
             per_sample = 64 * sum(b.filters for b in spec.blocks[1:]) * 2
             ms = 1 << 20
             while ms > (1 << 16) and ms * per_sample > 0.5 * free:
@@ -289,32 +378,33 @@ class _HipEngine:
             if world > 1:  # every rank must chunk the passes identically (one SyncBN all-reduce per chunk)
                 import torch.distributed as dist
 
-                t = torch.tensor([ms], dtype=torch.int64, device=params_mcd["conv1d_1/kernel"].device)
+                t = torch.tensor([ms], dtype=torch.int64, device=dev)
                 dist.all_reduce(t, op=dist.ReduceOp.MIN)
                 ms = int(t.item())
             self.max_samples = ms
         self.blob_mcd = fused.pack_blob(spec, params_mcd).unsqueeze(0)
         self.blobs_de = torch.stack([fused.pack_blob(spec, p) for p in params_de])
-        # the batch-BN model owns its own parameter copy: its moving statistics are mutated every pass
-        self.model = AlarconCNN1D(seed=seed, device=params_mcd["conv1d_1/kernel"].device,
-                                  params={k: v.clone() for k, v in params_mcd.items()})
+        self.model = AlarconCNN1D(seed=seed, device=dev, params={k: v.clone() for k, v in params_mcd.items()})
 
     def mcd(self, mode, x_loc, i):
+        import torch
+
         from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import train_ops
         from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel import inference as pinf
 
+        xb = x_loc.to(torch.bfloat16)
         if mode == "running":
-            return pinf.mcd_probs_local(self.blob_mcd, x_loc, self.passes, self.seed + i, self.start)
-        # reference semantics: every pass normalises with the batch statistics of ALL windows
-        return train_ops.forward_batch_stats(self.model, x_loc, self.passes, pass_base=i * self.passes, seed=self.seed,
+            return pinf.mcd_probs_local(self.blob_mcd, xb, self.passes, self.seed + i, self.start)
+        return train_ops.forward_batch_stats(self.model, xb, self.passes, pass_base=i * self.passes, seed=self.seed,
                                              update_moving=True, sync=self.sync, window_offset=self.start,
                                              global_n=self.n_glob, max_samples=self.max_samples)
 
     def de(self, x):
-        return self.fused.fused_forward(x, self.blobs_de, self.spec)[:, 0]
+        import torch
+
+        return self.fused.fused_forward(x.to(torch.bfloat16), self.blobs_de, self.spec)[:, 0]
 
     def deviation(self, x32, y):
-        """bf16 HIP results vs the fp32 PyTorch reference on the same windows, masks and weights."""
         import torch
 
         from uncertaintyquantification_sleepapnea_1dcnn_amd.models.cnn import AlarconCNN1D
@@ -322,36 +412,24 @@ class _HipEngine:
         from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel import inference as pinf
 
         R, spec = self.R, self.spec
-        n = x32.shape[0]
         xb = x32.to(torch.bfloat16)
-        ids = torch.arange(n, device=x32.device)
-        out = {"windows": n, "reference": "models/reference.py forward in fp32 (same weights, masks, fp32 input)"}
+        out = {"windows": x32.shape[0], "engine": "bf16",
+               "reference": "models/reference.py forward in fp32 (same weights, masks, fp32 input)"}
         with torch.no_grad():
-            # deterministic forward (DE member 0, inference BN)
             p_hip = self.fused.fused_forward(xb, self.blobs_de[:1], spec)[0, 0]
             p_ref = R.forward(spec, self.params_de[0], x32, training=False).reshape(-1)
             out["de_member_max_abs_dp"] = float((p_hip - p_ref).abs().max())
-            # MC Dropout, T passes, both BN modes; identical counter-based masks on both sides
             T, seed, base = self.passes, self.seed + 555, 777
-            agg = {}
-            for mode in ("batch", "running"):
+
+            def run_hip(mode):
                 if mode == "batch":
                     model = AlarconCNN1D(seed=seed, device=x32.device,
                                          params={k: v.clone() for k, v in self.params_mcd.items()})
-                    ph = train_ops.forward_batch_stats(model, xb, T, pass_base=base, seed=seed, update_moving=False)
-                else:
-                    ph = self.fused.fused_forward(xb, self.blob_mcd, spec, n_pass=T, dropout=True, seed=seed,
-                                                  pass_offset=base)[0]
-                pr = torch.stack([R.forward(spec, self.params_mcd, x32, dropout=True, bn_batch_stats=(mode == "batch"),
-                                            seed=seed, pass_id=base + t, sample_ids=ids).reshape(-1) for t in range(T)])
-                ah = pinf.finalize_aggregates(pinf.aggregate_sums(uq_ops.metrics(ph), y))
-                ar = pinf.finalize_aggregates(pinf.aggregate_sums(uq_ops.metrics_eager(pr), y))
-                agg[mode] = {
-                    "max_abs_dp": float((ph - pr).abs().max()),
-                    "mean_abs_dp": float((ph - pr).abs().mean()),
-                    "aggregates_hip": {k: round(v, 6) for k, v in ah.items()},
-                    "aggregates_delta": {k: float(f"{ah[k] - ar[k]:.3e}") for k in ah},
-                }
+                    return train_ops.forward_batch_stats(model, xb, T, pass_base=base, seed=seed, update_moving=False)
+                return self.fused.fused_forward(xb, self.blob_mcd, spec, n_pass=T, dropout=True, seed=seed,
+                                                pass_offset=base)[0]
+
+            agg = _mcd_deviation(R, spec, self.params_mcd, x32, y, T, seed, base, run_hip, uq_ops, pinf)
             out["mcd_T"] = T
             out["mcd_batch_bn"] = agg["batch"]
             out["mcd_running_bn"] = agg["running"]

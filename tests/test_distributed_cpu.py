@@ -178,3 +178,26 @@ def test_bootstrap_partial_sums_cover_all_draws():
     assert torch.all(tot[:, 2] + tot[:, 4] == 37)
     full = uq_ops.bootstrap(m, y, 9, seed=3)
     torch.testing.assert_close(uq_ops.finalize_bootstrap_sums(tot, 37), full, atol=1e-6, rtol=1e-6)
+
+
+def _driver_two_ranks(rank, world, outdir):
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.models.cnn import AlarconCNN1D
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.uq import drivers
+
+    x, y = _data(21, 6)
+    m = AlarconCNN1D(seed=4, device="cpu")
+    res = drivers.evaluate_mc_dropout(m, x, y.long().numpy(), None, "dist_driver", n_passes=3, n_bootstrap=5,
+                                      output_csv_dir=outdir, output_plot_dir=outdir, raw_pred_path="",
+                                      make_plots=False)
+    return res
+
+
+def test_mc_dropout_driver_under_two_ranks(tmp_path):
+    """under torchrun only rank 0 reaches evaluate_uq_methods -> bootstrap_metrics, so the
+    bootstrap must not be a collective there.  Rank 0 returns the full metrics dict with its confidence
+    intervals (no process-group timeout, no None), the other rank returns None."""
+    res = run_ranks(_driver_two_ranks, 2, (str(tmp_path),))
+    r0, r1 = res
+    assert r1 is None
+    assert r0 is not None and "overall_mean_variance_ci_lower" in r0 and "mean_mutual_info_ci_upper" in r0
+    assert all(np.isfinite(v) for v in r0.values())

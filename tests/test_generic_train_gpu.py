@@ -145,8 +145,9 @@ def test_data_parallel_hip_step_matches_single_process(name):
 @pytest.mark.parametrize("name", ["pooled", "single30"])
 def test_graphed_generic_step_matches_eager(name, monkeypatch):
     """The HIP-graph replay of the generic step (dropout keys read from device memory, Adam step from
-    a device counter) follows the eager step: same first loss, then losses within the fp32-atomic
-    summation-order noise two eager runs show, and the graph path really ran."""
+    a device counter) follows the eager step: both compute Adam's bias correction on the device from
+    the iteration counter, so they differ only by fp32-atomic summation order -- bounded here by the
+    spread of two EAGER runs -- and the graph's device counter advanced in lockstep with the host."""
     from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import generic_train
 
     spec = SPECS[name]
@@ -154,21 +155,20 @@ def test_graphed_generic_step_matches_eager(name, monkeypatch):
     x = torch.randn(256, spec.input_length, spec.input_channels, generator=g).cuda()
     y = (torch.rand(256, generator=g) < 0.4).float().cuda()
     runs = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("APNEAUQ_TRAIN_GRAPH", mode)
+    for mode in ("0", "0b", "1"):
+        monkeypatch.setenv("APNEAUQ_TRAIN_GRAPH", mode[0])
         m = AlarconCNN1D(spec=spec, seed=4, device="cuda")
         losses = [float(m.train_step(x[i * 64:(i + 1) * 64], y[i * 64:(i + 1) * 64])) for i in range(4)]
         runs[mode] = (losses, m.optimizer.iterations, m._train_step_counter, m.store.flat.clone())
         if mode == "1":
-            assert 64 in getattr(m, "_gtrain_graphs", {})
-    (le, ie, ce, we), (lg, ig, cg, wg) = runs["0"], runs["1"]
+            gs = getattr(m, "_gtrain_graphs", {})
+            assert 64 in gs
+            assert int(gs[64].counters[1].item()) == 4  # device-side Adam step == host iterations
+    (le, ie, ce, we), (le2, _, _, we2), (lg, ig, cg, wg) = runs["0"], runs["0b"], runs["1"]
     assert (ie, ce) == (ig, cg) == (4, 4)
     assert abs(lg[0] - le[0]) < 1e-4 * abs(le[0])
-    # later steps: fp32 atomic summation order (split-K wgrad, BN moments) makes even two EAGER runs of
-    # the pooled spec differ by up to ~0.5 % at step 3-4 (tools/probes/graph_generic_check.py); on
-    # random labels at batch 64 the gap compounds through Adam and reached 2.07 % at step 4 once (r2
-    # session 3), so later steps get 5 %; the first step above stays exact to 1e-4
-    np.testing.assert_allclose(lg, le, rtol=5e-2)
-    w0 = AlarconCNN1D(spec=spec, seed=4, device="cuda").store.flat
-    assert ((wg - we).norm() / (we - w0).norm()).item() < 0.2
+    for a, b, b2 in zip(lg, le, le2):
+        assert abs(a - b) <= max(3 * abs(b2 - b), 1e-4 * abs(b)), (lg, le, le2)
+    spread = (we2 - we).norm().item()
+    assert (wg - we).norm().item() <= max(3 * spread, 1e-6 * we.norm().item())
     assert isinstance(generic_train.GraphedGenericStep, type)

@@ -1,0 +1,544 @@
+// fp32-faithful layer-wise inference of the Alarcón 1D-CNN on gfx950 (MI355X): "fp16x3" MFMA.
+//
+// Replaces the reference's inference hot loops at fp32 precision (Keras runs fp32, no mixed-precision
+// policy anywhere in the reference):
+//   * MC Dropout  np.stack([model(x, training=True) for _ in range(T)])   (uq_techniques.py:22): BN on
+//     per-pass batch statistics of the WHOLE window set, dropout on, moving averages updated;
+//   * Deep Ensemble  np.stack([m.predict(x) for m in models])           (uq_techniques.py:29): BN on
+//     moving statistics, no dropout;
+//   * standard MC Dropout (BN on moving statistics, dropout on).
+//
+// Precision.  Every conv operand is split into two fp16 halves, v = hi + lo with hi = fp16(v) and
+// lo = fp16(v - hi) (22 significant bits), and each product is formed by three v_mfma_f32_16x16x32_f16
+// (hi*hi + hi*lo + lo*hi, fp32 accumulate): the dropped lo*lo term and the split residuals are ~2^-22
+// relative, below fp32 GEMM rounding over K = 28..2304.  Weights are pre-scaled by an exact power of
+// two per layer (host) so that both halves stay in the fp16 normal range; the epilogue undoes it.
+// Block 1 (Cin = 4, 0.4 % of the FLOPs) runs in plain fp32 FMAs.  BN moments are fp32 per tile, fp64
+// across tiles; the BN affine, dropout, GAP, Dense and sigmoid are fp32.
+//
+// Data flow (one launch per layer; the window set stays resident in HBM):
+//   l1_kernel      R_1 = relu(conv(x) + b) fp32 (+ batch moments)           [G1][N][60][128]
+//   aff_kernel     per-group BN affine of block l (batch moments or moving stats), pre-scaled by 1/(1-p)
+//   layer_kernel   stage A_{l-1} = dropout(BN(R_{l-1})) as fp16 hi/lo into LDS, conv on MFMA,
+//                  epilogue: bias + ReLU + moments + dropout mask of block l (sign bit of R_l, fp32)
+//                  block 6: per-sample masked channel sums  S1 = sum_t keep*R,  S0 = sum_t keep
+//   head_kernel    logit = b + (1/60) sum_c w_c (s_c S1_c + t_c S0_c)  (BN 6 + dropout 6 + GAP + Dense
+//                  are linear per channel), p = sigmoid(logit)
+//
+// Layer kernel geometry (CDNA4-first):
+//   * one persistent 512-thread workgroup (8 waves, 2 per SIMD) per CU walks a contiguous range of
+//     tiles; a tile = 4 samples of one group (MC-Dropout pass or ensemble member) = 256 GEMM rows,
+//     every sample a 64-row slot (60 time steps + 4 zero rows, the 'same' padding halo);
+//   * the input channels stream through LDS in chunks of 32, double-buffered: while the MFMAs consume
+//     chunk c the global loads of chunk c+1 are in flight in registers (transform + fp16 split + LDS
+//     write after the chunk, one LDS-only barrier per chunk -- no vmcnt drain);
+//   * LDS row = [hi 32 ch | lo 32 ch | 32 B pad] = 160 B = 10 16-B slots (stride = 2 mod 4 slots: the
+//     ds_read_b128 lane groups of a 16x16x32 B fragment hit 16 distinct slots at any row offset);
+//   * conv = implicit GEMM  D[co][row] = sum_{tap, ci} W[tap][ci][co] A[row + tap - pad][ci]: weights are
+//     the A operand (host-packed fragments, one 1-KiB coalesced load per fragment, prefetched one k-step
+//     ahead), activations the B operand (LDS).  Waves tile rows x output channels (WM x WN) per layer so
+//     that each weight fragment is re-read by at most WM waves of the 256-row tile.
+#include "common.h"
+#include "x3_args.h"
+
+namespace apneauq {
+namespace x3 {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const f16x8 gf16x8;
+
+constexpr int kThreads = 512, kWaves = 8;
+constexpr int kS = 4, kL = 60, kSR = 64, kHalo = 4;
+constexpr int kTileRows = kS * kSR;                  // 256 GEMM rows per tile
+constexpr int kLdsRows = kHalo + kTileRows + kHalo;  // 264
+constexpr int kCK = 32;                              // input channels per staged chunk
+constexpr int kRowB = 160;                           // LDS row: hi 64 B | lo 64 B | pad 32 B
+constexpr int kBufB = kLdsRows * kRowB;              // 42,240 B per chunk buffer
+constexpr int kValidRows = kS * kL;                  // 240 staged rows per tile
+constexpr int kNU = (kValidRows * (kCK / 4) + kThreads - 1) / kThreads;  // 16-B staging units per thread
+
+// global-address-space load (keeps global_load_*, never flat_*)
+template <typename T>
+__device__ __forceinline__ T gld(const void* p) {
+  return *(const __attribute__((address_space(1))) T*)(p);
+}
+
+// Thread index the optimiser cannot see through: per-iteration address math of the persistent tile
+// loop is recomputed instead of being hoisted into ~100 loop-invariant VGPRs.
+__device__ __forceinline__ int opaque_tid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
+__device__ __forceinline__ f32x4 mfma(const f16x8& a, const f16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// LDS hazard barrier: orders LDS traffic only (global loads in flight stay in flight)
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// XCD-aware workgroup id (T1): blocks that share an XCD get a contiguous range.  Bijective.
+__device__ __forceinline__ int xcd_wg() {
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q = nwg / 8, rem = nwg % 8, xcd = bid % 8;
+  return (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + bid / 8;
+}
+
+template <int CIN, int COUT, int KS, int WM, int WN, bool LAST, bool CTO>
+__global__ __launch_bounds__(kThreads, 2) void layer_kernel(const LayerArgs A) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NCH = CIN / kCK, NCTA = COUT / 16, NCT = NCTA / WN, NRT = 16 / WM, PAD = (KS - 1) / 2;
+  constexpr int NSTEP = NCH * KS;
+  constexpr long long FRAG_STEP = (long long)NCTA * 128;  // f16x8 per (chunk, tap) k-step
+  static_assert(CIN % kCK == 0 && COUT % 16 == 0, "channel tiling");
+  static_assert(WM * WN == kWaves && NCTA % WN == 0 && 16 % WM == 0, "wave tiling");
+  static_assert(!LAST || NRT == 4, "block 6: one sample per wave row");
+  double* st = reinterpret_cast<double*>(smem + 2 * kBufB);  // [2][COUT] per-workgroup moment sums
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave % WN, wm = wave / WN;
+  const int ct0 = wn * NCT, rt0 = wm * NRT;
+  const int m = lane & 15, h = lane >> 4;
+  APNEAUQ_DASSERT(blockDim.x == kThreads);
+
+  for (int i = tid; i < 2 * kBufB / 16; i += kThreads) reinterpret_cast<f32x4*>(smem)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = tid; i < 2 * COUT; i += kThreads) st[i] = 0.0;
+  __syncthreads();
+
+  const int wg = xcd_wg();
+  const int t_begin = (int)((long long)wg * A.total_tiles / gridDim.x);
+  const int t_end = (int)((long long)(wg + 1) * A.total_tiles / gridDim.x);
+  if (t_begin >= t_end) return;  // workgroup-uniform
+  const int slot = wg % kStatSlots;
+
+  // ---- staging: this thread's 16-B units of a chunk are (row ri = tid/8 + 64u, channel quad q)
+  f32x4 sv[kNU];
+  f32x4 sa, sb;  // BN affine (scale, shift) x 1/(1-p) of the thread's 4 channels
+  auto load_chunk = [&](int tile, int c) {
+    const int tid = opaque_tid(), q = tid & 7;
+    const int g = tile / A.tiles_per_group;
+    const int w0 = (tile - g * A.tiles_per_group) * kS;
+    const float* af = A.aff_in + (long long)g * A.aff_gstride + c * kCK + 4 * q;
+    sa = gld<f32x4>(af);
+    sb = gld<f32x4>(af + CIN);
+#pragma unroll
+    for (int u = 0; u < kNU; ++u) {
+      const int ri = (tid >> 3) + 64 * u;
+      sv[u] = f32x4{-0.f, -0.f, -0.f, -0.f};
+      if (ri < kValidRows) {
+        const int s = ri / kL, t = ri - s * kL, w = w0 + s;
+        if (w < A.n_win) {
+          const long long si = A.in_shared ? w : (long long)g * A.n_win + w;
+          sv[u] = gld<f32x4>(A.in + (si * kL + t) * CIN + c * kCK + 4 * q);
+        }
+      }
+    }
+  };
+  auto store_chunk = [&](int tile, int c, char* buf) {
+    const int tid = opaque_tid(), q = tid & 7;
+    const int g = tile / A.tiles_per_group;
+    const int w0 = (tile - g * A.tiles_per_group) * kS;
+    unsigned skey = 0;
+    if (A.hash_in) skey = stream_key(A.seed, A.layer - 1, A.pass_base + g);
+#pragma unroll
+    for (int u = 0; u < kNU; ++u) {
+      const int ri = (tid >> 3) + 64 * u;
+      if (ri >= kValidRows) continue;
+      const int s = ri / kL, t = ri - s * kL, w = w0 + s;
+      const f32x4 v = sv[u];
+      bool keep[4];
+      if (A.hash_in) {
+        const unsigned k = sample_key(skey, A.window_offset + w);
+        const unsigned b01 = dropout_bits2(k, t, c * kCK + 4 * q);
+        const unsigned b23 = dropout_bits2(k, t, c * kCK + 4 * q + 2);
+        keep[0] = (b01 & 0xFFFFu) >= A.thr_in;
+        keep[1] = (b01 >> 16) >= A.thr_in;
+        keep[2] = (b23 & 0xFFFFu) >= A.thr_in;
+        keep[3] = (b23 >> 16) >= A.thr_in;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) keep[i] = true;
+      }
+      const bool valid = w < A.n_win;
+      f16x4 hi, lo;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const unsigned bits = __float_as_uint(v[i]);
+        const bool k = valid && keep[i] && (bits >> 31) == 0u;
+        const float a = k ? __builtin_fmaf(__uint_as_float(bits & 0x7FFFFFFFu), sa[i], sb[i]) : 0.f;
+        hi[i] = (_Float16)a;
+        lo[i] = (_Float16)(a - (float)hi[i]);
+      }
+      char* row = buf + (kHalo + s * kSR + t) * kRowB + 8 * q;
+      *reinterpret_cast<f16x4*>(row) = hi;
+      *reinterpret_cast<f16x4*>(row + 64) = lo;
+    }
+  };
+
+  // ---- accumulators and weight fragments
+  f32x4 acc[NCT][NRT];
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt) acc[ct][rt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto wbase = [&](int tile) -> const gf16x8* {
+    const int g = tile / A.tiles_per_group;
+    return (const gf16x8*)(A.wfrag) + (long long)g * A.w_gstride + ct0 * 128 + lane;
+  };
+  f16x8 ah[NCT], al[NCT];
+  auto load_a = [&](const gf16x8* p, f16x8 (&xh)[NCT], f16x8 (&xl)[NCT]) {
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) {
+      xh[ct] = p[ct * 128];
+      xl[ct] = p[ct * 128 + 64];
+    }
+  };
+
+  // per-lane B-fragment base: row m of the wave's first row tile, 16-B slot h, tap offset -PAD
+  const int bofs = ((rt0 * 16 + m + kHalo - PAD) * kRowB) + 16 * h;
+
+  // conv over chunk c (k-steps c*KS .. c*KS+KS-1) from LDS buffer buf; wcur: this tile's fragments,
+  // wnxt: the next tile's (prefetch across the tile boundary)
+  auto compute_chunk = [&](int c, const char* buf, const gf16x8* wcur, const gf16x8* wnxt) {
+    const char* bb = buf + bofs;
+#pragma unroll
+    for (int j = 0; j < KS; ++j) {
+      const int s = c * KS + j;
+      const gf16x8* np = (s + 1 < NSTEP) ? wcur + (long long)(s + 1) * FRAG_STEP : wnxt;
+      if constexpr (!CTO) {
+        // row-tile outer: all NCT weight fragments resident, next k-step's prefetched; B streamed
+        f16x8 nh[NCT], nl[NCT];
+        load_a(np, nh, nl);
+#pragma unroll
+        for (int rt = 0; rt < NRT; ++rt) {
+          const f16x8 bh = *reinterpret_cast<const f16x8*>(bb + (rt * 16 + j) * kRowB);
+          const f16x8 bl = *reinterpret_cast<const f16x8*>(bb + (rt * 16 + j) * kRowB + 64);
+#pragma unroll
+          for (int ct = 0; ct < NCT; ++ct) acc[ct][rt] = mfma(ah[ct], bh, acc[ct][rt]);
+#pragma unroll
+          for (int ct = 0; ct < NCT; ++ct) acc[ct][rt] = mfma(al[ct], bh, acc[ct][rt]);
+#pragma unroll
+          for (int ct = 0; ct < NCT; ++ct) acc[ct][rt] = mfma(ah[ct], bl, acc[ct][rt]);
+        }
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) {
+          ah[ct] = nh[ct];
+          al[ct] = nl[ct];
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the next tap's LDS reads out of this tap (VGPR budget)
+      } else {
+        // channel-tile outer: all NRT B fragments resident; each weight fragment is reloaded for the
+        // next k-step right after its last MFMA (latency covered by the remaining channel tiles)
+        f16x8 bh[NRT], bl[NRT];
+#pragma unroll
+        for (int rt = 0; rt < NRT; ++rt) {
+          bh[rt] = *reinterpret_cast<const f16x8*>(bb + (rt * 16 + j) * kRowB);
+          bl[rt] = *reinterpret_cast<const f16x8*>(bb + (rt * 16 + j) * kRowB + 64);
+        }
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) {
+#pragma unroll
+          for (int rt = 0; rt < NRT; ++rt) acc[ct][rt] = mfma(ah[ct], bh[rt], acc[ct][rt]);
+#pragma unroll
+          for (int rt = 0; rt < NRT; ++rt) acc[ct][rt] = mfma(al[ct], bh[rt], acc[ct][rt]);
+#pragma unroll
+          for (int rt = 0; rt < NRT; ++rt) acc[ct][rt] = mfma(ah[ct], bl[rt], acc[ct][rt]);
+          ah[ct] = np[ct * 128];
+          al[ct] = np[ct * 128 + 64];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+
+  // ---- epilogue of one tile: bias + ReLU, moments, block-l dropout, store / per-sample sums
+  auto epilogue = [&](int tile) {
+    const int lane = opaque_tid() & 63, m = lane & 15, h = lane >> 4;
+    const int g = tile / A.tiles_per_group;
+    const int w0 = (tile - g * A.tiles_per_group) * kS;
+    const float ws = A.wscale[A.p_gstride ? g : 0];
+    const float* bias = A.bias + (long long)g * A.p_gstride;
+    const bool drop = A.thr_out != 0u;
+    unsigned skey = 0;
+    if (drop) skey = stream_key(A.seed, A.layer, A.pass_base + g);
+    // channel-tile outer: only one tile's 4 channels of sums are live at a time
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) {
+      const int co0 = (ct0 + ct) * 16 + 4 * h;
+      const f32x4 b4 = gld<f32x4>(bias + co0);
+      f32x4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1, k1 = s1, k0 = s1;
+#pragma unroll
+      for (int rt = 0; rt < NRT; ++rt) {
+        const int i = (rt0 + rt) * 16 + m;
+        const int s = i >> 6, t = i & 63, w = w0 + s;
+        const bool valid = t < kL && w < A.n_win;
+        f32x4 r;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) r[e] = fmaxf(__builtin_fmaf(acc[ct][rt][e], ws, b4[e]), 0.f);
+        acc[ct][rt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        bool keep[4] = {true, true, true, true};
+        if (drop) {
+          const unsigned key = sample_key(skey, A.window_offset + w);
+          const unsigned b01 = dropout_bits2(key, t, co0), b23 = dropout_bits2(key, t, co0 + 2);
+          keep[0] = (b01 & 0xFFFFu) >= A.thr_out;
+          keep[1] = (b01 >> 16) >= A.thr_out;
+          keep[2] = (b23 & 0xFFFFu) >= A.thr_out;
+          keep[3] = (b23 >> 16) >= A.thr_out;
+        }
+        if (valid) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            s1[e] += r[e];
+            s2[e] = __builtin_fmaf(r[e], r[e], s2[e]);
+            if constexpr (LAST) {
+              k1[e] += keep[e] ? r[e] : 0.f;
+              k0[e] += keep[e] ? 1.f : 0.f;
+            }
+          }
+          if constexpr (!LAST) {
+            f32x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = __uint_as_float(__float_as_uint(r[e]) | (keep[e] ? 0u : 0x80000000u));
+            const long long sample = (long long)g * A.n_win + w;
+            *reinterpret_cast<f32x4*>(A.out + (sample * kL + t) * COUT + co0) = o;
+          }
+        }
+      }
+      // reduce over the 16 rows of each lane group (lanes sharing h hold the same 4 channels)
+      if (A.stats != nullptr) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float a = group16_sum(s1[e]), b = group16_sum(s2[e]);
+          if (m == 0) {
+            atomicAdd(&st[co0 + e], (double)a);
+            atomicAdd(&st[COUT + co0 + e], (double)b);
+          }
+        }
+      }
+      if constexpr (LAST) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          k1[e] = group16_sum(k1[e]);
+          k0[e] = group16_sum(k0[e]);
+        }
+        const int w = w0 + wm;  // NRT == 4: this wave row is exactly sample slot wm
+        if (m == 0 && w < A.n_win) {
+          float* o = A.out + ((long long)g * A.n_win + w) * (2 * COUT);
+          *reinterpret_cast<f32x4*>(o + co0) = k1;
+          *reinterpret_cast<f32x4*>(o + COUT + co0) = k0;
+        }
+      }
+    }
+  };
+
+  auto flush_stats = [&](int g) {
+    __syncthreads();
+    if (A.stats != nullptr) {
+      double* dst = A.stats + ((long long)g * kStatSlots + slot) * 2 * COUT;
+      for (int i = tid; i < 2 * COUT; i += kThreads) {
+        atomicAdd(dst + i, st[i]);
+        st[i] = 0.0;
+      }
+    }
+    __syncthreads();
+  };
+
+  // ---- persistent tile loop, software-pipelined over chunks
+  int bsel = 0;
+  int g_cur = t_begin / A.tiles_per_group;
+  load_chunk(t_begin, 0);
+  load_a(wbase(t_begin), ah, al);
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int g = tile / A.tiles_per_group;
+    if (g != g_cur) {
+      flush_stats(g_cur);
+      g_cur = g;
+    }
+    const gf16x8* wcur = wbase(tile);
+    const gf16x8* wnxt = wbase(tile + 1 < t_end ? tile + 1 : tile);
+#pragma unroll 1
+    for (int c = 0; c < NCH; ++c) {
+      char* buf = smem + bsel * kBufB;
+      bsel ^= 1;
+      store_chunk(tile, c, buf);
+      lds_barrier();
+      if (c + 1 < NCH) {
+        load_chunk(tile, c + 1);
+      } else if (tile + 1 < t_end) {
+        load_chunk(tile + 1, 0);
+      }
+      compute_chunk(c, buf, wcur, wnxt);
+    }
+    epilogue(tile);
+  }
+  flush_stats(g_cur);
+}
+
+// ------------------------------------------------------------------------------- block 1 (fp32)
+// R_1[g][w][t][c] = relu(b[c] + sum_{j, ci} x[w][t + j - 3][ci] W[j][ci][c]) in fp32 FMAs, 8 windows
+// per 256-thread block (thread = one output channel x one half of the time steps), + batch moments.
+__global__ __launch_bounds__(256) void l1_kernel(const L1Args A) {
+  __shared__ float xs[kL1Win][kL + 6][4];
+  __shared__ float red[2][2][128];
+  const int g = blockIdx.x / A.blocks_per_group;
+  const int w0 = (blockIdx.x - g * A.blocks_per_group) * kL1Win;
+  const int tid = threadIdx.x, c = tid & 127, half = tid >> 7;
+  for (int i = tid; i < kL1Win * (kL + 6) * 4; i += 256) {
+    const int s = i / ((kL + 6) * 4), r = (i / 4) % (kL + 6), ci = i & 3;
+    const int t = r - 3, w = w0 + s;
+    xs[s][r][ci] = (t >= 0 && t < kL && w < A.n_win) ? A.x[((long long)w * kL + t) * 4 + ci] : 0.f;
+  }
+  float wr[7][4];
+#pragma unroll
+  for (int j = 0; j < 7; ++j)
+#pragma unroll
+    for (int ci = 0; ci < 4; ++ci) wr[j][ci] = A.w[(((long long)g * 7 + j) * 4 + ci) * 128 + c];
+  const float bc = A.b[g * 128 + c];
+  __syncthreads();
+  float s1 = 0.f, s2 = 0.f;
+  for (int s = 0; s < kL1Win; ++s) {
+    const int w = w0 + s;
+    if (w >= A.n_win) break;
+    float* o = A.out + (((long long)g * A.n_win + w) * kL) * 128 + c;
+    for (int t = half * 30; t < half * 30 + 30; ++t) {
+      float v = bc;
+#pragma unroll
+      for (int j = 0; j < 7; ++j)
+#pragma unroll
+        for (int ci = 0; ci < 4; ++ci) v = __builtin_fmaf(xs[s][t + j][ci], wr[j][ci], v);
+      v = fmaxf(v, 0.f);
+      o[t * 128] = v;
+      s1 += v;
+      s2 = __builtin_fmaf(v, v, s2);
+    }
+  }
+  if (A.stats != nullptr) {
+    red[half][0][c] = s1;
+    red[half][1][c] = s2;
+    __syncthreads();
+    if (tid < 128) {
+      double* dst = A.stats + ((long long)g * kStatSlots + (blockIdx.x % kStatSlots)) * 2 * 128;
+      atomicAdd(dst + c, (double)red[0][0][c] + (double)red[1][0][c]);
+      atomicAdd(dst + 128 + c, (double)red[0][1][c] + (double)red[1][1][c]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------- BN affine (+ moving update)
+// aff[g][0][c] = gamma * rstd * dsc, aff[g][1][c] = (beta - mean * gamma * rstd) * dsc, where (mean, var)
+// are the biased batch moments of group g (stats != nullptr) or the moving statistics.  With
+// update != 0 the Keras moving averages are updated once per group in group order (one MC-Dropout
+// pass after the other, the side effect of model(x, training=True)).
+__global__ void aff_kernel(const AffArgs A) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= A.C) return;
+  for (int g = 0; g < A.groups; ++g) {
+    const long long po = (long long)g * A.p_gstride + c;
+    float mean, var;
+    if (A.stats != nullptr) {
+      const double* p = A.stats + (long long)g * kStatSlots * 2 * A.C + c;
+      double a = 0.0, b = 0.0;
+      for (int s = 0; s < kStatSlots; ++s) {
+        a += p[s * 2 * A.C];
+        b += p[s * 2 * A.C + A.C];
+      }
+      const double mu = a * A.inv_count;
+      mean = (float)mu;
+      var = (float)fmax(b * A.inv_count - mu * mu, 0.0);
+      if (A.update) {
+        for (int r = 0; r < A.repeat; ++r) {
+          A.mmean[po] = A.mmean[po] * A.momentum + mean * (1.f - A.momentum);
+          A.mvar[po] = A.mvar[po] * A.momentum + var * (1.f - A.momentum);
+        }
+      }
+    } else {
+      mean = A.mmean[po];
+      var = A.mvar[po];
+    }
+    const float sc = A.gamma[po] / sqrtf(var + A.eps);
+    A.aff[((long long)g * 2) * A.C + c] = sc * A.dsc;
+    A.aff[((long long)g * 2 + 1) * A.C + c] = (A.beta[po] - mean * sc) * A.dsc;
+  }
+}
+
+// --------------------------------------------------------------------------------------- head
+// p[g][w] = sigmoid(b + (1/60) sum_c w_c (aff_s[c] S1[c] + aff_t[c] S0[c])): one wave per sample.
+__global__ __launch_bounds__(256) void head_kernel(const HeadArgs A) {
+  const int lane = threadIdx.x & 63;
+  const long long sidx = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (sidx >= A.samples) return;
+  const int g = (int)(sidx / A.n_win);
+  const float* s = A.sums + sidx * 2 * A.C;
+  const float* af = A.aff + (long long)g * A.aff_gstride;
+  const float* dw = A.dw + (long long)g * A.p_gstride;
+  float v = 0.f;
+  for (int c = lane; c < A.C; c += 64) v += dw[c] * __builtin_fmaf(af[c], s[c], af[A.C + c] * s[A.C + c]);
+  v = wave_sum(v);
+  if (lane == 0) {
+    const float logit = v * (1.0f / kL) + A.db[A.p_gstride ? g : 0];
+    A.out[sidx] = A.out_logits ? logit : 1.0f / (1.0f + expf(-logit));
+  }
+}
+
+// ------------------------------------------------------------------------------- launch helpers
+template <int CIN, int COUT, int KS, int WM, int WN, bool LAST, bool CTO>
+hipError_t launch_layer(const LayerArgs& A, int grid, hipStream_t stream) {
+  constexpr int lds = 2 * kBufB + 2 * COUT * 8;
+  auto k = layer_kernel<CIN, COUT, KS, WM, WN, LAST, CTO>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), lds, stream, A);
+  return hipGetLastError();
+}
+
+}  // namespace x3
+
+// Reference channel / kernel-size table (cnn_baseline_train.py:59-86): the layer kernels are
+// instantiated for blocks 2..6 of that architecture.
+int x3_lds_bytes(int layer) {
+  static const int cout[6] = {128, 192, 224, 96, 256, 96};
+  return 2 * x3::kBufB + 2 * cout[layer] * 8;
+}
+
+hipError_t x3_launch_layer(int layer, const x3::LayerArgs& A, int grid, hipStream_t stream) {
+  using namespace x3;
+  switch (layer) {
+    case 1: return launch_layer<128, 192, 5, 2, 4, false, false>(A, grid, stream);
+    case 2: return launch_layer<192, 224, 3, 4, 2, false, true>(A, grid, stream);
+    case 3: return launch_layer<224, 96, 7, 4, 2, false, false>(A, grid, stream);
+    case 4: return launch_layer<96, 256, 9, 1, 8, false, false>(A, grid, stream);
+    case 5: return launch_layer<256, 96, 9, 4, 2, true, false>(A, grid, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t x3_launch_l1(const x3::L1Args& A, hipStream_t stream) {
+  const int grid = A.groups * A.blocks_per_group;
+  if (grid <= 0) return hipSuccess;
+  hipLaunchKernelGGL(x3::l1_kernel, dim3(grid), dim3(256), 0, stream, A);
+  return hipGetLastError();
+}
+
+hipError_t x3_launch_aff(const x3::AffArgs& A, hipStream_t stream) {
+  hipLaunchKernelGGL(x3::aff_kernel, dim3((A.C + 255) / 256), dim3(256), 0, stream, A);
+  return hipGetLastError();
+}
+
+hipError_t x3_launch_head(const x3::HeadArgs& A, hipStream_t stream) {
+  if (A.samples <= 0) return hipSuccess;
+  hipLaunchKernelGGL(x3::head_kernel, dim3((A.samples + 3) / 4), dim3(256), 0, stream, A);
+  return hipGetLastError();
+}
+
+}  // namespace apneauq

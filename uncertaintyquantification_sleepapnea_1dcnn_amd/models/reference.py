@@ -109,6 +109,7 @@ def forward(
     sample_ids: Optional[torch.Tensor] = None,
     return_logits: bool = False,
     bn_stats_hook=None,
+    dtype: Optional[torch.dtype] = None,
 ) -> torch.Tensor:
     """Forward pass; returns probabilities (N, 1) (or logits).
 
@@ -118,13 +119,15 @@ def forward(
     ``update_moving`` applies the Keras moving-average update in place (the side effect of
     the reference MC Dropout loop).  ``bn_stats_hook(h) -> (mean, var)`` replaces the
     local batch statistics (data-parallel SyncBN: global moments via a differentiable all-reduce).
+    ``dtype`` (default fp32, the reference's precision) selects the compute dtype; tests use float64
+    (with float64 parameters) as the exact oracle the fp32 paths are measured against.
     """
     use_drop = training if dropout is None else dropout
     use_batch = training if bn_batch_stats is None else bn_batch_stats
     n = x.shape[0]
     if sample_ids is None:
         sample_ids = torch.arange(n, device=x.device)
-    h = x.float()
+    h = x.float() if dtype is None else x.to(dtype)
     for i, b in enumerate(spec.blocks, start=1):
         h = torch.relu(conv1d_same(h, p[f"conv1d_{i}/kernel"], p[f"conv1d_{i}/bias"]))
         gamma, beta = p[f"batchnorm_{i}/gamma"], p[f"batchnorm_{i}/beta"]

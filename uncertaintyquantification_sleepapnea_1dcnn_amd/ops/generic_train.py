@@ -94,6 +94,9 @@ class GenericTrainWorkspace:
             self.prob = torch.zeros(B, device=dev)
             self.dlog = torch.zeros(B, device=dev)
             self.head_loss = torch.zeros(1, device=dev)
+            # [unused, Adam iterations]: the eager step computes Adam's bias correction on the device from
+            # this counter, exactly as the captured step does (eager == graph arithmetic)
+            self.counters = torch.zeros(2, dtype=torch.int32, device=dev)
             store = model.store
             self.grad = torch.zeros_like(store.flat)
             self.gviews = {}
@@ -239,7 +242,7 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, syn
     scale = 1.0
     if grad_allreduce is not None:
         scale = grad_allreduce(ws.grad)
-    model.optimizer.step(model.store.flat, ws.grad, grad_scale=scale)
+    model.optimizer.step(model.store.flat, ws.grad, grad_scale=scale, counters=ws.counters)
     return ws.head_loss.double().sum(), ws.prob[:n]
 
 

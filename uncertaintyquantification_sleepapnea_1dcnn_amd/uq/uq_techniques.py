@@ -174,13 +174,15 @@ def uq_evaluation_dist(uq_predictions, y_true) -> Dict[str, np.ndarray]:
 # ===================== Confidence Intervals =====================
 def bootstrap_metrics(uq_predictions, y_true, n_bootstrap: int = 100, random_state: Optional[int] = None,
                       parity: bool = True, device: Optional[str] = None,
-                      distributed: Optional[bool] = None) -> Optional[List[Dict]]:
+                      distributed: bool = False) -> Optional[List[Dict]]:
     """B bootstrap replicates of the 6 aggregate UQ metrics.
 
     The per-window metrics are invariant under resampling, so each replicate is a gather + mean
     over the resampled windows (mathematically identical to the reference's full recomputation,
-    ``uq_techniques.py:137-157``).  Under a multi-rank process group the windows are sharded and
-    the replicate sums all-reduced (``distributed.bootstrap_sharded``).
+    ``uq_techniques.py:137-157``).  ``distributed=True`` shards the windows over the process group and
+    all-reduces the replicate sums (``distributed.bootstrap_sharded``); it is a collective, so
+    EVERY rank must call it.  The default is the local computation: the drivers reach this function on
+    rank 0 only (``drivers._finish``), where a collective would wait for the other ranks forever.
     """
     torch = _torch()
     p = uq_predictions
@@ -191,7 +193,7 @@ def bootstrap_metrics(uq_predictions, y_true, n_bootstrap: int = 100, random_sta
     from . import distributed as D
 
     try:
-        if D.active() if distributed is None else distributed:
+        if distributed and D.active():
             idx = M.parity_bootstrap_indices(n_samples, n_bootstrap, random_state) if parity else None
             res = D.bootstrap_sharded(p, y, n_bootstrap, seed=0 if random_state is None else random_state, idx=idx)
             out = [dict(zip(M.AGG_KEYS, (float(v) for v in row))) for row in res.cpu().numpy()]
