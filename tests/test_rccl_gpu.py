@@ -39,4 +39,5 @@ def test_bench_reports_rccl_world1():
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["backend"] == "nccl" and out["n_gpus"] == 1 and len(out["devices"]) == 1
-    assert out["config"]["bn_mode_mcd"] == "batch" and out["extra"]["running_bn"]["value"] > 0
+    assert out["config"]["bn_mode_mcd"] == "batch" and out["dtype"] == "fp32"
+    assert out["extra"]["bf16"]["value"] > 0  # the bf16 engine timed in the same run

@@ -18,7 +18,7 @@ struct LayerArgs {
   double* stats;          // [G][16 slots][2][COUT] moment sums of R_l (nullptr: none)
   int n_win;              // windows per group
   int groups;
-  int tiles_per_group;
+  int tiles_per_group;    // informational (the kernel derives its tiling from n_win, groups and its tile size)
   int total_tiles;
   int in_shared;          // input indexed by window only (block-1 output shared by all passes)
   int hash_in;            // input dropout drawn from the counter hash (block-1 output carries no sign mask)

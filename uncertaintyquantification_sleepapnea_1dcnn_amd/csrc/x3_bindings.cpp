@@ -12,6 +12,7 @@
 
 namespace apneauq {
 int x3_lds_bytes(int layer);
+int x3_tile_samples(int layer);
 hipError_t x3_launch_layer(int layer, const x3::LayerArgs& A, int grid, hipStream_t stream);
 hipError_t x3_launch_l1(const x3::L1Args& A, hipStream_t stream);
 hipError_t x3_launch_aff(const x3::AffArgs& A, hipStream_t stream);
@@ -22,7 +23,6 @@ namespace {
 
 constexpr int kCh[7] = {4, 128, 192, 224, 96, 256, 96};
 constexpr int kKs[6] = {7, 5, 3, 7, 9, 9};
-constexpr int kTileSamples = 4;
 
 inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 inline void check(hipError_t e, const char* what) { TORCH_CHECK(e == hipSuccess, what, " failed: ", hipGetErrorString(e)); }
@@ -50,7 +50,8 @@ void x3_layer(int64_t layer, const at::Tensor& in, at::Tensor& out, const at::Te
   TORCH_CHECK(n_win >= 1 && groups >= 1, "x3_layer: empty launch");
   const int cin = kCh[layer], cout = kCh[layer + 1], ks = kKs[layer];
   const int64_t samples = n_win * groups, samples_in = in_shared ? n_win : samples;
-  const int64_t tpg = (n_win + kTileSamples - 1) / kTileSamples;
+  const int ts = apneauq::x3_tile_samples((int)layer);
+  const int64_t tpg = (n_win + ts - 1) / ts;
   TORCH_CHECK(tpg * groups < (int64_t(1) << 31), "x3_layer: too many tiles");
   const int64_t wgroups = w_gstride ? groups : 1, pgroups = p_gstride ? groups : 1;
   need(in, at::kFloat, samples_in * 60 * cin, "x3_layer: in");

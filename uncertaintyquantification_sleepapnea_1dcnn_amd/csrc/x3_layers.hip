@@ -48,15 +48,29 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const f16x8 gf16x8;
 
-constexpr int kThreads = 512, kWaves = 8;
-constexpr int kS = 4, kL = 60, kSR = 64, kHalo = 4;
-constexpr int kTileRows = kS * kSR;                  // 256 GEMM rows per tile
-constexpr int kLdsRows = kHalo + kTileRows + kHalo;  // 264
+// Staging waves: the HBM loads of the next chunk are issued by waves 0..SW-1 only.  vmcnt retires in
+// order, so a wave that issued them waits for them at its next weight-fragment wait; with the loads
+// confined to one wave of each SIMD pair (waves w and w+4 share a SIMD), the partner keeps the matrix
+// pipe busy meanwhile.  APNEAUQ_X3_SW=0: every wave stages.
+#ifndef APNEAUQ_X3_SW
+#define APNEAUQ_X3_SW 4
+#endif
+// Timing-only ablation probes (0 in the library build; nonzero values compute garbage):
+// 1 = no input staging (loads + LDS writes), 2 = no epilogue stores, 4 = no MFMAs,
+// 8 = weight fragments re-read from k-step 0 (L1-resident: no L2 weight stream)
+#ifndef APNEAUQ_X3_RG  // row tiles per MFMA issue group (0: per-layer default; probes force 1 / 2)
+#define APNEAUQ_X3_RG 0
+#endif
+#ifndef APNEAUQ_X3_ABL
+#define APNEAUQ_X3_ABL 0
+#endif
+constexpr int kL = 60, kSR = 64, kHalo = 4;
 constexpr int kCK = 32;                              // input channels per staged chunk
 constexpr int kRowB = 160;                           // LDS row: hi 64 B | lo 64 B | pad 32 B
-constexpr int kBufB = kLdsRows * kRowB;              // 42,240 B per chunk buffer
-constexpr int kValidRows = kS * kL;                  // 240 staged rows per tile
-constexpr int kNU = (kValidRows * (kCK / 4) + kThreads - 1) / kThreads;  // 16-B staging units per thread
+// per tile of S samples (S x 64 GEMM rows): LDS rows, chunk-buffer bytes, staged rows, 16-B staging units
+__host__ __device__ constexpr int lds_rows(int S) { return kHalo + S * kSR + kHalo; }
+__host__ __device__ constexpr int buf_bytes(int S) { return lds_rows(S) * kRowB; }
+__host__ __device__ constexpr int lds_bytes(int S, int cout) { return 2 * buf_bytes(S) + 2 * cout * 8; }
 
 // global-address-space load (keeps global_load_*, never flat_*)
 template <typename T>
@@ -73,7 +87,13 @@ __device__ __forceinline__ int opaque_tid() {
 }
 
 __device__ __forceinline__ f32x4 mfma(const f16x8& a, const f16x8& b, const f32x4& c) {
+#if (APNEAUQ_X3_ABL & 4)
+  f32x4 r = c;
+  asm volatile("" : "+v"(r) : "v"(a), "v"(b));
+  return r;
+#else
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+#endif
 }
 
 // LDS hazard barrier: orders LDS traffic only (global loads in flight stay in flight)
@@ -90,14 +110,25 @@ __device__ __forceinline__ int xcd_wg() {
   return (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + bid / 8;
 }
 
-template <int CIN, int COUT, int KS, int WM, int WN, bool LAST, bool CTO>
-__global__ __launch_bounds__(kThreads, 2) void layer_kernel(const LayerArgs A) {
+template <int CIN, int COUT, int KS, int S, int WM, int WN, bool LAST>
+__global__ __launch_bounds__(WM * WN * 64, 2) void layer_kernel(const LayerArgs A) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int NCH = CIN / kCK, NCTA = COUT / 16, NCT = NCTA / WN, NRT = 16 / WM, PAD = (KS - 1) / 2;
+  constexpr int NW = WM * WN, kThreads = NW * 64;
+  constexpr int kS = S, kBufB = buf_bytes(S), kValidRows = S * kL, kUnits = kValidRows * (kCK / 4);
+  constexpr int SW = (APNEAUQ_X3_SW > 0 && APNEAUQ_X3_SW < NW) ? APNEAUQ_X3_SW : NW;  // staging waves
+  constexpr int kST = SW * 64;                                // staging threads
+  constexpr int kNU = (kUnits + kST - 1) / kST;              // 16-B staging units per staging thread
+  static_assert(kST % 8 == 0, "a staging thread keeps one channel quad");
+  constexpr int NCH = CIN / kCK, NCTA = COUT / 16, NCT = NCTA / WN, NRT = 4 * S / WM, PAD = (KS - 1) / 2;
   constexpr int NSTEP = NCH * KS;
+  // MFMA issue order: row tiles in groups of RG so that >= 4 accumulators rotate (dependent-issue
+  // latency); B fragments double-buffered one group ahead when the accumulators leave room
+  constexpr int RG = APNEAUQ_X3_RG > 0 ? APNEAUQ_X3_RG : NCT >= 4 ? 1 : (NCT >= 3 && NCT * NRT > 16) ? 1 : 2;
+  constexpr bool BDB = NCT * NRT <= 24;
+  static_assert(NRT % RG == 0, "row-tile groups");
   constexpr long long FRAG_STEP = (long long)NCTA * 128;  // f16x8 per (chunk, tap) k-step
   static_assert(CIN % kCK == 0 && COUT % 16 == 0, "channel tiling");
-  static_assert(WM * WN == kWaves && NCTA % WN == 0 && 16 % WM == 0, "wave tiling");
+  static_assert(NCTA % WN == 0 && (4 * S) % WM == 0, "wave tiling");
   static_assert(!LAST || NRT == 4, "block 6: one sample per wave row");
   double* st = reinterpret_cast<double*>(smem + 2 * kBufB);  // [2][COUT] per-workgroup moment sums
 
@@ -113,24 +144,28 @@ __global__ __launch_bounds__(kThreads, 2) void layer_kernel(const LayerArgs A) {
   __syncthreads();
 
   const int wg = xcd_wg();
-  const int t_begin = (int)((long long)wg * A.total_tiles / gridDim.x);
-  const int t_end = (int)((long long)(wg + 1) * A.total_tiles / gridDim.x);
+  const int tpg = (A.n_win + S - 1) / S;  // tiles per group at this kernel's tile size
+  const int total_tiles = tpg * A.groups;
+  const int t_begin = (int)((long long)wg * total_tiles / gridDim.x);
+  const int t_end = (int)((long long)(wg + 1) * total_tiles / gridDim.x);
   if (t_begin >= t_end) return;  // workgroup-uniform
   const int slot = wg % kStatSlots;
 
-  // ---- staging: this thread's 16-B units of a chunk are (row ri = tid/8 + 64u, channel quad q)
+  // ---- staging (waves < SW): a staging thread's 16-B units of a chunk are (row ri = tid/8 + kST/8 u,
+  // channel quad q = tid % 8)
+  const bool stager = wave < SW && (APNEAUQ_X3_ABL & 1) == 0;
   f32x4 sv[kNU];
   f32x4 sa, sb;  // BN affine (scale, shift) x 1/(1-p) of the thread's 4 channels
   auto load_chunk = [&](int tile, int c) {
     const int tid = opaque_tid(), q = tid & 7;
-    const int g = tile / A.tiles_per_group;
-    const int w0 = (tile - g * A.tiles_per_group) * kS;
+    const int g = tile / tpg;
+    const int w0 = (tile - g * tpg) * kS;
     const float* af = A.aff_in + (long long)g * A.aff_gstride + c * kCK + 4 * q;
     sa = gld<f32x4>(af);
     sb = gld<f32x4>(af + CIN);
 #pragma unroll
     for (int u = 0; u < kNU; ++u) {
-      const int ri = (tid >> 3) + 64 * u;
+      const int ri = (tid >> 3) + (kST / 8) * u;
       sv[u] = f32x4{-0.f, -0.f, -0.f, -0.f};
       if (ri < kValidRows) {
         const int s = ri / kL, t = ri - s * kL, w = w0 + s;
@@ -143,13 +178,13 @@ __global__ __launch_bounds__(kThreads, 2) void layer_kernel(const LayerArgs A) {
   };
   auto store_chunk = [&](int tile, int c, char* buf) {
     const int tid = opaque_tid(), q = tid & 7;
-    const int g = tile / A.tiles_per_group;
-    const int w0 = (tile - g * A.tiles_per_group) * kS;
+    const int g = tile / tpg;
+    const int w0 = (tile - g * tpg) * kS;
     unsigned skey = 0;
     if (A.hash_in) skey = stream_key(A.seed, A.layer - 1, A.pass_base + g);
 #pragma unroll
     for (int u = 0; u < kNU; ++u) {
-      const int ri = (tid >> 3) + 64 * u;
+      const int ri = (tid >> 3) + (kST / 8) * u;
       if (ri >= kValidRows) continue;
       const int s = ri / kL, t = ri - s * kL, w = w0 + s;
       const f32x4 v = sv[u];
@@ -189,7 +224,7 @@ __global__ __launch_bounds__(kThreads, 2) void layer_kernel(const LayerArgs A) {
 #pragma unroll
     for (int rt = 0; rt < NRT; ++rt) acc[ct][rt] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto wbase = [&](int tile) -> const gf16x8* {
-    const int g = tile / A.tiles_per_group;
+    const int g = tile / tpg;
     return (const gf16x8*)(A.wfrag) + (long long)g * A.w_gstride + ct0 * 128 + lane;
   };
   f16x8 ah[NCT], al[NCT];
@@ -205,64 +240,74 @@ __global__ __launch_bounds__(kThreads, 2) void layer_kernel(const LayerArgs A) {
   const int bofs = ((rt0 * 16 + m + kHalo - PAD) * kRowB) + 16 * h;
 
   // conv over chunk c (k-steps c*KS .. c*KS+KS-1) from LDS buffer buf; wcur: this tile's fragments,
-  // wnxt: the next tile's (prefetch across the tile boundary)
-  auto compute_chunk = [&](int c, const char* buf, const gf16x8* wcur, const gf16x8* wnxt) {
+  // wnxt: the next tile's (prefetch across the tile boundary).  hook() runs after tap KS/2: the staging
+  // waves write the NEXT chunk into the other LDS buffer there, so that VALU / LDS-write work overlaps
+  // the partner wave's MFMAs instead of sitting between two barriers.
+  auto compute_chunk = [&](int c, const char* buf, const gf16x8* wcur, const gf16x8* wnxt, auto&& hook) {
     const char* bb = buf + bofs;
 #pragma unroll
     for (int j = 0; j < KS; ++j) {
       const int s = c * KS + j;
-      const gf16x8* np = (s + 1 < NSTEP) ? wcur + (long long)(s + 1) * FRAG_STEP : wnxt;
-      if constexpr (!CTO) {
-        // row-tile outer: all NCT weight fragments resident, next k-step's prefetched; B streamed
-        f16x8 nh[NCT], nl[NCT];
-        load_a(np, nh, nl);
+      const gf16x8* np = (APNEAUQ_X3_ABL & 8) ? wcur : (s + 1 < NSTEP) ? wcur + (long long)(s + 1) * FRAG_STEP : wnxt;
+      // all NCT weight fragments resident, the next k-step's issued first (a full tap of MFMAs hides its
+      // L2 latency); B fragments double-buffered one row tile ahead when registers allow.  The
+      // sched_barriers pin that issue order (left alone, the scheduler sinks each load to its use).
+      f16x8 nh[NCT], nl[NCT];
+      load_a(np, nh, nl);
+      __builtin_amdgcn_sched_barrier(0);
+      // row tiles in groups of RG: the 3 x NCT x RG MFMAs of a group cycle through NCT x RG
+      // accumulators, so a dependent MFMA follows its predecessor >= 4 issues later
+      auto ldb = [&](int rt, f16x8& h_, f16x8& l_) {
+        h_ = *reinterpret_cast<const f16x8*>(bb + (rt * 16 + j) * kRowB);
+        l_ = *reinterpret_cast<const f16x8*>(bb + (rt * 16 + j) * kRowB + 64);
+      };
+      f16x8 bh[RG], bl[RG];
 #pragma unroll
-        for (int rt = 0; rt < NRT; ++rt) {
-          const f16x8 bh = *reinterpret_cast<const f16x8*>(bb + (rt * 16 + j) * kRowB);
-          const f16x8 bl = *reinterpret_cast<const f16x8*>(bb + (rt * 16 + j) * kRowB + 64);
+      for (int r = 0; r < RG; ++r) ldb(r, bh[r], bl[r]);
 #pragma unroll
-          for (int ct = 0; ct < NCT; ++ct) acc[ct][rt] = mfma(ah[ct], bh, acc[ct][rt]);
+      for (int rg = 0; rg < NRT; rg += RG) {
+        f16x8 bh2[RG], bl2[RG];
 #pragma unroll
-          for (int ct = 0; ct < NCT; ++ct) acc[ct][rt] = mfma(al[ct], bh, acc[ct][rt]);
-#pragma unroll
-          for (int ct = 0; ct < NCT; ++ct) acc[ct][rt] = mfma(ah[ct], bl, acc[ct][rt]);
-        }
-#pragma unroll
-        for (int ct = 0; ct < NCT; ++ct) {
-          ah[ct] = nh[ct];
-          al[ct] = nl[ct];
-        }
-        __builtin_amdgcn_sched_barrier(0);  // keep the next tap's LDS reads out of this tap (VGPR budget)
-      } else {
-        // channel-tile outer: all NRT B fragments resident; each weight fragment is reloaded for the
-        // next k-step right after its last MFMA (latency covered by the remaining channel tiles)
-        f16x8 bh[NRT], bl[NRT];
-#pragma unroll
-        for (int rt = 0; rt < NRT; ++rt) {
-          bh[rt] = *reinterpret_cast<const f16x8*>(bb + (rt * 16 + j) * kRowB);
-          bl[rt] = *reinterpret_cast<const f16x8*>(bb + (rt * 16 + j) * kRowB + 64);
-        }
-#pragma unroll
-        for (int ct = 0; ct < NCT; ++ct) {
-#pragma unroll
-          for (int rt = 0; rt < NRT; ++rt) acc[ct][rt] = mfma(ah[ct], bh[rt], acc[ct][rt]);
-#pragma unroll
-          for (int rt = 0; rt < NRT; ++rt) acc[ct][rt] = mfma(al[ct], bh[rt], acc[ct][rt]);
-#pragma unroll
-          for (int rt = 0; rt < NRT; ++rt) acc[ct][rt] = mfma(ah[ct], bl[rt], acc[ct][rt]);
-          ah[ct] = np[ct * 128];
-          al[ct] = np[ct * 128 + 64];
+        for (int r = 0; r < RG; ++r) {
+          bh2[r] = bh[r];
+          bl2[r] = bl[r];
+          if (BDB && rg + RG < NRT) ldb(rg + RG + r, bh2[r], bl2[r]);
+          if (!BDB) ldb(rg + r, bh[r], bl[r]);
         }
         __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int r = 0; r < RG; ++r)
+#pragma unroll
+          for (int ct = 0; ct < NCT; ++ct) acc[ct][rg + r] = mfma(ah[ct], bh[r], acc[ct][rg + r]);
+#pragma unroll
+        for (int r = 0; r < RG; ++r)
+#pragma unroll
+          for (int ct = 0; ct < NCT; ++ct) acc[ct][rg + r] = mfma(al[ct], bh[r], acc[ct][rg + r]);
+#pragma unroll
+        for (int r = 0; r < RG; ++r)
+#pragma unroll
+          for (int ct = 0; ct < NCT; ++ct) acc[ct][rg + r] = mfma(ah[ct], bl[r], acc[ct][rg + r]);
+#pragma unroll
+        for (int r = 0; r < RG; ++r) {
+          bh[r] = bh2[r];
+          bl[r] = bl2[r];
+        }
       }
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) {
+        ah[ct] = nh[ct];
+        al[ct] = nl[ct];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (j == KS / 2) hook();
     }
   };
 
   // ---- epilogue of one tile: bias + ReLU, moments, block-l dropout, store / per-sample sums
   auto epilogue = [&](int tile) {
     const int lane = opaque_tid() & 63, m = lane & 15, h = lane >> 4;
-    const int g = tile / A.tiles_per_group;
-    const int w0 = (tile - g * A.tiles_per_group) * kS;
+    const int g = tile / tpg;
+    const int w0 = (tile - g * tpg) * kS;
     const float ws = A.wscale[A.p_gstride ? g : 0];
     const float* bias = A.bias + (long long)g * A.p_gstride;
     const bool drop = A.thr_out != 0u;
@@ -307,7 +352,10 @@ __global__ __launch_bounds__(kThreads, 2) void layer_kernel(const LayerArgs A) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) o[e] = __uint_as_float(__float_as_uint(r[e]) | (keep[e] ? 0u : 0x80000000u));
             const long long sample = (long long)g * A.n_win + w;
-            *reinterpret_cast<f32x4*>(A.out + (sample * kL + t) * COUT + co0) = o;
+            if constexpr ((APNEAUQ_X3_ABL & 2) == 0)
+              *reinterpret_cast<f32x4*>(A.out + (sample * kL + t) * COUT + co0) = o;
+            else
+              asm volatile("" :: "v"(o));
           }
         }
       }
@@ -350,33 +398,40 @@ __global__ __launch_bounds__(kThreads, 2) void layer_kernel(const LayerArgs A) {
     __syncthreads();
   };
 
-  // ---- persistent tile loop, software-pipelined over chunks
-  int bsel = 0;
-  int g_cur = t_begin / A.tiles_per_group;
-  load_chunk(t_begin, 0);
+  // ---- persistent loop over the flattened (tile, chunk) sequence, software-pipelined:
+  //   iteration it: compute chunk it from buf[it & 1]; staging waves write chunk it+1 (loaded into
+  //   registers one iteration earlier) into buf[(it+1) & 1] mid-way; barrier; issue the loads of it+2.
+  // buf[(it+1) & 1] was last read by compute(it-1), which every wave finished before barrier(it-1).
+  const int total = (t_end - t_begin) * NCH;
+  auto chunk_tile = [&](int it) { return t_begin + it / NCH; };
+  int g_cur = t_begin / tpg;
+  if (stager) {
+    load_chunk(t_begin, 0);
+    store_chunk(t_begin, 0, smem);
+  }
+  lds_barrier();
+  if (stager && total > 1) load_chunk(chunk_tile(1), 1 % NCH);
   load_a(wbase(t_begin), ah, al);
-  for (int tile = t_begin; tile < t_end; ++tile) {
-    const int g = tile / A.tiles_per_group;
-    if (g != g_cur) {
-      flush_stats(g_cur);
-      g_cur = g;
+#pragma unroll 1
+  for (int it = 0; it < total; ++it) {
+    const int tile = chunk_tile(it), c = it - (tile - t_begin) * NCH;
+    if (c == 0) {
+      const int g = tile / tpg;
+      if (g != g_cur) {
+        flush_stats(g_cur);
+        g_cur = g;
+      }
     }
     const gf16x8* wcur = wbase(tile);
     const gf16x8* wnxt = wbase(tile + 1 < t_end ? tile + 1 : tile);
-#pragma unroll 1
-    for (int c = 0; c < NCH; ++c) {
-      char* buf = smem + bsel * kBufB;
-      bsel ^= 1;
-      store_chunk(tile, c, buf);
-      lds_barrier();
-      if (c + 1 < NCH) {
-        load_chunk(tile, c + 1);
-      } else if (tile + 1 < t_end) {
-        load_chunk(tile + 1, 0);
-      }
-      compute_chunk(c, buf, wcur, wnxt);
-    }
-    epilogue(tile);
+    char* buf = smem + (it & 1) * kBufB;
+    char* nbuf = smem + ((it + 1) & 1) * kBufB;
+    compute_chunk(c, buf, wcur, wnxt, [&]() {
+      if (stager && it + 1 < total) store_chunk(chunk_tile(it + 1), (it + 1) % NCH, nbuf);
+    });
+    if (c == NCH - 1) epilogue(tile);
+    lds_barrier();
+    if (stager && it + 2 < total) load_chunk(chunk_tile(it + 2), (it + 2) % NCH);
   }
   flush_stats(g_cur);
 }
@@ -488,39 +543,57 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs A) {
 }
 
 // ------------------------------------------------------------------------------- launch helpers
-template <int CIN, int COUT, int KS, int WM, int WN, bool LAST, bool CTO>
+template <int CIN, int COUT, int KS, int S, int WM, int WN, bool LAST>
 hipError_t launch_layer(const LayerArgs& A, int grid, hipStream_t stream) {
-  constexpr int lds = 2 * kBufB + 2 * COUT * 8;
-  auto k = layer_kernel<CIN, COUT, KS, WM, WN, LAST, CTO>;
+  constexpr int lds = lds_bytes(S, COUT);
+  auto k = layer_kernel<CIN, COUT, KS, S, WM, WN, LAST>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), lds, stream, A);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(WM * WN * 64), lds, stream, A);
   return hipGetLastError();
 }
 
 }  // namespace x3
 
-// Reference channel / kernel-size table (cnn_baseline_train.py:59-86): the layer kernels are
-// instantiated for blocks 2..6 of that architecture.
+// Layer table of the reference architecture (cnn_baseline_train.py:59-86), blocks 2..6:
+//   <Cin, Cout, k, samples per tile, wave rows WM, wave channel groups WN, block 6>
+// Each wave owns (4 S / WM) 16-row tiles x (Cout / 16 / WN) 16-channel tiles; the 64-accumulator-tile
+// layers (Cout 224 / 256) run 2-sample tiles so that the staging registers, the next k-step's weight
+// fragments and the B double-buffer fit beside the accumulators without spilling.
+#define APNEAUQ_X3_LAYERS(X)                       \
+  X(1, 128, 192, 5, 4, 2, 4, false)                \
+  X(2, 192, 224, 3, 2, 1, 7, false)                \
+  X(3, 224, 96, 7, 4, 4, 2, false)                 \
+  X(4, 96, 256, 9, 2, 1, 8, false)                 \
+  X(5, 256, 96, 9, 4, 4, 2, true)
+
 int x3_lds_bytes(int layer) {
-  static const int cout[6] = {128, 192, 224, 96, 256, 96};
-  return 2 * x3::kBufB + 2 * cout[layer] * 8;
+#define APNEAUQ_X3_LDS(L, CI, CO, K, S, WM, WN, LAST) \
+  if (layer == L) return x3::lds_bytes(S, CO);
+  APNEAUQ_X3_LAYERS(APNEAUQ_X3_LDS)
+#undef APNEAUQ_X3_LDS
+  return 0;
+}
+
+int x3_tile_samples(int layer) {
+#define APNEAUQ_X3_TS(L, CI, CO, K, S, WM, WN, LAST) \
+  if (layer == L) return S;
+  APNEAUQ_X3_LAYERS(APNEAUQ_X3_TS)
+#undef APNEAUQ_X3_TS
+  return 0;
 }
 
 hipError_t x3_launch_layer(int layer, const x3::LayerArgs& A, int grid, hipStream_t stream) {
   using namespace x3;
-  switch (layer) {
-    case 1: return launch_layer<128, 192, 5, 2, 4, false, false>(A, grid, stream);
-    case 2: return launch_layer<192, 224, 3, 4, 2, false, true>(A, grid, stream);
-    case 3: return launch_layer<224, 96, 7, 4, 2, false, false>(A, grid, stream);
-    case 4: return launch_layer<96, 256, 9, 1, 8, false, false>(A, grid, stream);
-    case 5: return launch_layer<256, 96, 9, 4, 2, true, false>(A, grid, stream);
-    default: return hipErrorInvalidValue;
-  }
+#define APNEAUQ_X3_LAUNCH(L, CI, CO, K, S, WM, WN, LAST) \
+  if (layer == L) return launch_layer<CI, CO, K, S, WM, WN, LAST>(A, grid, stream);
+  APNEAUQ_X3_LAYERS(APNEAUQ_X3_LAUNCH)
+#undef APNEAUQ_X3_LAUNCH
+  return hipErrorInvalidValue;
 }
 
 hipError_t x3_launch_l1(const x3::L1Args& A, hipStream_t stream) {
