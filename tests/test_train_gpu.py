@@ -71,9 +71,9 @@ def test_hip_train_step_matches_autograd(n):
 
 @pytest.mark.parametrize("n,max_samples", [(50, 1 << 20), (37, 80), (2049, 1 << 20), (2051, 4200)])
 def test_batch_stats_mc_dropout_matches_reference(n, max_samples):
-    """Odd n: tiles straddle pass boundaries; max_samples=80: 2 chunks share block 1's output/moments.
-    n >= ~2k (>= 8 tiles per CU per launch): the two-team ping-pong forward kernels; (2051, 4200): a
-    ping-pong first chunk (2 passes) and a single-team second chunk (1 pass)."""
+    """bf16 engine (the fp32-faithful one: tests/test_x3_gpu.py).  Odd n: tiles straddle pass
+    boundaries; max_samples=80 / 4200: several pass chunks share block 1's output and moments.  The
+    bound is set from the measured bf16 deviation (max |dp| 4.1e-3 at T=50 x 1024 windows, BENCH_r02)."""
     _ext.require()
     dev = torch.device("cuda")
     m = AlarconCNN1D(seed=6, device=dev)
@@ -88,36 +88,8 @@ def test_batch_stats_mc_dropout_matches_reference(n, max_samples):
         ref.append(torch.sigmoid(R.forward(m.spec, m.store.as_dict(), x, dropout=True, bn_batch_stats=True,
                                            update_moving=True, seed=m.seed, pass_id=t, return_logits=True)).reshape(-1))
     ref = torch.stack(ref)
-    torch.testing.assert_close(got, ref, atol=3e-2, rtol=3e-2)
+    torch.testing.assert_close(got, ref, atol=1e-2, rtol=0)
     torch.testing.assert_close(hip_stats, m.store.stats, atol=2e-3, rtol=2e-2)
-
-
-def test_pingpong_forward_matches_single_team_kernel():
-    """The two-team ping-pong forward (large batches) and the single-team forward compute the same
-    batch-BN MC-Dropout samples (same masks; moments differ only in fp64 summation order)."""
-    import subprocess
-    import sys
-
-    code = ("import torch,sys\n"
-            "from uncertaintyquantification_sleepapnea_1dcnn_amd.models.cnn import AlarconCNN1D\n"
-            "from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import train_ops\n"
-            "m = AlarconCNN1D(seed=8, device='cuda')\n"
-            "x = torch.randn(4097, 60, 4, generator=torch.Generator().manual_seed(3)).cuda()\n"
-            "p = train_ops.forward_batch_stats(m, x, 4, pass_base=5, seed=m.seed, update_moving=False)\n"
-            "torch.save(p.cpu(), sys.argv[1])\n")
-    import os
-    import tempfile
-
-    outs = []
-    with tempfile.TemporaryDirectory() as d:
-        for pp in ("1", "0"):  # opt-in ping-pong kernel vs the default single-team kernel
-            f = os.path.join(d, f"p{pp}.pt")
-            env = dict(os.environ, APNEAUQ_FWD_PP=pp)
-            r = subprocess.run([sys.executable, "-c", code, f], env=env, capture_output=True, text=True, timeout=240)
-            assert r.returncode == 0, r.stderr[-2000:]
-            outs.append(torch.load(f))
-    assert outs[0].shape == (4, 4097)
-    torch.testing.assert_close(outs[0], outs[1], atol=2e-3, rtol=0)
 
 
 def test_batch_bn_moments_fp64_at_bench_scale():

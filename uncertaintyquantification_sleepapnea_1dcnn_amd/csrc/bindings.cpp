@@ -62,7 +62,7 @@ namespace train {
 struct Layer {
   const void* wf; const void* wd; const float* bias; const float* gamma; const float* beta;
   float* mmean; float* mvar; float* gw; float* gb; float* ggamma; float* gbeta;
-  void* R; void* dY; void* dZ; double* st; double* bst; unsigned thr; float dsc; float* aff;
+  void* R; void* dY; void* dZ; double* st; double* bst; unsigned thr; float dsc;
 };
 struct Args {
   Layer L[6];
@@ -73,7 +73,6 @@ struct Args {
 };
 }  // namespace train
 int train_args_size();
-int train_read_stamps(void* dst, long long bytes);
 hipError_t launch_standardize(const double* x, double* out, long long n_win, int L, int C, double eps, hipStream_t stream);
 hipError_t launch_knn(const double* X, int n, int D, long long* out, int k, hipStream_t stream);
 int knn_lds_bytes(int D, int K);
@@ -238,7 +237,7 @@ void bump_counters(at::Tensor& counters) {
 }
 
 // ctx: int64 CPU tensor of device pointers / scalars built once per workspace (ops/train_ops.py)
-constexpr int kCtxLayer = 19, kCtxLen = 6 * kCtxLayer + 27;
+constexpr int kCtxLayer = 18, kCtxLen = 6 * kCtxLayer + 27;
 
 float bits_to_float(int64_t v) {
   uint32_t u = static_cast<uint32_t>(v);
@@ -276,7 +275,6 @@ apneauq::train::Args args_from_ctx(const at::Tensor& ctx, int64_t pass_base) {
     L.thr = static_cast<unsigned>(q[15]);
     L.dsc = bits_to_float(q[16]);
     L.dZ = reinterpret_cast<void*>(q[17]);
-    L.aff = reinterpret_cast<float*>(q[18]);
   }
   const int64_t* g = c + 6 * kCtxLayer;
   A.x = reinterpret_cast<const void*>(g[0]);
@@ -342,11 +340,6 @@ void train_call(const at::Tensor& ctx, int64_t op, int64_t layer, int64_t flag, 
 
 int64_t train_wgrad_part_size(int64_t B) { return apneauq::train_wgrad_part_floats((int)B); }
 int64_t train_det_size(int64_t B) { return apneauq::train_det_floats((int)B); }
-// probe builds only: forward phase stamps into a CPU uint8 tensor (returns -1 in the library build)
-int64_t train_stamps(const at::Tensor& out) {
-  TORCH_CHECK(out.device().is_cpu() && out.scalar_type() == at::kByte && out.is_contiguous(), "train_stamps: CPU uint8");
-  return apneauq::train_read_stamps(out.data_ptr(), out.numel());
-}
 
 void train_pack(const at::Tensor& w, int64_t k, int64_t cin, int64_t cout, at::Tensor& fwd, at::Tensor& dgr) {
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == k * cin * cout,
@@ -678,7 +671,6 @@ TORCH_LIBRARY(apneauq, m) {
   m.def("train_pack(Tensor w, int k, int cin, int cout, Tensor(a!) fwd, Tensor(b!) dgr) -> ()");
   m.def("train_wgrad_part_size(int B) -> int", &train_wgrad_part_size);
   m.def("train_det_size(int B) -> int", &train_det_size);
-  m.def("train_stamps(Tensor out) -> int", &train_stamps);
   m.def("prep_standardize(Tensor x, float eps) -> Tensor");
   m.def("prep_knn(Tensor X, int k) -> Tensor");
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, float b1, float b2, float alpha, float eps, "

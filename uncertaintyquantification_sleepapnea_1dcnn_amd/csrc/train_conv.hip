@@ -25,8 +25,9 @@
 // Forward and dgrad are implicit GEMMs on v_mfma_f32_16x16x32_bf16 with the weights as the A operand
 // (pre-packed fragments from global/L2) and the staged activations as the B operand (LDS,
 // ds_read_b128).  wgrad reduces over rows, so both operands are read with the CDNA4 transposing
-// LDS read ds_read_b64_tr_b16 from row-major tiles; each workgroup sums 16 row tiles in registers
-// and adds its output block to the fp32 gradient with global atomics.
+// LDS read ds_read_b64_tr_b16 from row-major tiles; each workgroup sums up to 16 row tiles in
+// registers and writes its output block to a per-row-group partial slot (Args::wpart), which
+// wgrad_reduce_kernel adds in a fixed order (deterministic, and cheaper than fp32 atomics).
 #include <algorithm>
 #include <cstdlib>
 
@@ -40,10 +41,7 @@ namespace train {
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 
 constexpr int kL = 60, kSR = 64, kSlots = 2, kR = 128, kRT = 8, kHalo = 4, kRows = 136;
-#ifndef APNEAUQ_KRS  // LDS row stride (bytes) of the staged activation tiles (probes vary it)
-#define APNEAUQ_KRS (256 * 2 + 32)
-#endif
-constexpr int kRS = APNEAUQ_KRS;
+constexpr int kRS = 256 * 2 + 32;  // LDS row stride (bytes) of the staged activation tiles
 constexpr int kThreads = 256;
 constexpr int C[7] = {4, 128, 192, 224, 96, 256, 96};
 constexpr int KS[6] = {7, 5, 3, 7, 9, 9};
@@ -69,8 +67,6 @@ struct Layer {
                        // BN-backward coefficients bit for bit in deterministic mode)
   unsigned thr;        // dropout threshold (16-bit units) and 1/(1-p)
   float dsc;
-  float* aff;          // [groups][2][C] BN affine (s = gamma * rstd, t = beta - mean * s) of the batch
-                       // statistics, written by aff_kernel for the ping-pong forward's staging
 };
 
 struct Args {
@@ -142,14 +138,8 @@ __device__ __forceinline__ uint32_t decode_pair(uint32_t d, float s0, float t0, 
 }
 constexpr uint32_t kNegZero2 = 0x80008000u;  // a pair of -0.0: "dropped" = decodes to A = 0
 
-// LDS tile addressing (SWZ 0: row-major; 1 / 2: XOR / row-permutation swizzles, kept for probes).
-// The transposed operand reads need no swizzle: see tr_frag.
-template <int SWZ>
-__device__ __forceinline__ int lds_off(int r, int b, int rs) {
-  if constexpr (SWZ == 1) return r * rs + (b ^ (((r >> 3) & 1) << 7));
-  if constexpr (SWZ == 2) return (r ^ (((r >> 3) & 1) << 2)) * rs + b;
-  return r * rs + b;
-}
+// LDS tile addressing: row-major (the transposed operand reads need no swizzle: see tr_frag)
+__device__ __forceinline__ int lds_off(int r, int b, int rs) { return r * rs + b; }
 
 __device__ __forceinline__ int row_sample(int grow) { return (grow - kHalo) >> 6; }  // may be -1 / >= B
 __device__ __forceinline__ int row_time(int grow) { return (grow - kHalo) & 63; }
@@ -157,59 +147,9 @@ __device__ __forceinline__ int row_time(int grow) { return (grow - kHalo) & 63; 
 // BN moment sums are accumulated into kStatSlots interleaved copies (slot = workgroup % kStatSlots)
 // so that the ~512 workgroups of a layer do not serialise on the same 2*C L2 atomic addresses;
 // readers add the slots.  Layout per layer: st[slot][group][2][C], bst[slot][2][C].
-// Probe hooks for timing the forward kernel's phases (always 0 in the library build; nonzero
-// values compute garbage): 4 = no copy-out, 8 = no conv MFMAs, 16 = no input staging, 32 = no epilogue
-// moments, 64 = no dropout hashing (copy-out / hash-in staging), 128 = every weight-fragment load reads
-// k-step 0 (L1-resident: the conv without its L2 weight stream), 256 = staging reads an L2-resident
-// 16-tile window instead of its own rows (decode kept), 512 = one workgroup per CU (LDS request doubled),
-// 1024 = constant BN affine (no slot sums in the prologue: 1-2 us per training launch, session 3).
-#ifndef APNEAUQ_FWD_ABL
-#define APNEAUQ_FWD_ABL 0
-#endif
-// 1: the forward kernels load tile i+1's input while tile i's moments and copy-out run (0: probe)
-#ifndef APNEAUQ_FWD_STAGEPAD
-#define APNEAUQ_FWD_STAGEPAD 1
-#endif
-#ifndef APNEAUQ_FWD_NB
-#define APNEAUQ_FWD_NB 4
-#endif
-#ifndef APNEAUQ_FWD_SKIPPAD
-#define APNEAUQ_FWD_SKIPPAD 1
-#endif
-#ifndef APNEAUQ_FWD_PIPE
-#define APNEAUQ_FWD_PIPE 0
-#endif
-// s_setprio 1 around the forward conv MFMAs (the co-resident workgroup's staging / copy-out VALU
-// gets the leftover issue slots: -1.5 % per chunk); probe: an initial s_sleep offset (x 127*64
-// cycles) for the second half of the grid (phase offset between co-resident workgroups: no effect)
-#ifndef APNEAUQ_FWD_PRIO
-#define APNEAUQ_FWD_PRIO 1
-#endif
-#ifndef APNEAUQ_FWD_DELAY
-#define APNEAUQ_FWD_DELAY 0
-#endif
-// dgrad probe hooks (0 in the library build; nonzero values compute garbage): 1 = epilogue without
-// the R_{l-1} loads, 2 = stage_dz without the global dZ write, 4 = no dY copy-out, 8 = no MFMAs,
-// 16 = stage_dz without its global loads
-#ifndef APNEAUQ_DG_ABL
-#define APNEAUQ_DG_ABL 0
-#endif
-
-// Phase stamps of the forward kernel (probe builds with -DAPNEAUQ_FWD_STAMPS only): s_memtime at the
-// phase boundaries of the first kFstT tiles of the first kFstWG workgroups (wave 0, lane 0), plus
-// the workgroup's XCC and CU ids; read back with train_read_stamps (tools/probes/fwd_stamps.py).
-constexpr int kFstWG = 1024, kFstT = 16, kFstN = 6;
-#ifdef APNEAUQ_FWD_STAMPS
-__device__ unsigned long long g_fst[kFstWG][kFstT][kFstN];
-__device__ unsigned g_fst_cu[kFstWG][2];
-#define APNEAUQ_FST(i, k)                                                                      \
-  do {                                                                                         \
-    if (l == APNEAUQ_FWD_STAMPS && blockIdx.x < kFstWG && (k) < kFstT && threadIdx.x == 0)    \
-      g_fst[blockIdx.x][(k)][(i)] = __builtin_amdgcn_s_memtime();                              \
-  } while (0)
-#else
-#define APNEAUQ_FST(i, k) ((void)0)
-#endif
+// s_setprio 1 around the forward conv MFMAs: the co-resident workgroup's staging / copy-out VALU gets
+// the leftover issue slots (-1.5 % per batch-BN chunk, profiles/batch_bn_fwd_r2.md).
+constexpr bool kFwdPrio = true;
 
 constexpr int kStatSlots = 16;
 constexpr int kHeadRec = 2 + 3 * 96;  // deterministic head record per sample: loss, dlogit, dW, sum dY, sum dY xhat
@@ -224,7 +164,7 @@ __device__ __forceinline__ float slot_sum(const float* p, int stride) {
 }
 // All kStatSlots loads are issued before the first add: the training kernels run one tile per
 // workgroup at batch 1024, so their per-channel prologue (2-6 of these sums per channel) is exposed
-// latency -- 4 dependent round trips per sum cost dgrad 6-9 us (session-3 probe APNEAUQ_DG_ABL=32).
+// latency -- 4 dependent round trips per sum cost dgrad 6-9 us (round 2, session 3).
 __device__ __forceinline__ double slot_sumd(const double* p, int stride) {
   double v[kStatSlots];
 #pragma unroll
@@ -375,26 +315,12 @@ __device__ __forceinline__ void lds_row8(const float* tab, int c0, float scale, 
 // the second stats group (a tile straddling an MC-Dropout pass boundary, g1 = s/t + 256) is selected
 // per row only when it differs.  The dropout mask is R_l's sign bit (set by the producer), so the
 // transform is  a = sign ? 0 : |r| * s + t  on the packed bf16 pairs.
-//
-//
-// CMP (NR = kRows only): load just the tile's 2 x 60 valid rows; the caller keeps the 16 halo / pad
-// rows of the LDS tile (0-3, 64-67, 128-135) at zero.
-template <int l, int NR, int NCW, int UMAX = kStageU, int SWZ = 0, bool CMP = false>
+template <int l, int NR, int NCW, int UMAX = kStageU>
 __device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, int row0, int c0, const float* s,
                                           const float* t, int g0) {
-  static_assert(!CMP || NR == kRows, "compact staging covers a whole 136-row tile");
   constexpr int Cc = C[l + 1];
   constexpr int RP = kThreads / NCW;  // rows per pass over the workgroup
-  constexpr int NRL = CMP ? kSlots * kL : NR;  // rows loaded
-  constexpr int NK = (NRL + RP - 1) / RP;
-  auto lrow = [](int rc) {  // LDS / tile row of loaded row rc
-    if constexpr (CMP) {
-      const int slot = rc >= kL;
-      return kHalo + slot * kSR + (rc - kL * slot);
-    } else {
-      return rc;
-    }
-  };
+  constexpr int NK = (NR + RP - 1) / RP;
   constexpr int U = NK < UMAX ? NK : UMAX;
   const Layer& Ly = A.L[l];
   // opaque thread index (see staged_loop): keeps the per-row addresses out of enclosing tile loops
@@ -431,13 +357,13 @@ __device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, i
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int rc = rin + (b + u) * RP;
-          if (b + u < NK && active && rc < NRL) v[u] = gld<u32x4>(Ly.R + (long long)(row0 + lrow(rc)) * Cc + c);
+          if (b + u < NK && active && rc < NR) v[u] = gld<u32x4>(Ly.R + (long long)(row0 + rc) * Cc + c);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int rc = rin + (b + u) * RP;
-          if (b + u >= NK || !active || rc >= NRL) continue;
-          const int r = lrow(rc);
+          if (b + u >= NK || !active || rc >= NR) continue;
+          const int r = rc;
           u32x4 o;
           if constexpr (decltype(two_groups)::value) {  // rare: a tile straddling an MC-Dropout pass boundary
             const bool hi = row_sample(row0 + r) != smp0;
@@ -449,7 +375,7 @@ __device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, i
 #pragma unroll
             for (int q = 0; q < 4; ++q) o[q] = decode_pair(v[u][q], s0[2 * q], t0[2 * q], s0[2 * q + 1], t0[2 * q + 1]);
           }
-          *reinterpret_cast<u32x4*>(lds + lds_off<SWZ>(r, cw * 16, ldsrs)) = o;
+          *reinterpret_cast<u32x4*>(lds + lds_off(r, cw * 16, ldsrs)) = o;
         }
       }
     };
@@ -471,26 +397,21 @@ __device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, i
 // row 60, which holds -0.0 and decodes to 0 -- and block 1's dropout mask is drawn here from the
 // counter hash on every row, as sign bits (pad rows stay -0.0 whatever it draws).
 //
-// APNEAUQ_FWD_STAGEPAD (default): only the tile's 2 x 60 valid rows are loaded; the 16 halo / pad rows
-// of the LDS tile (0-3, 64-67, 128-135) are written as zeros instead (no global load, no decode).
+// Only the tile's 2 x 60 valid rows are loaded; the 16 halo / pad rows of the LDS tile (0-3, 64-67,
+// 128-135) are written as zeros instead (no global load, no decode).
 template <int l, bool HASH_IN>  // HASH_IN: may run in hash_in mode (runtime flag, workgroup-uniform)
 struct ActStager {
   static constexpr int Cc = C[l + 1];
   static constexpr int NCW = Cc / 8;
   static constexpr int RP = kThreads / NCW;  // rows per pass over the workgroup
-  static constexpr bool CMP = APNEAUQ_FWD_STAGEPAD != 0;
-  static constexpr int NR = CMP ? kSlots * kL : kRows;  // rows loaded from memory
+  static constexpr int NR = kSlots * kL;  // rows loaded from memory (the two samples' valid rows)
   static constexpr int NK = (NR + RP - 1) / RP;
   u32x4 v[NK];
 
-  // LDS row of loaded row rc (compact: the slot's time step, skipping halo and pad rows)
+  // LDS row of loaded row rc: the slot's time step, skipping halo and pad rows
   __device__ __forceinline__ static int lds_row(int rc) {
-    if constexpr (CMP) {
-      const int slot = rc >= kL;
-      return kHalo + slot * kSR + (rc - kL * slot);
-    } else {
-      return rc;
-    }
+    const int slot = rc >= kL;
+    return kHalo + slot * kSR + (rc - kL * slot);
   }
 
   __device__ __forceinline__ static int tid() {
@@ -519,22 +440,15 @@ struct ActStager {
       for (int u = U0; u < U1; ++u) {
         const int rc = rin + u * RP;
         if (rc >= NR) continue;
-        if constexpr (CMP) {
-          const int slot = rc >= kL;
-          v[u] = gld<u32x4>((slot ? src1 : src0) + (long long)(rc - kL * slot) * Cc);
-        } else {
-          const int grow = row0 + rc;
-          const int n = row_sample(grow);
-          const bool own = grow >= kHalo && (n == smp0 || n == smp0 + 1);
-          v[u] = gld<u32x4>((n == smp0 + 1 ? src1 : src0) + (long long)(own ? row_time(grow) : kL) * Cc);
-        }
+        const int slot = rc >= kL;
+        v[u] = gld<u32x4>((slot ? src1 : src0) + (long long)(rc - kL * slot) * Cc);
       }
     } else {
 #pragma unroll
       for (int u = U0; u < U1; ++u) {
         const int rc = rin + u * RP;
         if (rc < NR)
-          v[u] = gld<u32x4>(R + (long long)(((APNEAUQ_FWD_ABL & 256) ? (row0 & 2047) : row0) + lds_row(rc)) * Cc);
+          v[u] = gld<u32x4>(R + (long long)(row0 + lds_row(rc)) * Cc);
       }
     }
   }
@@ -544,13 +458,11 @@ struct ActStager {
   __device__ __forceinline__ void store(const Args& A, char* lds, int row0, const float* s, const float* t,
                                         int g0, bool hash_in) const {
     const int tt_ = tid(), cw = tt_ % NCW, rin = tt_ / NCW;
-    if constexpr (CMP) {
-      if (U0 == 0)  // the 16 halo / pad rows of the LDS tile: zeros (0-3, 64-67, 128-135)
-        for (int i = tt_; i < 16 * NCW; i += kThreads) {
-          const int pi = i / NCW, pr = pi < 4 ? pi : (pi < 8 ? kL + pi : 2 * kL + pi);
-          *reinterpret_cast<u32x4*>(lds + pr * kRS + (i - pi * NCW) * 16) = u32x4{0u, 0u, 0u, 0u};
-        }
-    }
+    if (U0 == 0)  // the 16 halo / pad rows of the LDS tile: zeros (0-3, 64-67, 128-135)
+      for (int i = tt_; i < 16 * NCW; i += kThreads) {
+        const int pi = i / NCW, pr = pi < 4 ? pi : (pi < 8 ? kL + pi : 2 * kL + pi);
+        *reinterpret_cast<u32x4*>(lds + pr * kRS + (i - pi * NCW) * 16) = u32x4{0u, 0u, 0u, 0u};
+      }
     if (rin >= RP) return;
     const Layer& Ly = A.L[l];
     const int c = cw * 8;
@@ -576,9 +488,8 @@ struct ActStager {
         const int rc = rin + u * RP;
         if (rc >= NR) continue;
         const int r = lds_row(rc);
-        const int grow = row0 + r;
-        const bool hi = CMP ? rc >= kL : row_sample(grow) == smp0 + 1;
-        const int tstep = CMP ? rc - kL * (rc >= kL) : row_time(grow);
+        const bool hi = rc >= kL;
+        const int tstep = rc - kL * (rc >= kL);
         u32x4 o;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -599,7 +510,7 @@ struct ActStager {
       else
         run(std::false_type{}, hashed);
     };
-    if (HASH_IN && hash_in && !(APNEAUQ_FWD_ABL & 64))
+    if (HASH_IN && hash_in)
       dispatch(std::integral_constant<bool, HASH_IN>{});
     else
       dispatch(std::false_type{});
@@ -613,7 +524,7 @@ struct ActStager {
 //   dz = relu'(r) * g*rstd * (dy - mean(dy) - xhat * mean(dy*xhat)),  xhat = (r - mean) * rstd
 // is folded per channel into dz = relu'(r) * (al * dy + be * r + ga), evaluated from registers
 // (r = |R_l|: the sign bit carries block l's dropout mask).
-template <int l, int NR, int NCW, int SWZ = 0>
+template <int l, int NR, int NCW>
 __device__ __forceinline__ void stage_dz(const Args& A, char* lds, int ldsrs, int row0, int c0,
                                          const float* gam_rstd, const float* mean, const float* rstd, const float* mdy,
                                          const float* mdyx, __bf16* gout = nullptr,
@@ -659,7 +570,7 @@ __device__ __forceinline__ void stage_dz(const Args& A, char* lds, int ldsrs, in
       const int r = rin + (b + u) * RP;
       const int grow = row0 + r;
       if (b + u >= NK) continue;
-      const bool ok = active && r < NR && valid(grow) && !(APNEAUQ_DG_ABL & 16);
+      const bool ok = active && r < NR && valid(grow);
       q[u].a = ok ? gld<bf16x8>(Ly.R + (long long)grow * Cc + c) : zero8();
       if constexpr (l < 5) q[u].b = ok ? gld<bf16x8>(Ly.dY + (long long)grow * Cc + c) : zero8();
     }
@@ -687,37 +598,26 @@ __device__ __forceinline__ void stage_dz(const Args& A, char* lds, int ldsrs, in
           o[j] = (__bf16)(rr > 0.f ? dz : 0.f);
         }
       }
-      *reinterpret_cast<bf16x8*>(lds + lds_off<SWZ>(r, cw * 16, ldsrs)) = o;
-      if (gout != nullptr && r >= own_lo && r < own_hi && !(APNEAUQ_DG_ABL & 2))
+      *reinterpret_cast<bf16x8*>(lds + lds_off(r, cw * 16, ldsrs)) = o;
+      if (gout != nullptr && r >= own_lo && r < own_hi)
         *reinterpret_cast<bf16x8*>(gout + (long long)grow * Cc + c) = o;  // pad rows get their zeros too
     }
   }
 }
 
-// CMP (NR = kR only): copy just the 2 x 60 valid rows of the tile; its 8 pad rows (60-63, 124-127)
-// stay at the zeros the caller wrote once (dZ is 0 there).
-template <int l, int NR, int NCW, int UMAX, int SWZ = 0, bool CMP = false>
+// dZ_l rows [row0, row0+NR) x channels [c0, c0+NCW*8) into LDS (wgrad; dgrad materialised them)
+template <int l, int NR, int NCW, int UMAX>
 __device__ __forceinline__ void stage_dz_copy(const Args& A, char* lds, int ldsrs, int row0, int c0) {
-  static_assert(!CMP || NR == kR, "compact copy covers a whole 128-row tile");
   constexpr int Cc = C[l + 1];
-  constexpr int NRL = CMP ? kSlots * kL : NR;
   const Layer& Ly = A.L[l];
-  auto lrow = [](int rc) {
-    if constexpr (CMP) {
-      const int slot = rc >= kL;
-      return slot * kSR + (rc - kL * slot);
-    } else {
-      return rc;
-    }
-  };
-  staged_loop<NRL * NCW, UMAX>(
+  staged_loop<NR * NCW, UMAX>(
       [&](int i) -> bf16x8 {
         const int rc = i / NCW, cw = i - rc * NCW;
-        return gld<bf16x8>(Ly.dZ + (long long)(row0 + lrow(rc)) * Cc + c0 + cw * 8);
+        return gld<bf16x8>(Ly.dZ + (long long)(row0 + rc) * Cc + c0 + cw * 8);
       },
       [&](int i, const bf16x8& o) {
         const int rc = i / NCW, cw = i - rc * NCW;
-        *reinterpret_cast<bf16x8*>(lds + lds_off<SWZ>(lrow(rc), cw * 16, ldsrs)) = o;
+        *reinterpret_cast<bf16x8*>(lds + lds_off(rc, cw * 16, ldsrs)) = o;
       });
 }
 
@@ -768,7 +668,7 @@ struct Conv {
     };
     auto load_a = [&](int s, bf16x8 (&a)[CT]) {
 #pragma unroll
-      for (int c = 0; c < CT; ++c) a[c] = wp[((APNEAUQ_FWD_ABL & 128) ? 0 : s * NCT + c) * 64];
+      for (int c = 0; c < CT; ++c) a[c] = wp[(s * NCT + c) * 64];
     };
     // Weight fragments (A, from L2) run through a ring of PD + 1 stages: step s + PD's loads are issued
     // before step s's MFMAs (the fused kernel's scheme; see FwdPD for the measured depths).
@@ -777,7 +677,7 @@ struct Conv {
     // NB - 1 LDS reads stay in flight.  RING = false reads each B fragment just in time (dgrad: one
     // tile per workgroup, two workgroups per CU, measured 5-17 % faster per layer without the ring).
     constexpr int NSA = PD + 1;
-    constexpr int NB = RT < APNEAUQ_FWD_NB ? RT : APNEAUQ_FWD_NB;  // B-fragment ring depth (probe macro)
+    constexpr int NB = RT < 4 ? RT : 4;  // B-fragment ring depth (2 and 8 measured equal / slower)
     static_assert(RT % NB == 0, "B ring phase restarts at every step");
     constexpr int DSN = FIRST ? 2 : 1;  // LDS reads per B fragment
     bf16x8 bq[NB];
@@ -829,84 +729,7 @@ struct Conv {
   }
 };
 
-// Pair-split implicit-GEMM conv tile (4 waves, every wave over all 8 row tiles): the NCT = 2 * PT
-// channel tiles go to two wave pairs, pair p owning tiles [p PT, p PT + PT) with PT odd; wave q of a
-// pair takes CT = (PT - 1) / 2 full tiles and the pair's middle tile for its own sample slot (row
-// tiles 4q .. 4q + 3).  Every wave issues the same MFMA count, and a weight fragment is loaded by one
-// wave (full tiles) or two (middle tiles) instead of by both wave rows of the WM = 2 tiling the
-// 96- and 224-channel layers use otherwise; the price is 8 instead of 4 B-fragment LDS reads per
-// k-step.  (The fused inference kernel measured this split slower for 96 channels, being bound by
-// LDS there; the batch-BN layer kernels are bound by the vector-memory return path.)
-template <int CIN, int COUT, int K>
-struct ConvHalf {
-  static constexpr int NSTEP = (CIN * K + 31) / 32;
-  static constexpr int NCT = COUT / 16, PT = NCT / 2, CT = (PT - 1) / 2, RT = kRT, HR = kRT / 2;
-  static constexpr int PAD = (K - 1) / 2;
-  static_assert(NCT % 2 == 0 && PT % 2 == 1 && CIN % 32 == 0, "pair split tiling");
 
-  // first full tile / middle tile of wave (p, q)
-  __device__ __forceinline__ static int full0(int wave) { return (wave >> 1) * PT + ((wave & 1) ? CT + 1 : 0); }
-  __device__ __forceinline__ static int mid(int wave) { return (wave >> 1) * PT + CT; }
-
-  template <int Q>
-  __device__ __forceinline__ static void run_q(const gbf16x8* wfrag, const char* lds, int ldsrs, f32x4 (&acc)[CT][RT],
-                                               f32x4 (&acch)[HR]) {
-    const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3;
-    const int m = lane & 15, h = lane >> 4;
-    const gbf16x8* wp = wfrag + full0(wave) * 64 + lane;
-    const gbf16x8* wph = wfrag + mid(wave) * 64 + lane;
-    const char* bbase = lds + (kHalo + m - PAD) * ldsrs + 16 * h;
-#pragma unroll
-    for (int c = 0; c < CT; ++c)
-#pragma unroll
-      for (int r = 0; r < RT; ++r) acc[c][r] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int r = 0; r < HR; ++r) acch[r] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto load_b = [&](int s, int r) -> bf16x8 {
-      constexpr int CB = CIN / 32;
-      const int tap = s / CB, cb = s - tap * CB;
-      const int soff = __builtin_amdgcn_readfirstlane(tap * ldsrs + cb * 64);
-      return *reinterpret_cast<const bf16x8*>(bbase + soff + r * 16 * ldsrs);
-    };
-    bf16x8 a[2][CT], ah[2];
-    auto load_a = [&](int s, int st) {
-#pragma unroll
-      for (int c = 0; c < CT; ++c) a[st][c] = wp[(s * NCT + c) * 64];
-      ah[st] = wph[s * NCT * 64];
-    };
-    auto step = [&](int s, int st) {
-#pragma unroll
-      for (int r = 0; r < RT; ++r) {
-        const bf16x8 b = load_b(s, r);
-#pragma unroll
-        for (int c = 0; c < CT; ++c) acc[c][r] = mfma16(a[st][c], b, acc[c][r]);
-        if ((r >> 2) == Q) acch[r & 3] = mfma16(ah[st], b, acch[r & 3]);  // unrolled: compile-time
-      }
-    };
-    load_a(0, 0);
-    constexpr int NFULL = NSTEP / 2 * 2;
-#pragma unroll 1
-    for (int s0 = 0; s0 < NFULL; s0 += 2) {
-      load_a(s0 + 1, 1);  // s0 + 1 < NFULL <= NSTEP
-      __builtin_amdgcn_sched_barrier(0);
-      step(s0, 0);
-      load_a(s0 + 2 < NSTEP ? s0 + 2 : NSTEP - 1, 0);  // clamped, unconditional
-      __builtin_amdgcn_sched_barrier(0);
-      step(s0 + 1, 1);
-    }
-    if constexpr (NSTEP % 2) step(NSTEP - 1, 0);
-  }
-
-  __device__ __forceinline__ static void run(const gbf16x8* wfrag, const char* lds, int ldsrs, f32x4 (&acc)[CT][RT],
-                                             f32x4 (&acch)[HR]) {
-    if ((threadIdx.x >> 6) & 1)  // wave-uniform
-      run_q<1>(wfrag, lds, ldsrs, acc, acch);
-    else
-      run_q<0>(wfrag, lds, ldsrs, acc, acch);
-  }
-};
-
-template <int SWZ = 0>
 __device__ __forceinline__ bf16x8 tr_frag(const char* lds, int ldsrs, int row_base, int col0) {
   // fragment for a 16x16x32 operand whose K index is the LDS row, 32 rows from row_base.  Lane
   // group h (16 lanes) reads 4 rows x 16 cols per ds_read_b64_tr_b16; k-slot (h, j) of the fragment
@@ -918,8 +741,8 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* lds, int ldsrs, int row_ba
   const int lane = threadIdx.x & 63;
   const int h = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
   const int ra = row_base + 4 * h + q;
-  const char* a0 = lds + lds_off<SWZ>(ra, (col0 + 4 * p) * 2, ldsrs);
-  const char* a1 = lds + lds_off<SWZ>(ra + 16, (col0 + 4 * p) * 2, ldsrs);
+  const char* a0 = lds + lds_off(ra, (col0 + 4 * p) * 2, ldsrs);
+  const char* a1 = lds + lds_off(ra + 16, (col0 + 4 * p) * 2, ldsrs);
   const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)a0);
   const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)a1);
   bf16x8 r;
@@ -933,37 +756,16 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* lds, int ldsrs, int row_ba
   return r;
 }
 
-// Weight-fragment prefetch depth of the forward conv of block l (k-steps in flight).  Measured on a
-// 16-pass x 16384-window batch-BN chunk (tools/probes/so_chunk.sh): depth 1 everywhere 29.8 ms, depth 2
-// 30.0, per-layer (1,3,2,3,2,3) 30.4, depth 4 38.7 (spills) -- the conv is not bound by the L2 round
-// trip of its weight fragments (profiles/batch_bn_fwd_r2.md).  APNEAUQ_FWD_PD overrides (probes).
-template <int l> struct FwdPD { static constexpr int v = 1; };
-#ifndef APNEAUQ_FWD_RING  // B-fragment register ring in the forward conv (probe: 0 = just-in-time reads)
-#define APNEAUQ_FWD_RING 1
-#endif
-#ifdef APNEAUQ_FWD_PD
-#define APNEAUQ_FWD_PDV(l) APNEAUQ_FWD_PD
-#else
-#define APNEAUQ_FWD_PDV(l) (FwdPD<l>::v)
-#endif
+// Weight-fragment prefetch depth of the forward conv (k-steps in flight): depth 1 everywhere 29.8 ms
+// per 16-pass x 16384-window batch-BN chunk, depth 2 30.0, per-layer (1,3,2,3,2,3) 30.4, depth 4 38.7
+// (spills) -- the conv is not bound by the L2 round trip of its weight fragments
+// (profiles/batch_bn_fwd_r2.md).
+constexpr int kFwdPD = 1;
 
 // Forward input staging of block l in two row batches instead of all of a tile's row loads in flight
-// at once (ActStager).  Block 6 (256 staged channels = 17 x 16-B loads per thread) spilled 44 VGPRs
-// into scratch with one batch; split, it spills none and its batch-BN MC-Dropout chunk is ~2 % faster
-// (profiles/batch_bn_fwd_r2.md, session 3).  APNEAUQ_FWD_SPLIT = bit mask over blocks (probes).
-#ifndef APNEAUQ_FWD_SPLIT
-#define APNEAUQ_FWD_SPLIT 36  // blocks 3 and 6 (block 3 spilled 22 VGPRs with the compact staging)
-#endif
-template <int l> struct FwdStageSplit { static constexpr bool v = (APNEAUQ_FWD_SPLIT >> l) & 1; };
-// Forward conv of block l on the pair-split tiling (ConvHalf; 96- and 224-channel outputs, l >= 1).
-// APNEAUQ_FWD_HALF = bit mask over blocks; off: batch-BN MCD phase 90.5-90.8 ms with the WM = 2
-// tilings, 90.6-90.8 with block 3 (224 ch) split, 92.0-92.4 / 93.0 with block 6 / block 4 (96 ch)
-// split (tools/probes/half_check.sh, one box): the extra B-fragment LDS reads cost more than the
-// weight loads they save.  Tested for correctness against the reference (same probe).
-#ifndef APNEAUQ_FWD_HALF
-#define APNEAUQ_FWD_HALF 0
-#endif
-template <int l> struct FwdHalf { static constexpr bool v = l >= 1 && ((APNEAUQ_FWD_HALF >> l) & 1); };
+// at once (ActStager): blocks 3 and 6 spilled 22 / 44 VGPRs with one batch; split, neither spills and
+// the batch-BN MC-Dropout chunk is ~2 % faster (profiles/batch_bn_fwd_r2.md, session 3).
+template <int l> struct FwdStageSplit { static constexpr bool v = l == 2 || l == 5; };
 
 // wave tilings (WM, WN) per output-channel count
 template <int COUT> struct Tiling;
@@ -1016,9 +818,9 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
   double* st = Ly.st + (blockIdx.x % kStatSlots) * st_stride(A, COUT);
   constexpr int CW = COUT / 8;             // 16-B chunks per output row
   constexpr int RPo = kThreads / CW;       // rows per copy-out pass
-  // copy-out rows: the tile's 2 x 60 valid time steps only (APNEAUQ_FWD_SKIPPAD; the R buffers are
-  // allocated filled with -0.0 and their pad rows are never written), else all 128 rows
-  constexpr int kOutRows = APNEAUQ_FWD_SKIPPAD ? kSlots * kL : kR;
+  // copy-out rows: the tile's 2 x 60 valid time steps only (the R buffers are allocated filled with
+  // -0.0 and their pad rows are never written)
+  constexpr int kOutRows = kSlots * kL;
   constexpr int NPo = (kOutRows + RPo - 1) / RPo;
   const int ocw = threadIdx.x % CW, orin = threadIdx.x / CW;
   const bool oact = orin < RPo;
@@ -1052,50 +854,29 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
     __syncthreads();
   };
   // this block's dropout mask goes into the sign bit of R_l (not for the pass-shared block 1)
-  const bool enc = A.dropout != 0 && !(l == 0 && A.shared0) && !(APNEAUQ_FWD_ABL & 64);
+  const bool enc = A.dropout != 0 && !(l == 0 && A.shared0);
   const bool hash_in = l == 1 && A.shared0;  // workgroup-uniform
   int gaff = -1;  // stats group whose BN affine (of block l-1) is in prm
-  // input staging, software-pipelined: tile i+1's rows are loaded into registers while tile i's
-  // moments and copy-out run, and decoded into LDS at the top of the next iteration
+  // input staging: loads of a tile's rows, then A = dropout(BN(R)) decoded into LDS
   ActStager<(l > 0 ? l - 1 : 0), l == 1> stg;
-  if constexpr (APNEAUQ_FWD_DELAY > 0)
-    if (blockIdx.x >= gridDim.x / 2)
-      for (int i = 0; i < APNEAUQ_FWD_DELAY; ++i) __builtin_amdgcn_s_sleep(127);
-  if constexpr (l > 0 && !(APNEAUQ_FWD_ABL & 16) && APNEAUQ_FWD_PIPE)
-    if (t_begin < t_end) stg.load(A, kR * t_begin, hash_in);
-#ifdef APNEAUQ_FWD_STAMPS
-  if (l == APNEAUQ_FWD_STAMPS && blockIdx.x < kFstWG && threadIdx.x == 0) {
-    g_fst_cu[blockIdx.x][0] = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID
-    g_fst_cu[blockIdx.x][1] = __smid();
-  }
-#endif
   for (int tile = t_begin; tile < t_end; ++tile) {
     APNEAUQ_DASSERT(2 * tile < A.B + 1 && blockDim.x == kThreads);
-    const int kst = tile - t_begin;
-    APNEAUQ_FST(0, kst);
     const int row0 = kR * tile;                        // first staged row (global PL index)
     const int smp0 = 2 * tile;
     const int g0 = min(smp0, A.B - 1) / A.n_win, g1 = min(smp0 + 1, A.B - 1) / A.n_win;
     __syncthreads();  // previous tile's copy-out has read the LDS tile
-    if constexpr ((APNEAUQ_FWD_ABL & 16) != 0) {
-    } else if constexpr (l == 0) {
+    if constexpr (l == 0) {
       staged_loop<kRows * 8 / 16>(
           [&](int i) -> bf16x8 { return gld<bf16x8>(A.x + (long long)row0 * 4 + i * 8); },
           [&](int i, const bf16x8& v) { reinterpret_cast<bf16x8*>(act)[i] = v; });
     } else {
-      if ((APNEAUQ_FWD_ABL & 1024) && gaff < 0) {  // probe: constant affine (no slot loads)
-        for (int c = threadIdx.x; c < 1024; c += kThreads) prm[c] = 0.5f;
-        gaff = g0;
-        __syncthreads();
-      } else if (g0 != gaff || g1 != g0) {  // (re)load the affine of block l-1 for this tile's group(s)
+      if (g0 != gaff || g1 != g0) {  // (re)load the affine of block l-1 for this tile's group(s)
         bn_affine_to_lds(A, l - 1, g0, prm, prm + 512, nullptr, nullptr);
         if (g1 != g0) bn_affine_to_lds(A, l - 1, g1, prm + 256, prm + 768, nullptr, nullptr);
         gaff = (g1 == g0) ? g0 : -1;
         __syncthreads();
       }
-      if constexpr (APNEAUQ_FWD_PIPE) {
-        stg.store(A, act, row0, prm, prm + 512, g0, hash_in);
-      } else if constexpr (FwdStageSplit<l>::v) {  // two row batches: fewer loads in flight, no spills
+      if constexpr (FwdStageSplit<l>::v) {  // two row batches: fewer loads in flight, no spills
         constexpr int NK = decltype(stg)::NK, H = (NK + 1) / 2;
         stg.template load<0, H>(A, row0, hash_in);
         stg.template store<0, H>(A, act, row0, prm, prm + 512, g0, hash_in);
@@ -1107,7 +888,6 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
       }
     }
     __syncthreads();
-    APNEAUQ_FST(1, kst);
     // epilogue of one 16 x 16 accumulator tile: bias + ReLU -> bf16 LDS tile (rows outside the batch /
     // pad rows: 0).  Only the row tiles holding t = 48..63 (pad rows on lanes m >= 12) and the batch's
     // last tile need the select.
@@ -1128,45 +908,11 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
       bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
       *reinterpret_cast<bf16x4*>(act + row * kRS + co0 * 2) = o;
     };
-    if constexpr (FwdHalf<l>::v) {  // pair-split tiling (ConvHalf)
-      using CH = ConvHalf<CIN, COUT, KS[l]>;
-      f32x4 acc[CH::CT][CH::RT], acch[CH::HR];
-      if constexpr (APNEAUQ_FWD_PRIO) __builtin_amdgcn_s_setprio(1);
-      CH::run(Ly.wf, act, IN_RS, acc, acch);
-      if constexpr (APNEAUQ_FWD_PRIO) __builtin_amdgcn_s_setprio(0);
-      APNEAUQ_FST(2, kst);
-      __syncthreads();  // all waves done reading the staged input; reuse it for the output tile
-      APNEAUQ_FST(3, kst);
-      const int f0 = CH::full0(wave), q = wave & 1;
-#pragma unroll
-      for (int c = 0; c < CH::CT; ++c) {
-        const int co0 = (f0 + c) * 16 + 4 * h;
-        const f32x4 bias = gld<f32x4>(Ly.bias + co0);
-#pragma unroll
-        for (int r = 0; r < CH::RT; ++r) epi(acc[c][r], co0, r, bias);
-      }
-      const int coh = CH::mid(wave) * 16 + 4 * h;
-      const f32x4 biash = gld<f32x4>(Ly.bias + coh);
-#pragma unroll
-      for (int r = 0; r < CH::HR; ++r) epi(acch[r], coh, q * CH::HR + r, biash);
-    } else {
     f32x4 acc[CV::CT][CV::RT];
-#if (APNEAUQ_FWD_ABL & 8)
-#pragma unroll
-    for (int c = 0; c < CV::CT; ++c)
-#pragma unroll
-      for (int r = 0; r < CV::RT; ++r) acc[c][r] = f32x4{(float)act[threadIdx.x], 0.f, 0.f, (float)r};
-#else
-    if constexpr (APNEAUQ_FWD_PRIO) __builtin_amdgcn_s_setprio(1);
-    CV::template run<APNEAUQ_FWD_PDV(l), APNEAUQ_FWD_RING != 0>(Ly.wf, act, IN_RS, acc);
-    if constexpr (APNEAUQ_FWD_PRIO) __builtin_amdgcn_s_setprio(0);
-#endif
-#ifdef APNEAUQ_FWD_STAMPS
-    if (threadIdx.x == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-#endif
-    APNEAUQ_FST(2, kst);
+    if constexpr (kFwdPrio) __builtin_amdgcn_s_setprio(1);
+    CV::template run<kFwdPD, true>(Ly.wf, act, IN_RS, acc);
+    if constexpr (kFwdPrio) __builtin_amdgcn_s_setprio(0);
     __syncthreads();  // all waves done reading the staged input; reuse it for the output tile
-    APNEAUQ_FST(3, kst);
 #pragma unroll
     for (int c = 0; c < CV::CT; ++c) {
       const int co0 = (wn * CV::CT + c) * 16 + 4 * h;
@@ -1174,12 +920,10 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
 #pragma unroll
       for (int r = 0; r < CV::RT; ++r) epi(acc[c][r], co0, wm * CV::RT + r, bias);
     }
-    }
     __syncthreads();
-    APNEAUQ_FST(4, kst);
     // channel moments of the stored tile (zero rows add nothing) on the matrix cores
     auto moments = [&](int sel) {  // sel: sample slot (rows 64*sel .. +64 = 32-row chunks 2sel, 2sel+1), -1: both
-      if constexpr (!(APNEAUQ_FWD_ABL & 32)) {
+      {
         bf16x8 ones;
 #pragma unroll
         for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.f;
@@ -1219,14 +963,7 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
       for (int k = 0; k < NPo; ++k) {
         const int rc = rin + k * RPo;
         if (!oact || rc >= kOutRows) continue;
-        int slot, tt;
-        if constexpr (APNEAUQ_FWD_SKIPPAD) {
-          slot = rc >= kL;
-          tt = rc - kL * slot;
-        } else {
-          slot = rc >> 6;
-          tt = rc & 63;
-        }
+        const int slot = rc >= kL, tt = rc - kL * slot;
         const int r = slot * kSR + tt;
         bf16x8 o = *reinterpret_cast<const bf16x8*>(act + r * kRS + ocw * 16);
         uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
@@ -1237,12 +974,9 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) ow[q] |= drop_signs2(dropout_bits2(key[slot], tt, ocw * 8 + 2 * q), thr2);
         }
-        if constexpr (!(APNEAUQ_FWD_ABL & 4))
-          *reinterpret_cast<bf16x8*>(Ly.R + (long long)(row0 + kHalo + r) * COUT + ocw * 8) = o;
+        *reinterpret_cast<bf16x8*>(Ly.R + (long long)(row0 + kHalo + r) * COUT + ocw * 8) = o;
       }
     };
-    if constexpr (l > 0 && !(APNEAUQ_FWD_ABL & 16) && APNEAUQ_FWD_PIPE)
-      if (tile + 1 < t_end) stg.load(A, row0 + kR, hash_in);  // next tile's input, in flight from here
     if (g0 == g1) {
       if (g0 != gcur) {
         flush();
@@ -1258,29 +992,11 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
       moments(1);
     }
     copy_out();
-    APNEAUQ_FST(5, kst);
   }
   flush();
   if (A.det != nullptr) {  // deterministic mode (one stats group): this workgroup's moment partials
     float* dp = A.det + (long long)blockIdx.x * 2 * COUT;
     for (int c = threadIdx.x; c < 2 * COUT; c += kThreads) dp[c] = lstat[c];
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// BN affine of block l for every stats group, for the ping-pong forward's staging (one small launch
-// before each layer instead of ~256 workgroups re-summing the fp64 slots).
-// ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void aff_kernel(Args A, int l) {
-  const int g = blockIdx.x;
-  const int Cc = C[l + 1];
-  const Layer& Ly = A.L[l];
-  for (int c = threadIdx.x; c < Cc; c += blockDim.x) {
-    float mu, var;
-    bn_moments(A, l, g, c, mu, var);
-    const float sc = Ly.gamma[c] * rsqrtf(var + A.eps);
-    Ly.aff[(g * 2 + 0) * Cc + c] = sc;
-    Ly.aff[(g * 2 + 1) * Cc + c] = Ly.beta[c] - mu * sc;
   }
 }
 
@@ -1293,296 +1009,6 @@ __global__ __launch_bounds__(256) void tab_kernel(Args A, int mode, int l) {
     tab_write_fwd(A, blockIdx.x);
   else
     tab_write_bwd(A, l);
-}
-
-// ------------------------------------------------------------------------------------------------
-// Ping-pong forward of block l >= 1 for large batches (batch-BN MC Dropout runs T x N samples through
-// every layer).  One 512-thread workgroup per CU = two 4-wave teams, each with its own LDS tile
-// buffer and its own 2-sample tiles (team h takes tiles t_begin + 2i + h).  A team's tile goes
-// through four phases -- S: stage A_{l-1} = dropout(BN(R_{l-1})) into LDS; C1, C2: the two halves of
-// the implicit-GEMM MFMA steps; E: bias + ReLU epilogue into LDS, channel moments on the matrix
-// cores, coalesced copy-out of R_l with the dropout mask in the sign bits -- and the teams run two
-// phases apart, separated by workgroup barriers:
-//     segment   4i    4i+1   4i+2   4i+3
-//     team 0    S      C1     C2     E
-//     team 1    C2     E      S      C1
-// (each team runs its own copy of the loop; s_barrier counts arrivals, not code locations)
-// so on every SIMD (one wave of each team) a conv half always runs beside the other team's memory /
-// VALU phase.  With the single-team kernel both co-resident workgroups spent their staging and
-// copy-out with idle matrix cores.  E is wave-local (each wave stores, reduces and copies out only
-// its own accumulator block), so no barrier is needed inside a phase.  Moment partials stay per
-// lane (fp32) until the stats group changes and then go to the fp64 slots with global atomics.
-// ------------------------------------------------------------------------------------------------
-template <int l> struct PP {
-  static constexpr int CIN = C[l], COUT = C[l + 1];
-  static constexpr int IN_RS = CIN * 2 + 32, OUT_RS = COUT * 2 + 32;  // odd multiples of 32 B
-  static constexpr int BUF = (kRows * IN_RS > kR * OUT_RS) ? kRows * IN_RS : kR * OUT_RS;
-  static constexpr int LDS = 2 * BUF;
-  static_assert(LDS <= 160 * 1024, "ping-pong tiles exceed the LDS");
-};
-
-template <int l>
-__global__ __launch_bounds__(512, 1) void fwd_pp_kernel(Args A) {
-  static_assert(l >= 1, "block 1 reads the input: fwd_kernel<0>");
-  using P = PP<l>;
-  constexpr int CIN = P::CIN, COUT = P::COUT, lr = l - 1;
-  using T = Tiling<COUT>;
-  using CV = Conv<CIN, COUT, KS[l], T::WM, T::WN, false>;
-  constexpr int NS1 = (CV::NSTEP / 2) & ~1;
-  constexpr int CRin = C[l];  // channels of R_{l-1}
-  constexpr int NCW = CRin / 8, RP = kThreads / NCW, NK = (kRows + RP - 1) / RP;
-  const int team = threadIdx.x >> 8;  // wave-uniform
-  const int ht = threadIdx.x & 255;
-  const int lane = threadIdx.x & 63, hw = (threadIdx.x >> 6) & 3;
-  const int wm = hw / T::WN, wn = hw % T::WN;
-  const int m = lane & 15, h = lane >> 4;
-  char* buf = smem + team * P::BUF;
-  const Layer& Ly = A.L[l];
-  const Layer& Lr = A.L[lr];
-  const int tiles = (A.B + 1) / 2;
-  const int tpw = (tiles + gridDim.x - 1) / gridDim.x;
-  const int t_begin = blockIdx.x * tpw;
-  const int n_t = max(0, min(tiles, t_begin + tpw) - t_begin);
-  const int n_team = (n_t + 1 - team) / 2;
-  const int nseg = 4 * ((n_t + 1) / 2) + 2;
-  const bool hash_in = l == 1 && A.shared0;  // block 2 reads the pass-shared block-1 output
-  const bool drop = A.dropout != 0;
-  const bool enc = drop;  // blocks >= 2 always encode their dropout mask
-  const uint32_t thr_in = (hash_in && drop) ? Lr.thr * 0x10001u : 0u;
-  const uint32_t thr_out = Ly.thr * 0x10001u;
-  const float dsc_in = drop ? Lr.dsc : 1.f;
-  // moments: per-lane partials of this wave's channel tiles (diag lanes hold D[sn][sn])
-  const int sn = lane & 15, si = sn & 3;
-  const bool diag_lane = (lane >> 4) == (sn >> 2);
-  float ps1[CV::CT], ps2[CV::CT];
-#pragma unroll
-  for (int j = 0; j < CV::CT; ++j) ps1[j] = ps2[j] = 0.f;
-  int gcur = -1;
-  double* st = Ly.st + ((blockIdx.x * 2 + team) % kStatSlots) * st_stride(A, COUT);
-  auto flush = [&]() __attribute__((always_inline)) {  // wave-local: fp32 lane partials into the fp64 slots
-    if (gcur >= 0 && diag_lane) {
-#pragma unroll
-      for (int j = 0; j < CV::CT; ++j) {
-        const int c = (wn * CV::CT + j) * 16 + sn;
-        atomicAdd(st + (gcur * 2 + 0) * COUT + c, (double)ps1[j]);
-        atomicAdd(st + (gcur * 2 + 1) * COUT + c, (double)ps2[j]);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < CV::CT; ++j) ps1[j] = ps2[j] = 0.f;
-  };
-  // ---- S: stage A_{l-1} rows [row0, row0 + 136) into buf (all CIN channels), PPU rows per thread
-  // in flight (the phase runs beside the other team's conv half, which covers the second round trip)
-  constexpr int PPB = 1, PPU = NK;  // every row of the tile in flight: one round trip
-  auto stage = [&](int tile) __attribute__((always_inline)) {
-    const int row0 = kR * tile, smp0 = 2 * tile;
-    int t_ = ht;
-    asm volatile("" : "+v"(t_));  // opaque: keeps per-row addresses out of the segment loop
-    const int cw = t_ % NCW, rin = t_ / NCW;
-    if (rin >= RP) return;
-    const int c = cw * 8;
-    const int n0 = min(smp0, A.B - 1), n1 = min(smp0 + 1, A.B - 1);
-    const int g0 = n0 / A.n_win, g1 = n1 / A.n_win;
-    const __bf16* src0 = Lr.R + c;
-    const __bf16* src1 = src0;
-    if (hash_in) {  // R_0: one unencoded copy per window
-      src0 += (long long)(kHalo + (n0 - g0 * A.n_win) * kSR) * CRin;
-      src1 += (long long)(kHalo + (n1 - g1 * A.n_win) * kSR) * CRin;
-    }
-    // BN affine of the tile's stats group(s) (x 1/(1-rate)), from aff_kernel; the second group's
-    // only in the rare tile that straddles an MC-Dropout pass boundary
-    auto affine = [&](int g, float (&sv)[8], float (&tv)[8]) {
-      const float* a = Lr.aff + (long long)(stat_group(A, lr, g) * 2) * CRin + c;
-#pragma unroll
-      for (int j = 0; j < 8; j += 4) {
-        const f32x4 sa = gld<f32x4>(a + j), ta = gld<f32x4>(a + CRin + j);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          sv[j + q] = sa[q] * dsc_in;
-          tv[j + q] = ta[q] * dsc_in;
-        }
-      }
-    };
-    float s0[8], t0[8];
-    affine(g0, s0, t0);
-    const unsigned key0 = hash_in ? layer_sample_key(A, lr, n0) : 0u;
-    const unsigned key1 = hash_in ? layer_sample_key(A, lr, n1) : 0u;
-    auto run = [&](auto two_groups, auto hashed) {
-      constexpr bool HSH = decltype(hashed)::value;
-      float s1[8], t1[8];
-      if constexpr (decltype(two_groups)::value) affine(g1, s1, t1);
-#pragma unroll
-      for (int b = 0; b < NK; b += PPU) {
-        u32x4 v[PPU];
-#pragma unroll
-        for (int u = 0; u < PPU; ++u) {
-          if (b + u >= NK) continue;
-          const int grow = row0 + min(rin + (b + u) * RP, kRows - 1);
-          if constexpr (HSH) {  // non-own rows (neighbours' halo rows) -> pad row 60 (-0.0)
-            const int n = row_sample(grow);
-            const bool own = grow >= kHalo && (n == smp0 || n == smp0 + 1);
-            v[u] = gld<u32x4>((n == smp0 + 1 ? src1 : src0) + (long long)(own ? row_time(grow) : kL) * CRin);
-          } else {
-            v[u] = gld<u32x4>(src0 + (long long)grow * CRin);
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < PPU; ++u) {
-          const int r = rin + (b + u) * RP;
-          if (b + u >= NK || r >= kRows) continue;
-          const int grow = row0 + r;
-          const bool hi = row_sample(grow) == smp0 + 1;
-          u32x4 o;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            uint32_t d = v[u][q];
-            if constexpr (HSH) d |= drop_signs2(dropout_bits2(hi ? key1 : key0, row_time(grow), c + 2 * q), thr_in);
-            if constexpr (decltype(two_groups)::value)
-              o[q] = decode_pair(d, hi ? s1[2 * q] : s0[2 * q], hi ? t1[2 * q] : t0[2 * q],
-                                 hi ? s1[2 * q + 1] : s0[2 * q + 1], hi ? t1[2 * q + 1] : t0[2 * q + 1]);
-            else
-              o[q] = decode_pair(d, s0[2 * q], t0[2 * q], s0[2 * q + 1], t0[2 * q + 1]);
-          }
-          *reinterpret_cast<u32x4*>(buf + r * P::IN_RS + cw * 16) = o;
-        }
-      }
-    };
-    auto dispatch = [&](auto hashed) {
-      if (g1 != g0)
-        run(std::true_type{}, hashed);
-      else
-        run(std::false_type{}, hashed);
-    };
-    if (l == 1 && hash_in)
-      dispatch(std::integral_constant<bool, l == 1>{});
-    else
-      dispatch(std::false_type{});
-  };
-
-  // ---- E: epilogue, moments and copy-out of this wave's accumulator block (wave-local)
-  auto finish = [&](int tile, const f32x4 (&acc)[CV::CT][CV::RT]) __attribute__((always_inline)) {
-    // opaque lane index: every lane-derived LDS / global address of this phase is recomputed here
-    // instead of being hoisted out of the segment loop (and held across the other phases)
-    int lane_ = lane;
-    asm volatile("" : "+v"(lane_));
-    const int m = lane_ & 15, h = lane_ >> 4;
-    const int row0 = kR * tile, smp0 = 2 * tile;
-    const bool last_tile = smp0 + 1 >= A.B;
-#pragma unroll
-    for (int c = 0; c < CV::CT; ++c) {
-      const int co0 = (wn * CV::CT + c) * 16 + 4 * h;
-      const f32x4 bias = gld<f32x4>(Ly.bias + co0);
-#pragma unroll
-      for (int r = 0; r < CV::RT; ++r) {
-        const int rtg = wm * CV::RT + r;
-        const int row = rtg * 16 + m;
-        f32x4 v;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = fmaxf(acc[c][r][i] + bias[i], 0.f);
-        if ((rtg & 3) == 3 || last_tile) {
-          const bool valid = (row & 63) < kL && (smp0 + (row >> 6)) < A.B;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            v[i] = valid ? v[i] : 0.f;
-            asm volatile("" : "+v"(v[i]));
-          }
-        }
-        bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
-        *reinterpret_cast<bf16x4*>(buf + row * P::OUT_RS + co0 * 2) = o;
-      }
-    }
-    // the wave reads back what its other lanes wrote: LDS is in order within a wave, keep the
-    // compiler from hoisting the reads above the stores
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // channel moments over the wave's rows, per stats group (slot 0 / slot 1 rows of a tile that
-    // straddles an MC-Dropout pass boundary)
-    const int g0 = min(smp0, A.B - 1) / A.n_win, g1 = min(smp0 + 1, A.B - 1) / A.n_win;
-    bf16x8 ones;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.f;
-    constexpr int KC = CV::RT / 2;  // 32-row chunks of the wave's rows
-#pragma unroll
-    for (int kq = 0; kq < KC; ++kq) {
-      const int kc = wm * KC + kq;
-      const int g = (kc >> 1) ? g1 : g0;  // rows 64.. belong to the tile's second sample
-      if (g != gcur) {  // wave-uniform
-        flush();
-        gcur = g;
-      }
-#pragma unroll
-      for (int j = 0; j < CV::CT; ++j) {
-        const int ct = wn * CV::CT + j;
-        const bf16x8 f = tr_frag(buf, P::OUT_RS, kc * 32, ct * 16);
-        f32x4 gg = mfma16(f, f, f32x4{0.f, 0.f, 0.f, 0.f});
-        f32x4 sm = mfma16(ones, f, f32x4{0.f, 0.f, 0.f, 0.f});
-        const int si_ = lane_ & 3;
-        ps2[j] += si_ == 0 ? gg[0] : si_ == 1 ? gg[1] : si_ == 2 ? gg[2] : gg[3];
-        ps1[j] += si_ == 0 ? sm[0] : si_ == 1 ? sm[1] : si_ == 2 ? sm[2] : sm[3];
-      }
-    }
-    // copy-out of the wave's block: RT*16 rows x CT*16 channels, 16 B per item
-    unsigned key[kSlots] = {0u, 0u};
-    if (enc) {
-      key[0] = layer_sample_key(A, l, min(smp0, A.B - 1));
-      key[1] = layer_sample_key(A, l, min(smp0 + 1, A.B - 1));
-    }
-    constexpr int CPR = CV::CT * 2, NIT = CV::RT * 16 * CPR / 64;
-    static_assert(CV::RT * 16 * CPR % 64 == 0, "copy-out items per wave");
-    int li = lane_;
-    asm volatile("" : "+v"(li));
-#pragma unroll 2
-    for (int k = 0; k < NIT; ++k) {
-      const int i = li + 64 * k;
-      const int r = wm * CV::RT * 16 + i / CPR;
-      const int ch = (wn * CV::CT * 16) / 8 + i % CPR;
-      const int slot = r >> 6, tt = r & 63;
-      bf16x8 o = *reinterpret_cast<const bf16x8*>(buf + r * P::OUT_RS + ch * 16);
-      uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
-      if (!(tt < kL && smp0 + slot < A.B)) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) ow[q] = kNegZero2;
-      } else if (enc) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) ow[q] |= drop_signs2(dropout_bits2(key[slot], tt, ch * 8 + 2 * q), thr_out);
-      }
-      *reinterpret_cast<bf16x8*>(Ly.R + (long long)(row0 + kHalo + r) * COUT + ch * 8) = o;
-    }
-  };
-
-  // Each team runs its own copy of the loop (team 1 two barriers later), so a team's accumulators
-  // are dead during its staging phase and the staging keeps every row load in flight.  Both copies
-  // execute the same number of workgroup barriers (nseg).
-  auto team_loop = [&](auto team_c) {
-    constexpr int tm = decltype(team_c)::value;
-    int seg = 0;
-    for (; seg < 2 * tm; ++seg) __syncthreads();
-#pragma unroll 1
-    for (int i = 0; i < n_team; ++i, seg += 4) {
-      const int tile = t_begin + 2 * i + tm;
-      if constexpr (!(APNEAUQ_FWD_ABL & 16)) stage(tile);
-      __syncthreads();
-      f32x4 acc[CV::CT][CV::RT];
-#pragma unroll
-      for (int c = 0; c < CV::CT; ++c)
-#pragma unroll
-        for (int r = 0; r < CV::RT; ++r)
-          acc[c][r] = f32x4{0.f, 0.f, (APNEAUQ_FWD_ABL & 8) ? (float)buf[ht] : 0.f, 0.f};  // probe: opaque
-      if constexpr (!(APNEAUQ_FWD_ABL & 8)) CV::template steps<0, NS1>(Ly.wf, buf, P::IN_RS, acc);
-      __syncthreads();
-      if constexpr (!(APNEAUQ_FWD_ABL & 8)) CV::template steps<NS1, CV::NSTEP>(Ly.wf, buf, P::IN_RS, acc);
-      __syncthreads();
-      if constexpr (!(APNEAUQ_FWD_ABL & 32)) finish(tile, acc);
-      __syncthreads();
-    }
-#pragma unroll 1
-    for (; seg < nseg; ++seg) __syncthreads();
-  };
-  if (team == 0)
-    team_loop(std::integral_constant<int, 0>{});
-  else
-    team_loop(std::integral_constant<int, 1>{});
-  flush();
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1740,9 +1166,6 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A, int backward) {
     }
     if (A.det != nullptr) return;  // det_reduce_kernel sums the per-sample records
     __syncthreads();
-#ifdef APNEAUQ_HEAD_NOATOMIC  // probe: no per-workgroup global atomics (wrong gradients, timing only)
-    return;
-#endif
     float* hp = A.hpart != nullptr ? A.hpart + (blockIdx.x % kStatSlots) * (Cc + 2) : nullptr;
     for (int c = threadIdx.x; c < Cc; c += kThreads) {
       if (hp != nullptr) {  // slotted: summed by bn_finalize_kernel
@@ -1769,11 +1192,8 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A, int backward) {
 // dgrad of block l (l >= 1): dA_{l-1} = conv^T(dZ_l, W_l);  epilogue -> dY_{l-1} = dA * mask_{l-1}
 // plus the backward sums of block l-1.
 // ------------------------------------------------------------------------------------------------
-// dgrad: prefetch the epilogue's R_{l-1} loads ahead of the conv (APNEAUQ_DG_PRE = bit mask over l)
-#ifndef APNEAUQ_DG_PRE
-#define APNEAUQ_DG_PRE 30
-#endif
-template <int l> struct DgPre { static constexpr bool v = (APNEAUQ_DG_PRE >> l) & 1; };
+// dgrad: prefetch the epilogue's R_{l-1} loads ahead of the conv on blocks 2-5 (block 6: registers)
+template <int l> struct DgPre { static constexpr bool v = l >= 1 && l <= 4; };
 
 template <int l>
 __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
@@ -1795,9 +1215,7 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
   APNEAUQ_DASSERT(2 * tile < A.B + 1 && blockDim.x == kThreads);
   const int row0 = kR * tile;
   const int smp0 = 2 * tile;
-  if constexpr ((APNEAUQ_DG_ABL & 32) != 0) {  // probe: constant parameters (no prologue loads)
-    for (int c = threadIdx.x; c < 256; c += kThreads) gr[c] = mean[c] = rstd[c] = mdy[c] = mdyx[c] = mean_prev[c] = rstd_prev[c] = 0.5f;
-  } else if (A.tab != nullptr) {  // single-device training: T[l] (block 6: backward sums), T[l-1]
+  if (A.tab != nullptr) {  // single-device training: T[l] (block 6: backward sums), T[l-1]
     const int c = threadIdx.x;
     if (c < CIN) {
       gr[c] = tab_row(A, l, kTabS)[c];
@@ -1847,7 +1265,7 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
   const Layer& Lp = A.L[l - 1];
   // R_{l-1} at this lane's epilogue elements (|R| for xhat, sign = block l-1's dropout mask), loaded
   // before the conv so the MFMAs cover their latency (DgPre: where the registers allow)
-  constexpr bool PRE = DgPre<l>::v && !(APNEAUQ_DG_ABL & 1);
+  constexpr bool PRE = DgPre<l>::v;
   bf16x4 rpre[PRE ? CV::CT : 1][PRE ? CV::RT : 1];
   if constexpr (PRE) {
 #pragma unroll
@@ -1862,14 +1280,7 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
       }
   }
   f32x4 acc[CV::CT][CV::RT];
-#if (APNEAUQ_DG_ABL & 8)
-#pragma unroll
-  for (int c = 0; c < CV::CT; ++c)
-#pragma unroll
-    for (int r = 0; r < CV::RT; ++r) acc[c][r] = f32x4{(float)act[threadIdx.x], 0.f, 0.f, (float)r};
-#else
   CV::template run<1, false>(A.L[l].wd, act, kRS, acc);
-#endif
   __syncthreads();
   const float dscp = A.dropout ? Lp.dsc : 1.f;
 #pragma unroll
@@ -1882,15 +1293,11 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
       const int slot = row >> 6, tt = row & 63;
       const bool valid = tt < kL && (smp0 + slot) < A.B;
       // R_{l-1}: |R| for xhat, its sign bit = the dropout mask of block l-1
-#if (APNEAUQ_DG_ABL & 1)
-      bf16x4 rr = {(__bf16)acc[c][r][0], (__bf16)acc[c][r][1], (__bf16)acc[c][r][2], (__bf16)acc[c][r][3]};
-#else
       bf16x4 rr = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
       if constexpr (PRE)
         rr = rpre[c][r];
       else if (valid)
         rr = gld<bf16x4>(Lp.R + (long long)(row0 + kHalo + row) * COUT + co0);
-#endif
       f32x4 v = acc[c][r];
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = (!valid || bf_dropped(rr[i])) ? 0.f : v[i] * dscp;
@@ -1924,7 +1331,7 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
   }
   __syncthreads();
   constexpr int CW = COUT / 8;
-  for (int i = threadIdx.x; i < ((APNEAUQ_DG_ABL & 4) ? 0 : kR * CW); i += kThreads) {
+  for (int i = threadIdx.x; i < kR * CW; i += kThreads) {
     const int r = i / CW, cw = i - r * CW;
     *reinterpret_cast<bf16x8*>(Lp.dY + (long long)(row0 + kHalo + r) * COUT + cw * 8) =
         *reinterpret_cast<const bf16x8*>(act + r * kRS + cw * 16);
@@ -1946,36 +1353,14 @@ template <int l> struct WgCfg;
 // workgroups per CU save 17 % on block 4 and spill on block 6)
 // wgrad LDS tiles: the row stride is an odd multiple of 32 B (conflict-free tr_frag reads)
 __host__ __device__ constexpr int wg_rs(int width_bytes) { return (width_bytes / 32) % 2 ? width_bytes : width_bytes + 32; }
-// minimum wgrad workgroup counts of blocks 2-5 (probe overrides; batch-1024 step measured with
-// tools/probes/train_variants.sh: block 5 512 -> 768 took the step 0.795 -> 0.786 ms, block 2
-// 256 -> 512 0.766-0.775 -> 0.758-0.768 ms over three interleaved rounds)
-#ifndef APNEAUQ_WG_CMP  // wgrad stages only the tiles' valid rows (pad rows zeroed once per workgroup)
-#define APNEAUQ_WG_CMP 0  // measured slower at batch 1024: 0.778-0.785 vs 0.769-0.771 ms (session 3)
-#endif
-#ifndef APNEAUQ_WG0_MINWG
-#define APNEAUQ_WG0_MINWG 512
-#endif
-#ifndef APNEAUQ_WG5_MINWG
-#define APNEAUQ_WG5_MINWG 512
-#endif
-#ifndef APNEAUQ_WG1_MINWG
-#define APNEAUQ_WG1_MINWG 512
-#endif
-#ifndef APNEAUQ_WG2_MINWG
-#define APNEAUQ_WG2_MINWG 256
-#endif
-#ifndef APNEAUQ_WG3_MINWG
-#define APNEAUQ_WG3_MINWG 512
-#endif
-#ifndef APNEAUQ_WG4_MINWG
-#define APNEAUQ_WG4_MINWG 768
-#endif
-template <> struct WgCfg<0> { static constexpr int CIB = 32, COB = 128, WCO = 4, WCI = 1, RTILES = 2, MINWG = APNEAUQ_WG0_MINWG, U = 4, MINB = 2; };  // im2col kk=32
-template <> struct WgCfg<1> { static constexpr int CIB = 32, COB = 192, WCO = 2, WCI = 2, RTILES = 8, MINWG = APNEAUQ_WG1_MINWG, U = 8, MINB = 2; };
-template <> struct WgCfg<2> { static constexpr int CIB = 32, COB = 224, WCO = 2, WCI = 2, RTILES = 8, MINWG = APNEAUQ_WG2_MINWG, U = 8, MINB = 2; };
-template <> struct WgCfg<3> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = APNEAUQ_WG3_MINWG, U = 8, MINB = 3; };
-template <> struct WgCfg<4> { static constexpr int CIB = 16, COB = 128, WCO = 4, WCI = 1, RTILES = 16, MINWG = APNEAUQ_WG4_MINWG, U = 8, MINB = 3; };
-template <> struct WgCfg<5> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = APNEAUQ_WG5_MINWG, U = 4, MINB = 2; };
+// MINWG values: batch-1024 step measured with tools/probes/train_variants.sh (block 5 512 -> 768 took
+// the step 0.795 -> 0.786 ms, block 2 256 -> 512 0.766-0.775 -> 0.758-0.768 ms, three interleaved rounds)
+template <> struct WgCfg<0> { static constexpr int CIB = 32, COB = 128, WCO = 4, WCI = 1, RTILES = 2, MINWG = 512, U = 4, MINB = 2; };  // im2col kk=32
+template <> struct WgCfg<1> { static constexpr int CIB = 32, COB = 192, WCO = 2, WCI = 2, RTILES = 8, MINWG = 512, U = 8, MINB = 2; };
+template <> struct WgCfg<2> { static constexpr int CIB = 32, COB = 224, WCO = 2, WCI = 2, RTILES = 8, MINWG = 256, U = 8, MINB = 2; };
+template <> struct WgCfg<3> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = 512, U = 8, MINB = 3; };
+template <> struct WgCfg<4> { static constexpr int CIB = 16, COB = 128, WCO = 4, WCI = 1, RTILES = 16, MINWG = 768, U = 8, MINB = 3; };
+template <> struct WgCfg<5> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = 512, U = 4, MINB = 2; };
 
 
 template <int l>
@@ -1983,7 +1368,6 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A)
   using W = WgCfg<l>;
   constexpr int CIN = C[l], COUT = C[l + 1], K = KS[l], PAD = (K - 1) / 2;
   constexpr bool FIRST = (l == 0);
-  constexpr bool WG_CMP = !FIRST && APNEAUQ_WG_CMP;  // compact dZ / A staging (valid rows only)
   constexpr int NTAP = FIRST ? 1 : K;           // block 1: taps folded into the im2col columns
   constexpr int NCO = W::COB / 16 / W::WCO;     // co tiles per wave
   constexpr int NCI = W::CIB / 16 / W::WCI;     // ci tiles per wave
@@ -2012,11 +1396,7 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A)
   const int blk = wg % (nci_blk * nco_blk);
   const int rg = wg / (nci_blk * nco_blk);
   const int ci0 = (blk % nci_blk) * W::CIB, co0 = (blk / nci_blk) * W::COB;
-#ifdef APNEAUQ_WG_NOBIAS  // probe: skip the bias-gradient column sums (wrong db, timing only)
-  const bool do_bias = false;
-#else
   const bool do_bias = (ci0 == 0);
-#endif
   if (A.tab != nullptr) {  // single-device training: T[l] (block 6: backward sums), T[l-1]
     const int c = threadIdx.x;
     if (c < COUT) {
@@ -2088,31 +1468,15 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A)
   // sizes the grid for >= ~512 workgroups)
   const int rgs = gridDim.x / (nci_blk * nco_blk);
   const int rt = (ntiles + rgs - 1) / rgs;
-  // compact staging (blocks 2-6): the tiles' halo / pad rows are never staged and read as zeros, so
-  // they are zeroed once here (dZ rows 60-63 / 124-127, A rows 0-3 / 64-67 / 128-135)
-  if constexpr (WG_CMP) {
-    constexpr int DW = W::COB / 8, AW = W::CIB / 8;
-    for (int i = threadIdx.x; i < 8 * DW; i += kThreads) {
-      const int pi = i / DW, pr = pi < 4 ? kL + pi : kSR + kL + (pi - 4);
-      *reinterpret_cast<u32x4*>(dz_lds + lds_off<0>(pr, (i - pi * DW) * 16, DZRS)) = u32x4{0u, 0u, 0u, 0u};
-    }
-    for (int i = threadIdx.x; i < 16 * AW; i += kThreads) {
-      const int pi = i / AW, pr = pi < 4 ? pi : (pi < 8 ? kL + pi : 2 * kL + pi);
-      *reinterpret_cast<u32x4*>(a_lds + lds_off<0>(pr, (i - pi * AW) * 16, ARS)) = u32x4{0u, 0u, 0u, 0u};
-    }
-  }
   for (int it = 0; it < rt; ++it) {
     const int tile = rg * rt + it;
     if (tile >= ntiles) break;
     const int row0 = kR * tile;
     __syncthreads();
     if constexpr (FIRST)  // no dgrad for block 1: dZ_1 is recomputed here (a single ci block)
-      stage_dz<l, kR, W::COB / 8, 0>(A, dz_lds, DZRS, row0 + kHalo, co0, gr, mean, rstd, mdy, mdyx);
-    else {
-#ifndef APNEAUQ_WG_NODZ  // probe: no dZ staging (wrong dW, timing only)
-      stage_dz_copy<l, kR, W::COB / 8, W::U, 0, WG_CMP>(A, dz_lds, DZRS, row0 + kHalo, co0);
-#endif
-    }
+      stage_dz<l, kR, W::COB / 8>(A, dz_lds, DZRS, row0 + kHalo, co0, gr, mean, rstd, mdy, mdyx);
+    else
+      stage_dz_copy<l, kR, W::COB / 8, W::U>(A, dz_lds, DZRS, row0 + kHalo, co0);
     if constexpr (FIRST) {
       // im2col of the raw input: col kk = tap*4 + ci (kk < 28), rows = tile rows
       for (int i = threadIdx.x; i < kR * 32; i += kThreads) {
@@ -2120,19 +1484,17 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A)
         const int tap = kk >> 2, ci = kk & 3;
         __bf16 v = (__bf16)0.f;
         if (tap < K) v = A.x[(long long)(row0 + kHalo + r + tap - PAD) * 4 + ci];
-        *reinterpret_cast<__bf16*>(a_lds + lds_off<0>(r, kk * 2, ARS)) = v;
+        *reinterpret_cast<__bf16*>(a_lds + lds_off(r, kk * 2, ARS)) = v;
       }
     } else {
-#ifndef APNEAUQ_WG_NOA  // probe: no A_{l-1} staging (wrong dW, timing only)
-      stage_act<l - 1, kRows, W::CIB / 8, 4, 0, WG_CMP>(A, a_lds, ARS, row0, ci0, sp, tp, 0);
-#endif
+      stage_act<l - 1, kRows, W::CIB / 8, 4>(A, a_lds, ARS, row0, ci0, sp, tp, 0);
     }
     __syncthreads();
 #pragma unroll
     for (int ks = 0; ks < kR / 32; ++ks) {
       bf16x8 fb[NCO];
 #pragma unroll
-      for (int a = 0; a < NCO; ++a) fb[a] = tr_frag<0>(dz_lds, DZRS, ks * 32, (wco * NCO + a) * 16);
+      for (int a = 0; a < NCO; ++a) fb[a] = tr_frag(dz_lds, DZRS, ks * 32, (wco * NCO + a) * 16);
       if (bias_wave) {  // db[co] = sum_rows dZ[row][co]: one MFMA with an all-ones A fragment
 #pragma unroll
         for (int a = 0; a < NCO; ++a) accb[a] = mfma16(ones, fb[a], accb[a]);
@@ -2142,13 +1504,9 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A)
 #pragma unroll
         for (int b = 0; b < NCI; ++b) {
           const int arow = FIRST ? ks * 32 : kHalo + ks * 32 + k - PAD;
-          const bf16x8 fa = tr_frag<0>(a_lds, ARS, arow, (wci * NCI + b) * 16);
-#ifndef APNEAUQ_WG_NOMFMA  // probe: staging only (wrong dW, timing only)
+          const bf16x8 fa = tr_frag(a_lds, ARS, arow, (wci * NCI + b) * 16);
 #pragma unroll
           for (int a = 0; a < NCO; ++a) acc[k][b][a] = mfma16(fa, fb[a], acc[k][b][a]);
-#else
-          if (fa[0] == (__bf16)123.f) acc[k][b][0][0] += 1.f;
-#endif
         }
       }
     }
@@ -2360,9 +1718,7 @@ __global__ void pack_kernel(const float* __restrict__ w, int k, int cin, int cou
 // ------------------------------------------------------------------------------------------------ host
 using train::Args;
 
-constexpr int lds_fwd() {  // tile + affine + lstat (probe 512: twice that, one workgroup per CU)
-  return (train::kRows * train::kRS + (1024 + 2 * 256) * 4) * ((APNEAUQ_FWD_ABL & 512) ? 2 : 1);
-}
+constexpr int lds_fwd() { return train::kRows * train::kRS + (1024 + 2 * 256) * 4; }  // tile + affine + lstat
 constexpr int lds_dgrad() { return train::kRows * train::kRS + 1792 * 4; }
 static_assert(2 * lds_dgrad() <= 160 * 1024, "dgrad must fit two workgroups per CU");
 template <int l>
@@ -2375,20 +1731,6 @@ static_assert(2 * lds_wgrad<1>() <= 160 * 1024 && 2 * lds_wgrad<2>() <= 160 * 10
 
 int train_args_size() { return (int)sizeof(Args); }
 
-// probe builds (-DAPNEAUQ_FWD_STAMPS): copy the forward phase stamps out; -1 in the library build
-int train_read_stamps(void* dst, long long bytes) {
-#ifdef APNEAUQ_FWD_STAMPS
-  const size_t n1 = sizeof(unsigned) * train::kFstWG * 2, n2 = sizeof(unsigned long long) * train::kFstWG * train::kFstT * train::kFstN;
-  if (bytes < (long long)(n1 + n2)) return -2;
-  if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(train::g_fst_cu), n1) != hipSuccess) return -3;
-  if (hipMemcpyFromSymbol((char*)dst + n1, HIP_SYMBOL(train::g_fst), n2) != hipSuccess) return -3;
-  return 0;
-#else
-  (void)dst;
-  (void)bytes;
-  return -1;
-#endif
-}
 int train_layer_size() { return (int)sizeof(train::Layer); }
 
 __global__ void bump_counters_kernel(int* c, int n) {
@@ -2409,20 +1751,6 @@ static int cu_count() {
       n = 256;
   }
   return n;
-}
-
-// APNEAUQ_FWD_PP=1: batches of at least kPPMinTilesPerCU 2-sample tiles per CU take the ping-pong
-// forward.  Opt-in: it measured 8 % SLOWER than the single-team kernel (profiles/batch_bn_fwd_r2.md:
-// the texture/L1 return path, loaded mostly by the per-tile weight fragments, is the limiter, and
-// overlapping staging with MFMA does not relieve it).  Kept, tested against the default path.
-constexpr int kPPMinTilesPerCU = 8;
-static bool pp_enabled() {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("APNEAUQ_FWD_PP");
-    on = (e != nullptr && e[0] == '1') ? 1 : 0;
-  }
-  return on == 1;
 }
 
 static hipError_t det_reduce(const float* part, int n, int w, train::DetDst d, hipStream_t st) {
@@ -2446,10 +1774,8 @@ static train::DetDst det_dst(void* p0, int c0, int f0, void* p1 = nullptr, int c
 // 91.9 / 91.1-91.4 / 91.0-91.4 / 90.5-90.9 ms (tools/probes/so_bench1.sh, one box), and 64 / 128 / 256
 // on another: 90.8-90.9 / 91.2-91.8 / 91.9-92.1 ms: shorter ranges
 // balance the launch tail.  Batches of <= 16384 tiles (training) get one tile per workgroup anyway.
-#ifndef APNEAUQ_FWD_WG_PER_CU
-#define APNEAUQ_FWD_WG_PER_CU 64
-#endif
-static int fwd_grid(int B) { return std::min((B + 1) / 2, 256 * APNEAUQ_FWD_WG_PER_CU); }
+constexpr int kFwdWgPerCu = 64;
+static int fwd_grid(int B) { return std::min((B + 1) / 2, 256 * kFwdWgPerCu); }
 int train_det_floats(int B) {
   const int tiles = (B + 1) / 2;
   return std::max({fwd_grid(B) * 2 * 256, B * train::kHeadRec, tiles * 2 * 2 * 256});
@@ -2474,19 +1800,6 @@ hipError_t train_launch_fwd(const Args& A, int l, hipStream_t st) {
     if (e != hipSuccess) return e;
     const int cc = train::C[l + 1];
     return det_reduce(A.det, grid, 2 * cc, det_dst(A.L[l].st, 2 * cc, 1), st);
-  }
-  if (l >= 1 && A.L[l - 1].aff != nullptr && all_tiles >= kPPMinTilesPerCU * ncu && pp_enabled()) {
-    hipLaunchKernelGGL(train::aff_kernel, dim3(A.groups), dim3(256), 0, st, A, l - 1);
-    const int grid = ncu;  // one two-team workgroup per CU, contiguous tile ranges
-    switch (l) {
-      case 1: hipLaunchKernelGGL(train::fwd_pp_kernel<1>, dim3(grid), dim3(512), train::PP<1>::LDS, st, A); break;
-      case 2: hipLaunchKernelGGL(train::fwd_pp_kernel<2>, dim3(grid), dim3(512), train::PP<2>::LDS, st, A); break;
-      case 3: hipLaunchKernelGGL(train::fwd_pp_kernel<3>, dim3(grid), dim3(512), train::PP<3>::LDS, st, A); break;
-      case 4: hipLaunchKernelGGL(train::fwd_pp_kernel<4>, dim3(grid), dim3(512), train::PP<4>::LDS, st, A); break;
-      case 5: hipLaunchKernelGGL(train::fwd_pp_kernel<5>, dim3(grid), dim3(512), train::PP<5>::LDS, st, A); break;
-      default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
   }
   // persistent forward: at most 4 workgroups per CU-slot pair, each over a contiguous tile range
   const int tiles = fwd_grid(A.B);

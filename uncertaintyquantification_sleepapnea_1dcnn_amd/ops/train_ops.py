@@ -6,7 +6,7 @@ One optimizer step (Keras semantics) is ~22 launches on one stream
   fwd 1..6          R_l = relu(conv(dropout(BN(R_{l-1}))) + b), per-channel moments (atomics)
   head              GAP + Dense + BCE + dlogit + dense grads + backward moments of block 6
   dgrad 6..2        dY_{l-1} and the backward moments of block l-1
-  wgrad 6..1        dW_l, db_l (row-reduced in registers, fp32 atomics)
+  wgrad 6..1        dW_l, db_l (row-reduced in registers, per-row-group partial slots + ordered reduce)
   finalize          moving-average update + dgamma / dbeta
   Adam              one multi-tensor launch over the flat buffer
 
@@ -84,7 +84,7 @@ class TrainWorkspace:
         bf = torch.bfloat16
         self.x = torch.zeros(rows0, ch[0], dtype=bf, device=dev)
         # -0.0 everywhere: the halo rows before the first / after the last tile and the 4 pad rows of
-        # every sample are never written by the kernels (train_conv.hip APNEAUQ_FWD_SKIPPAD), and -0.0
+        # every sample are never written by the kernels (train_conv.hip copy-out of the valid rows), and -0.0
         # decodes to A = 0 (decode_pair) like a dropped element
         self.R = [torch.empty(rows0 if l == 0 else rows, ch[l + 1], dtype=bf, device=dev).fill_(-0.0)
                   for l in range(6)]
@@ -99,13 +99,6 @@ class TrainWorkspace:
         self.st_all = torch.zeros(sum(S * self.groups * 2 * ch[l + 1] for l in range(6)), dtype=torch.float64,
                                   device=dev)
         self.bst_all = torch.zeros(sum(S * 2 * ch[l + 1] for l in range(6)), dtype=torch.float64, device=dev)
-        # per-group BN affine of every layer, written by aff_kernel for the ping-pong forward
-        self.aff_all = torch.zeros(sum(self.groups * 2 * ch[l + 1] for l in range(6)), device=dev)
-        self.aff = []
-        o3 = 0
-        for l in range(6):
-            self.aff.append(self.aff_all[o3: o3 + self.groups * 2 * ch[l + 1]])
-            o3 += self.groups * 2 * ch[l + 1]
         self.st, self.bst = [], []
         o1 = o2 = 0
         for l in range(6):
@@ -170,8 +163,7 @@ class TrainWorkspace:
                      g[f"conv1d_{i}/kernel"].data_ptr(), g[f"conv1d_{i}/bias"].data_ptr(),
                      g[f"batchnorm_{i}/gamma"].data_ptr(), g[f"batchnorm_{i}/beta"].data_ptr(),
                      self.R[l].data_ptr(), self.dY[l].data_ptr(), self.st[l].data_ptr(), self.bst[l].data_ptr(),
-                     rng.dropout_threshold(p), _fbits(1.0 / (1.0 - p) if p < 1 else 0.0), self.dZ[l].data_ptr(),
-                     self.aff[l].data_ptr()]
+                     rng.dropout_threshold(p), _fbits(1.0 / (1.0 - p) if p < 1 else 0.0), self.dZ[l].data_ptr()]
         vals += [self.x.data_ptr(), self.y.data_ptr(), v["output_layer/kernel"].data_ptr(),
                  v["output_layer/bias"].data_ptr(), g["output_layer/kernel"].data_ptr(),
                  g["output_layer/bias"].data_ptr(), self.logits.data_ptr(), self.dlogit.data_ptr(),
