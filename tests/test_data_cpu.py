@@ -116,3 +116,14 @@ def test_pr_fallback_gates_resample_reshape(tmp_path):
     flat = np.arange(2 * 240, dtype=np.float64).reshape(2, 240)  # t-major: SaO2_t0, PR_t0, THOR_t0, ABDO_t0, ...
     x3 = prepare.reshape_flat_to_3d(flat, 60, 4)
     assert x3.shape == (2, 60, 4) and x3[0, 1, 0] == 4 and x3[1, 0, 3] == 243
+
+
+def test_knn_routes_agree_and_hip_range():
+    """The distance-GEMM route (the fallback outside the HIP kernel's k <= 16 / D <= 320 range) agrees
+    with the exact search, including for k > 16."""
+    assert balance.hip_knn_supported(240, 5) and not balance.hip_knn_supported(240, 17)
+    assert not balance.hip_knn_supported(321, 5)
+    rs = np.random.RandomState(4)
+    X = rs.randn(150, 9)
+    for k in (5, 20):
+        np.testing.assert_array_equal(balance.knn_indices(X, k, "cpu"), balance.knn_indices(X, k, "sklearn"))

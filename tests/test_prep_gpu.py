@@ -55,3 +55,14 @@ def test_smote_hip_knn_matches_sklearn():
     b = balance.SMOTE(random_state=2025, knn_device="sklearn").fit_resample(X, y)
     np.testing.assert_array_equal(a[1], b[1])
     np.testing.assert_allclose(a[0], b[0], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("n,d,k", [(300, 17, 20), (200, 400, 3)])
+def test_knn_hip_route_falls_back_outside_kernel_range(n, d, k):
+    """k > 16 or rows wider than the kernel's LDS tile: the 'hip' (and default) route must take the
+    distance-GEMM path instead of raising from prep_knn."""
+    assert not balance.hip_knn_supported(d, k)
+    rs = np.random.RandomState(n)
+    X = rs.randn(n, d)
+    np.testing.assert_array_equal(balance.knn_indices(X, k, device="hip"), _knn_ref(X, k))
+    np.testing.assert_array_equal(balance.knn_indices(X, k), _knn_ref(X, k))

@@ -63,7 +63,9 @@ constexpr int kBootThreads = 512;
 
 // PARTIAL (sharded windows): this rank holds the metrics of global windows [lo, lo + n_loc);
 // every draw is enumerated, only those landing in the shard are summed, and the 8 raw sums per
-// replicate go out for an all-reduce (ops/uq.py bootstrap_partial) instead of the 6 means.
+// replicate go out for an all-reduce (ops/uq.py bootstrap_partial) instead of the 6 means.  What the
+// sharding divides is the window data (metric rows, memory, the per-window metric pass); the B x n draw
+// enumeration (index reads or hashes, ~1 integer op per draw) is replicated on every rank.
 template <bool PARTIAL>
 __global__ __launch_bounds__(kBootThreads) void bootstrap_kernel(const float* __restrict__ metrics, const int* __restrict__ y,
                                                                  const int* __restrict__ idx, unsigned seed, int n,

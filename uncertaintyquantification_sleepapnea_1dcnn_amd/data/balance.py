@@ -79,9 +79,16 @@ def knn_indices(X: np.ndarray, k: int = 5, device: Optional[str] = None) -> np.n
             device = "sklearn"
     if device == "sklearn" or X.shape[0] <= k + 1:
         return _knn_numpy(X, k)
-    if device == "hip" or (device == "cuda" and k <= 16 and X.shape[1] <= 320):
+    if device in ("hip", "cuda") and hip_knn_supported(X.shape[1], k):
         return _knn_hip(X, k)
-    return _knn_torch(X, k, "cuda" if device == "torch" else device)
+    # outside the kernel's range (k > 16 or rows too wide for its LDS tile) the distance-GEMM path
+    return _knn_torch(X, k, "cuda" if device in ("torch", "hip") else device)
+
+
+def hip_knn_supported(n_features: int, k: int) -> bool:
+    """Range of the prep_knn kernel (csrc: top-k list of <= 16 in registers, a row tile of <= 320
+    fp64 features in LDS)."""
+    return k <= 16 and n_features <= 320
 
 
 class SMOTE:

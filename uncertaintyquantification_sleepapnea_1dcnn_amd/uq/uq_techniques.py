@@ -181,7 +181,8 @@ def bootstrap_metrics(uq_predictions, y_true, n_bootstrap: int = 100, random_sta
     over the resampled windows (mathematically identical to the reference's full recomputation,
     ``uq_techniques.py:137-157``).  ``distributed=True`` shards the windows over the process group and
     all-reduces the replicate sums (``distributed.bootstrap_sharded``); it is a collective, so
-    EVERY rank must call it.  The default is the local computation: the drivers reach this function on
+    EVERY rank must call it.  Sharding divides the window data and the per-window metric pass; every rank
+    still enumerates all B x n draws (cheap integer work) and keeps those landing in its shard.  The default is the local computation: the drivers reach this function on
     rank 0 only (``drivers._finish``), where a collective would wait for the other ranks forever.
     """
     torch = _torch()
