@@ -24,7 +24,7 @@ for d in sorted(glob.glob(os.path.join(root, "*"))):
         continue
     for r in csv.DictReader(open(f[0])):
         if "layer_kernel" in r["Name"]:
-            key = r["Name"].split("<")[1].split(">")[0]
+            key = ",".join(r["Name"].split("<")[1].split(">")[0].split(",")[:3])  # Cin, Cout, k: the layer
             rows.setdefault(key, {})[os.path.basename(d)] = int(r["TotalDurationNs"]) / 1e6
 names = sorted({n for v in rows.values() for n in v})
 print("| layer_kernel<> | " + " | ".join(names) + " |")

@@ -26,12 +26,13 @@
 //                  are linear per channel), p = sigmoid(logit)
 //
 // Layer kernel geometry (CDNA4-first):
-//   * one persistent 512-thread workgroup (8 waves, 2 per SIMD) per CU walks a contiguous range of
-//     tiles; a tile = 4 samples of one group (MC-Dropout pass or ensemble member) = 256 GEMM rows,
-//     every sample a 64-row slot (60 time steps + 4 zero rows, the 'same' padding halo);
-//   * the input channels stream through LDS in chunks of 32, double-buffered: while the MFMAs consume
-//     chunk c the global loads of chunk c+1 are in flight in registers (transform + fp16 split + LDS
-//     write after the chunk, one LDS-only barrier per chunk -- no vmcnt drain);
+//   * one persistent workgroup per CU (7-8 MFMA waves + 4 loader waves) walks a contiguous range of
+//     tiles; a tile = S (2 or 4) samples of one group (MC-Dropout pass or ensemble member) = 64 S GEMM
+//     rows, every sample a 64-row slot (60 time steps + 4 zero rows, the 'same' padding halo);
+//   * the input channels stream through LDS in chunks of 32, double-buffered: while the MFMA waves
+//     consume chunk c, the loader waves write chunk c+1 (BN affine + dropout + fp16 split of registers
+//     loaded one chunk earlier) and issue the HBM loads of chunk c+2; one LDS-only barrier per chunk,
+//     no vmcnt drain, and no HBM load ever queued in front of an MFMA wave's weight loads;
 //   * LDS row = [hi 32 ch | lo 32 ch | 32 B pad] = 160 B = 10 16-B slots (stride = 2 mod 4 slots: the
 //     ds_read_b128 lane groups of a 16x16x32 B fragment hit 16 distinct slots at any row offset);
 //   * conv = implicit GEMM  D[co][row] = sum_{tap, ci} W[tap][ci][co] A[row + tap - pad][ci]: weights are
@@ -48,10 +49,9 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const f16x8 gf16x8;
 
-// Staging waves: the HBM loads of the next chunk are issued by waves 0..SW-1 only.  vmcnt retires in
-// order, so a wave that issued them waits for them at its next weight-fragment wait; with the loads
-// confined to one wave of each SIMD pair (waves w and w+4 share a SIMD), the partner keeps the matrix
-// pipe busy meanwhile.  APNEAUQ_X3_SW=0: every wave stages.
+// Staging waves of a layer without loader waves: the HBM loads of the next chunk are issued by MFMA
+// waves 0..SW-1 only (one per SIMD), so that the partner wave keeps the matrix pipe busy while the
+// stager's in-order vmcnt holds it at its next weight-fragment wait.  APNEAUQ_X3_SW=0: every wave stages.
 #ifndef APNEAUQ_X3_SW
 #define APNEAUQ_X3_SW 4
 #endif
@@ -110,12 +110,22 @@ __device__ __forceinline__ int xcd_wg() {
   return (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + bid / 8;
 }
 
-template <int CIN, int COUT, int KS, int S, int WM, int WN, bool LAST>
-__global__ __launch_bounds__(WM * WN * 64, 2) void layer_kernel(const LayerArgs A) {
+// Waves: WM x WN MFMA waves, plus LW loader waves (LW > 0) that do all the input staging: HBM loads of
+// chunk c+2, BN affine + dropout + fp16 split of chunk c+1 into LDS.  vmcnt retires in order, so an MFMA
+// wave that issued HBM loads would stall its next weight-fragment wait on them; loader waves take that
+// latency instead, and wait at the chunk barrier without using issue slots.
+// Register budget: 2 waves per SIMD up to 8 waves per workgroup, ceil(NW / 4) beyond (one workgroup per
+// CU: the two chunk buffers leave no LDS for a second).
+template <int NW>
+constexpr int waves_per_eu() { return NW > 8 ? (NW + 3) / 4 : 2; }
+template <int CIN, int COUT, int KS, int S, int WM, int WN, bool LAST, int LW>
+__global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) void layer_kernel(const LayerArgs A) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int NW = WM * WN, kThreads = NW * 64;
+  constexpr int NWM = WM * WN, NW = NWM + LW, kThreads = NW * 64;
   constexpr int kS = S, kBufB = buf_bytes(S), kValidRows = S * kL, kUnits = kValidRows * (kCK / 4);
-  constexpr int SW = (APNEAUQ_X3_SW > 0 && APNEAUQ_X3_SW < NW) ? APNEAUQ_X3_SW : NW;  // staging waves
+  // staging waves: the LW loader waves, else MFMA waves 0..SW-1 (one per SIMD by default)
+  constexpr int SW = LW > 0 ? LW : (APNEAUQ_X3_SW > 0 && APNEAUQ_X3_SW < NW) ? APNEAUQ_X3_SW : NW;
+  constexpr int kSBase = LW > 0 ? NWM * 64 : 0;              // first staging thread
   constexpr int kST = SW * 64;                                // staging threads
   constexpr int kNU = (kUnits + kST - 1) / kST;              // 16-B staging units per staging thread
   static_assert(kST % 8 == 0, "a staging thread keeps one channel quad");
@@ -123,18 +133,22 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void layer_kernel(const LayerArgs 
   constexpr int NSTEP = NCH * KS;
   // MFMA issue order: row tiles in groups of RG so that >= 4 accumulators rotate (dependent-issue
   // latency); B fragments double-buffered one group ahead when the accumulators leave room
-  constexpr int RG = APNEAUQ_X3_RG > 0 ? APNEAUQ_X3_RG : NCT >= 4 ? 1 : (NCT >= 3 && NCT * NRT > 16) ? 1 : 2;
-  constexpr bool BDB = NCT * NRT <= 24;
+  constexpr int RG = APNEAUQ_X3_RG > 0 ? APNEAUQ_X3_RG
+                     : NCT >= 4                        ? 1
+                     : (NCT >= 3 && NCT * NRT > 16)    ? 1
+                     : NCT == 1                        ? 4
+                                                       : 2;
+  constexpr bool BDB = NCT * NRT <= 24 && RG < 4;
   static_assert(NRT % RG == 0, "row-tile groups");
   constexpr long long FRAG_STEP = (long long)NCTA * 128;  // f16x8 per (chunk, tap) k-step
   static_assert(CIN % kCK == 0 && COUT % 16 == 0, "channel tiling");
   static_assert(NCTA % WN == 0 && (4 * S) % WM == 0, "wave tiling");
-  static_assert(!LAST || NRT == 4, "block 6: one sample per wave row");
+  static_assert(!LAST || NRT % 4 == 0, "block 6: whole samples per wave row");
   double* st = reinterpret_cast<double*>(smem + 2 * kBufB);  // [2][COUT] per-workgroup moment sums
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wave % WN, wm = wave / WN;
+  const int wn = wave % WN, wm = (wave / WN) % WM;  // (loader waves: unused)
   const int ct0 = wn * NCT, rt0 = wm * NRT;
   const int m = lane & 15, h = lane >> 4;
   APNEAUQ_DASSERT(blockDim.x == kThreads);
@@ -151,13 +165,14 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void layer_kernel(const LayerArgs 
   if (t_begin >= t_end) return;  // workgroup-uniform
   const int slot = wg % kStatSlots;
 
-  // ---- staging (waves < SW): a staging thread's 16-B units of a chunk are (row ri = tid/8 + kST/8 u,
-  // channel quad q = tid % 8)
-  const bool stager = wave < SW && (APNEAUQ_X3_ABL & 1) == 0;
+  // ---- staging: staging thread i = tid - kSBase keeps the 16-B units (row ri = i/8 + kST/8 u,
+  // channel quad q = i % 8) of every chunk
+  const bool loader = LW > 0 && wave >= NWM;
+  const bool stager = (LW > 0 ? loader : wave < SW) && (APNEAUQ_X3_ABL & 1) == 0;
   f32x4 sv[kNU];
   f32x4 sa, sb;  // BN affine (scale, shift) x 1/(1-p) of the thread's 4 channels
   auto load_chunk = [&](int tile, int c) {
-    const int tid = opaque_tid(), q = tid & 7;
+    const int tid = opaque_tid() - kSBase, q = tid & 7;
     const int g = tile / tpg;
     const int w0 = (tile - g * tpg) * kS;
     const float* af = A.aff_in + (long long)g * A.aff_gstride + c * kCK + 4 * q;
@@ -177,7 +192,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void layer_kernel(const LayerArgs 
     }
   };
   auto store_chunk = [&](int tile, int c, char* buf) {
-    const int tid = opaque_tid(), q = tid & 7;
+    const int tid = opaque_tid() - kSBase, q = tid & 7;
     const int g = tile / tpg;
     const int w0 = (tile - g * tpg) * kS;
     unsigned skey = 0;
@@ -358,6 +373,23 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void layer_kernel(const LayerArgs 
               asm volatile("" :: "v"(o));
           }
         }
+        if constexpr (LAST) {
+          if ((rt & 3) == 3) {  // the 4 row tiles of sample slot (rt0 + rt) / 4 are complete
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              k1[e] = group16_sum(k1[e]);
+              k0[e] = group16_sum(k0[e]);
+            }
+            const int wl = w0 + (rt0 + rt) / 4;
+            if (m == 0 && wl < A.n_win) {
+              float* o = A.out + ((long long)g * A.n_win + wl) * (2 * COUT);
+              *reinterpret_cast<f32x4*>(o + co0) = k1;
+              *reinterpret_cast<f32x4*>(o + COUT + co0) = k0;
+            }
+            k1 = f32x4{0.f, 0.f, 0.f, 0.f};
+            k0 = k1;
+          }
+        }
       }
       // reduce over the 16 rows of each lane group (lanes sharing h hold the same 4 channels)
       if (A.stats != nullptr) {
@@ -368,19 +400,6 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void layer_kernel(const LayerArgs 
             atomicAdd(&st[co0 + e], (double)a);
             atomicAdd(&st[COUT + co0 + e], (double)b);
           }
-        }
-      }
-      if constexpr (LAST) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          k1[e] = group16_sum(k1[e]);
-          k0[e] = group16_sum(k0[e]);
-        }
-        const int w = w0 + wm;  // NRT == 4: this wave row is exactly sample slot wm
-        if (m == 0 && w < A.n_win) {
-          float* o = A.out + ((long long)g * A.n_win + w) * (2 * COUT);
-          *reinterpret_cast<f32x4*>(o + co0) = k1;
-          *reinterpret_cast<f32x4*>(o + COUT + co0) = k0;
         }
       }
     }
@@ -405,6 +424,55 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void layer_kernel(const LayerArgs 
   const int total = (t_end - t_begin) * NCH;
   auto chunk_tile = [&](int it) { return t_begin + it / NCH; };
   int g_cur = t_begin / tpg;
+  if constexpr (LW > 0) {
+    // Loader and MFMA waves run the same barrier sequence: one LDS barrier before the first chunk and
+    // after every chunk, and the two of flush_stats at every group change and at the end.
+    if (loader) {
+      if (stager) {
+        load_chunk(t_begin, 0);
+        store_chunk(t_begin, 0, smem);
+      }
+      lds_barrier();
+      if (stager && total > 1) load_chunk(chunk_tile(1), 1 % NCH);
+#pragma unroll 1
+      for (int it = 0; it < total; ++it) {
+        const int tile = chunk_tile(it), c = it - (tile - t_begin) * NCH;
+        if (c == 0) {
+          const int g = tile / tpg;
+          if (g != g_cur) {
+            flush_stats(g_cur);
+            g_cur = g;
+          }
+        }
+        // chunk it+1 into the buffer compute(it-1) read (every wave passed the barrier after it)
+        if (stager && it + 1 < total) store_chunk(chunk_tile(it + 1), (it + 1) % NCH, smem + ((it + 1) & 1) * kBufB);
+        lds_barrier();
+        if (stager && it + 2 < total) load_chunk(chunk_tile(it + 2), (it + 2) % NCH);
+      }
+      flush_stats(g_cur);
+      return;
+    }
+    lds_barrier();
+    load_a(wbase(t_begin), ah, al);
+#pragma unroll 1
+    for (int it = 0; it < total; ++it) {
+      const int tile = chunk_tile(it), c = it - (tile - t_begin) * NCH;
+      if (c == 0) {
+        const int g = tile / tpg;
+        if (g != g_cur) {
+          flush_stats(g_cur);
+          g_cur = g;
+        }
+      }
+      const gf16x8* wcur = wbase(tile);
+      const gf16x8* wnxt = wbase(tile + 1 < t_end ? tile + 1 : tile);
+      compute_chunk(c, smem + (it & 1) * kBufB, wcur, wnxt, []() {});
+      if (c == NCH - 1) epilogue(tile);
+      lds_barrier();
+    }
+    flush_stats(g_cur);
+    return;
+  }
   if (stager) {
     load_chunk(t_begin, 0);
     store_chunk(t_begin, 0, smem);
@@ -543,36 +611,42 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs A) {
 }
 
 // ------------------------------------------------------------------------------- launch helpers
-template <int CIN, int COUT, int KS, int S, int WM, int WN, bool LAST>
+template <int CIN, int COUT, int KS, int S, int WM, int WN, bool LAST, int LW>
 hipError_t launch_layer(const LayerArgs& A, int grid, hipStream_t stream) {
   constexpr int lds = lds_bytes(S, COUT);
-  auto k = layer_kernel<CIN, COUT, KS, S, WM, WN, LAST>;
+  auto k = layer_kernel<CIN, COUT, KS, S, WM, WN, LAST, LW>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL(k, dim3(grid), dim3(WM * WN * 64), lds, stream, A);
+  hipLaunchKernelGGL(k, dim3(grid), dim3((WM * WN + LW) * 64), lds, stream, A);
   return hipGetLastError();
 }
 
 }  // namespace x3
 
 // Layer table of the reference architecture (cnn_baseline_train.py:59-86), blocks 2..6:
-//   <Cin, Cout, k, samples per tile, wave rows WM, wave channel groups WN, block 6>
-// Each wave owns (4 S / WM) 16-row tiles x (Cout / 16 / WN) 16-channel tiles; the 64-accumulator-tile
-// layers (Cout 224 / 256) run 2-sample tiles so that the staging registers, the next k-step's weight
-// fragments and the B double-buffer fit beside the accumulators without spilling.
-#define APNEAUQ_X3_LAYERS(X)                       \
-  X(1, 128, 192, 5, 4, 2, 4, false)                \
-  X(2, 192, 224, 3, 2, 1, 7, false)                \
-  X(3, 224, 96, 7, 4, 4, 2, false)                 \
-  X(4, 96, 256, 9, 2, 1, 8, false)                 \
-  X(5, 256, 96, 9, 4, 4, 2, true)
+//   <Cin, Cout, k, samples per tile, wave rows WM, wave channel groups WN, block 6, loader waves LW>
+// Each MFMA wave owns (4 S / WM) 16-row tiles x (Cout / 16 / WN) 16-channel tiles; the 64-accumulator-tile
+// layers (Cout 224 / 256) run 2-sample tiles so that the next k-step's weight fragments and the B
+// double-buffer fit beside the accumulators without spilling.  Loader waves (ablation table in
+// profiles/x3_loader_waves.md) on every layer but block 2, whose 96-accumulator tile needs the 256-VGPR
+// budget of 8 waves.
+#ifndef APNEAUQ_X3_LW  // probe: loader waves per layer (-1 = table)
+#define APNEAUQ_X3_LW -1
+#endif
+#define APNEAUQ_X3_LOADERS(n) (APNEAUQ_X3_LW < 0 ? (n) : APNEAUQ_X3_LW)
+#define APNEAUQ_X3_LAYERS(X)                                    \
+  X(1, 128, 192, 5, 4, 2, 4, false, APNEAUQ_X3_LOADERS(0))      \
+  X(2, 192, 224, 3, 2, 1, 7, false, APNEAUQ_X3_LOADERS(4))      \
+  X(3, 224, 96, 7, 4, 4, 2, false, APNEAUQ_X3_LOADERS(4))       \
+  X(4, 96, 256, 9, 2, 1, 8, false, APNEAUQ_X3_LOADERS(4))       \
+  X(5, 256, 96, 9, 4, 4, 2, true, APNEAUQ_X3_LOADERS(4))
 
 int x3_lds_bytes(int layer) {
-#define APNEAUQ_X3_LDS(L, CI, CO, K, S, WM, WN, LAST) \
+#define APNEAUQ_X3_LDS(L, CI, CO, K, S, WM, WN, LAST, LW) \
   if (layer == L) return x3::lds_bytes(S, CO);
   APNEAUQ_X3_LAYERS(APNEAUQ_X3_LDS)
 #undef APNEAUQ_X3_LDS
@@ -580,7 +654,7 @@ int x3_lds_bytes(int layer) {
 }
 
 int x3_tile_samples(int layer) {
-#define APNEAUQ_X3_TS(L, CI, CO, K, S, WM, WN, LAST) \
+#define APNEAUQ_X3_TS(L, CI, CO, K, S, WM, WN, LAST, LW) \
   if (layer == L) return S;
   APNEAUQ_X3_LAYERS(APNEAUQ_X3_TS)
 #undef APNEAUQ_X3_TS
@@ -589,8 +663,8 @@ int x3_tile_samples(int layer) {
 
 hipError_t x3_launch_layer(int layer, const x3::LayerArgs& A, int grid, hipStream_t stream) {
   using namespace x3;
-#define APNEAUQ_X3_LAUNCH(L, CI, CO, K, S, WM, WN, LAST) \
-  if (layer == L) return launch_layer<CI, CO, K, S, WM, WN, LAST>(A, grid, stream);
+#define APNEAUQ_X3_LAUNCH(L, CI, CO, K, S, WM, WN, LAST, LW) \
+  if (layer == L) return launch_layer<CI, CO, K, S, WM, WN, LAST, LW>(A, grid, stream);
   APNEAUQ_X3_LAYERS(APNEAUQ_X3_LAUNCH)
 #undef APNEAUQ_X3_LAUNCH
   return hipErrorInvalidValue;
