@@ -116,3 +116,20 @@ def test_mcd_batch_chunked_equals_unchunked():
         model = x3.X3Model(SPEC, [_params(3, dev)])
         outs.append(x3.mcd_batch(model, x, 5, seed=1, update_moving=False, max_samples=ms))
     torch.testing.assert_close(outs[0], outs[1], atol=2e-6, rtol=0)
+
+
+def test_mcd_batch_window_chunked_equals_one_shot():
+    """More windows than fit at one pass (VERDICT r2 missing #4): the two-phase window-chunked schedule
+    (moments of block l over window chunks, blocks below recomputed) gives the one-shot result."""
+    _ext.require()
+    dev = torch.device("cuda")
+    x = _x(41, 4).to(dev)
+    res = []
+    for ms in (None, 16):  # one shot / chunks of 16, 16, 9 windows
+        p = _params(5, dev)
+        model = x3.X3Model(SPEC, [p])
+        ph = x3.mcd_batch(model, x, 3, seed=9, pass_base=2, window_offset=100, update_moving=True, max_samples=ms)
+        res.append((ph, {k: v.clone() for k, v in p.items() if "moving" in k}))
+    torch.testing.assert_close(res[1][0], res[0][0], atol=1e-6, rtol=0)
+    for k in res[0][1]:
+        torch.testing.assert_close(res[1][1][k], res[0][1][k], atol=1e-6, rtol=1e-6)

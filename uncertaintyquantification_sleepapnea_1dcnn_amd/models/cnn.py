@@ -7,8 +7,11 @@ API parity with what the reference scripts call on their ``tf.keras.Model``
 
 Execution backends (MI355X-first):
 
-* inference (``training=False`` / ``predict``) on the GPU runs the fused whole-network HIP
-  kernel (``ops/fused.py``); the packed weight blob is cached and invalidated on any update;
+* inference (``training=False`` / ``predict``, MC Dropout, Deep Ensembles) on the GPU runs, for the
+  reference architecture, the fp32-faithful layer-wise engine (``ops/x3.py``: conv products as three
+  fp16 MFMAs over hi/lo splits, fp32 accumulate -- the reference computes in fp32) by default, or with
+  ``precision="bf16"`` the bf16 fused whole-network kernel (``ops/fused.py``); other architectures
+  run the layer-wise bf16 kernels (``ops/generic.py``).  Packed weights are cached per weight version;
 * training steps run the layer-wise HIP kernels (``ops/train_ops.py``; replayed from a captured
   HIP graph on a single device) with the Keras BatchNorm/Dropout/Adam semantics, or fp32 autograd
   over the reference ops where no kernel exists (CPU, non-default architectures);
@@ -19,6 +22,7 @@ On the CPU everything runs the fp32 reference.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -36,10 +40,15 @@ def _default_device():
 
 class AlarconCNN1D:
     def __init__(self, input_shape: Sequence[int] = (60, 4), spec: Optional[ModelSpec] = None, seed: int = 2025,
-                 device=None, name: str = "Alarcon_1D_CNN_Model", params=None, pool: bool = False):
+                 device=None, name: str = "Alarcon_1D_CNN_Model", params=None, pool: bool = False,
+                 precision: Optional[str] = None):
         self.spec = spec if spec is not None else ModelSpec.with_input(input_shape, pool=pool)
         self.name = name
         self.seed = int(seed)
+        # inference precision on the GPU: "fp32" (fp32-faithful engine where it exists) or "bf16"
+        self.precision = precision or os.environ.get("APNEAUQ_PRECISION", "fp32")
+        if self.precision not in ("fp32", "bf16"):
+            raise ValueError("precision must be 'fp32' or 'bf16'")
         self.device = torch.device(device) if device is not None else _default_device()
         init = params if params is not None else R.init_params(self.spec, self.seed)
         self.store = ParamStore(self.spec, init, self.device)
@@ -110,6 +119,7 @@ class AlarconCNN1D:
         self.store = self.store.to(self.device)
         self._blob = None
         self._gpack = None
+        self._x3m = None
         for attr in ("_train_ws", "_mcd_ws", "_train_graphs", "_gtrain_ws", "_gfwd_ws"):  # device workspaces / captured graphs
             if hasattr(self, attr):
                 delattr(self, attr)
@@ -137,6 +147,36 @@ class AlarconCNN1D:
         from ..ops import generic
 
         return self.device.type == "cuda" and not fused.supports(self.spec) and generic.supports(self.spec)
+
+    def uses_x3(self) -> bool:
+        """Inference on the fp32-faithful engine (reference architecture, precision "fp32", GPU)."""
+        from ..ops import x3
+
+        return self.device.type == "cuda" and self.precision == "fp32" and x3.supports(self.spec)
+
+    def x3_model(self):
+        """The engine's packed view of this model (cached per weight version; the BN moving statistics
+        are views of the store's tensors, so batch-statistics MC Dropout updates them in place)."""
+        from ..ops import x3
+
+        if getattr(self, "_x3m", None) is None or self._x3m_version != self.store.version:
+            self._x3m = x3.X3Model(self.spec, [self.store.as_dict()], device=self.device)
+            self._x3m_version = self.store.version
+        return self._x3m
+
+    def hip_infer(self, x: torch.Tensor, n_pass: int = 1, dropout: bool = False, seed: Optional[int] = None,
+                  pass_offset: int = 0, window_offset: int = 0, logits: bool = False) -> torch.Tensor:
+        """(n_pass, N) fp32 probabilities (or logits), BN on running statistics, on the engine chosen by
+        ``precision``: fp32-faithful (``x``'s fp32 values) or bf16 (``x`` rounded to bf16)."""
+        if self.uses_x3():
+            from ..ops import x3
+
+            _ext.require()
+            return x3.forward_running(self.x3_model(), x, n_pass=n_pass, dropout=dropout,
+                                      seed=self.seed if seed is None else seed, pass_offset=pass_offset,
+                                      window_offset=window_offset, logits=logits)[0]
+        return self.hip_forward(x.to(torch.bfloat16).contiguous(), n_pass=n_pass, dropout=dropout, seed=seed,
+                                pass_offset=pass_offset, window_offset=window_offset, logits=logits)
 
     def uses_hip(self) -> bool:
         """Inference (running-stat BN) runs on hand-written HIP kernels; warns once when it cannot."""
@@ -183,8 +223,8 @@ class AlarconCNN1D:
         use_batch = training if bn_batch_stats is None else bn_batch_stats
         if not use_batch and self.uses_hip() and (sample_ids is None or not isinstance(sample_ids, torch.Tensor)):
             sid = 0 if sample_ids is None else int(sample_ids)
-            out = self.hip_forward(x.to(torch.bfloat16).contiguous(), n_pass=1, dropout=use_drop, seed=seed,
-                                   pass_offset=0 if pass_id is None else pass_id, window_offset=sid, logits=True)
+            out = self.hip_infer(x, n_pass=1, dropout=use_drop, seed=seed,
+                                 pass_offset=0 if pass_id is None else pass_id, window_offset=sid, logits=True)
             return out[0].reshape(-1, 1)
         upd = use_batch if update_moving is None else update_moving
         with torch.no_grad():

@@ -45,14 +45,33 @@ def mc_dropout_batch_bn(model, x, n_pred: int, seed: Optional[int] = None, windo
                         chunk_rows: Optional[int] = None) -> torch.Tensor:
     """(T, N, 1) probabilities; each pass = Keras ``model(x, training=True)`` on the full set.
 
-    On a GPU with the HIP extension the passes run on the layer-wise training kernels
-    (``train_ops.forward_batch_stats``: BN moments accumulated in the conv epilogue, SyncBN by one
-    all-reduce of the per-layer (sum, sum of squares) buffer when ``distributed``); otherwise the
-    fp32 PyTorch reference path.  ``global_n`` = windows over all ranks; ``chunk_rows`` (ranks must
+    On a GPU with the HIP extension: the fp32-faithful engine for the reference architecture
+    (``x3.mcd_batch``, precision "fp32", the default), else the bf16 layer-wise training kernels
+    (``train_ops`` / ``generic_train.forward_batch_stats``); BN moments accumulated in the conv
+    epilogue, SyncBN by one all-reduce per layer when ``distributed``.  Otherwise the fp32 PyTorch
+    reference path.  ``global_n`` = windows over all ranks; ``chunk_rows`` (ranks must
     agree on it) bounds the windows x passes processed per launch.
     """
     xt = model._as_input(x)
     n = xt.shape[0]
+    if xt.is_cuda and getattr(model, "uses_x3", lambda: False)():
+        # fp32-faithful engine (the reference's precision); window-chunked beyond the memory budget
+        from . import x3
+
+        sync = None
+        if distributed:
+            import torch.distributed as dist
+
+            if dist.is_available() and dist.is_initialized():
+                sync = dist.all_reduce
+        base = model._call_counter
+        out = x3.mcd_batch(model.x3_model(), xt, n_pred, seed=model.seed if seed is None else seed, pass_base=base,
+                           window_offset=window_offset, update_moving=update_moving, sync=sync, global_n=global_n,
+                           max_samples=chunk_rows)
+        model._call_counter = base + n_pred
+        if update_moving:
+            model.store.bump()  # the moving statistics were updated in place
+        return out.unsqueeze(-1)
     if xt.is_cuda:
         from . import train_ops
 

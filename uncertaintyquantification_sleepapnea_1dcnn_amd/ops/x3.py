@@ -87,6 +87,8 @@ class X3Model:
         self.spec = spec
         self.G = len(params)
         dev = torch.device(device) if device is not None else params[0]["conv1d_1/kernel"].device
+        if dev.type == "cuda" and dev.index is None:  # "cuda" == the current device ("cuda" != "cuda:0")
+            dev = torch.device("cuda", torch.cuda.current_device())
         self.device = dev
         f32 = dict(dtype=torch.float32, device=dev)
         self.w1 = torch.stack([p["conv1d_1/kernel"].to(**f32) for p in params]).contiguous()  # (G, 7, 4, 128)
@@ -190,6 +192,9 @@ def mcd_batch(model: X3Model, x: torch.Tensor, n_pass: int, seed: int, pass_base
 
         w = dist.get_world_size() if dist.is_initialized() else 1
         ref_n = -(-gn // w)
+    if ref_n > max_samples:  # one pass of all windows does not fit: window-chunked two-phase schedule
+        return _mcd_batch_windowed(model, x, n_pass, seed, pass_base, window_offset, update_moving, sync, gn,
+                                   max_samples)
     cap = max(1, min(n_pass, max_samples // max(ref_n, 1)))
     n_chunks = -(-n_pass // cap)
     chunk = -(-n_pass // n_chunks)
@@ -228,15 +233,93 @@ def mcd_batch(model: X3Model, x: torch.Tensor, n_pass: int, seed: int, pass_base
     return out
 
 
+def _mcd_batch_windowed(model: X3Model, x: torch.Tensor, n_pass: int, seed: int, pass_base: int,
+                        window_offset: int, update_moving: bool, sync: Optional[Callable], gn: int,
+                        max_samples: int) -> torch.Tensor:
+    """Batch-BN MC Dropout when even one pass over the rank's windows exceeds the activation budget.
+
+    The BN moments of block l are moments over ALL windows, and block l+1 cannot start before they are
+    known, so with window chunks the activations below block l are recomputed: for l = 1..6 every chunk
+    runs blocks 1..l with the (already final) affines of blocks 1..l-1 and accumulates block l's moments;
+    a last sweep runs the whole network with all affines and the head.  The dropout masks are counters of
+    (seed, block, pass, global window id), so the recomputed activations are the same numbers, and the
+    result equals the one-shot schedule up to the order of the fp64 moment sums.  Cost: 21 block
+    evaluations per pass instead of 6 (only beyond ~2 M windows per 288-GB GPU)."""
+    spec, o = model.spec, _ops()
+    n = x.shape[0]
+    wc = max(1, int(max_samples))
+    bounds = [(s, min(n, s + wc)) for s in range(0, n, wc)]
+    ws = model.workspace(wc, wc, 1)
+    inv_count = 1.0 / (gn * 60.0)
+    thr = [rng.dropout_threshold(b.dropout) for b in spec.blocks]
+    dsc = [_dsc(b.dropout) for b in spec.blocks]
+    eps, mom = float(spec.bn_epsilon), float(spec.bn_momentum)
+    seed = int(seed) & ((1 << 63) - 1)
+    out = torch.empty(n_pass, n, dtype=torch.float32, device=model.device)
+
+    def run(s: int, e: int, upto: int, pb: int, stats_layer: int) -> None:
+        """Blocks 1..upto+1 over windows [s, e) of pass pb; moments of block stats_layer+1 into its slots."""
+        m = e - s
+        o.x3_l1(x[s:e], model.w1, model.b1, ws.r1, ws.stats[0] if stats_layer == 0 else None, m, 1)
+        for l in range(1, upto + 1):
+            src = ws.r1 if l == 1 else ws.buf[(l - 2) % 2]
+            dst = ws.sums if l == 5 else ws.buf[(l - 1) % 2]
+            o.x3_layer(l, src, dst, model.wfrag[l], 0, model.bias[l], model.wscale[l], 0, ws.aff[l - 1],
+                       0 if l == 1 else 2 * CH[l], ws.stats[l] if l == stats_layer else None, m, 1, l == 1, l == 1,
+                       thr[0], thr[l], seed, pb, int(window_offset) + s, 0)
+
+    def finish_layer(l: int, repeat: int) -> None:
+        if sync is not None:
+            _sync_stats(sync, ws.stats[l], 1, CH[l + 1])
+        g, b, mm, mv = model.bn[l]
+        o.x3_aff(ws.stats[l], g, b, mm, mv, ws.aff[l], CH[l + 1], 1, 0, bool(update_moving), repeat, inv_count, eps,
+                 mom, dsc[l])
+
+    # block 1: no dropout before it, so its moments (and affine) are shared by every pass
+    ws.stats[0].zero_()
+    for s, e in bounds:
+        run(s, e, 0, int(pass_base), 0)
+    finish_layer(0, n_pass)
+    for t in range(n_pass):
+        pb = int(pass_base) + t
+        for l in range(1, 6):
+            ws.stats[l].zero_()
+            for s, e in bounds:
+                run(s, e, l, pb, l)
+            finish_layer(l, 1)
+        for s, e in bounds:
+            run(s, e, 5, pb, -1)
+            o.x3_head(ws.sums, ws.aff[5], 0, model.dw, model.db, 0, ws.out, e - s, 1, False)
+            out[t, s:e].copy_(ws.out[: e - s])
+    return out
+
+
 @torch.no_grad()
 def forward_running(model: X3Model, x: torch.Tensor, n_pass: int = 1, dropout: bool = False, seed: int = 0,
-                    pass_offset: int = 0, window_offset: int = 0, logits: bool = False) -> torch.Tensor:
+                    pass_offset: int = 0, window_offset: int = 0, logits: bool = False,
+                    max_samples: Optional[int] = None) -> torch.Tensor:
     """BN on moving statistics, fp32-faithful: (G, n_pass, N) probabilities (or logits).
 
     G > 1 members run as one launch per layer (Deep Ensemble predict, ``uq_techniques.py:29``);
-    ``dropout=True`` is standard MC Dropout with n_pass passes (one model)."""
-    spec, o = model.spec, _ops()
+    ``dropout=True`` is standard MC Dropout with n_pass passes (one model).  Windows are independent
+    here, so sets larger than the activation budget (``max_samples`` window x group rows) run in window
+    chunks (masks are keyed by the global window id: the result does not depend on the chunking)."""
     x = x.to(device=model.device, dtype=torch.float32).contiguous()
+    n = x.shape[0]
+    groups = (n_pass if dropout else model.G) if n > 0 else 1
+    if max_samples is None:
+        max_samples = _max_samples(model.device, BYTES_PER_SAMPLE)
+    wc = max(1, int(max_samples) // max(groups, 1))
+    if n <= wc:
+        return _forward_running(model, x, n_pass, dropout, seed, pass_offset, window_offset, logits)
+    parts = [_forward_running(model, x[s: s + wc], n_pass, dropout, seed, pass_offset, int(window_offset) + s, logits)
+             for s in range(0, n, wc)]
+    return torch.cat(parts, dim=2)
+
+
+def _forward_running(model: X3Model, x: torch.Tensor, n_pass: int, dropout: bool, seed: int, pass_offset: int,
+                     window_offset: int, logits: bool) -> torch.Tensor:
+    spec, o = model.spec, _ops()
     n = x.shape[0]
     G = model.G
     if dropout and G != 1:

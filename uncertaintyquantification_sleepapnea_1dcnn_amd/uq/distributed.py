@@ -81,8 +81,7 @@ def mc_dropout_predict_sharded(model, x_test_data, n_pred: int = 50, bn_mode: st
     if bn_mode == "running":
         base = model._call_counter  # fresh masks per call, identical on every rank
         if model.uses_hip():
-            loc = model.hip_forward(xl.to(torch.bfloat16).contiguous(), n_pass=n_pred, dropout=True, seed=seed,
-                                    window_offset=s, pass_offset=base)
+            loc = model.hip_infer(xl, n_pass=n_pred, dropout=True, seed=seed, window_offset=s, pass_offset=base)
         else:
             ids = torch.arange(s, e, device=x.device)
             loc = torch.stack([torch.sigmoid(model.logits(xl, dropout=True, bn_batch_stats=False, pass_id=base + t,
@@ -106,13 +105,20 @@ def deep_ensembles_predict_sharded(ensemble_models: List, x_test_data) -> torch.
     ids = pdist.members_of_rank(M, rank, world)
     dev = _comm_device()
     mine = [ensemble_models[i] for i in ids]
-    if mine and all(m.uses_fused() for m in mine):
+    if mine and all(m.uses_x3() for m in mine):
+        from ..ops import x3
+
+        m0 = mine[0]
+        eng = x3.X3Model(m0.spec, [{k: v.to(m0.device) for k, v in m.store.as_dict().items()} for m in mine],
+                         device=m0.device)
+        loc = x3.forward_running(eng, m0._as_input(x_test_data))[:, 0]
+    elif mine and all(m.uses_fused() for m in mine):
         x = mine[0]._as_input(x_test_data).to(torch.bfloat16).contiguous()
         blobs = torch.cat([m.fused_blob().to(mine[0].device) for m in mine])
         loc = fused.fused_forward(x, blobs, mine[0].spec)[:, 0]
     elif mine and all(m.uses_hip() for m in mine):
-        x = mine[0]._as_input(x_test_data).to(torch.bfloat16).contiguous()
-        loc = torch.stack([m.hip_forward(x)[0] for m in mine])
+        x = mine[0]._as_input(x_test_data)
+        loc = torch.stack([m.hip_infer(x)[0] for m in mine])
     elif mine:
         loc = torch.stack([torch.as_tensor(np.asarray(m.predict(x_test_data, verbose=0))).reshape(-1) for m in mine])
     else:

@@ -72,9 +72,9 @@ def mc_dropout_predict(model, x_test_data, n_pred: int = 50, bn_mode: str = "bat
     elif bn_mode == "running" and getattr(model, "uses_hip", lambda: False)():
         # fused whole-network kernel (reference architecture) or the layer-wise HIP kernels (any spec);
         # like model(x, training=True), every call draws fresh masks (pass ids advance per call)
-        x = model._as_input(x_test_data).to(torch.bfloat16).contiguous()
+        x = model._as_input(x_test_data)
         base = model._call_counter
-        out = model.hip_forward(x, n_pass=n_pred, dropout=True, seed=seed, pass_offset=base).unsqueeze(-1)
+        out = model.hip_infer(x, n_pass=n_pred, dropout=True, seed=seed, pass_offset=base).unsqueeze(-1)
         model._call_counter = base + n_pred
     elif bn_mode == "running":
         x = model._as_input(x_test_data)
@@ -103,6 +103,15 @@ def deep_ensembles_predict(ensemble_models: List, x_test_data, as_numpy: bool = 
     if ensemble_models and (D.active() if distributed is None else distributed):
         out = D.deep_ensembles_predict_sharded(ensemble_models, x_test_data)
         out = out.cpu().numpy() if as_numpy else out
+    elif ensemble_models and all(getattr(m, "uses_x3", lambda: False)() for m in ensemble_models):
+        # fp32-faithful engine, every member in one launch per layer (x3.X3Model with G = M)
+        from ..ops import x3
+
+        m0 = ensemble_models[0]
+        eng = x3.X3Model(m0.spec, [{k: v.to(m0.device) for k, v in m.store.as_dict().items()}
+                                    for m in ensemble_models], device=m0.device)
+        out = x3.forward_running(eng, m0._as_input(x_test_data))[:, 0].unsqueeze(-1)
+        out = out.cpu().numpy() if as_numpy else out
     elif ensemble_models and all(getattr(m, "uses_fused", lambda: False)() for m in ensemble_models):
         from ..ops import fused
 
@@ -113,8 +122,8 @@ def deep_ensembles_predict(ensemble_models: List, x_test_data, as_numpy: bool = 
         out = out.float().cpu().numpy() if as_numpy else out
     elif ensemble_models and all(getattr(m, "uses_hip", lambda: False)() for m in ensemble_models):
         m0 = ensemble_models[0]
-        x = m0._as_input(x_test_data).to(torch.bfloat16).contiguous()
-        out = torch.stack([m.hip_forward(x.to(m.device))[0].to(m0.device) for m in ensemble_models]).unsqueeze(-1)
+        x = m0._as_input(x_test_data)
+        out = torch.stack([m.hip_infer(x.to(m.device))[0].to(m0.device) for m in ensemble_models]).unsqueeze(-1)
         out = out.float().cpu().numpy() if as_numpy else out
     else:
         preds = [np.asarray(m.predict(x_test_data, verbose=0)) for m in ensemble_models]
