@@ -28,6 +28,8 @@ hipError_t launch_zero(int nb, void* const* ptrs, const long long* words, hipStr
 hipError_t launch_adam(float* p, const float* g, float* m, float* v, long long n, float b1, float b2, float alpha,
                        float eps, float gscale, const int* step_dev, hipStream_t stream);
 hipError_t train_bump_counters(int* c, int n, hipStream_t st);
+hipError_t train_stream_keys(unsigned* keys, const int* c, int n, unsigned long long seed, unsigned pass_base,
+                             hipStream_t st);
 hipError_t launch_generic_conv(const void* x, const void* wfrag, const float* epi, void* y, int n, int L, int cin,
                                int cout, int cout_pad, int ksize, int pool, int dropout, unsigned thr, int layer,
                                int n_win, unsigned pass_offset, unsigned window_offset, unsigned long long seed,
@@ -234,6 +236,18 @@ void bump_counters(at::Tensor& counters) {
               "bump_counters: int32 GPU tensor of <= 64 counters");
   const at::DeviceGuard guard(counters.device());
   check(apneauq::train_bump_counters(counters.data_ptr<int>(), (int)counters.numel(), cur_stream()), "bump_counters");
+}
+
+void stream_keys(at::Tensor& keys, const at::Tensor& counters, int64_t seed, int64_t pass_base) {
+  TORCH_CHECK(keys.is_cuda() && keys.scalar_type() == at::kInt && keys.is_contiguous() && keys.numel() <= 64,
+              "stream_keys: contiguous int32 GPU tensor of <= 64 keys");
+  TORCH_CHECK(counters.is_cuda() && counters.scalar_type() == at::kInt && counters.numel() >= 1 &&
+                  counters.device() == keys.device(), "stream_keys: int32 GPU counters on the keys' device");
+  const at::DeviceGuard guard(keys.device());
+  check(apneauq::train_stream_keys(reinterpret_cast<unsigned*>(keys.data_ptr<int>()), counters.data_ptr<int>(),
+                                   (int)keys.numel(), static_cast<unsigned long long>(seed),
+                                   static_cast<unsigned>(pass_base), cur_stream()),
+        "stream_keys");
 }
 
 // ctx: int64 CPU tensor of device pointers / scalars built once per workspace (ops/train_ops.py)
@@ -676,6 +690,7 @@ TORCH_LIBRARY(apneauq, m) {
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, float b1, float b2, float alpha, float eps, "
         "float gscale, Tensor? counters=None) -> ()");
   m.def("bump_counters(Tensor(a!) counters) -> ()");
+  m.def("stream_keys(Tensor(a!) keys, Tensor counters, int seed, int pass_base) -> ()");
   m.def("zero_buffers(Tensor(a!)[] ts) -> ()");
   m.def("generic_conv(Tensor x, Tensor wfrag, Tensor epi, int cout, int ksize, bool pool, bool dropout, int thr, "
         "int layer, int n_win, int pass_offset, int window_offset, int seed) -> Tensor");
@@ -704,6 +719,7 @@ TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
   m.impl("bootstrap_partial", &bootstrap_partial);
   m.impl("adam_step", &adam_step);
   m.impl("bump_counters", &bump_counters);
+  m.impl("stream_keys", &stream_keys);
   m.impl("zero_buffers", &zero_buffers);
   m.impl("train_pack", &train_pack);
   m.impl("generic_conv", &generic_conv);

@@ -1742,6 +1742,18 @@ hipError_t train_bump_counters(int* c, int n, hipStream_t st) {
   return hipGetLastError();
 }
 
+// Dropout stream keys of one training step computed on the device from the step counter c[0]
+// (keys[l] = stream_key(seed, l, pass_base + c[0])): a graph replay reads no host-written key array.
+__global__ void stream_keys_kernel(unsigned* keys, const int* c, int n, unsigned long long seed, unsigned pass_base) {
+  if (threadIdx.x < n) keys[threadIdx.x] = stream_key(seed, threadIdx.x, pass_base + (unsigned)c[0]);
+}
+
+hipError_t train_stream_keys(unsigned* keys, const int* c, int n, unsigned long long seed, unsigned pass_base,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(stream_keys_kernel, dim3(1), dim3(64), 0, st, keys, c, n, seed, pass_base);
+  return hipGetLastError();
+}
+
 static int cu_count() {
   static int n = 0;
   if (n == 0) {

@@ -64,6 +64,9 @@ typedef __attribute__((address_space(1))) const f16x8 gf16x8;
 #ifndef APNEAUQ_X3_ABL
 #define APNEAUQ_X3_ABL 0
 #endif
+#ifndef APNEAUQ_X3_PF  // loader waves: chunks of HBM loads in flight ahead of the LDS write (1 or 2)
+#define APNEAUQ_X3_PF 1
+#endif
 constexpr int kL = 60, kSR = 64, kHalo = 4;
 constexpr int kCK = 32;                              // input channels per staged chunk
 constexpr int kRowB = 160;                           // LDS row: hi 64 B | lo 64 B | pad 32 B
@@ -93,6 +96,27 @@ __device__ __forceinline__ f32x4 mfma(const f16x8& a, const f16x8& b, const f32x
   return r;
 #else
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+#endif
+}
+
+// Sum over the 16 lanes of each DPP row (lanes sharing lane >> 4) on the VALU: two quad permutes and
+// two row rotations, no LDS round trips (group16_sum's __shfl_xor lowers to ds_swizzle / ds_bpermute).
+#ifndef APNEAUQ_X3_DPP
+#define APNEAUQ_X3_DPP 0
+#endif
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+#if APNEAUQ_X3_DPP
+  v += dpp_f<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+  v += dpp_f<0x124>(v);  // row_ror 4
+  v += dpp_f<0x128>(v);  // row_ror 8
+  return v;
+#else
+  return group16_sum(v);
 #endif
 }
 
@@ -169,29 +193,34 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
   // channel quad q = i % 8) of every chunk
   const bool loader = LW > 0 && wave >= NWM;
   const bool stager = (LW > 0 ? loader : wave < SW) && (APNEAUQ_X3_ABL & 1) == 0;
-  f32x4 sv[kNU];
-  f32x4 sa, sb;  // BN affine (scale, shift) x 1/(1-p) of the thread's 4 channels
-  auto load_chunk = [&](int tile, int c) {
+  // staging register set: the chunk's 16-B units + the BN affine (scale, shift) x 1/(1-p) of the
+  // thread's 4 channels
+  struct Stage {
+    f32x4 v[kNU];
+    f32x4 a, b;
+  };
+  Stage s0;
+  auto load_chunk = [&](int tile, int c, Stage& R) {
     const int tid = opaque_tid() - kSBase, q = tid & 7;
     const int g = tile / tpg;
     const int w0 = (tile - g * tpg) * kS;
     const float* af = A.aff_in + (long long)g * A.aff_gstride + c * kCK + 4 * q;
-    sa = gld<f32x4>(af);
-    sb = gld<f32x4>(af + CIN);
+    R.a = gld<f32x4>(af);
+    R.b = gld<f32x4>(af + CIN);
 #pragma unroll
     for (int u = 0; u < kNU; ++u) {
       const int ri = (tid >> 3) + (kST / 8) * u;
-      sv[u] = f32x4{-0.f, -0.f, -0.f, -0.f};
+      R.v[u] = f32x4{-0.f, -0.f, -0.f, -0.f};
       if (ri < kValidRows) {
         const int s = ri / kL, t = ri - s * kL, w = w0 + s;
         if (w < A.n_win) {
           const long long si = A.in_shared ? w : (long long)g * A.n_win + w;
-          sv[u] = gld<f32x4>(A.in + (si * kL + t) * CIN + c * kCK + 4 * q);
+          R.v[u] = gld<f32x4>(A.in + (si * kL + t) * CIN + c * kCK + 4 * q);
         }
       }
     }
   };
-  auto store_chunk = [&](int tile, int c, char* buf) {
+  auto store_chunk = [&](int tile, int c, char* buf, const Stage& R) {
     const int tid = opaque_tid() - kSBase, q = tid & 7;
     const int g = tile / tpg;
     const int w0 = (tile - g * tpg) * kS;
@@ -202,7 +231,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
       const int ri = (tid >> 3) + (kST / 8) * u;
       if (ri >= kValidRows) continue;
       const int s = ri / kL, t = ri - s * kL, w = w0 + s;
-      const f32x4 v = sv[u];
+      const f32x4 v = R.v[u];
       bool keep[4];
       if (A.hash_in) {
         const unsigned k = sample_key(skey, A.window_offset + w);
@@ -222,7 +251,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
       for (int i = 0; i < 4; ++i) {
         const unsigned bits = __float_as_uint(v[i]);
         const bool k = valid && keep[i] && (bits >> 31) == 0u;
-        const float a = k ? __builtin_fmaf(__uint_as_float(bits & 0x7FFFFFFFu), sa[i], sb[i]) : 0.f;
+        const float a = k ? __builtin_fmaf(__uint_as_float(bits & 0x7FFFFFFFu), R.a[i], R.b[i]) : 0.f;
         hi[i] = (_Float16)a;
         lo[i] = (_Float16)(a - (float)hi[i]);
       }
@@ -377,8 +406,8 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
           if ((rt & 3) == 3) {  // the 4 row tiles of sample slot (rt0 + rt) / 4 are complete
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              k1[e] = group16_sum(k1[e]);
-              k0[e] = group16_sum(k0[e]);
+              k1[e] = row16_sum(k1[e]);
+              k0[e] = row16_sum(k0[e]);
             }
             const int wl = w0 + (rt0 + rt) / 4;
             if (m == 0 && wl < A.n_win) {
@@ -395,7 +424,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
       if (A.stats != nullptr) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float a = group16_sum(s1[e]), b = group16_sum(s2[e]);
+          const float a = row16_sum(s1[e]), b = row16_sum(s2[e]);
           if (m == 0) {
             atomicAdd(&st[co0 + e], (double)a);
             atomicAdd(&st[COUT + co0 + e], (double)b);
@@ -428,14 +457,18 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
     // Loader and MFMA waves run the same barrier sequence: one LDS barrier before the first chunk and
     // after every chunk, and the two of flush_stats at every group change and at the end.
     if (loader) {
+      // chunk j's HBM loads go to register set j & 1 and are issued PF iterations before its LDS
+      // write (PF = 2: two chunks in flight, the HBM latency hidden behind two chunk computes)
+      constexpr int PF = APNEAUQ_X3_PF;
+      Stage s1;
       if (stager) {
-        load_chunk(t_begin, 0);
-        store_chunk(t_begin, 0, smem);
+        load_chunk(t_begin, 0, s0);
+        store_chunk(t_begin, 0, smem, s0);
       }
       lds_barrier();
-      if (stager && total > 1) load_chunk(chunk_tile(1), 1 % NCH);
-#pragma unroll 1
-      for (int it = 0; it < total; ++it) {
+      if (stager && total > 1) load_chunk(chunk_tile(1), 1 % NCH, s1);
+      if (PF > 1 && stager && total > 2) load_chunk(chunk_tile(2), 2 % NCH, s0);
+      auto step = [&](int it, Stage& R) {
         const int tile = chunk_tile(it), c = it - (tile - t_begin) * NCH;
         if (c == 0) {
           const int g = tile / tpg;
@@ -445,9 +478,20 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
           }
         }
         // chunk it+1 into the buffer compute(it-1) read (every wave passed the barrier after it)
-        if (stager && it + 1 < total) store_chunk(chunk_tile(it + 1), (it + 1) % NCH, smem + ((it + 1) & 1) * kBufB);
+        if (stager && it + 1 < total) store_chunk(chunk_tile(it + 1), (it + 1) % NCH, smem + ((it + 1) & 1) * kBufB, R);
         lds_barrier();
-        if (stager && it + 2 < total) load_chunk(chunk_tile(it + 2), (it + 2) % NCH);
+        const int nx = it + 1 + PF;
+        if (stager && nx < total) load_chunk(chunk_tile(nx), nx % NCH, R);
+      };
+      if constexpr (PF > 1) {
+#pragma unroll 1
+        for (int it = 0; it < total; it += 2) {
+          step(it, s1);
+          if (it + 1 < total) step(it + 1, s0);
+        }
+      } else {
+#pragma unroll 1
+        for (int it = 0; it < total; ++it) step(it, s1);
       }
       flush_stats(g_cur);
       return;
@@ -474,11 +518,11 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
     return;
   }
   if (stager) {
-    load_chunk(t_begin, 0);
-    store_chunk(t_begin, 0, smem);
+    load_chunk(t_begin, 0, s0);
+    store_chunk(t_begin, 0, smem, s0);
   }
   lds_barrier();
-  if (stager && total > 1) load_chunk(chunk_tile(1), 1 % NCH);
+  if (stager && total > 1) load_chunk(chunk_tile(1), 1 % NCH, s0);
   load_a(wbase(t_begin), ah, al);
 #pragma unroll 1
   for (int it = 0; it < total; ++it) {
@@ -495,11 +539,11 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
     char* buf = smem + (it & 1) * kBufB;
     char* nbuf = smem + ((it + 1) & 1) * kBufB;
     compute_chunk(c, buf, wcur, wnxt, [&]() {
-      if (stager && it + 1 < total) store_chunk(chunk_tile(it + 1), (it + 1) % NCH, nbuf);
+      if (stager && it + 1 < total) store_chunk(chunk_tile(it + 1), (it + 1) % NCH, nbuf, s0);
     });
     if (c == NCH - 1) epilogue(tile);
     lds_barrier();
-    if (stager && it + 2 < total) load_chunk(chunk_tile(it + 2), (it + 2) % NCH);
+    if (stager && it + 2 < total) load_chunk(chunk_tile(it + 2), (it + 2) % NCH, s0);
   }
   flush_stats(g_cur);
 }

@@ -251,10 +251,12 @@ class GraphedGenericStep:
 
     Per step the generic path issues ~9 launches per block (conv, BN finalize, apply, two backward
     passes, finalize, bias sum, dgrad, wgrad) plus head, packing and Adam: ~60 launches for six
-    blocks, ~1 ms of host dispatch at batch 1024.  The dropout stream keys of the step are written to
-    a device array before each replay (the kernels read them through ``skey_dev``) and Adam's
-    bias-correction step comes from a device counter, so a replay is exactly the eager step.
-    Single device only (data-parallel steps all-reduce through torch.distributed)."""
+    blocks, ~1 ms of host dispatch at batch 1024.  Everything a step varies comes from device counters
+    ``[dropout step, Adam iterations]`` bumped by the graph's last node: its first node derives the
+    dropout stream keys from the step counter (``stream_keys``) and Adam's bias correction reads the
+    iteration counter, so a replay reads no host-written memory and is exactly the eager step.  The
+    host mirrors the counters and re-syncs them only when they were changed outside (an eager step,
+    a restore).  Single device only (data-parallel steps all-reduce through torch.distributed)."""
 
     def __init__(self, model, batch: int):
         self.model = model
@@ -265,23 +267,30 @@ class GraphedGenericStep:
         self.x_in = torch.zeros(self.batch, spec.input_length, spec.input_channels, device=dev)
         self.y_in = torch.zeros(self.batch, device=dev)
         self.keys = torch.zeros(len(spec.blocks), dtype=torch.int32, device=dev)
-        self.counters = torch.zeros(2, dtype=torch.int32, device=dev)  # [unused, Adam iterations]
+        self.counters = torch.zeros(2, dtype=torch.int32, device=dev)  # [dropout step, Adam iterations]
         model.optimizer._ensure(model.store.flat)
         from . import train_ops
 
         self.bound = train_ops.bound_key(model)
-        self._set_counters()
+        self._sync_counters()
         self.ws.pack(backward=True)  # allocates the fragment buffers outside the capture (no model change)
         from .train_ops import capture_graph
 
         self.graph = capture_graph(self._body, dev)
-        self._iters_dev = int(model.optimizer.iterations)
 
-    def _set_counters(self):
-        self.counters.copy_(torch.tensor([0, int(self.model.optimizer.iterations)], dtype=torch.int32))
+    def _state(self):
+        return (int(self.model._train_step_counter), int(self.model.optimizer.iterations))
+
+    def _sync_counters(self):
+        st = self._state()
+        self.counters.copy_(torch.tensor(st, dtype=torch.int32))
+        self._dev_state = st
 
     def _body(self):
         ws, n, m = self.ws, self.batch, self.model
+        seed = int(m.seed) & ((1 << 64) - 1)
+        _ext.ops().stream_keys(self.keys, self.counters, seed - (1 << 64) if seed >= (1 << 63) else seed,
+                               TRAIN_PASS_BASE)
         ws.load_input(self.x_in)
         _grads(m, ws, self.y_in, n, n, TRAIN_PASS_BASE, 0, None, keys_dev=self.keys)
         opt = m.optimizer
@@ -291,19 +300,14 @@ class GraphedGenericStep:
 
     def __call__(self, x: torch.Tensor, y: torch.Tensor):
         m = self.model
-        pass_id = TRAIN_PASS_BASE + m._train_step_counter
-        k = [rng.stream_key(m.seed, l, pass_id) for l in range(len(m.spec.blocks))]
-        self.keys.copy_(torch.tensor([v - (1 << 32) if v >= (1 << 31) else v for v in k], dtype=torch.int32))
-        if int(m.optimizer.iterations) != self._iters_dev:
-            self._set_counters()
+        if self._state() != self._dev_state:
+            self._sync_counters()
         self.x_in.copy_(x)
         self.y_in.copy_(y.reshape(-1))
         self.graph.replay()
         m.optimizer.iterations += 1
-        self._iters_dev = int(m.optimizer.iterations)
+        self._dev_state = (self._dev_state[0] + 1, self._dev_state[1] + 1)
         return self.ws.head_loss.double().sum(), self.ws.prob[: self.batch]
-
-    _iters_dev = -1
 
 
 def graph_train_step(model, x: torch.Tensor, y: torch.Tensor):

@@ -289,7 +289,8 @@ def capture_graph(body, dev):
         if was:
             gc.enable()
     torch.cuda.current_stream(dev).wait_stream(side)
-    torch.cuda.synchronize(dev)
+    if os.environ.get("APNEAUQ_CAPTURE_SYNC", "1") == "1":
+        torch.cuda.synchronize(dev)
     return graph
 
 
