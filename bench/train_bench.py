@@ -33,7 +33,10 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--seed", type=int, default=2025)
     ap.add_argument("--streams", type=int, default=3, help="HIP streams the members of one GPU round-robin over "
-                    "(3 + the default stream fit the 4 hardware queues HIP uses per process)")
+                    "(3 + the default stream fit the 4 hardware queues HIP uses per process; --mode streams)")
+    ap.add_argument("--mode", choices=["batched", "streams"], default="batched",
+                    help="batched: one member-batched HIP graph per step (ops/train_ops.py:GraphedEnsembleStep); "
+                         "streams: members' graphs overlapped on HIP streams")
     a = ap.parse_args(argv)
     from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel import launch
 
@@ -60,7 +63,17 @@ def main(argv=None):
     for s in streams:
         s.wait_stream(torch.cuda.current_stream(dev))
 
+    batched = a.mode == "batched" and len(models) > 1
+    if batched:
+        from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import train_ops
+
+        ens = train_ops.GraphedEnsembleStep(models, a.batch)
+        xs, ys = [x] * len(models), [y] * len(models)
+
     def step():
+        if batched:
+            ens(xs, ys)
+            return
         for i, mdl in enumerate(models):
             with torch.cuda.stream(streams[i % len(streams)]):
                 mdl.train_step(x, y, return_probs=True)
@@ -82,7 +95,8 @@ def main(argv=None):
                           "n_gpus": info.world, "members": a.members, "batch": a.batch, "steps": a.steps,
                           "ms_per_step_all_members": round(dt * 1e3 / a.steps, 3), "dtype": "bf16",
                           "data": "synthetic", "backend": info.backend, "devices": devices,
-                          "parallelism": f"ensemble-parallel over {info.world} GPU(s), {len(streams)} stream(s)/GPU"}))
+                          "parallelism": f"ensemble-parallel over {info.world} GPU(s), " +
+                          ("member-batched launches" if batched else f"{len(streams)} stream(s)/GPU")}))
     pdist.shutdown()
 
 

@@ -211,3 +211,57 @@ def test_bf16_hip_training_matches_fp32_training(monkeypatch):
     # best 0.9919 vs 0.9926, last 0.949 vs 0.936)
     assert abs(max(hh["val_auc"]) - max(ht["val_auc"])) < 0.01, (hh["val_auc"], ht["val_auc"])
     assert abs(hh["val_auc"][-1] - ht["val_auc"][-1]) < 0.05, (hh["val_auc"], ht["val_auc"])
+
+
+def test_member_batched_step_matches_single_graphs():
+    """GraphedEnsembleStep (one member-batched launch per layer for 3 members) follows each member's
+    own graphed step: same first-step losses, and (up to fp32 atomic summation order) same losses
+    and weights after 4 steps on member-specific batches; the host / device counters advance alike."""
+    _ext.require()
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import train_ops
+
+    g = torch.Generator().manual_seed(8)
+    x = torch.randn(3, 4, 64, 60, 4, generator=g).cuda()
+    y = (torch.rand(3, 4, 64, generator=g) < 0.4).float().cuda()
+    single = [AlarconCNN1D(seed=10 + i, device="cuda") for i in range(3)]
+    ls = [[float(m.train_step(x[i, s], y[i, s])) for s in range(4)] for i, m in enumerate(single)]
+    batched = [AlarconCNN1D(seed=10 + i, device="cuda") for i in range(3)]
+    st = train_ops.GraphedEnsembleStep(batched, 64)
+    lb = [[], [], []]
+    for s in range(4):
+        out = st([x[i, s] for i in range(3)], [y[i, s] for i in range(3)])
+        for i, (loss, p) in enumerate(out):
+            lb[i].append(float(loss))
+            assert p.shape == (64,) and bool(((p > 0) & (p < 1)).all())
+    for i in range(3):
+        assert (batched[i].optimizer.iterations, batched[i]._train_step_counter) == (4, 4)
+        assert abs(lb[i][0] - ls[i][0]) < 1e-4 * abs(ls[i][0])
+        np.testing.assert_allclose(lb[i], ls[i], rtol=5e-3, atol=1e-3)
+        w0 = AlarconCNN1D(seed=10 + i, device="cuda").store.flat
+        rel = ((batched[i].store.flat - single[i].store.flat).norm() / (single[i].store.flat - w0).norm()).item()
+        assert rel < 0.2, rel
+    # members stay independent: member 1 with another seed's weights differs from member 0
+    assert abs(lb[0][0] - lb[1][0]) > 1e-3
+
+
+def test_fit_concurrent_batched_matches_streams():
+    """fit_concurrent's member-batched mode (one GraphedEnsembleStep per round, tail batches and
+    members that stop early included) tracks the stream mode epoch by epoch."""
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.training.callbacks import EarlyStopping
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.training.trainer import fit_concurrent
+
+    _ext.require()
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(1100, 60, 4, generator=g)
+    y = (x[:, :, 0].mean(1) > 0).float()
+    hs = {}
+    for mode in (False, True):
+        ms = [AlarconCNN1D(seed=30 + i, device="cuda") for i in range(3)]
+        cbs = [[EarlyStopping(monitor="loss", patience=0, min_delta=10.0)] if i == 2 else [] for i in range(3)]
+        hs[mode] = fit_concurrent(ms, x, y, batched=mode, batch_size=256, epochs=3, verbose=0, shuffle=True,
+                                  callbacks=cbs)
+    for a, b in zip(hs[False], hs[True]):
+        la, lb = a.history["loss"], b.history["loss"]
+        assert len(la) == len(lb)
+        np.testing.assert_allclose(lb, la, rtol=2e-2)
+    assert len(hs[True][2].history["loss"]) < 3  # the early-stopped member left the batched rounds

@@ -63,7 +63,7 @@ hipError_t launch_adam(float* p, const float* g, float* m, float* v, long long n
 // Zero up to kZeroMax buffers in ONE launch (the training step clears its moment / gradient / loss
 // accumulators: four fill kernels, ~5 us per graph node each, became one).  Buffer y = blockIdx.y;
 // sizes in 4-byte words, 16-B stores where the buffer allows.
-constexpr int kZeroMax = 8;
+constexpr int kZeroMax = 64;  // 8 ensemble members x 5 accumulators in one member-batched step
 struct ZeroArgs {
   uint32_t* p[kZeroMax];
   long long words[kZeroMax];

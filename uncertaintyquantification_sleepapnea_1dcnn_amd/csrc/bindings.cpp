@@ -85,6 +85,8 @@ hipError_t train_launch_dgrad(const train::Args& A, int l, hipStream_t st);
 hipError_t train_launch_wgrad(const train::Args& A, int l, hipStream_t st);
 hipError_t train_launch_finalize(const train::Args& A, int update_moving, int grads, hipStream_t st);
 hipError_t train_launch_tab(const apneauq::train::Args& A, int mode, int l, hipStream_t st);
+hipError_t train_launch_mb(const train::Args& A0, const train::Args* Am, int M, int op, int layer, int flag,
+                           hipStream_t st);
 hipError_t train_launch_pack(const float* w, int k, int cin, int cout, void* fwd, void* dgr, hipStream_t st);
 }  // namespace apneauq
 
@@ -350,6 +352,42 @@ void train_call(const at::Tensor& ctx, int64_t op, int64_t layer, int64_t flag, 
     case 5: check(apneauq::train_launch_tab(A, (int)flag, (int)layer, s), "train param table"); break;
     default: TORCH_CHECK(false, "train_call: unknown op ", op);
   }
+}
+
+// Member-batched training (train_conv.hip train_launch_mb): the Args of M members' contexts in one device
+// array, validated to share every size / mode the launch geometry depends on.
+at::Tensor train_args_dev(const std::vector<at::Tensor>& ctxs, int64_t device) {
+  const int64_t M = (int64_t)ctxs.size();
+  TORCH_CHECK(M >= 1 && M <= 65535, "train_args_dev: 1..65535 member contexts");
+  std::vector<apneauq::train::Args> v;
+  v.reserve(M);
+  for (const auto& c : ctxs) v.push_back(args_from_ctx(c, -1));
+  const auto& a = v[0];
+  for (const auto& x : v) {
+    TORCH_CHECK(x.B == a.B && x.n_win == a.n_win && x.groups == 1 && x.st_groups == a.st_groups && x.det == nullptr &&
+                    !x.shared0 && (x.tab == nullptr) == (a.tab == nullptr) && x.wpart != nullptr &&
+                    (x.hpart == nullptr) == (a.hpart == nullptr) && x.pass_dev != nullptr,
+                "train_args_dev: member contexts must share batch size, stats groups and modes (atomic, device "
+                "counters, wgrad partials)");
+  }
+  auto cpu = at::empty({M * (int64_t)sizeof(apneauq::train::Args)}, at::TensorOptions().dtype(at::kByte));
+  std::memcpy(cpu.data_ptr(), v.data(), M * sizeof(apneauq::train::Args));
+  return cpu.to(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(device)));
+}
+
+void train_call_mb(const at::Tensor& args_dev, const at::Tensor& ctx0, int64_t M, int64_t op, int64_t layer, int64_t flag) {
+  TORCH_CHECK(args_dev.is_cuda() && args_dev.scalar_type() == at::kByte && args_dev.is_contiguous() &&
+                  args_dev.numel() == M * (int64_t)sizeof(apneauq::train::Args),
+              "train_call_mb: args_dev must hold M device Args (train_args_dev)");
+  const auto A0 = args_from_ctx(ctx0, -1);
+  TORCH_CHECK(op >= 0 && op <= 5, "train_call_mb: unknown op ", op);
+  TORCH_CHECK((op != 0 || (layer >= 0 && layer < 6)) && (op != 2 || (layer >= 1 && layer < 6)) &&
+                  (op != 3 || (layer >= 0 && layer < 6)),
+              "train_call_mb: bad layer");
+  const at::DeviceGuard guard(args_dev.device());
+  check(apneauq::train_launch_mb(A0, reinterpret_cast<const apneauq::train::Args*>(args_dev.data_ptr()), (int)M,
+                                 (int)op, (int)layer, (int)flag, cur_stream()),
+        "train_call_mb");
 }
 
 int64_t train_wgrad_part_size(int64_t B) { return apneauq::train_wgrad_part_floats((int)B); }
@@ -682,6 +720,8 @@ TORCH_LIBRARY(apneauq, m) {
   m.def("bootstrap_partial(Tensor metrics, Tensor y, Tensor? idx, int seed, int n_boot, int n_global, int lo) -> Tensor");
   m.def("fused_layout() -> int[]", &fused_layout);
   m.def("train_call(Tensor ctx, int op, int layer, int flag, int pass_base, int device) -> ()", &train_call);
+  m.def("train_args_dev(Tensor[] ctxs, int device) -> Tensor", &train_args_dev);
+  m.def("train_call_mb(Tensor args_dev, Tensor ctx0, int M, int op, int layer, int flag) -> ()", &train_call_mb);
   m.def("train_pack(Tensor w, int k, int cin, int cout, Tensor(a!) fwd, Tensor(b!) dgr) -> ()");
   m.def("train_wgrad_part_size(int B) -> int", &train_wgrad_part_size);
   m.def("train_det_size(int B) -> int", &train_det_size);

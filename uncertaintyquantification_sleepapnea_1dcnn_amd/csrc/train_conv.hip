@@ -117,6 +117,17 @@ __device__ __forceinline__ T gld(const void* p) {
   return *(const __attribute__((address_space(1))) T*)(p);
 }
 
+// Member-batched launches (MB = true): gridDim.z = members, each member's Args in a device array
+// (one per ensemble member: its own weights, activations, moments and gradients), read with scalar
+// loads; MB = false takes the launch's by-value Args.
+template <bool MB>
+__device__ __forceinline__ const Args& member_args(const Args& a, const Args* __restrict__ am) {
+  if constexpr (MB)
+    return am[blockIdx.z];
+  else
+    return a;
+}
+
 // R_l's sign bit = block l's dropout mask (set: dropped); |R_l| is the post-ReLU activation
 __device__ __forceinline__ bool bf_dropped(__bf16 v) { return (__builtin_bit_cast(unsigned short, v) & 0x8000u) != 0; }
 __device__ __forceinline__ float bf_abs(__bf16 v) {
@@ -790,8 +801,9 @@ __device__ __forceinline__ void atomic_channel_sums(double* dst, int co0, const 
 // ------------------------------------------------------------------------------------------------
 // Forward of block l:  R_l = relu(conv(A_{l-1}) + b), fwd sums of R_l per stats group.
 // ------------------------------------------------------------------------------------------------
-template <int l>
-__global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
+template <int l, bool MB>
+__global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A_, const Args* __restrict__ Am) {
+  const Args& A = member_args<MB>(A_, Am);
   constexpr int CIN = C[l], COUT = C[l + 1];
   using T = Tiling<COUT>;
   using CV = Conv<CIN, COUT, KS[l], T::WM, T::WN, l == 0>;
@@ -1004,7 +1016,9 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A) {
 // (one workgroup per block, launched after the six forward kernels; read by the head, dgrad and wgrad),
 // mode 1 = the backward rows of block l (not on the default step: the backward kernels sum bst[l]
 // themselves, 2 x 16 slots per channel, which measured cheaper than one more graph node per block).
-__global__ __launch_bounds__(256) void tab_kernel(Args A, int mode, int l) {
+template <bool MB>
+__global__ __launch_bounds__(256) void tab_kernel(Args A_, const Args* __restrict__ Am, int mode, int l) {
+  const Args& A = member_args<MB>(A_, Am);
   if (mode == 0)
     tab_write_fwd(A, blockIdx.x);
   else
@@ -1016,7 +1030,9 @@ __global__ __launch_bounds__(256) void tab_kernel(Args A, int mode, int l) {
 // dense gradients, and the backward sums of dY_6 (sum dY, sum dY * xhat) — one sample per wave,
 // each lane owning channels (lane, lane + 64).
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kThreads) void head_kernel(Args A, int backward) {
+template <bool MB>
+__global__ __launch_bounds__(kThreads) void head_kernel(Args A_, const Args* __restrict__ Am, int backward) {
+  const Args& A = member_args<MB>(A_, Am);
   // One sample per wave.  Lane (cw, ph) = (lane % 12, lane / 12), lanes 0..59: channels
   // [8cw, 8cw+8) of rows ph, ph+5, ..., ph+55 — twelve 16-B loads per lane, all in flight at once
   // (the previous per-channel/per-row scalar loop was load-latency bound: ~50 us at any batch size).
@@ -1195,8 +1211,9 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A, int backward) {
 // dgrad: prefetch the epilogue's R_{l-1} loads ahead of the conv on blocks 2-5 (block 6: registers)
 template <int l> struct DgPre { static constexpr bool v = l >= 1 && l <= 4; };
 
-template <int l>
-__global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A) {
+template <int l, bool MB>
+__global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A_, const Args* __restrict__ Am) {
+  const Args& A = member_args<MB>(A_, Am);
   constexpr int CIN = C[l + 1], COUT = C[l];  // conv^T: input = dZ_l channels, output = block l-1 channels
   using T = Tiling<COUT>;
   using CV = Conv<CIN, COUT, KS[l], T::WM, T::WN, false>;
@@ -1363,8 +1380,9 @@ template <> struct WgCfg<4> { static constexpr int CIB = 16, COB = 128, WCO = 4,
 template <> struct WgCfg<5> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = 512, U = 4, MINB = 2; };
 
 
-template <int l>
-__global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A) {
+template <int l, bool MB>
+__global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A_, const Args* __restrict__ Am) {
+  const Args& A = member_args<MB>(A_, Am);
   using W = WgCfg<l>;
   constexpr int CIN = C[l], COUT = C[l + 1], K = KS[l], PAD = (K - 1) / 2;
   constexpr bool FIRST = (l == 0);
@@ -1564,9 +1582,9 @@ struct TabBwd {  // backward rows of one block's parameter table entry (wgrad_re
   int cc;
   float inv_count;
 };
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int rgs, int kcc, int cout,
-                                                           float* __restrict__ gw, float* __restrict__ gb, int J,
-                                                           TabBwd tb) {
+__device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ part, int rgs, int kcc, int cout,
+                                                  float* __restrict__ gw, float* __restrict__ gb, int J,
+                                                  const TabBwd& tb) {
   __shared__ f32x4 red[256];
   if (blockIdx.y == 1) {  // the table's backward rows of the block the NEXT dgrad / wgrad read
     const int c = threadIdx.x;
@@ -1612,6 +1630,27 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   }
 }
 
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int rgs, int kcc, int cout,
+                                                           float* __restrict__ gw, float* __restrict__ gb, int J,
+                                                           TabBwd tb) {
+  wgrad_reduce_body(part, rgs, kcc, cout, gw, gb, J, tb);
+}
+
+// member-batched: member blockIdx.z's partial slots, gradients and table rows from its Args
+__global__ __launch_bounds__(256) void wgrad_reduce_mb_kernel(const Args* __restrict__ Am, int l, int rgs, int kcc,
+                                                              int cout, int J, int side) {
+  const Args& A = Am[blockIdx.z];
+  TabBwd tb = {};
+  if (side) {
+    tb.bst = A.L[l - 1].bst;
+    tb.cc = C[l];
+    tb.mdy = A.tab + ((l - 1) * kTabRows + kTabMdy) * 256;
+    tb.mdyx = A.tab + ((l - 1) * kTabRows + kTabMdyx) * 256;
+    tb.inv_count = A.inv_count;
+  }
+  wgrad_reduce_body(A.wpart, rgs, kcc, cout, A.L[l].gw, A.L[l].gb, J, tb);
+}
+
 // ------------------------------------------------------------------------------------------------
 // BN finalize: moving averages (Keras momentum update on batch moments) and dgamma / dbeta.
 // ------------------------------------------------------------------------------------------------
@@ -1652,7 +1691,9 @@ __global__ __launch_bounds__(256) void det_reduce_kernel(const float* __restrict
   }
 }
 
-__global__ void bn_finalize_kernel(Args A, int update_moving, int grads) {
+template <bool MB>
+__global__ void bn_finalize_kernel(Args A_, const Args* __restrict__ Am, int update_moving, int grads) {
+  const Args& A = member_args<MB>(A_, Am);
   const int l = blockIdx.x;
   const Layer& Ly = A.L[l];
   const int Cc = (l == 0) ? C[1] : (l == 1) ? C[2] : (l == 2) ? C[3] : (l == 3) ? C[4] : (l == 4) ? C[5] : C[6];
@@ -1793,49 +1834,60 @@ int train_det_floats(int B) {
   return std::max({fwd_grid(B) * 2 * 256, B * train::kHeadRec, tiles * 2 * 2 * 256});
 }
 
-hipError_t train_launch_fwd(const Args& A, int l, hipStream_t st) {
-  const int all_tiles = (A.B + 1) / 2;
-  const int ncu = cu_count();
-  if (A.det != nullptr) {  // deterministic training: single-team kernel, ordered moment reduction
-    if (A.groups != 1 || A.shared0) return hipErrorInvalidValue;
-    const int grid = fwd_grid(A.B);
-    switch (l) {
-      case 0: hipLaunchKernelGGL(train::fwd_kernel<0>, dim3(grid), dim3(256), lds_fwd(), st, A); break;
-      case 1: hipLaunchKernelGGL(train::fwd_kernel<1>, dim3(grid), dim3(256), lds_fwd(), st, A); break;
-      case 2: hipLaunchKernelGGL(train::fwd_kernel<2>, dim3(grid), dim3(256), lds_fwd(), st, A); break;
-      case 3: hipLaunchKernelGGL(train::fwd_kernel<3>, dim3(grid), dim3(256), lds_fwd(), st, A); break;
-      case 4: hipLaunchKernelGGL(train::fwd_kernel<4>, dim3(grid), dim3(256), lds_fwd(), st, A); break;
-      case 5: hipLaunchKernelGGL(train::fwd_kernel<5>, dim3(grid), dim3(256), lds_fwd(), st, A); break;
-      default: return hipErrorInvalidValue;
-    }
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    const int cc = train::C[l + 1];
-    return det_reduce(A.det, grid, 2 * cc, det_dst(A.L[l].st, 2 * cc, 1), st);
-  }
-  // persistent forward: at most 4 workgroups per CU-slot pair, each over a contiguous tile range
-  const int tiles = fwd_grid(A.B);
+// Kernel launches shared by the single-model path (MB = false: by-value Args, Am = nullptr, M = 1)
+// and the member-batched path (MB = true: gridDim.z = M members, Args from the device array Am).
+template <bool MB>
+static hipError_t fwd_launch(const Args& A, const Args* Am, int M, int l, int grid, hipStream_t st) {
+  const dim3 g(grid, 1, M);
   switch (l) {
-    case 0: hipLaunchKernelGGL(train::fwd_kernel<0>, dim3(tiles), dim3(256), lds_fwd(), st, A); break;
-    case 1: hipLaunchKernelGGL(train::fwd_kernel<1>, dim3(tiles), dim3(256), lds_fwd(), st, A); break;
-    case 2: hipLaunchKernelGGL(train::fwd_kernel<2>, dim3(tiles), dim3(256), lds_fwd(), st, A); break;
-    case 3: hipLaunchKernelGGL(train::fwd_kernel<3>, dim3(tiles), dim3(256), lds_fwd(), st, A); break;
-    case 4: hipLaunchKernelGGL(train::fwd_kernel<4>, dim3(tiles), dim3(256), lds_fwd(), st, A); break;
-    case 5: hipLaunchKernelGGL(train::fwd_kernel<5>, dim3(tiles), dim3(256), lds_fwd(), st, A); break;
+    case 0: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::fwd_kernel<0, MB>), g, dim3(256), lds_fwd(), st, A, Am); break;
+    case 1: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::fwd_kernel<1, MB>), g, dim3(256), lds_fwd(), st, A, Am); break;
+    case 2: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::fwd_kernel<2, MB>), g, dim3(256), lds_fwd(), st, A, Am); break;
+    case 3: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::fwd_kernel<3, MB>), g, dim3(256), lds_fwd(), st, A, Am); break;
+    case 4: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::fwd_kernel<4, MB>), g, dim3(256), lds_fwd(), st, A, Am); break;
+    case 5: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::fwd_kernel<5, MB>), g, dim3(256), lds_fwd(), st, A, Am); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
+template <bool MB>
+static hipError_t dgrad_launch(const Args& A, const Args* Am, int M, int l, hipStream_t st) {
+  const dim3 g((A.B + 1) / 2, 1, M);
+  switch (l) {
+    case 1: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::dgrad_kernel<1, MB>), g, dim3(256), lds_dgrad(), st, A, Am); break;
+    case 2: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::dgrad_kernel<2, MB>), g, dim3(256), lds_dgrad(), st, A, Am); break;
+    case 3: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::dgrad_kernel<3, MB>), g, dim3(256), lds_dgrad(), st, A, Am); break;
+    case 4: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::dgrad_kernel<4, MB>), g, dim3(256), lds_dgrad(), st, A, Am); break;
+    case 5: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::dgrad_kernel<5, MB>), g, dim3(256), lds_dgrad(), st, A, Am); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t train_launch_fwd(const Args& A, int l, hipStream_t st) {
+  const int grid = fwd_grid(A.B);
+  if (A.det != nullptr) {  // deterministic training: single-team kernel, ordered moment reduction
+    if (A.groups != 1 || A.shared0) return hipErrorInvalidValue;
+    const hipError_t e = fwd_launch<false>(A, nullptr, 1, l, grid, st);
+    if (e != hipSuccess) return e;
+    const int cc = train::C[l + 1];
+    return det_reduce(A.det, grid, 2 * cc, det_dst(A.L[l].st, 2 * cc, 1), st);
+  }
+  // persistent forward: each workgroup over a contiguous tile range
+  return fwd_launch<false>(A, nullptr, 1, l, grid, st);
+}
+
 hipError_t train_launch_tab(const Args& A, int mode, int l, hipStream_t st) {
   if (A.tab == nullptr) return hipSuccess;  // no table (multi-rank / deterministic / MC-Dropout ctx)
   if (l < 0 || l >= 6) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(train::tab_kernel, dim3(mode == 0 ? 6 : 1), dim3(256), 0, st, A, mode, l);
+  hipLaunchKernelGGL(train::tab_kernel<false>, dim3(mode == 0 ? 6 : 1), dim3(256), 0, st, A, nullptr, mode, l);
   return hipGetLastError();
 }
 
 hipError_t train_launch_head(const Args& A, int backward, hipStream_t st) {
-  hipLaunchKernelGGL(train::head_kernel, dim3((A.B + 3) / 4), dim3(256), (8 * train::C[6] + 2) * 4, st, A, backward);
+  hipLaunchKernelGGL(train::head_kernel<false>, dim3((A.B + 3) / 4), dim3(256), (8 * train::C[6] + 2) * 4, st, A, nullptr,
+                     backward);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess || !backward || A.det == nullptr) return e;
   constexpr int cc = train::C[6];  // per-sample records: loss, dlogit, dW, sum dY, sum dY xhat
@@ -1844,17 +1896,9 @@ hipError_t train_launch_head(const Args& A, int backward, hipStream_t st) {
 }
 
 hipError_t train_launch_dgrad(const Args& A, int l, hipStream_t st) {
-  const int tiles = (A.B + 1) / 2;
-  switch (l) {
-    case 1: hipLaunchKernelGGL(train::dgrad_kernel<1>, dim3(tiles), dim3(256), lds_dgrad(), st, A); break;
-    case 2: hipLaunchKernelGGL(train::dgrad_kernel<2>, dim3(tiles), dim3(256), lds_dgrad(), st, A); break;
-    case 3: hipLaunchKernelGGL(train::dgrad_kernel<3>, dim3(tiles), dim3(256), lds_dgrad(), st, A); break;
-    case 4: hipLaunchKernelGGL(train::dgrad_kernel<4>, dim3(tiles), dim3(256), lds_dgrad(), st, A); break;
-    case 5: hipLaunchKernelGGL(train::dgrad_kernel<5>, dim3(tiles), dim3(256), lds_dgrad(), st, A); break;
-    default: return hipErrorInvalidValue;
-  }
-  const hipError_t e = hipGetLastError();
+  const hipError_t e = dgrad_launch<false>(A, nullptr, 1, l, st);
   if (e != hipSuccess || A.det == nullptr) return e;
+  const int tiles = (A.B + 1) / 2;
   static constexpr int wm[6] = {0, train::Tiling<train::C[1]>::WM, train::Tiling<train::C[2]>::WM,
                                 train::Tiling<train::C[3]>::WM, train::Tiling<train::C[4]>::WM,
                                 train::Tiling<train::C[5]>::WM};
@@ -1879,13 +1923,14 @@ static long long wg_part_floats(int B) {
   return (long long)wg_rgs<l>(B) * (train::KS[l] * train::C[l] * train::C[l + 1] + train::C[l + 1]);
 }
 
-template <int l>
-static void wg_launch(const Args& A, hipStream_t st) {
+template <int l, bool MB>
+static void wg_launch(const Args& A, const Args* Am, int M, hipStream_t st) {
   using W = train::WgCfg<l>;
   const int nci = (l == 0) ? 1 : train::C[l] / W::CIB;
   const int nco = train::C[l + 1] / W::COB;
   const int rgs = wg_rgs<l>(A.B);
-  hipLaunchKernelGGL(train::wgrad_kernel<l>, dim3(nci * nco * rgs), dim3(256), lds_wgrad<l>(), st, A);
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(train::wgrad_kernel<l, MB>), dim3(nci * nco * rgs, 1, M), dim3(256), lds_wgrad<l>(),
+                     st, A, Am);
   if (A.wpart != nullptr) {
     const int kcc = train::KS[l] * train::C[l] * train::C[l + 1];
     const int s4 = (kcc + train::C[l + 1]) / 4;
@@ -1895,17 +1940,24 @@ static void wg_launch(const Args& A, hipStream_t st) {
     const int blocks = std::min(2048, (s4 * J + 255) / 256);
     // side job: block l-1's backward rows of the parameter table (bst[l-1] is complete after dgrad<l>,
     // which ran before this wgrad) for dgrad<l-1> / wgrad<l-1>
-    train::TabBwd tb = {};
     const bool side = A.tab != nullptr && l >= 1;
-    if (side) {
-      tb.bst = A.L[l - 1].bst;
-      tb.cc = train::C[l];
-      tb.mdy = A.tab + ((l - 1) * train::kTabRows + train::kTabMdy) * 256;
-      tb.mdyx = A.tab + ((l - 1) * train::kTabRows + train::kTabMdyx) * 256;
-      tb.inv_count = A.inv_count;
+    if constexpr (MB) {
+      hipLaunchKernelGGL(train::wgrad_reduce_mb_kernel, dim3(blocks, side ? 2 : 1, M), dim3(256), 0, st, Am, l, rgs,
+                         kcc, train::C[l + 1], J, side ? 1 : 0);
+    } else {
+      train::TabBwd tb = {};
+      if constexpr (l >= 1) {
+        if (side) {
+          tb.bst = A.L[l - 1].bst;
+          tb.cc = train::C[l];
+          tb.mdy = A.tab + ((l - 1) * train::kTabRows + train::kTabMdy) * 256;
+          tb.mdyx = A.tab + ((l - 1) * train::kTabRows + train::kTabMdyx) * 256;
+          tb.inv_count = A.inv_count;
+        }
+      }
+      hipLaunchKernelGGL(train::wgrad_reduce_kernel, dim3(blocks, side ? 2 : 1), dim3(256), 0, st, A.wpart, rgs, kcc,
+                         train::C[l + 1], A.L[l].gw, A.L[l].gb, J, tb);
     }
-    hipLaunchKernelGGL(train::wgrad_reduce_kernel, dim3(blocks, side ? 2 : 1), dim3(256), 0, st, A.wpart, rgs, kcc,
-                       train::C[l + 1], A.L[l].gw, A.L[l].gb, J, tb);
   }
 }
 
@@ -1914,22 +1966,51 @@ long long train_wgrad_part_floats(int B) {
                    wg_part_floats<4>(B), wg_part_floats<5>(B)});
 }
 
-hipError_t train_launch_wgrad(const Args& A, int l, hipStream_t st) {
+template <bool MB>
+static hipError_t wgrad_launch(const Args& A, const Args* Am, int M, int l, hipStream_t st) {
   switch (l) {
-    case 0: wg_launch<0>(A, st); break;
-    case 1: wg_launch<1>(A, st); break;
-    case 2: wg_launch<2>(A, st); break;
-    case 3: wg_launch<3>(A, st); break;
-    case 4: wg_launch<4>(A, st); break;
-    case 5: wg_launch<5>(A, st); break;
+    case 0: wg_launch<0, MB>(A, Am, M, st); break;
+    case 1: wg_launch<1, MB>(A, Am, M, st); break;
+    case 2: wg_launch<2, MB>(A, Am, M, st); break;
+    case 3: wg_launch<3, MB>(A, Am, M, st); break;
+    case 4: wg_launch<4, MB>(A, Am, M, st); break;
+    case 5: wg_launch<5, MB>(A, Am, M, st); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
+hipError_t train_launch_wgrad(const Args& A, int l, hipStream_t st) { return wgrad_launch<false>(A, nullptr, 1, l, st); }
+
 hipError_t train_launch_finalize(const Args& A, int update_moving, int grads, hipStream_t st) {
-  hipLaunchKernelGGL(train::bn_finalize_kernel, dim3(6), dim3(256), 0, st, A, update_moving, grads);
+  hipLaunchKernelGGL(train::bn_finalize_kernel<false>, dim3(6), dim3(256), 0, st, A, nullptr, update_moving, grads);
   return hipGetLastError();
+}
+
+// Member-batched training step ops (one launch for M ensemble members of identical batch size):
+// A0 = member 0's Args (host copy: sizes and flags, identical for every member), Am = the device array of
+// all M members' Args.  op: 0 fwd(layer) | 1 head(flag = backward) | 2 dgrad(layer) | 3 wgrad(layer)
+// | 4 finalize(layer = update_moving, flag = grads) | 5 forward rows of the parameter table.
+// Atomic-mode single-device training only (no deterministic partials, no shared block 1).
+hipError_t train_launch_mb(const Args& A0, const Args* Am, int M, int op, int layer, int flag, hipStream_t st) {
+  if (M < 1 || M > 65535 || Am == nullptr || A0.det != nullptr || A0.shared0 || A0.groups != 1) return hipErrorInvalidValue;
+  switch (op) {
+    case 0: return fwd_launch<true>(A0, Am, M, layer, fwd_grid(A0.B), st);
+    case 1:
+      hipLaunchKernelGGL(train::head_kernel<true>, dim3((A0.B + 3) / 4, 1, M), dim3(256), (8 * train::C[6] + 2) * 4, st, A0,
+                         Am, flag);
+      return hipGetLastError();
+    case 2: return dgrad_launch<true>(A0, Am, M, layer, st);
+    case 3: return wgrad_launch<true>(A0, Am, M, layer, st);
+    case 4:
+      hipLaunchKernelGGL(train::bn_finalize_kernel<true>, dim3(6, 1, M), dim3(256), 0, st, A0, Am, layer, flag);
+      return hipGetLastError();
+    case 5:
+      if (A0.tab == nullptr) return hipSuccess;
+      hipLaunchKernelGGL(train::tab_kernel<true>, dim3(6, 1, M), dim3(256), 0, st, A0, Am, 0, 0);
+      return hipGetLastError();
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t train_launch_pack(const float* w, int k, int cin, int cout, void* fwd, void* dgr, hipStream_t st) {

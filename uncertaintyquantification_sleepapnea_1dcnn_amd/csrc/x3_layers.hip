@@ -64,8 +64,8 @@ typedef __attribute__((address_space(1))) const f16x8 gf16x8;
 #ifndef APNEAUQ_X3_ABL
 #define APNEAUQ_X3_ABL 0
 #endif
-#ifndef APNEAUQ_X3_PF  // loader waves: chunks of HBM loads in flight ahead of the LDS write (1 or 2)
-#define APNEAUQ_X3_PF 1
+#ifndef APNEAUQ_X3_PF  // loader waves: chunks of HBM loads in flight ahead of the LDS write (1 or 2;
+#define APNEAUQ_X3_PF 1   // 2 measured neutral, profiles/x3_epilogue_ab_r3.md)
 #endif
 constexpr int kL = 60, kSR = 64, kHalo = 4;
 constexpr int kCK = 32;                              // input channels per staged chunk
@@ -101,8 +101,9 @@ __device__ __forceinline__ f32x4 mfma(const f16x8& a, const f16x8& b, const f32x
 
 // Sum over the 16 lanes of each DPP row (lanes sharing lane >> 4) on the VALU: two quad permutes and
 // two row rotations, no LDS round trips (group16_sum's __shfl_xor lowers to ds_swizzle / ds_bpermute).
+// Batch-BN MCD 225.3 -> 220.2 ms (profiles/x3_epilogue_ab_r3.md); APNEAUQ_X3_DPP=0: the shuffle sums.
 #ifndef APNEAUQ_X3_DPP
-#define APNEAUQ_X3_DPP 0
+#define APNEAUQ_X3_DPP 1
 #endif
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {

@@ -269,10 +269,14 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, syn
 def capture_graph(body, dev):
     """Capture ``body()`` (HIP launches only) as a graph on a side stream.
 
-    Two hazards handled here: a garbage collection during the capture can destroy an OLD graph,
-    which HIP refuses while a stream is capturing (abort); and the first replay of a freshly
-    instantiated graph was seen reading stale step inputs about once in 40 captures unless the
-    device is synchronised after the capture (tools/probes/generic_step1_keys.py)."""
+    A garbage collection during the capture can destroy an OLD graph, which HIP refuses while a stream
+    is capturing (abort), so collection is paused.  No device synchronisation after the capture: the
+    stale first-replay inputs once seen on the generic path (round 2: ~1 in 40 captures, hidden by a
+    post-capture synchronize) came with a per-step host-written dropout-key array; the step now
+    derives its keys on the device from its counters (``stream_keys``), and 40 + 40 fresh captures
+    of both training paths give step-1 losses identical to the eager step without the synchronize
+    (``tools/probes/capture_race.py``, ``profiles/capture_race_r3.txt``).  ``APNEAUQ_CAPTURE_SYNC=1``
+    restores it."""
     import gc
 
     graph = torch.cuda.CUDAGraph()
@@ -289,7 +293,7 @@ def capture_graph(body, dev):
         if was:
             gc.enable()
     torch.cuda.current_stream(dev).wait_stream(side)
-    if os.environ.get("APNEAUQ_CAPTURE_SYNC", "1") == "1":
+    if os.environ.get("APNEAUQ_CAPTURE_SYNC", "0") == "1":
         torch.cuda.synchronize(dev)
     return graph
 
@@ -392,6 +396,116 @@ def graph_train_step(model, x: torch.Tensor, y: torch.Tensor):
     if cur is None or not _same_bound(cur.bound, bound_key(model)) or cur.deterministic != DETERMINISTIC:
         g[n] = cur = GraphedTrainStep(model, n)
     return cur(x, y)
+
+
+class GraphedEnsembleStep:
+    """One optimizer step of M ensemble members (same architecture and batch size, one GPU) as ONE
+    captured HIP graph whose layer kernels are member-batched: every forward / head / dgrad / wgrad /
+    finalize launch covers all members (``gridDim.z = M``, each member's pointers from a device array
+    of kernel arguments, ``csrc/train_conv.hip:train_launch_mb``).  A batch-1024 step of this CNN is
+    ~500 workgroups per launch -- one round on 256 CUs with its memory phases exposed back to back --
+    so stacking the members in one launch fills the machine instead of overlapping them on streams
+    (``training/trainer.py:fit_concurrent``).  Per member the step is exactly
+    :class:`GraphedTrainStep`'s: own workspace, dropout step and Adam counters (bumped in the graph),
+    own weights and optimizer state; replaces the reference's sequential member loop
+    (``train_deep_ensemble_cnns.py:125-177``)."""
+
+    def __init__(self, models, batch: int):
+        self.models = list(models)
+        self.batch = n = int(batch)
+        M = len(self.models)
+        if M < 1:
+            raise ValueError("GraphedEnsembleStep needs at least one member")
+        dev = self.models[0].store.device
+        if any(m.store.device != dev for m in self.models):
+            raise ValueError("ensemble members must share one device")
+        self.ws, self.ctx, self.x_in, self.y_in = [], [], [], []
+        for m in self.models:
+            ws = TrainWorkspace(m, n)
+            self.ws.append(ws)
+            self.x_in.append(ws.x[HALO: HALO + SR * n].view(n, SR, ws.ch[0])[:, :60])
+            self.y_in.append(ws.y[:n])
+            self.ctx.append(ws.build_ctx(n, n, 1, 0, m.seed, True, 1.0 / (n * 60), 1.0 / n, device_counters=True,
+                                         table=True))
+            m.optimizer._ensure(m.store.flat)
+        self.args = _ext.ops().train_args_dev(self.ctx, dev.index or 0)
+        self.bound = [bound_key(m) for m in self.models]
+        self._sync_counters()
+        outs = []
+        self.graph = capture_graph(lambda: outs.extend(self._body()), dev)
+        self.loss_out = outs[:M]
+        self.probs_out = outs[M:]
+
+    def _state(self):
+        return [(int(m._train_step_counter), int(m.optimizer.iterations)) for m in self.models]
+
+    def _sync_counters(self):
+        st = self._state()
+        for ws, v in zip(self.ws, st):
+            ws.counters.copy_(torch.tensor(v, dtype=torch.int32))
+        self._dev_state = st
+
+    def _body(self):
+        o, M, n = _ext.ops(), len(self.models), self.batch
+        bufs = []
+        for ws in self.ws:
+            bufs += [ws.st_all, ws.bst_all, ws.grad, ws.loss, ws.hpart]
+        o.zero_buffers(bufs)
+        for ws in self.ws:
+            ws.pack()
+        a, c0 = self.args, self.ctx[0]
+        for l in range(6):
+            o.train_call_mb(a, c0, M, 0, l, 0)
+        o.train_call_mb(a, c0, M, 5, 0, 0)  # BN parameter tables (forward rows)
+        o.train_call_mb(a, c0, M, 1, 0, 1)  # head + dlogit + backward sums of block 6
+        for l in range(5, 0, -1):
+            o.train_call_mb(a, c0, M, 2, l, 0)
+            o.train_call_mb(a, c0, M, 3, l, 0)
+        o.train_call_mb(a, c0, M, 3, 0, 0)
+        o.train_call_mb(a, c0, M, 4, 1, 1)  # moving averages + dgamma / dbeta
+        for m, ws in zip(self.models, self.ws):
+            opt = m.optimizer
+            o.adam_step(m.store.flat, ws.grad, opt.m, opt.v, opt.beta_1, opt.beta_2, opt.learning_rate, opt.epsilon,
+                        1.0, ws.counters)
+            o.bump_counters(ws.counters)
+        return [ws.loss.view(()) for ws in self.ws] + [torch.sigmoid(ws.logits[:n]) for ws in self.ws]
+
+    def valid_for(self, models) -> bool:
+        return (len(models) == len(self.models) and all(a is b for a, b in zip(models, self.models)) and
+                all(_same_bound(b, bound_key(m)) for b, m in zip(self.bound, self.models)) and not DETERMINISTIC)
+
+    def __call__(self, xs, ys):
+        """One step of every member on its own batch (lists of (n, 60, 4) / (n,) device tensors);
+        returns per-member (loss_sum, probs) views of static buffers (valid until the next replay)."""
+        if self._state() != self._dev_state:
+            self._sync_counters()
+        for i in range(len(self.models)):
+            self.x_in[i].copy_(xs[i])
+            self.y_in[i].copy_(ys[i].reshape(-1))
+        self.graph.replay()
+        for m in self.models:
+            m.optimizer.iterations += 1
+            m._train_step_counter += 1
+            m.store.bump()
+        self._dev_state = [(a + 1, b + 1) for a, b in self._dev_state]
+        return list(zip(self.loss_out, self.probs_out))
+
+
+def ensemble_supported(models) -> bool:
+    """True when :class:`GraphedEnsembleStep` can batch these members: HIP backend on one GPU, the
+    reference architecture, single-device training (no data parallelism), atomic (non-deterministic)
+    mode and graph replay enabled."""
+    if not models or DETERMINISTIC or os.environ.get("APNEAUQ_TRAIN_GRAPH", "1") == "0":
+        return False
+    if os.environ.get("APNEAUQ_TRAIN_BACKEND", "auto") not in ("auto", "hip"):
+        return False
+    dev = models[0].device
+    if dev.type != "cuda":
+        return False
+    for m in models:
+        if m.device != dev or not supports(m.spec) or getattr(m, "dp", None) is not None:
+            return False
+    return True
 
 
 def _sync_slots(sync: Callable, st: torch.Tensor, used: int) -> None:

@@ -81,16 +81,18 @@ def fit(model, x, y, batch_size: int = 32, epochs: int = 1, verbose: int = 1, ca
             return stop.value
 
 
-def fit_concurrent(models: List, x, y, streams: Optional[List] = None, **fit_kwargs) -> List[History]:
+def fit_concurrent(models: List, x, y, streams: Optional[List] = None, batched: Optional[bool] = None,
+                   **fit_kwargs) -> List[History]:
     """Train several independent models (ensemble members sharing one GPU) at the same time.
 
-    Each model's :func:`fit_steps` runs on its own HIP stream and the host round-robins one
-    optimizer step per model, so the kernels of different members overlap on the device (a
-    batch-1024 step of this small CNN fills only part of the GPU: 8 members on 3 streams train
-    1.39-1.48x faster than back to back, ``profiles/multistream_train_r1.json``).  Every model keeps its own data
-    order, callbacks (EarlyStopping, BackupAndRestore) and epoch-end host synchronisation; results
-    are identical to sequential ``fit`` calls.  ``fit_kwargs`` as for :func:`fit`; per-model
-    ``callbacks`` may be given as a list of lists.
+    ``batched`` (default: whenever ``ops/train_ops.py:ensemble_supported``): every round, the live
+    members' next optimizer steps run as ONE member-batched HIP graph (``GraphedEnsembleStep``: each
+    layer kernel launched once for all members).  Otherwise each model's :func:`fit_steps` runs on
+    its own HIP stream and the host round-robins one optimizer step per model, so the kernels of
+    different members overlap on the device (``profiles/multistream_train_r1.json``).  Every model
+    keeps its own data order, callbacks (EarlyStopping, BackupAndRestore) and epoch-end host
+    synchronisation; results match sequential ``fit`` calls up to the summation order of fp32
+    atomics.  ``fit_kwargs`` as for :func:`fit`; per-model ``callbacks`` may be given as a list of lists.
     """
     import contextlib
 
@@ -98,6 +100,13 @@ def fit_concurrent(models: List, x, y, streams: Optional[List] = None, **fit_kwa
     per_cbs = cbs if (cbs and isinstance(cbs[0], (list, tuple))) else [cbs] * len(models)
     dev = models[0].device if models else torch.device("cpu")
     x, y = _to_device(x, dev), _to_device(y, dev)  # one device copy shared by every member
+    if batched is None:
+        from ..ops import train_ops
+
+        batched = len(models) > 1 and train_ops.ensemble_supported(models) and \
+            fit_kwargs.get("grad_allreduce") is None
+    if batched:
+        return _fit_batched(models, x, y, per_cbs, **fit_kwargs)
     if streams is None:
         # 3 streams + the default one fit HIP's 4 hardware queues per process (GPU_MAX_HW_QUEUES);
         # more streams share queues and measured no faster (profiles/multistream_train_r1.json)
@@ -128,10 +137,49 @@ def fit_concurrent(models: List, x, y, streams: Optional[List] = None, **fit_kwa
     return hist
 
 
+def _fit_batched(models: List, x, y, per_cbs, **fit_kwargs) -> List[History]:
+    """fit_concurrent's member-batched mode: the members' fit_steps generators hand their batches out
+    (``external_step``) and one GraphedEnsembleStep per (live member set, batch size) runs them."""
+    from ..ops import train_ops
+
+    gens = [fit_steps(m, x, y, callbacks=per_cbs[i], external_step=True, **fit_kwargs) for i, m in enumerate(models)]
+    hist: List[Optional[History]] = [None] * len(models)
+    req = {}
+    for i, g in enumerate(gens):
+        try:
+            req[i] = next(g)
+        except StopIteration as stop:
+            hist[i] = stop.value
+    steps = {}
+    while req:
+        live = sorted(req)
+        by_n = {}
+        for i in live:
+            by_n.setdefault(int(req[i][0].shape[0]), []).append(i)
+        for n, ids in by_n.items():
+            ms = [models[i] for i in ids]
+            key = (tuple(ids), n)
+            st = steps.get(key)
+            if st is None or not st.valid_for(ms):
+                st = steps[key] = train_ops.GraphedEnsembleStep(ms, n)
+            out = st([req[i][0] for i in ids], [req[i][1] for i in ids])
+            for i, res in zip(ids, out):
+                try:
+                    req[i] = gens[i].send(res)
+                except StopIteration as stop:
+                    hist[i] = stop.value
+                    del req[i]
+    return hist
+
+
 def fit_steps(model, x, y, batch_size: int = 32, epochs: int = 1, verbose: int = 1,
               callbacks: Optional[List[Callback]] = None, validation_split: float = 0.0, validation_data=None,
-              shuffle: bool = True, seed: Optional[int] = None, initial_epoch: int = 0, grad_allreduce=None):
-    """Generator form of :func:`fit`: yields after every optimizer step, returns the History."""
+              shuffle: bool = True, seed: Optional[int] = None, initial_epoch: int = 0, grad_allreduce=None,
+              external_step: bool = False):
+    """Generator form of :func:`fit`: yields after every optimizer step, returns the History.
+
+    ``external_step``: instead of calling ``model.train_step`` the generator yields ``(xb, yb)`` and
+    expects ``(loss_sum, probs)`` of that step to be sent back (member-batched ensemble training)."""
     dev = model.device
     X = _to_device(x, dev)
     Y = _to_device(y, dev)
@@ -177,13 +225,17 @@ def fit_steps(model, x, y, batch_size: int = 32, epochs: int = 1, verbose: int =
                 continue  # a tail batch smaller than the DP group is dropped on every rank
             idx, off = split_batch(gidx, dp)
             xb, yb = Xt.index_select(0, idx), Yt.index_select(0, idx)
-            loss_sum, p = model.train_step(xb, yb, return_probs=True, grad_allreduce=grad_allreduce,
-                                           dp_step=(int(gidx.numel()), off))
+            if external_step:
+                loss_sum, p = yield (xb, yb)
+            else:
+                loss_sum, p = model.train_step(xb, yb, return_probs=True, grad_allreduce=grad_allreduce,
+                                               dp_step=(int(gidx.numel()), off))
             loss_acc += loss_sum
             n_seen += int(gidx.numel())
             acc_m.update_state(yb, p)
             auc_m.update_state(yb, p)
-            yield
+            if not external_step:
+                yield
         if dp is not None and dp.size > 1:
             _sync_metrics(dp, loss_acc, acc_m, auc_m)
         loss_m.update(loss_acc.item(), n_seen)
