@@ -11,10 +11,9 @@
 
 namespace apneauq {
 
-__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
-                                                    float* __restrict__ m, float* __restrict__ v, long long n,
-                                                    float b1, float b2, float alpha, float eps, float gscale,
-                                                    const int* __restrict__ step_dev) {
+__device__ __forceinline__ void adam_body(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                          float* __restrict__ v, long long n, float b1, float b2, float alpha,
+                                          float eps, float gscale, const int* __restrict__ step_dev) {
   if (step_dev != nullptr) {  // HIP-graph replays: alpha_t from the device iteration counter (alpha = lr)
     const float t = (float)(*step_dev + 1);
     alpha = alpha * sqrtf(1.f - powf(b2, t)) / (1.f - powf(b1, t));
@@ -47,6 +46,53 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     m[t] = mm;
     v[t] = vv;
   }
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v, long long n,
+                                                    float b1, float b2, float alpha, float eps, float gscale,
+                                                    const int* __restrict__ step_dev) {
+  adam_body(p, g, m, v, n, b1, b2, alpha, eps, gscale, step_dev);
+}
+
+// Member-batched Adam (ensemble members of one architecture sharing the hyper-parameters): set
+// blockIdx.y = one member's (params, grads, moments, device iteration counter), one launch for all.
+constexpr int kAdamMaxSets = 16;
+struct AdamSets {
+  float* p[kAdamMaxSets];
+  const float* g[kAdamMaxSets];
+  float* m[kAdamMaxSets];
+  float* v[kAdamMaxSets];
+  const int* step[kAdamMaxSets];
+};
+
+__global__ __launch_bounds__(256) void adam_multi_kernel(AdamSets S, long long n, float b1, float b2, float alpha,
+                                                          float eps) {
+  const int i = blockIdx.y;
+  adam_body(S.p[i], S.g[i], S.m[i], S.v[i], n, b1, b2, alpha, eps, 1.f, S.step[i]);
+}
+
+int adam_max_sets() { return kAdamMaxSets; }
+
+hipError_t launch_adam_multi(int ns, float* const* p, const float* const* g, float* const* m, float* const* v,
+                             const int* const* step, long long n, float b1, float b2, float alpha, float eps,
+                             hipStream_t stream) {
+  if (ns < 1 || ns > kAdamMaxSets) return hipErrorInvalidValue;
+  if (n <= 0) return hipSuccess;
+  AdamSets S = {};
+  for (int i = 0; i < ns; ++i) {
+    S.p[i] = p[i];
+    S.g[i] = g[i];
+    S.m[i] = m[i];
+    S.v[i] = v[i];
+    S.step[i] = step[i];
+  }
+  long long blocks = ((n >> 2) + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)blocks, (unsigned)ns), dim3(256), 0, stream, S, n, b1, b2, alpha,
+                     eps);
+  return hipGetLastError();
 }
 
 hipError_t launch_adam(float* p, const float* g, float* m, float* v, long long n, float b1, float b2, float alpha,

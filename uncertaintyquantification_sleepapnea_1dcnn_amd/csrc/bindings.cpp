@@ -25,6 +25,10 @@ hipError_t launch_bootstrap_partial(const float* metrics, const int* y, const in
                                     int n_loc, int n_boot, double* out, hipStream_t stream);
 int zero_max_buffers();
 hipError_t launch_zero(int nb, void* const* ptrs, const long long* words, hipStream_t stream);
+int adam_max_sets();
+hipError_t launch_adam_multi(int ns, float* const* p, const float* const* g, float* const* m, float* const* v,
+                             const int* const* step, long long n, float b1, float b2, float alpha, float eps,
+                             hipStream_t stream);
 hipError_t launch_adam(float* p, const float* g, float* m, float* v, long long n, float b1, float b2, float alpha,
                        float eps, float gscale, const int* step_dev, hipStream_t stream);
 hipError_t train_bump_counters(int* c, int n, hipStream_t st);
@@ -213,6 +217,37 @@ void adam_step(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
                              p.numel(), (float)b1, (float)b2, (float)alpha, (float)eps, (float)gscale, step_dev,
                              cur_stream()),
         "adam_step");
+}
+
+// Adam over M members' flat buffers in one launch (same size and hyper-parameters; per-member device
+// iteration counters [pass, iterations] as in adam_step).
+void adam_step_multi(at::TensorList p, at::TensorList g, at::TensorList m, at::TensorList v, double b1, double b2,
+                     double alpha, double eps, at::TensorList counters) {
+  const int ns = (int)p.size();
+  TORCH_CHECK(ns >= 1 && ns <= apneauq::adam_max_sets() && (int)g.size() == ns && (int)m.size() == ns &&
+                  (int)v.size() == ns && (int)counters.size() == ns,
+              "adam_step_multi: 1..", apneauq::adam_max_sets(), " equally long lists");
+  std::vector<float*> pp(ns), mm(ns), vv(ns);
+  std::vector<const float*> gg(ns);
+  std::vector<const int*> st(ns);
+  const int64_t n = p[0].numel();
+  for (int i = 0; i < ns; ++i) {
+    for (const at::Tensor* t : {&p[i], &g[i], &m[i], &v[i]})
+      TORCH_CHECK(t->is_cuda() && t->device() == p[0].device() && t->scalar_type() == at::kFloat && t->is_contiguous() &&
+                      t->numel() == n && reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
+                  "adam_step_multi: contiguous, 16-B aligned fp32 GPU tensors of equal size on one device required");
+    TORCH_CHECK(counters[i].is_cuda() && counters[i].scalar_type() == at::kInt && counters[i].numel() >= 2,
+                "adam_step_multi: counters must be int32 GPU tensors [pass, iterations]");
+    pp[i] = p[i].data_ptr<float>();
+    gg[i] = g[i].data_ptr<float>();
+    mm[i] = m[i].data_ptr<float>();
+    vv[i] = v[i].data_ptr<float>();
+    st[i] = counters[i].data_ptr<int>() + 1;
+  }
+  const at::DeviceGuard guard(p[0].device());
+  check(apneauq::launch_adam_multi(ns, pp.data(), gg.data(), mm.data(), vv.data(), st.data(), n, (float)b1, (float)b2,
+                                   (float)alpha, (float)eps, cur_stream()),
+        "adam_step_multi");
 }
 
 // Zero several GPU buffers (4-byte multiples) in one launch.
@@ -729,6 +764,8 @@ TORCH_LIBRARY(apneauq, m) {
   m.def("prep_knn(Tensor X, int k) -> Tensor");
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, float b1, float b2, float alpha, float eps, "
         "float gscale, Tensor? counters=None) -> ()");
+  m.def("adam_step_multi(Tensor(a!)[] p, Tensor[] g, Tensor(b!)[] m, Tensor(c!)[] v, float b1, float b2, float alpha, "
+        "float eps, Tensor[] counters) -> ()");
   m.def("bump_counters(Tensor(a!) counters) -> ()");
   m.def("stream_keys(Tensor(a!) keys, Tensor counters, int seed, int pass_base) -> ()");
   m.def("zero_buffers(Tensor(a!)[] ts) -> ()");
@@ -758,6 +795,7 @@ TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
   m.impl("bootstrap", &bootstrap);
   m.impl("bootstrap_partial", &bootstrap_partial);
   m.impl("adam_step", &adam_step);
+  m.impl("adam_step_multi", &adam_step_multi);
   m.impl("bump_counters", &bump_counters);
   m.impl("stream_keys", &stream_keys);
   m.impl("zero_buffers", &zero_buffers);

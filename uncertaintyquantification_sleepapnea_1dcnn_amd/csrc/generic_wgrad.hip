@@ -299,7 +299,7 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs A) {
 // kk = tap*cin + ci, co = 16 ct + (lane & 15), and dgrad fragments of W'[tap'][co][ci] =
 // W[k-1-tap'][ci][co] (output channels ci padded to 16).  Zero outside the real ranges.
 // ---------------------------------------------------------------------------------------------
-constexpr int kMaxBlocks = 16;
+constexpr int kMaxBlocks = 48;  // 8 ensemble members x 6 blocks in one member-batched pack
 struct PackBlock {
   const float* w;
   __bf16* fwd;

@@ -117,13 +117,34 @@ __device__ __forceinline__ T gld(const void* p) {
   return *(const __attribute__((address_space(1))) T*)(p);
 }
 
-// Member-batched launches (MB = true): gridDim.z = members, each member's Args in a device array
-// (one per ensemble member: its own weights, activations, moments and gradients), read with scalar
-// loads; MB = false takes the launch's by-value Args.
+// Member-batched launches (MB = true): a (gx, 1, M) grid runs M ensemble members, each member's Args
+// (its own weights, activations, moments and gradients) in a device array read with scalar loads;
+// MB = false takes the launch's by-value Args.  Placement is XCD-aware: workgroups are dispatched
+// round-robin over the 8 XCDs in linear order, so when M divides 8 member m owns XCDs
+// [m * 8/M, (m+1) * 8/M) -- its weights and activations stay in those L2s instead of 8 members'
+// working sets thrashing every L2.  pos.bx is the member-local workgroup id (0 .. gx-1) the kernels
+// use in place of blockIdx.x, pos.nxcd the XCDs a member spans.
+struct MbPos {
+  int member, bx, nxcd;
+};
 template <bool MB>
-__device__ __forceinline__ const Args& member_args(const Args& a, const Args* __restrict__ am) {
+__device__ __forceinline__ MbPos mb_pos() {
+  if constexpr (!MB) {
+    return {0, (int)blockIdx.x, 8};
+  } else {
+    const int M = gridDim.z, gx = gridDim.x;
+    if (M <= 8 && (8 % M) == 0 && ((gx * M) & 7) == 0) {
+      const int lin = blockIdx.x + gx * blockIdx.z;  // dispatch order
+      const int xcd = lin & 7, per = 8 / M;
+      return {xcd / per, (lin >> 3) * per + xcd % per, per};
+    }
+    return {(int)blockIdx.z, (int)blockIdx.x, 8};
+  }
+}
+template <bool MB>
+__device__ __forceinline__ const Args& member_args(const Args& a, const Args* __restrict__ am, const MbPos& p) {
   if constexpr (MB)
-    return am[blockIdx.z];
+    return am[p.member];
   else
     return a;
 }
@@ -803,7 +824,8 @@ __device__ __forceinline__ void atomic_channel_sums(double* dst, int co0, const 
 // ------------------------------------------------------------------------------------------------
 template <int l, bool MB>
 __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A_, const Args* __restrict__ Am) {
-  const Args& A = member_args<MB>(A_, Am);
+  const MbPos pos = mb_pos<MB>();
+  const Args& A = member_args<MB>(A_, Am, pos);
   constexpr int CIN = C[l], COUT = C[l + 1];
   using T = Tiling<COUT>;
   using CV = Conv<CIN, COUT, KS[l], T::WM, T::WN, l == 0>;
@@ -822,12 +844,12 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A_, const Args* _
   // atomics, then fp64 global slots) only when the group changes.
   const int tiles = (A.B + 1) / 2;
   const int tpw = (tiles + gridDim.x - 1) / gridDim.x;
-  const int t_begin = blockIdx.x * tpw;
+  const int t_begin = pos.bx * tpw;
   const int t_end = min(tiles, t_begin + tpw);
   float* lstat = prm + 1024;  // [2][COUT]: sum r, sum r^2 of the current group run
   for (int c = threadIdx.x; c < 2 * COUT; c += kThreads) lstat[c] = 0.f;
   int gcur = -1;
-  double* st = Ly.st + (blockIdx.x % kStatSlots) * st_stride(A, COUT);
+  double* st = Ly.st + (pos.bx % kStatSlots) * st_stride(A, COUT);
   constexpr int CW = COUT / 8;             // 16-B chunks per output row
   constexpr int RPo = kThreads / CW;       // rows per copy-out pass
   // copy-out rows: the tile's 2 x 60 valid time steps only (the R buffers are allocated filled with
@@ -1007,7 +1029,7 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A_, const Args* _
   }
   flush();
   if (A.det != nullptr) {  // deterministic mode (one stats group): this workgroup's moment partials
-    float* dp = A.det + (long long)blockIdx.x * 2 * COUT;
+    float* dp = A.det + (long long)pos.bx * 2 * COUT;
     for (int c = threadIdx.x; c < 2 * COUT; c += kThreads) dp[c] = lstat[c];
   }
 }
@@ -1018,9 +1040,10 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A_, const Args* _
 // themselves, 2 x 16 slots per channel, which measured cheaper than one more graph node per block).
 template <bool MB>
 __global__ __launch_bounds__(256) void tab_kernel(Args A_, const Args* __restrict__ Am, int mode, int l) {
-  const Args& A = member_args<MB>(A_, Am);
+  const MbPos pos = mb_pos<MB>();
+  const Args& A = member_args<MB>(A_, Am, pos);
   if (mode == 0)
-    tab_write_fwd(A, blockIdx.x);
+    tab_write_fwd(A, pos.bx);
   else
     tab_write_bwd(A, l);
 }
@@ -1032,7 +1055,8 @@ __global__ __launch_bounds__(256) void tab_kernel(Args A_, const Args* __restric
 // ------------------------------------------------------------------------------------------------
 template <bool MB>
 __global__ __launch_bounds__(kThreads) void head_kernel(Args A_, const Args* __restrict__ Am, int backward) {
-  const Args& A = member_args<MB>(A_, Am);
+  const MbPos pos = mb_pos<MB>();
+  const Args& A = member_args<MB>(A_, Am, pos);
   // One sample per wave.  Lane (cw, ph) = (lane % 12, lane / 12), lanes 0..59: channels
   // [8cw, 8cw+8) of rows ph, ph+5, ..., ph+55 — twelve 16-B loads per lane, all in flight at once
   // (the previous per-channel/per-row scalar loop was load-latency bound: ~50 us at any batch size).
@@ -1045,10 +1069,10 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A_, const Args* __r
   float* bsum1 = bsum0 + Cc;
   float* red = bsum1 + Cc;      // per-workgroup loss / dense-bias sums: one global atomic per workgroup
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int n = blockIdx.x * 4 + wave;
+  const int n = pos.bx * 4 + wave;
   const Layer& Ly = A.L[5];
-  const int g_first = min(blockIdx.x * 4, A.B - 1) / A.n_win;
-  const int g_last = min(blockIdx.x * 4 + 3, A.B - 1) / A.n_win;
+  const int g_first = min(pos.bx * 4, A.B - 1) / A.n_win;
+  const int g_last = min(pos.bx * 4 + 3, A.B - 1) / A.n_win;
   for (int c = threadIdx.x; c < 3 * Cc + 2; c += kThreads) dw[c] = 0.f;
   auto params = [&](int g) {
     if (A.tab != nullptr) {  // single-device training (one group): the forward rows of T[5]
@@ -1182,7 +1206,7 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A_, const Args* __r
     }
     if (A.det != nullptr) return;  // det_reduce_kernel sums the per-sample records
     __syncthreads();
-    float* hp = A.hpart != nullptr ? A.hpart + (blockIdx.x % kStatSlots) * (Cc + 2) : nullptr;
+    float* hp = A.hpart != nullptr ? A.hpart + (pos.bx % kStatSlots) * (Cc + 2) : nullptr;
     for (int c = threadIdx.x; c < Cc; c += kThreads) {
       if (hp != nullptr) {  // slotted: summed by bn_finalize_kernel
         if (c == 0) {
@@ -1197,7 +1221,7 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A_, const Args* __r
         }
         atomicAdd(A.g_dense_w + c, dw[c]);
       }
-      double* bst = Ly.bst + (blockIdx.x % kStatSlots) * 2 * Cc;
+      double* bst = Ly.bst + (pos.bx % kStatSlots) * 2 * Cc;
       atomicAdd(bst + c, (double)bsum0[c]);
       atomicAdd(bst + Cc + c, (double)bsum1[c]);
     }
@@ -1213,7 +1237,8 @@ template <int l> struct DgPre { static constexpr bool v = l >= 1 && l <= 4; };
 
 template <int l, bool MB>
 __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A_, const Args* __restrict__ Am) {
-  const Args& A = member_args<MB>(A_, Am);
+  const MbPos pos = mb_pos<MB>();
+  const Args& A = member_args<MB>(A_, Am, pos);
   constexpr int CIN = C[l + 1], COUT = C[l];  // conv^T: input = dZ_l channels, output = block l-1 channels
   using T = Tiling<COUT>;
   using CV = Conv<CIN, COUT, KS[l], T::WM, T::WN, false>;
@@ -1228,7 +1253,7 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A_, const Args*
   float* mdyx = prm + 1024;
   float* mean_prev = prm + 1280;  // block l-1 mean / rstd for xhat
   float* rstd_prev = prm + 1536;
-  const int tile = blockIdx.x;
+  const int tile = pos.bx;
   APNEAUQ_DASSERT(2 * tile < A.B + 1 && blockDim.x == kThreads);
   const int row0 = kR * tile;
   const int smp0 = 2 * tile;
@@ -1341,7 +1366,7 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A_, const Args*
         }
       }
     } else {
-      double* bst = Lp.bst + (blockIdx.x % kStatSlots) * 2 * COUT;
+      double* bst = Lp.bst + (pos.bx % kStatSlots) * 2 * COUT;
       atomic_channel_sums(bst, co0, b0, m == 0);
       atomic_channel_sums(bst + COUT, co0, b1, m == 0);
     }
@@ -1382,7 +1407,8 @@ template <> struct WgCfg<5> { static constexpr int CIB = 32, COB = 96, WCO = 2, 
 
 template <int l, bool MB>
 __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A_, const Args* __restrict__ Am) {
-  const Args& A = member_args<MB>(A_, Am);
+  const MbPos pos = mb_pos<MB>();
+  const Args& A = member_args<MB>(A_, Am, pos);
   using W = WgCfg<l>;
   constexpr int CIN = C[l], COUT = C[l + 1], K = KS[l], PAD = (K - 1) / 2;
   constexpr bool FIRST = (l == 0);
@@ -1408,9 +1434,10 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A_
   // workgroups of one row group (which stage the same dZ / A rows) would land on 8 different L2s
   // and each re-read the rows from HBM.  Contiguous logical ids per XCD keep a row group's blocks
   // on one XCD, running together, so its rows come from HBM once (bijective for any grid size).
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xq = nwg / 8, xr = nwg % 8, xcd = bid % 8;
-  const int wg = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + bid / 8;
+  // (member-batched: the same remap over the XCDs the member spans)
+  const int nwg = gridDim.x, bid = pos.bx, nx = pos.nxcd;
+  const int xq = nwg / nx, xr = nwg % nx, xcd = bid % nx;
+  const int wg = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + bid / nx;
   const int blk = wg % (nci_blk * nco_blk);
   const int rg = wg / (nci_blk * nco_blk);
   const int ci0 = (blk % nci_blk) * W::CIB, co0 = (blk / nci_blk) * W::COB;
@@ -1584,11 +1611,11 @@ struct TabBwd {  // backward rows of one block's parameter table entry (wgrad_re
 };
 __device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ part, int rgs, int kcc, int cout,
                                                   float* __restrict__ gw, float* __restrict__ gb, int J,
-                                                  const TabBwd& tb) {
+                                                  const TabBwd& tb, int bx, int nbx, bool side_block) {
   __shared__ f32x4 red[256];
-  if (blockIdx.y == 1) {  // the table's backward rows of the block the NEXT dgrad / wgrad read
+  if (side_block) {  // the table's backward rows of the block the NEXT dgrad / wgrad read
     const int c = threadIdx.x;
-    if (blockIdx.x == 0 && c < tb.cc) {
+    if (c < tb.cc) {
       tb.mdy[c] = (float)(slot_sumd(tb.bst + c, 2 * tb.cc) * (double)tb.inv_count);
       tb.mdyx[c] = (float)(slot_sumd(tb.bst + tb.cc + c, 2 * tb.cc) * (double)tb.inv_count);
     }
@@ -1599,7 +1626,7 @@ __device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ part
   const int ncol = 256 / J;
   const int cl = threadIdx.x % ncol, j = threadIdx.x / ncol;
   const f32x4* p4 = reinterpret_cast<const f32x4*>(part);
-  for (int base = blockIdx.x * ncol; base < S4; base += gridDim.x * ncol) {  // workgroup-uniform
+  for (int base = bx * ncol; base < S4; base += nbx * ncol) {  // workgroup-uniform
     const int e4 = base + cl;
     f32x4 acc[8];
 #pragma unroll
@@ -1633,13 +1660,16 @@ __device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ part
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int rgs, int kcc, int cout,
                                                            float* __restrict__ gw, float* __restrict__ gb, int J,
                                                            TabBwd tb) {
-  wgrad_reduce_body(part, rgs, kcc, cout, gw, gb, J, tb);
+  if (blockIdx.y == 1 && blockIdx.x != 0) return;
+  wgrad_reduce_body(part, rgs, kcc, cout, gw, gb, J, tb, blockIdx.x, gridDim.x, blockIdx.y == 1);
 }
 
-// member-batched: member blockIdx.z's partial slots, gradients and table rows from its Args
+// member-batched: the member's partial slots (written by its wgrad on its XCDs), gradients and table
+// rows from its Args; with the table the last x-block of each member does the side job
 __global__ __launch_bounds__(256) void wgrad_reduce_mb_kernel(const Args* __restrict__ Am, int l, int rgs, int kcc,
                                                               int cout, int J, int side) {
-  const Args& A = Am[blockIdx.z];
+  const MbPos pos = mb_pos<true>();
+  const Args& A = Am[pos.member];
   TabBwd tb = {};
   if (side) {
     tb.bst = A.L[l - 1].bst;
@@ -1648,7 +1678,8 @@ __global__ __launch_bounds__(256) void wgrad_reduce_mb_kernel(const Args* __rest
     tb.mdyx = A.tab + ((l - 1) * kTabRows + kTabMdyx) * 256;
     tb.inv_count = A.inv_count;
   }
-  wgrad_reduce_body(A.wpart, rgs, kcc, cout, A.L[l].gw, A.L[l].gb, J, tb);
+  const int nbx = gridDim.x - (side ? 1 : 0);
+  wgrad_reduce_body(A.wpart, rgs, kcc, cout, A.L[l].gw, A.L[l].gb, J, tb, pos.bx, nbx, side && pos.bx == nbx);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1693,8 +1724,9 @@ __global__ __launch_bounds__(256) void det_reduce_kernel(const float* __restrict
 
 template <bool MB>
 __global__ void bn_finalize_kernel(Args A_, const Args* __restrict__ Am, int update_moving, int grads) {
-  const Args& A = member_args<MB>(A_, Am);
-  const int l = blockIdx.x;
+  const MbPos pos = mb_pos<MB>();
+  const Args& A = member_args<MB>(A_, Am, pos);
+  const int l = pos.bx;
   const Layer& Ly = A.L[l];
   const int Cc = (l == 0) ? C[1] : (l == 1) ? C[2] : (l == 2) ? C[3] : (l == 3) ? C[4] : (l == 4) ? C[5] : C[6];
   for (int c = threadIdx.x; c < Cc; c += blockDim.x) {
@@ -1907,14 +1939,15 @@ hipError_t train_launch_dgrad(const Args& A, int l, hipStream_t st) {
 }
 
 template <int l>
-static int wg_rgs(int B) {
+static int wg_rgs(int B, int M = 1) {
   using W = train::WgCfg<l>;
   const int nci = (l == 0) ? 1 : train::C[l] / W::CIB;
   const int nco = train::C[l + 1] / W::COB;
   const int tiles = (B + 1) / 2;
-  // RTILES row tiles per workgroup, but never fewer than ~MINWG workgroups while tiles remain
+  // RTILES row tiles per workgroup, but never fewer than ~MINWG workgroups (over all M members of a
+  // member-batched launch) while tiles remain
   const int nblk = nci * nco;
-  const int rt = std::max(1, std::min(W::RTILES, (tiles * nblk + W::MINWG - 1) / W::MINWG));
+  const int rt = std::max(1, std::min(W::RTILES, (tiles * M * nblk + W::MINWG - 1) / W::MINWG));
   return (tiles + rt - 1) / rt;
 }
 
@@ -1928,7 +1961,7 @@ static void wg_launch(const Args& A, const Args* Am, int M, hipStream_t st) {
   using W = train::WgCfg<l>;
   const int nci = (l == 0) ? 1 : train::C[l] / W::CIB;
   const int nco = train::C[l + 1] / W::COB;
-  const int rgs = wg_rgs<l>(A.B);
+  const int rgs = wg_rgs<l>(A.B, M);
   hipLaunchKernelGGL(HIP_KERNEL_NAME(train::wgrad_kernel<l, MB>), dim3(nci * nco * rgs, 1, M), dim3(256), lds_wgrad<l>(),
                      st, A, Am);
   if (A.wpart != nullptr) {
@@ -1942,8 +1975,8 @@ static void wg_launch(const Args& A, const Args* Am, int M, hipStream_t st) {
     // which ran before this wgrad) for dgrad<l-1> / wgrad<l-1>
     const bool side = A.tab != nullptr && l >= 1;
     if constexpr (MB) {
-      hipLaunchKernelGGL(train::wgrad_reduce_mb_kernel, dim3(blocks, side ? 2 : 1, M), dim3(256), 0, st, Am, l, rgs,
-                         kcc, train::C[l + 1], J, side ? 1 : 0);
+      hipLaunchKernelGGL(train::wgrad_reduce_mb_kernel, dim3(blocks + (side ? 1 : 0), 1, M), dim3(256), 0, st, Am, l,
+                         rgs, kcc, train::C[l + 1], J, side ? 1 : 0);
     } else {
       train::TabBwd tb = {};
       if constexpr (l >= 1) {

@@ -99,28 +99,6 @@ __device__ __forceinline__ f32x4 mfma(const f16x8& a, const f16x8& b, const f32x
 #endif
 }
 
-// Sum over the 16 lanes of each DPP row (lanes sharing lane >> 4) on the VALU: two quad permutes and
-// two row rotations, no LDS round trips (group16_sum's __shfl_xor lowers to ds_swizzle / ds_bpermute).
-// Batch-BN MCD 225.3 -> 220.2 ms (profiles/x3_epilogue_ab_r3.md); APNEAUQ_X3_DPP=0: the shuffle sums.
-#ifndef APNEAUQ_X3_DPP
-#define APNEAUQ_X3_DPP 1
-#endif
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float row16_sum(float v) {
-#if APNEAUQ_X3_DPP
-  v += dpp_f<0xB1>(v);   // quad_perm [1, 0, 3, 2]
-  v += dpp_f<0x4E>(v);   // quad_perm [2, 3, 0, 1]
-  v += dpp_f<0x124>(v);  // row_ror 4
-  v += dpp_f<0x128>(v);  // row_ror 8
-  return v;
-#else
-  return group16_sum(v);
-#endif
-}
-
 // LDS hazard barrier: orders LDS traffic only (global loads in flight stay in flight)
 __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -407,8 +385,8 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
           if ((rt & 3) == 3) {  // the 4 row tiles of sample slot (rt0 + rt) / 4 are complete
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              k1[e] = row16_sum(k1[e]);
-              k0[e] = row16_sum(k0[e]);
+              k1[e] = group16_sum(k1[e]);
+              k0[e] = group16_sum(k0[e]);
             }
             const int wl = w0 + (rt0 + rt) / 4;
             if (m == 0 && wl < A.n_win) {
@@ -425,7 +403,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
       if (A.stats != nullptr) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float a = row16_sum(s1[e]), b = row16_sum(s2[e]);
+          const float a = group16_sum(s1[e]), b = group16_sum(s2[e]);
           if (m == 0) {
             atomicAdd(&st[co0 + e], (double)a);
             atomicAdd(&st[COUT + co0 + e], (double)b);

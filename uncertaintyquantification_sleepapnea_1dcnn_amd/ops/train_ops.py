@@ -420,8 +420,11 @@ class GraphedEnsembleStep:
         if any(m.store.device != dev for m in self.models):
             raise ValueError("ensemble members must share one device")
         self.ws, self.ctx, self.x_in, self.y_in = [], [], [], []
-        for m in self.models:
+        # every member's device counters [dropout step, Adam iterations] are rows of one tensor: one bump
+        self.counters = torch.zeros(M, 2, dtype=torch.int32, device=dev)
+        for i, m in enumerate(self.models):
             ws = TrainWorkspace(m, n)
+            ws.counters = self.counters[i]
             self.ws.append(ws)
             self.x_in.append(ws.x[HALO: HALO + SR * n].view(n, SR, ws.ch[0])[:, :60])
             self.y_in.append(ws.y[:n])
@@ -441,8 +444,7 @@ class GraphedEnsembleStep:
 
     def _sync_counters(self):
         st = self._state()
-        for ws, v in zip(self.ws, st):
-            ws.counters.copy_(torch.tensor(v, dtype=torch.int32))
+        self.counters.copy_(torch.tensor(st, dtype=torch.int32))
         self._dev_state = st
 
     def _body(self):
@@ -451,8 +453,20 @@ class GraphedEnsembleStep:
         for ws in self.ws:
             bufs += [ws.st_all, ws.bst_all, ws.grad, ws.loss, ws.hpart]
         o.zero_buffers(bufs)
-        for ws in self.ws:
-            ws.pack()
+        # bf16 fragments of every member's six kernels: one launch (up to 8 members)
+        for g0 in range(0, M, 8):
+            grp = list(zip(self.models[g0:g0 + 8], self.ws[g0:g0 + 8]))
+            w, wf, wd, ks, ci, co = [], [], [], [], [], []
+            for m, ws in grp:
+                if not hasattr(ws, "_no_dgr"):
+                    ws._no_dgr = torch.empty(0, dtype=torch.bfloat16, device=ws.wf[0].device)
+                w += [m.store.views[f"conv1d_{l + 1}/kernel"] for l in range(6)]
+                wf += ws.wf
+                wd += [ws._no_dgr] + ws.wd[1:]
+                ks += ws.ks
+                ci += ws.ch[:6]
+                co += ws.ch[1:]
+            o.gt_pack(w, wf, wd, ks, ci, co)
         a, c0 = self.args, self.ctx[0]
         for l in range(6):
             o.train_call_mb(a, c0, M, 0, l, 0)
@@ -463,11 +477,19 @@ class GraphedEnsembleStep:
             o.train_call_mb(a, c0, M, 3, l, 0)
         o.train_call_mb(a, c0, M, 3, 0, 0)
         o.train_call_mb(a, c0, M, 4, 1, 1)  # moving averages + dgamma / dbeta
-        for m, ws in zip(self.models, self.ws):
-            opt = m.optimizer
-            o.adam_step(m.store.flat, ws.grad, opt.m, opt.v, opt.beta_1, opt.beta_2, opt.learning_rate, opt.epsilon,
-                        1.0, ws.counters)
-            o.bump_counters(ws.counters)
+        hyper = {(float(m.optimizer.learning_rate), float(m.optimizer.beta_1), float(m.optimizer.beta_2),
+                  float(m.optimizer.epsilon)) for m in self.models}
+        if len(hyper) == 1 and M <= 16:  # one Adam launch for all members
+            lr, b1, b2, eps = hyper.pop()
+            o.adam_step_multi([m.store.flat for m in self.models], [ws.grad for ws in self.ws],
+                              [m.optimizer.m for m in self.models], [m.optimizer.v for m in self.models], b1, b2, lr,
+                              eps, [ws.counters for ws in self.ws])
+        else:
+            for m, ws in zip(self.models, self.ws):
+                opt = m.optimizer
+                o.adam_step(m.store.flat, ws.grad, opt.m, opt.v, opt.beta_1, opt.beta_2, opt.learning_rate,
+                            opt.epsilon, 1.0, ws.counters)
+        o.bump_counters(self.counters.view(-1))
         return [ws.loss.view(()) for ws in self.ws] + [torch.sigmoid(ws.logits[:n]) for ws in self.ws]
 
     def valid_for(self, models) -> bool:
