@@ -1,0 +1,12 @@
+# full GPU check: smoke, GPU suite, headline bench, member-batched training bench
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp PYTHONPATH=/root/repo
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/s5_smoke.log 2>&1 || { echo SMOKE FAILED; tail -20 gpurun_out/s5_smoke.log; exit 1; }
+tail -1 gpurun_out/s5_smoke.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/s5_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/s5_tests.log
+[ $rc -eq 0 ] || { grep -E "FAILED|Error" gpurun_out/s5_tests.log | head; exit $rc; }
+timeout -k 10 400 python bench.py > gpurun_out/s5_bench.json 2> gpurun_out/s5_bench.err && cat gpurun_out/s5_bench.json &&
+timeout -k 10 200 python3 bench/train_bench.py --members 8 --steps 30 --mode batched &&
+timeout -k 10 200 python3 bench/train_micro.py --batch 1024 --steps 50

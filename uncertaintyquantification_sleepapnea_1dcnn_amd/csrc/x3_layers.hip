@@ -661,8 +661,17 @@ hipError_t launch_layer(const LayerArgs& A, int grid, hipStream_t stream) {
 #define APNEAUQ_X3_LW -1
 #endif
 #define APNEAUQ_X3_LOADERS(n) (APNEAUQ_X3_LW < 0 ? (n) : APNEAUQ_X3_LW)
+#ifndef APNEAUQ_X3_LW2  // probe: block 2's loader waves
+#define APNEAUQ_X3_LW2 0
+#endif
+#ifndef APNEAUQ_X3_B2S  // probe: block 2's samples per tile and wave rows
+#define APNEAUQ_X3_B2S 4
+#endif
+#ifndef APNEAUQ_X3_B2WM
+#define APNEAUQ_X3_B2WM 2
+#endif
 #define APNEAUQ_X3_LAYERS(X)                                    \
-  X(1, 128, 192, 5, 4, 2, 4, false, APNEAUQ_X3_LOADERS(0))      \
+  X(1, 128, 192, 5, APNEAUQ_X3_B2S, APNEAUQ_X3_B2WM, 4, false, APNEAUQ_X3_LOADERS(APNEAUQ_X3_LW2)) \
   X(2, 192, 224, 3, 2, 1, 7, false, APNEAUQ_X3_LOADERS(4))      \
   X(3, 224, 96, 7, 4, 4, 2, false, APNEAUQ_X3_LOADERS(4))       \
   X(4, 96, 256, 9, 2, 1, 8, false, APNEAUQ_X3_LOADERS(4))       \

@@ -9,9 +9,11 @@ Training replaces the reference's sequential member loop (``train_deep_ensemble_
 * **resume** at member granularity: a member whose checkpoint exists is skipped (the reference's
   skip-if-exists, ``:130-132``) — a killed job rerun retrains only the missing members; checkpoints
   are written atomically (tmp + rename) so a crash never leaves a half-written member;
-* **concurrent members**: the members one rank owns (``world < M``) train at the same time on
-  separate HIP streams (``training/trainer.py:fit_concurrent``; a batch-1024 step fills only part of
-  the GPU), then are saved in member order;
+* **concurrent members**: the members one rank owns (``world < M``) train at the same time
+  (``training/trainer.py:fit_concurrent``; a batch-1024 step fills only part of the GPU): each round
+  of optimizer steps is ONE member-batched HIP graph whose layer kernels cover all members
+  (``ops/train_ops.py:GraphedEnsembleStep``, XCD-aware member placement), or, where that does not
+  apply, the members' steps overlap on HIP streams; then they are saved in member order;
 * **resume** at epoch granularity inside a member (``epoch_backup``): a per-member
   ``BackupAndRestore`` file holds weights + Adam state + epoch, so a member killed mid-training
   continues from its last finished epoch (fault sites for tests: ``utils/faults.py``).
@@ -56,7 +58,8 @@ def train_ensemble(x_train, y_train, num_models: int = 5, seed_base: int = 2025,
                    patience: int = 5, validation_split: float = 0.1, verbose: int = 2, resume: bool = True,
                    device=None, input_shape: Optional[Sequence[int]] = None, epoch_backup: bool = True,
                    extra_callbacks: Optional[Sequence] = None, concurrent: Optional[bool] = None) -> List[str]:
-    """Train the members this rank owns; ``concurrent`` (default: on a GPU) overlaps them on streams."""
+    """Train the members this rank owns; ``concurrent`` (default: on a GPU) trains them together
+    (member-batched launches, or HIP streams)."""
     info = pdist.init()
     world, rank = info.world, info.rank
     groups = plan(num_models, world)
