@@ -146,7 +146,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
   constexpr long long FRAG_STEP = (long long)NCTA * 128;  // f16x8 per (chunk, tap) k-step
   static_assert(CIN % kCK == 0 && COUT % 16 == 0, "channel tiling");
   static_assert(NCTA % WN == 0 && (4 * S) % WM == 0, "wave tiling");
-  static_assert(!LAST || NRT % 4 == 0, "block 6: whole samples per wave row");
+  static_assert(NRT % 4 == 0, "whole 64-row sample slots per wave row (epilogue keys, block 6 sums)");
   double* st = reinterpret_cast<double*>(smem + 2 * kBufB);  // [2][COUT] per-workgroup moment sums
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -334,8 +334,15 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
     const float ws = A.wscale[A.p_gstride ? g : 0];
     const float* bias = A.bias + (long long)g * A.p_gstride;
     const bool drop = A.thr_out != 0u;
-    unsigned skey = 0;
-    if (drop) skey = stream_key(A.seed, A.layer, A.pass_base + g);
+    // a wave's row tiles cover whole 64-row sample slots (NRT % 4 == 0): the sample of row tile rt is
+    // wave-uniform, so its dropout key is computed once per sample (scalar ALU), not per (ct, rt, lane)
+    unsigned skeys[NRT / 4];
+    if (drop) {
+      const unsigned skey = stream_key(A.seed, A.layer, A.pass_base + g);
+#pragma unroll
+      for (int q = 0; q < NRT / 4; ++q)
+        skeys[q] = sample_key(skey, A.window_offset + w0 + (rt0 >> 2) + q);
+    }
     // channel-tile outer: only one tile's 4 channels of sums are live at a time
 #pragma unroll
     for (int ct = 0; ct < NCT; ++ct) {
@@ -344,8 +351,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
       f32x4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1, k1 = s1, k0 = s1;
 #pragma unroll
       for (int rt = 0; rt < NRT; ++rt) {
-        const int i = (rt0 + rt) * 16 + m;
-        const int s = i >> 6, t = i & 63, w = w0 + s;
+        const int s = (rt0 + rt) >> 2, t = (((rt0 + rt) & 3) << 4) + m, w = w0 + s;
         const bool valid = t < kL && w < A.n_win;
         f32x4 r;
 #pragma unroll
@@ -353,7 +359,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
         acc[ct][rt] = f32x4{0.f, 0.f, 0.f, 0.f};
         bool keep[4] = {true, true, true, true};
         if (drop) {
-          const unsigned key = sample_key(skey, A.window_offset + w);
+          const unsigned key = skeys[rt >> 2];
           const unsigned b01 = dropout_bits2(key, t, co0), b23 = dropout_bits2(key, t, co0 + 2);
           keep[0] = (b01 & 0xFFFFu) >= A.thr_out;
           keep[1] = (b01 >> 16) >= A.thr_out;

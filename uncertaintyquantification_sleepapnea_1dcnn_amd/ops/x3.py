@@ -168,8 +168,14 @@ def _mask_in() -> bool:
 
 
 def _max_samples(dev, per_sample: int, frac: float = 0.45) -> int:
+    """Samples (windows x passes / members) per layer launch: at most ``frac`` of the free HBM and at most
+    ``APNEAUQ_X3_WS_GB`` (default 24 GB) of activation workspace, so that the engine co-resides with
+    other work (a 50-pass chunk of 16384 windows would hold ~88 GB)."""
+    import os
+
     free = torch.cuda.mem_get_info(dev)[0]
-    return max(1, int(free * frac) // per_sample)
+    cap = float(os.environ.get("APNEAUQ_X3_WS_GB", "24")) * 2 ** 30
+    return max(1, int(min(free * frac, cap)) // per_sample)
 
 
 @torch.no_grad()
