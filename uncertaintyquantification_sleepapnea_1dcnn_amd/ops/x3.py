@@ -169,12 +169,14 @@ def _mask_in() -> bool:
 
 def _max_samples(dev, per_sample: int, frac: float = 0.45) -> int:
     """Samples (windows x passes / members) per layer launch: at most ``frac`` of the free HBM and at most
-    ``APNEAUQ_X3_WS_GB`` (default 24 GB) of activation workspace, so that the engine co-resides with
-    other work (a 50-pass chunk of 16384 windows would hold ~88 GB)."""
+    ``APNEAUQ_X3_WS_GB`` (default 16 GB) of activation workspace, so that the engine co-resides with
+    other work (one 50-pass chunk of 16384 windows would hold ~88 GB).  Batch-BN MC Dropout over 16384
+    windows, T = 50: 219.2-220.3 ms in one chunk (100 GB cap), 219.6-220.0 ms in 12-GB chunks
+    (``profiles/x3_epilogue_ab_r3.md``): pass chunks of >= 30 k samples keep the launches full."""
     import os
 
     free = torch.cuda.mem_get_info(dev)[0]
-    cap = float(os.environ.get("APNEAUQ_X3_WS_GB", "24")) * 2 ** 30
+    cap = float(os.environ.get("APNEAUQ_X3_WS_GB", "16")) * 2 ** 30
     return max(1, int(min(free * frac, cap)) // per_sample)
 
 
