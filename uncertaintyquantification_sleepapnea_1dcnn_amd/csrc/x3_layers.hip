@@ -68,12 +68,14 @@ typedef __attribute__((address_space(1))) const f16x8 gf16x8;
 #define APNEAUQ_X3_PF 1   // 2 measured neutral, profiles/x3_epilogue_ab_r3.md)
 #endif
 constexpr int kL = 60, kSR = 64, kHalo = 4;
-constexpr int kCK = 32;                              // input channels per staged chunk
-constexpr int kRowB = 160;                           // LDS row: hi 64 B | lo 64 B | pad 32 B
+// A chunk = CK input channels (32 or 64) of the tile's rows; LDS row: hi 2CK B | lo 2CK B | pad 32 B
+// (row stride 2 mod 4 16-B slots for either CK).  Layers with few taps take 64-channel chunks: twice the
+// k-steps per chunk barrier.
+__host__ __device__ constexpr int row_bytes(int ck) { return 4 * ck + 32; }
 // per tile of S samples (S x 64 GEMM rows): LDS rows, chunk-buffer bytes, staged rows, 16-B staging units
 __host__ __device__ constexpr int lds_rows(int S) { return kHalo + S * kSR + kHalo; }
-__host__ __device__ constexpr int buf_bytes(int S) { return lds_rows(S) * kRowB; }
-__host__ __device__ constexpr int lds_bytes(int S, int cout) { return 2 * buf_bytes(S) + 2 * cout * 8; }
+__host__ __device__ constexpr int buf_bytes(int S, int ck) { return lds_rows(S) * row_bytes(ck); }
+__host__ __device__ constexpr int lds_bytes(int S, int cout, int ck) { return 2 * buf_bytes(S, ck) + 2 * cout * 8; }
 
 // global-address-space load (keeps global_load_*, never flat_*)
 template <typename T>
@@ -121,19 +123,20 @@ __device__ __forceinline__ int xcd_wg() {
 // CU: the two chunk buffers leave no LDS for a second).
 template <int NW>
 constexpr int waves_per_eu() { return NW > 8 ? (NW + 3) / 4 : 2; }
-template <int CIN, int COUT, int KS, int S, int WM, int WN, bool LAST, int LW>
+template <int CIN, int COUT, int KS, int S, int WM, int WN, bool LAST, int LW, int CK>
 __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) void layer_kernel(const LayerArgs A) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NWM = WM * WN, NW = NWM + LW, kThreads = NW * 64;
-  constexpr int kS = S, kBufB = buf_bytes(S), kValidRows = S * kL, kUnits = kValidRows * (kCK / 4);
+  constexpr int kCK = CK, kRowB = row_bytes(CK), NQ = CK / 32, kQ = CK / 4;  // 32-ch sub-chunks, quads / row
+  constexpr int kS = S, kBufB = buf_bytes(S, CK), kValidRows = S * kL, kUnits = kValidRows * kQ;
   // staging waves: the LW loader waves, else MFMA waves 0..SW-1 (one per SIMD by default)
   constexpr int SW = LW > 0 ? LW : (APNEAUQ_X3_SW > 0 && APNEAUQ_X3_SW < NW) ? APNEAUQ_X3_SW : NW;
   constexpr int kSBase = LW > 0 ? NWM * 64 : 0;              // first staging thread
   constexpr int kST = SW * 64;                                // staging threads
   constexpr int kNU = (kUnits + kST - 1) / kST;              // 16-B staging units per staging thread
-  static_assert(kST % 8 == 0, "a staging thread keeps one channel quad");
+  static_assert(kST % kQ == 0 && (CK == 32 || CK == 64), "a staging thread keeps one channel quad");
   constexpr int NCH = CIN / kCK, NCTA = COUT / 16, NCT = NCTA / WN, NRT = 4 * S / WM, PAD = (KS - 1) / 2;
-  constexpr int NSTEP = NCH * KS;
+  constexpr int NSTEP = NCH * NQ * KS;  // k-steps (32 input channels x one tap) per tile
   // MFMA issue order: row tiles in groups of RG so that >= 4 accumulators rotate (dependent-issue
   // latency); B fragments double-buffered one group ahead when the accumulators leave room
   constexpr int RG = APNEAUQ_X3_RG > 0 ? APNEAUQ_X3_RG
@@ -180,7 +183,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
   };
   Stage s0;
   auto load_chunk = [&](int tile, int c, Stage& R) {
-    const int tid = opaque_tid() - kSBase, q = tid & 7;
+    const int tid = opaque_tid() - kSBase, q = tid % kQ;
     const int g = tile / tpg;
     const int w0 = (tile - g * tpg) * kS;
     const float* af = A.aff_in + (long long)g * A.aff_gstride + c * kCK + 4 * q;
@@ -188,7 +191,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
     R.b = gld<f32x4>(af + CIN);
 #pragma unroll
     for (int u = 0; u < kNU; ++u) {
-      const int ri = (tid >> 3) + (kST / 8) * u;
+      const int ri = tid / kQ + (kST / kQ) * u;
       R.v[u] = f32x4{-0.f, -0.f, -0.f, -0.f};
       if (ri < kValidRows) {
         const int s = ri / kL, t = ri - s * kL, w = w0 + s;
@@ -200,14 +203,14 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
     }
   };
   auto store_chunk = [&](int tile, int c, char* buf, const Stage& R) {
-    const int tid = opaque_tid() - kSBase, q = tid & 7;
+    const int tid = opaque_tid() - kSBase, q = tid % kQ;
     const int g = tile / tpg;
     const int w0 = (tile - g * tpg) * kS;
     unsigned skey = 0;
     if (A.hash_in) skey = stream_key(A.seed, A.layer - 1, A.pass_base + g);
 #pragma unroll
     for (int u = 0; u < kNU; ++u) {
-      const int ri = (tid >> 3) + (kST / 8) * u;
+      const int ri = tid / kQ + (kST / kQ) * u;
       if (ri >= kValidRows) continue;
       const int s = ri / kL, t = ri - s * kL, w = w0 + s;
       const f32x4 v = R.v[u];
@@ -236,7 +239,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
       }
       char* row = buf + (kHalo + s * kSR + t) * kRowB + 8 * q;
       *reinterpret_cast<f16x4*>(row) = hi;
-      *reinterpret_cast<f16x4*>(row + 64) = lo;
+      *reinterpret_cast<f16x4*>(row + 2 * kCK) = lo;
     }
   };
 
@@ -267,10 +270,11 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
   // waves write the NEXT chunk into the other LDS buffer there, so that VALU / LDS-write work overlaps
   // the partner wave's MFMAs instead of sitting between two barriers.
   auto compute_chunk = [&](int c, const char* buf, const gf16x8* wcur, const gf16x8* wnxt, auto&& hook) {
-    const char* bb = buf + bofs;
 #pragma unroll
-    for (int j = 0; j < KS; ++j) {
-      const int s = c * KS + j;
+    for (int kk = 0; kk < NQ * KS; ++kk) {
+      const int q2 = kk / KS, j = kk - q2 * KS;  // 32-channel sub-chunk, tap
+      const char* bb = buf + bofs + q2 * 64;
+      const int s = c * NQ * KS + kk;
       const gf16x8* np = (APNEAUQ_X3_ABL & 8) ? wcur : (s + 1 < NSTEP) ? wcur + (long long)(s + 1) * FRAG_STEP : wnxt;
       // all NCT weight fragments resident, the next k-step's issued first (a full tap of MFMAs hides its
       // L2 latency); B fragments double-buffered one row tile ahead when registers allow.  The
@@ -282,7 +286,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
       // accumulators, so a dependent MFMA follows its predecessor >= 4 issues later
       auto ldb = [&](int rt, f16x8& h_, f16x8& l_) {
         h_ = *reinterpret_cast<const f16x8*>(bb + (rt * 16 + j) * kRowB);
-        l_ = *reinterpret_cast<const f16x8*>(bb + (rt * 16 + j) * kRowB + 64);
+        l_ = *reinterpret_cast<const f16x8*>(bb + (rt * 16 + j) * kRowB + 2 * kCK);
       };
       f16x8 bh[RG], bl[RG];
 #pragma unroll
@@ -322,7 +326,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
         al[ct] = nl[ct];
       }
       __builtin_amdgcn_sched_barrier(0);
-      if (j == KS / 2) hook();
+      if (kk == (NQ * KS) / 2) hook();
     }
   };
 
@@ -640,10 +644,11 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs A) {
 }
 
 // ------------------------------------------------------------------------------- launch helpers
-template <int CIN, int COUT, int KS, int S, int WM, int WN, bool LAST, int LW>
+template <int CIN, int COUT, int KS, int S, int WM, int WN, bool LAST, int LW, int CK>
 hipError_t launch_layer(const LayerArgs& A, int grid, hipStream_t stream) {
-  constexpr int lds = lds_bytes(S, COUT);
-  auto k = layer_kernel<CIN, COUT, KS, S, WM, WN, LAST, LW>;
+  constexpr int lds = lds_bytes(S, COUT, CK);
+  static_assert(lds <= 160 * 1024, "LDS per workgroup");
+  auto k = layer_kernel<CIN, COUT, KS, S, WM, WN, LAST, LW, CK>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -676,23 +681,32 @@ hipError_t launch_layer(const LayerArgs& A, int grid, hipStream_t stream) {
 #ifndef APNEAUQ_X3_B2WM
 #define APNEAUQ_X3_B2WM 2
 #endif
-#define APNEAUQ_X3_LAYERS(X)                                    \
-  X(1, 128, 192, 5, APNEAUQ_X3_B2S, APNEAUQ_X3_B2WM, 4, false, APNEAUQ_X3_LOADERS(APNEAUQ_X3_LW2)) \
-  X(2, 192, 224, 3, 2, 1, 7, false, APNEAUQ_X3_LOADERS(4))      \
-  X(3, 224, 96, 7, 4, 4, 2, false, APNEAUQ_X3_LOADERS(4))       \
-  X(4, 96, 256, 9, 2, 1, 8, false, APNEAUQ_X3_LOADERS(4))       \
-  X(5, 256, 96, 9, 4, 4, 2, true, APNEAUQ_X3_LOADERS(4))
+#ifndef APNEAUQ_X3_CK2  // probes: input channels per staged chunk of blocks 2, 3, 6 (32 or 64)
+#define APNEAUQ_X3_CK2 32
+#endif
+#ifndef APNEAUQ_X3_CK3
+#define APNEAUQ_X3_CK3 64
+#endif
+#ifndef APNEAUQ_X3_CK6
+#define APNEAUQ_X3_CK6 64
+#endif
+#define APNEAUQ_X3_LAYERS(X)                                                                              \
+  X(1, 128, 192, 5, APNEAUQ_X3_B2S, APNEAUQ_X3_B2WM, 4, false, APNEAUQ_X3_LOADERS(APNEAUQ_X3_LW2), APNEAUQ_X3_CK2) \
+  X(2, 192, 224, 3, 2, 1, 7, false, APNEAUQ_X3_LOADERS(4), APNEAUQ_X3_CK3)                                 \
+  X(3, 224, 96, 7, 4, 4, 2, false, APNEAUQ_X3_LOADERS(4), 32)                                              \
+  X(4, 96, 256, 9, 2, 1, 8, false, APNEAUQ_X3_LOADERS(4), 32)                                              \
+  X(5, 256, 96, 9, 4, 4, 2, true, APNEAUQ_X3_LOADERS(4), APNEAUQ_X3_CK6)
 
 int x3_lds_bytes(int layer) {
-#define APNEAUQ_X3_LDS(L, CI, CO, K, S, WM, WN, LAST, LW) \
-  if (layer == L) return x3::lds_bytes(S, CO);
+#define APNEAUQ_X3_LDS(L, CI, CO, K, S, WM, WN, LAST, LW, CK) \
+  if (layer == L) return x3::lds_bytes(S, CO, CK);
   APNEAUQ_X3_LAYERS(APNEAUQ_X3_LDS)
 #undef APNEAUQ_X3_LDS
   return 0;
 }
 
 int x3_tile_samples(int layer) {
-#define APNEAUQ_X3_TS(L, CI, CO, K, S, WM, WN, LAST, LW) \
+#define APNEAUQ_X3_TS(L, CI, CO, K, S, WM, WN, LAST, LW, CK) \
   if (layer == L) return S;
   APNEAUQ_X3_LAYERS(APNEAUQ_X3_TS)
 #undef APNEAUQ_X3_TS
@@ -701,8 +715,8 @@ int x3_tile_samples(int layer) {
 
 hipError_t x3_launch_layer(int layer, const x3::LayerArgs& A, int grid, hipStream_t stream) {
   using namespace x3;
-#define APNEAUQ_X3_LAUNCH(L, CI, CO, K, S, WM, WN, LAST, LW) \
-  if (layer == L) return launch_layer<CI, CO, K, S, WM, WN, LAST, LW>(A, grid, stream);
+#define APNEAUQ_X3_LAUNCH(L, CI, CO, K, S, WM, WN, LAST, LW, CK) \
+  if (layer == L) return launch_layer<CI, CO, K, S, WM, WN, LAST, LW, CK>(A, grid, stream);
   APNEAUQ_X3_LAYERS(APNEAUQ_X3_LAUNCH)
 #undef APNEAUQ_X3_LAUNCH
   return hipErrorInvalidValue;
