@@ -153,6 +153,8 @@ def _fit_batched(models: List, x, y, per_cbs, **fit_kwargs) -> List[History]:
     steps = {}
     while req:
         live = sorted(req)
+        for key in [k for k in steps if not set(k[0]) <= set(live)]:  # a member finished: free its graphs
+            del steps[key]
         by_n = {}
         for i in live:
             by_n.setdefault(int(req[i][0].shape[0]), []).append(i)
