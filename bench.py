@@ -92,7 +92,24 @@ def main(argv=None):
         os.environ["CUDA_VISIBLE_DEVICES"] = ""
     else:
         os.environ.setdefault("APNEAUQ_FORCE_PG", "1")  # RCCL group even at world size 1 (same path as N=8)
+    # the driver reads ONE JSON line from stdout: everything else any library prints there (RCCL's
+    # version banner at communicator creation goes to fd 1 from C) is sent to stderr
+    sys.stdout.flush()
+    global _RESULT_FD
+    _RESULT_FD = os.dup(1)
+    os.dup2(2, 1)
     run(a)
+
+
+_RESULT_FD = None
+
+
+def _emit(line: str) -> None:
+    sys.stdout.flush()
+    if _RESULT_FD is None:
+        print(line, flush=True)
+    else:
+        os.write(_RESULT_FD, (line + "\n").encode())
 
 
 def run(a):
@@ -271,7 +288,7 @@ def run(a):
                 ("bf16" if head_prec == "fp32" else "fp32"): secondary,
             },
         }
-        print(json.dumps(out), flush=True)
+        _emit(json.dumps(out))
     pdist.shutdown()
 
 
