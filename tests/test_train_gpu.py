@@ -154,9 +154,9 @@ def test_graphed_training_step_matches_eager(monkeypatch):
 
 
 def test_fit_concurrent_on_streams_matches_sequential():
-    """Three members trained concurrently on HIP streams (training/trainer.py:fit_concurrent) track
-    back-to-back fits (atomics make the kernels order-nondeterministic, so loss histories are
-    compared to 2 %), and train_ensemble on one GPU uses the concurrent path."""
+    """Three members trained concurrently (training/trainer.py:fit_concurrent), on HIP streams and as
+    member-batched launches, track back-to-back fits (atomics make the kernels order-nondeterministic,
+    so loss histories are compared to 2 %), and train_ensemble on one GPU uses the concurrent path."""
     import os
     import tempfile
 
@@ -170,10 +170,11 @@ def test_fit_concurrent_on_streams_matches_sequential():
     kw = dict(epochs=3, batch_size=512, validation_split=0.1, verbose=0)
     seq = [AlarconCNN1D(seed=20 + i, device="cuda") for i in range(3)]
     h_seq = [m.fit(x, y, **kw) for m in seq]
-    con = [AlarconCNN1D(seed=20 + i, device="cuda") for i in range(3)]
-    h_con = fit_concurrent(con, x, y, **kw)
-    for hs, hc in zip(h_seq, h_con):
-        np.testing.assert_allclose(hc.history["loss"], hs.history["loss"], rtol=2e-2)
+    for batched in (False, True):
+        con = [AlarconCNN1D(seed=20 + i, device="cuda") for i in range(3)]
+        h_con = fit_concurrent(con, x, y, batched=batched, **kw)
+        for hs, hc in zip(h_seq, h_con):
+            np.testing.assert_allclose(hc.history["loss"], hs.history["loss"], rtol=2e-2)
     with tempfile.TemporaryDirectory() as d:
         paths = train_ensemble(x.numpy(), y.numpy(), num_models=3, save_dir=d, prefix="m", name_offset=0, epochs=2,
                                batch_size=512, verbose=0, epoch_backup=False)
