@@ -64,9 +64,6 @@ typedef __attribute__((address_space(1))) const f16x8 gf16x8;
 #ifndef APNEAUQ_X3_ABL
 #define APNEAUQ_X3_ABL 0
 #endif
-#ifndef APNEAUQ_X3_PF  // loader waves: chunks of HBM loads in flight ahead of the LDS write (1 or 2;
-#define APNEAUQ_X3_PF 1   // 2 measured neutral, profiles/x3_epilogue_ab_r3.md)
-#endif
 constexpr int kL = 60, kSR = 64, kHalo = 4;
 // A chunk = CK input channels (32 or 64) of the tile's rows; LDS row: hi 2CK B | lo 2CK B | pad 32 B
 // (row stride 2 mod 4 16-B slots for either CK).  Layers with few taps take 64-channel chunks: twice the
@@ -446,18 +443,16 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
     // Loader and MFMA waves run the same barrier sequence: one LDS barrier before the first chunk and
     // after every chunk, and the two of flush_stats at every group change and at the end.
     if (loader) {
-      // chunk j's HBM loads go to register set j & 1 and are issued PF iterations before its LDS
-      // write (PF = 2: two chunks in flight, the HBM latency hidden behind two chunk computes)
-      constexpr int PF = APNEAUQ_X3_PF;
-      Stage s1;
+      // chunk it+2's HBM loads are issued right after barrier(it) and land in registers during
+      // compute(it+1) (two chunks of loads in flight measured no faster: profiles/x3_epilogue_ab_r3.md)
       if (stager) {
         load_chunk(t_begin, 0, s0);
         store_chunk(t_begin, 0, smem, s0);
       }
       lds_barrier();
-      if (stager && total > 1) load_chunk(chunk_tile(1), 1 % NCH, s1);
-      if (PF > 1 && stager && total > 2) load_chunk(chunk_tile(2), 2 % NCH, s0);
-      auto step = [&](int it, Stage& R) {
+      if (stager && total > 1) load_chunk(chunk_tile(1), 1 % NCH, s0);
+#pragma unroll 1
+      for (int it = 0; it < total; ++it) {
         const int tile = chunk_tile(it), c = it - (tile - t_begin) * NCH;
         if (c == 0) {
           const int g = tile / tpg;
@@ -467,20 +462,9 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
           }
         }
         // chunk it+1 into the buffer compute(it-1) read (every wave passed the barrier after it)
-        if (stager && it + 1 < total) store_chunk(chunk_tile(it + 1), (it + 1) % NCH, smem + ((it + 1) & 1) * kBufB, R);
+        if (stager && it + 1 < total) store_chunk(chunk_tile(it + 1), (it + 1) % NCH, smem + ((it + 1) & 1) * kBufB, s0);
         lds_barrier();
-        const int nx = it + 1 + PF;
-        if (stager && nx < total) load_chunk(chunk_tile(nx), nx % NCH, R);
-      };
-      if constexpr (PF > 1) {
-#pragma unroll 1
-        for (int it = 0; it < total; it += 2) {
-          step(it, s1);
-          if (it + 1 < total) step(it + 1, s0);
-        }
-      } else {
-#pragma unroll 1
-        for (int it = 0; it < total; ++it) step(it, s1);
+        if (stager && it + 2 < total) load_chunk(chunk_tile(it + 2), (it + 2) % NCH, s0);
       }
       flush_stats(g_cur);
       return;
@@ -662,40 +646,25 @@ hipError_t launch_layer(const LayerArgs& A, int grid, hipStream_t stream) {
 }  // namespace x3
 
 // Layer table of the reference architecture (cnn_baseline_train.py:59-86), blocks 2..6:
-//   <Cin, Cout, k, samples per tile, wave rows WM, wave channel groups WN, block 6, loader waves LW>
+//   <Cin, Cout, k, samples per tile, wave rows WM, wave channel groups WN, block 6, loader waves LW,
+//    input channels per staged chunk CK>
 // Each MFMA wave owns (4 S / WM) 16-row tiles x (Cout / 16 / WN) 16-channel tiles; the 64-accumulator-tile
 // layers (Cout 224 / 256) run 2-sample tiles so that the next k-step's weight fragments and the B
 // double-buffer fit beside the accumulators without spilling.  Loader waves (ablation table in
 // profiles/x3_loader_waves.md) on every layer but block 2, whose 96-accumulator tile needs the 256-VGPR
-// budget of 8 waves.
+// budget of 8 waves (loaders at 2-sample tiles: slower; at 4: 99 VGPRs spilled).  64-channel chunks for
+// blocks 3 and 6 (block 2 would spill; Cin 224 / 96 are not multiples of 64).  Measurements:
+// profiles/x3_epilogue_ab_r3.md.
 #ifndef APNEAUQ_X3_LW  // probe: loader waves per layer (-1 = table)
 #define APNEAUQ_X3_LW -1
 #endif
 #define APNEAUQ_X3_LOADERS(n) (APNEAUQ_X3_LW < 0 ? (n) : APNEAUQ_X3_LW)
-#ifndef APNEAUQ_X3_LW2  // probe: block 2's loader waves
-#define APNEAUQ_X3_LW2 0
-#endif
-#ifndef APNEAUQ_X3_B2S  // probe: block 2's samples per tile and wave rows
-#define APNEAUQ_X3_B2S 4
-#endif
-#ifndef APNEAUQ_X3_B2WM
-#define APNEAUQ_X3_B2WM 2
-#endif
-#ifndef APNEAUQ_X3_CK2  // probes: input channels per staged chunk of blocks 2, 3, 6 (32 or 64)
-#define APNEAUQ_X3_CK2 32
-#endif
-#ifndef APNEAUQ_X3_CK3
-#define APNEAUQ_X3_CK3 64
-#endif
-#ifndef APNEAUQ_X3_CK6
-#define APNEAUQ_X3_CK6 64
-#endif
-#define APNEAUQ_X3_LAYERS(X)                                                                              \
-  X(1, 128, 192, 5, APNEAUQ_X3_B2S, APNEAUQ_X3_B2WM, 4, false, APNEAUQ_X3_LOADERS(APNEAUQ_X3_LW2), APNEAUQ_X3_CK2) \
-  X(2, 192, 224, 3, 2, 1, 7, false, APNEAUQ_X3_LOADERS(4), APNEAUQ_X3_CK3)                                 \
-  X(3, 224, 96, 7, 4, 4, 2, false, APNEAUQ_X3_LOADERS(4), 32)                                              \
-  X(4, 96, 256, 9, 2, 1, 8, false, APNEAUQ_X3_LOADERS(4), 32)                                              \
-  X(5, 256, 96, 9, 4, 4, 2, true, APNEAUQ_X3_LOADERS(4), APNEAUQ_X3_CK6)
+#define APNEAUQ_X3_LAYERS(X)                                    \
+  X(1, 128, 192, 5, 4, 2, 4, false, APNEAUQ_X3_LOADERS(0), 32)  \
+  X(2, 192, 224, 3, 2, 1, 7, false, APNEAUQ_X3_LOADERS(4), 64)  \
+  X(3, 224, 96, 7, 4, 4, 2, false, APNEAUQ_X3_LOADERS(4), 32)   \
+  X(4, 96, 256, 9, 2, 1, 8, false, APNEAUQ_X3_LOADERS(4), 32)   \
+  X(5, 256, 96, 9, 4, 4, 2, true, APNEAUQ_X3_LOADERS(4), 64)
 
 int x3_lds_bytes(int layer) {
 #define APNEAUQ_X3_LDS(L, CI, CO, K, S, WM, WN, LAST, LW, CK) \

@@ -159,14 +159,6 @@ def _sync_stats(sync: Callable, st: torch.Tensor, groups: int, c: int) -> None:
     v[:, 0].copy_(tot)
 
 
-def _mask_in() -> bool:
-    """Probe switch: draw every block's dropout mask in the consumer's staging (loader waves) instead of
-    the producer's epilogue."""
-    import os
-
-    return os.environ.get("APNEAUQ_X3_MASK_IN", "0") == "1"
-
-
 def _max_samples(dev, per_sample: int, frac: float = 0.45) -> int:
     """Samples (windows x passes / members) per layer launch: at most ``frac`` of the free HBM and at most
     ``APNEAUQ_X3_WS_GB`` (default 16 GB) of activation workspace, so that the engine co-resides with
@@ -221,7 +213,6 @@ def mcd_batch(model: X3Model, x: torch.Tensor, n_pass: int, seed: int, pass_base
     eps, mom = float(spec.bn_epsilon), float(spec.bn_momentum)
     seed = int(seed) & ((1 << 63) - 1)
     out = torch.empty(n_pass, n, dtype=torch.float32, device=model.device)
-    mi = _mask_in()
     # block 1 once: no dropout precedes it, so every pass sees the same R_1 and the same moments
     ws.stats[0].zero_()
     o.x3_l1(x, model.w1, model.b1, ws.r1, ws.stats[0], n, 1)
@@ -239,8 +230,8 @@ def mcd_batch(model: X3Model, x: torch.Tensor, n_pass: int, seed: int, pass_base
             src = ws.r1 if l == 1 else ws.buf[(l - 2) % 2]
             dst = ws.sums if l == 5 else ws.buf[(l - 1) % 2]
             o.x3_layer(l, src, dst, model.wfrag[l], 0, model.bias[l], model.wscale[l], 0, ws.aff[l - 1],
-                       0 if l == 1 else 2 * CH[l], st, n, tc, l == 1, l == 1 or mi, thr[l - 1],
-                       thr[l] if (l == 5 or not mi) else 0, seed, pb, int(window_offset), 0)
+                       0 if l == 1 else 2 * CH[l], st, n, tc, l == 1, l == 1, thr[l - 1], thr[l], seed, pb,
+                       int(window_offset), 0)
             if sync is not None:
                 _sync_stats(sync, st, tc, c)
             g, b, mm, mv = model.bn[l]
@@ -273,7 +264,6 @@ def _mcd_batch_windowed(model: X3Model, x: torch.Tensor, n_pass: int, seed: int,
     eps, mom = float(spec.bn_epsilon), float(spec.bn_momentum)
     seed = int(seed) & ((1 << 63) - 1)
     out = torch.empty(n_pass, n, dtype=torch.float32, device=model.device)
-    mi = _mask_in()
 
     def run(s: int, e: int, upto: int, pb: int, stats_layer: int) -> None:
         """Blocks 1..upto+1 over windows [s, e) of pass pb; moments of block stats_layer+1 into its slots."""
@@ -284,8 +274,7 @@ def _mcd_batch_windowed(model: X3Model, x: torch.Tensor, n_pass: int, seed: int,
             dst = ws.sums if l == 5 else ws.buf[(l - 1) % 2]
             o.x3_layer(l, src, dst, model.wfrag[l], 0, model.bias[l], model.wscale[l], 0, ws.aff[l - 1],
                        0 if l == 1 else 2 * CH[l], ws.stats[l] if l == stats_layer else None, m, 1, l == 1,
-                       l == 1 or mi, thr[l - 1], thr[l] if (l == 5 or not mi) else 0, seed, pb,
-                       int(window_offset) + s, 0)
+                       l == 1, thr[l - 1], thr[l], seed, pb, int(window_offset) + s, 0)
 
     def finish_layer(l: int, repeat: int) -> None:
         if sync is not None:
@@ -351,7 +340,6 @@ def _forward_running(model: X3Model, x: torch.Tensor, n_pass: int, dropout: bool
     dsc = [_dsc(b.dropout) if dropout else 1.0 for b in spec.blocks]
     eps, mom = float(spec.bn_epsilon), float(spec.bn_momentum)
     seed = int(seed) & ((1 << 63) - 1)
-    mi = _mask_in()
     # BN affine of the moving statistics, per member (shared by all passes with dropout)
     for l in range(6):
         g, b, mm, mv = model.bn[l]
@@ -365,8 +353,8 @@ def _forward_running(model: X3Model, x: torch.Tensor, n_pass: int, dropout: bool
         wstride = model.wfrag[l].shape[1] // 8 if per_member else 0
         o.x3_layer(l, src, dst, model.wfrag[l], wstride, model.bias[l], model.wscale[l],
                    CH[l + 1] if per_member else 0, ws.aff[l - 1], 2 * CH[l] if per_member else 0, None, n, groups,
-                   dropout and l == 1, dropout and (l == 1 or mi), thr[l - 1], thr[l] if (l == 5 or not mi) else 0,
-                   seed, int(pass_offset), int(window_offset), 0)
+                   dropout and l == 1, dropout and l == 1, thr[l - 1], thr[l], seed, int(pass_offset),
+                   int(window_offset), 0)
     o.x3_head(ws.sums, ws.aff[5], 2 * CH[6] if per_member else 0, model.dw, model.db, CH[6] if per_member else 0,
               ws.out, n, groups, bool(logits))
     return ws.out[: groups * n].view(G, n_pass, n).clone()
