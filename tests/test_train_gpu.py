@@ -266,3 +266,22 @@ def test_fit_concurrent_batched_matches_streams():
         assert len(la) == len(lb)
         np.testing.assert_allclose(lb, la, rtol=2e-2)
     assert len(hs[True][2].history["loss"]) < 3  # the early-stopped member left the batched rounds
+
+
+def test_member_batched_step_many_members():
+    """17 members (beyond one zero / Adam launch; no XCD-aligned placement): every member's first-step
+    loss equals its own graphed single-model step."""
+    _ext.require()
+    g = torch.Generator().manual_seed(9)
+    M = 17
+    x = torch.randn(M, 32, 60, 4, generator=g).cuda()
+    y = (torch.rand(M, 32, generator=g) < 0.5).float().cuda()
+    ref = [float(AlarconCNN1D(seed=40 + i, device="cuda").train_step(x[i], y[i])) for i in (0, 8, 16)]
+    ms = [AlarconCNN1D(seed=40 + i, device="cuda") for i in range(M)]
+    st = train_ops.GraphedEnsembleStep(ms, 32)
+    out = st([x[i] for i in range(M)], [y[i] for i in range(M)])
+    got = [float(out[i][0]) for i in (0, 8, 16)]
+    np.testing.assert_allclose(got, ref, rtol=1e-4)
+    out = st([x[i] for i in range(M)], [y[i] for i in range(M)])
+    assert all(m.optimizer.iterations == 2 and m._train_step_counter == 2 for m in ms)
+    assert all(np.isfinite(float(o[0])) for o in out)

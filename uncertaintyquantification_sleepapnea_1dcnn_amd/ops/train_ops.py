@@ -452,7 +452,9 @@ class GraphedEnsembleStep:
         bufs = []
         for ws in self.ws:
             bufs += [ws.st_all, ws.bst_all, ws.grad, ws.loss, ws.hpart]
-        o.zero_buffers(bufs)
+        zmax = 60  # csrc/adam.hip kZeroMax = 64 buffers per launch
+        for b0 in range(0, len(bufs), zmax):
+            o.zero_buffers(bufs[b0:b0 + zmax])
         # bf16 fragments of every member's six kernels: one launch (up to 8 members)
         for g0 in range(0, M, 8):
             grp = list(zip(self.models[g0:g0 + 8], self.ws[g0:g0 + 8]))
@@ -479,17 +481,20 @@ class GraphedEnsembleStep:
         o.train_call_mb(a, c0, M, 4, 1, 1)  # moving averages + dgamma / dbeta
         hyper = {(float(m.optimizer.learning_rate), float(m.optimizer.beta_1), float(m.optimizer.beta_2),
                   float(m.optimizer.epsilon)) for m in self.models}
-        if len(hyper) == 1 and M <= 16:  # one Adam launch for all members
+        if len(hyper) == 1:  # one Adam launch per 16 members (csrc/adam.hip kAdamMaxSets)
             lr, b1, b2, eps = hyper.pop()
-            o.adam_step_multi([m.store.flat for m in self.models], [ws.grad for ws in self.ws],
-                              [m.optimizer.m for m in self.models], [m.optimizer.v for m in self.models], b1, b2, lr,
-                              eps, [ws.counters for ws in self.ws])
+            for g0 in range(0, M, 16):
+                ms, wss = self.models[g0:g0 + 16], self.ws[g0:g0 + 16]
+                o.adam_step_multi([m.store.flat for m in ms], [ws.grad for ws in wss], [m.optimizer.m for m in ms],
+                                  [m.optimizer.v for m in ms], b1, b2, lr, eps, [ws.counters for ws in wss])
         else:
             for m, ws in zip(self.models, self.ws):
                 opt = m.optimizer
                 o.adam_step(m.store.flat, ws.grad, opt.m, opt.v, opt.beta_1, opt.beta_2, opt.learning_rate,
                             opt.epsilon, 1.0, ws.counters)
-        o.bump_counters(self.counters.view(-1))
+        flat = self.counters.view(-1)
+        for c0 in range(0, flat.numel(), 64):  # <= 64 counters per launch
+            o.bump_counters(flat[c0:c0 + 64])
         return [ws.loss.view(()) for ws in self.ws] + [torch.sigmoid(ws.logits[:n]) for ws in self.ws]
 
     def valid_for(self, models) -> bool:
