@@ -144,11 +144,14 @@ def test_data_parallel_hip_step_matches_single_process(name):
 
 @pytest.mark.parametrize("name", ["pooled", "single30"])
 def test_graphed_generic_step_matches_eager(name, monkeypatch):
-    """The HIP-graph replay of the generic step (dropout keys read from device memory, Adam step from
-    a device counter) follows the eager step: both compute Adam's bias correction on the device from
-    the iteration counter, so they differ only by fp32-atomic summation order -- bounded here by the
-    spread of two EAGER runs -- and the graph's device counter advanced in lockstep with the host."""
-    from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import generic_train
+    """The HIP-graph replay of the generic step (dropout keys derived on the device from the step
+    counter, Adam step from the iteration counter) follows the eager step.  Exact checks: step 1's loss
+    (identical weights, masks and inputs) and the device state after 4 replays (the dropout keys of step
+    4 equal the host formula, both counters advanced in lockstep).  Later losses and the weights differ by
+    fp32-atomic summation order, which bf16 rounding flips amplify to ~1e-3 of the loss by step 2 in
+    eager runs too (tools/probes/capture_race.py: step-2 losses of fresh eager runs spread over 0.1):
+    bounded by 3x the spread of two eager runs, with a 3e-3 relative floor."""
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import generic_train, rng
 
     spec = SPECS[name]
     g = torch.Generator().manual_seed(3)
@@ -163,12 +166,15 @@ def test_graphed_generic_step_matches_eager(name, monkeypatch):
         if mode == "1":
             gs = getattr(m, "_gtrain_graphs", {})
             assert 64 in gs
-            assert int(gs[64].counters[1].item()) == 4  # device-side Adam step == host iterations
+            assert gs[64].counters.tolist() == [4, 4]  # device dropout step / Adam step == host counters
+            want = [rng.stream_key(m.seed, l, generic_train.TRAIN_PASS_BASE + 3) for l in range(len(spec.blocks))]
+            assert [k & 0xFFFFFFFF for k in gs[64].keys.tolist()] == want  # the keys step 4 ran with
     (le, ie, ce, we), (le2, _, _, we2), (lg, ig, cg, wg) = runs["0"], runs["0b"], runs["1"]
     assert (ie, ce) == (ig, cg) == (4, 4)
     assert abs(lg[0] - le[0]) < 1e-4 * abs(le[0])
     for a, b, b2 in zip(lg, le, le2):
-        assert abs(a - b) <= max(3 * abs(b2 - b), 1e-4 * abs(b)), (lg, le, le2)
+        assert abs(a - b) <= max(3 * abs(b2 - b), 3e-3 * abs(b)), (lg, le, le2)
     spread = (we2 - we).norm().item()
-    assert (wg - we).norm().item() <= max(3 * spread, 1e-6 * we.norm().item())
+    upd = (we - AlarconCNN1D(spec=spec, seed=4, device="cuda").store.flat).norm().item()
+    assert (wg - we).norm().item() <= max(3 * spread, 0.05 * upd)
     assert isinstance(generic_train.GraphedGenericStep, type)
