@@ -34,6 +34,8 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=2025)
     ap.add_argument("--streams", type=int, default=3, help="HIP streams the members of one GPU round-robin over "
                     "(3 + the default stream fit the 4 hardware queues HIP uses per process; --mode streams)")
+    ap.add_argument("--groups", type=int, default=4, help="batched mode: member groups, one batched graph each, "
+                    "replayed on their own HIP streams (4: the best of 1/2/3/4/8 for 8 members)")
     ap.add_argument("--mode", choices=["batched", "streams"], default="batched",
                     help="batched: one member-batched HIP graph per step (ops/train_ops.py:GraphedEnsembleStep); "
                          "streams: members' graphs overlapped on HIP streams")
@@ -67,12 +69,22 @@ def main(argv=None):
     if batched:
         from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import train_ops
 
-        ens = train_ops.GraphedEnsembleStep(models, a.batch)
-        xs, ys = [x] * len(models), [y] * len(models)
+        ng = max(1, min(a.groups, len(models)))
+        parts = [models[i::ng] for i in range(ng)]
+        ens = [train_ops.GraphedEnsembleStep(p, a.batch) for p in parts]
+        gstreams = [torch.cuda.Stream(device=dev) for _ in parts] if ng > 1 else [None]
+        for s_ in gstreams:
+            if s_ is not None:
+                s_.wait_stream(torch.cuda.current_stream(dev))
 
     def step():
         if batched:
-            ens(xs, ys)
+            for e, p, s_ in zip(ens, parts, gstreams):
+                if s_ is None:
+                    e([x] * len(p), [y] * len(p))
+                else:
+                    with torch.cuda.stream(s_):
+                        e([x] * len(p), [y] * len(p))
             return
         for i, mdl in enumerate(models):
             with torch.cuda.stream(streams[i % len(streams)]):
@@ -96,7 +108,7 @@ def main(argv=None):
                           "ms_per_step_all_members": round(dt * 1e3 / a.steps, 3), "dtype": "bf16",
                           "data": "synthetic", "backend": info.backend, "devices": devices,
                           "parallelism": f"ensemble-parallel over {info.world} GPU(s), " +
-                          ("member-batched launches" if batched else f"{len(streams)} stream(s)/GPU")}))
+                          (f"member-batched launches ({len(parts)} group(s))" if batched else f"{len(streams)} stream(s)/GPU")}))
     pdist.shutdown()
 
 
