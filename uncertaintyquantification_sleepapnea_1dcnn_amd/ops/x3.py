@@ -175,7 +175,7 @@ def _max_samples(dev, per_sample: int, frac: float = 0.45) -> int:
 @torch.no_grad()
 def mcd_batch(model: X3Model, x: torch.Tensor, n_pass: int, seed: int, pass_base: int = 0, window_offset: int = 0,
               update_moving: bool = True, sync: Optional[Callable] = None, global_n: Optional[int] = None,
-              max_samples: Optional[int] = None) -> torch.Tensor:
+              max_samples: Optional[int] = None, grid: int = 0) -> torch.Tensor:
     """MC Dropout with BN on per-pass batch statistics (reference semantics), fp32-faithful: (T, N).
 
     ``x``: (N, 60, 4) windows of this rank; with ``sync`` (all-reduce of fp64 tensors) the BN moments are
@@ -231,7 +231,7 @@ def mcd_batch(model: X3Model, x: torch.Tensor, n_pass: int, seed: int, pass_base
             dst = ws.sums if l == 5 else ws.buf[(l - 1) % 2]
             o.x3_layer(l, src, dst, model.wfrag[l], 0, model.bias[l], model.wscale[l], 0, ws.aff[l - 1],
                        0 if l == 1 else 2 * CH[l], st, n, tc, l == 1, l == 1, thr[l - 1], thr[l], seed, pb,
-                       int(window_offset), 0)
+                       int(window_offset), int(grid))
             if sync is not None:
                 _sync_stats(sync, st, tc, c)
             g, b, mm, mv = model.bn[l]
