@@ -180,7 +180,8 @@ def mcd_batch(model: X3Model, x: torch.Tensor, n_pass: int, seed: int, pass_base
 
     ``x``: (N, 60, 4) windows of this rank; with ``sync`` (all-reduce of fp64 tensors) the BN moments are
     those of all ``global_n`` windows of all ranks.  Passes are processed in chunks that fit the device
-    (statistics are per pass, so chunking is exact; every rank must use the same chunking)."""
+    (statistics are per pass, so chunking is exact; every rank must use the same chunking).  ``grid``:
+    persistent workgroups per layer launch (0: one per CU)."""
     assert model.G == 1, "mcd_batch runs one model"
     spec, o = model.spec, _ops()
     x = x.to(device=model.device, dtype=torch.float32).contiguous()
