@@ -49,7 +49,8 @@ METRIC = "30s-windows/sec for MCD T=50 & DE M=8 inference at 1/2/4/8 MI355X"
 # The reference publishes no throughput number.  vs_baseline divides by OUR
 # measurement of its exact loops in eager fp32 PyTorch on 1 x MI355X (bench/comparator.py, N=16384,
 # MCD T=50 with BN batch statistics as the reference runs it + DE M=8 predict(batch 32) + NumPy UQ
-# metrics): profiles/comparator_eager_fp32_batchbn_r1.json — the same MCD semantics as the headline.
+# metrics): profiles/comparator_eager_fp32_batchbn_r1.json — the same MCD semantics as the headline
+# (re-measured in round 3 on the current image: 4933.7, profiles/comparator_eager_fp32_batchbn_r3.json).
 BASELINE = 4925.9
 BASELINE_BASIS = ("eager fp32 PyTorch running the reference's loops (MCD: 50 x model(X, training=True) with BN batch "
                   "stats; DE: 8 x predict(batch 32)) on 1 x MI355X, profiles/comparator_eager_fp32_batchbn_r1.json")
