@@ -138,3 +138,29 @@ def test_generic_emulation_matches_reference_pooled():
             a = generic.emulate(spec, p, x, dropout=drop, seed=3, pass_id=1)
             b = R.forward(spec, p, x, dropout=drop, bn_batch_stats=False, seed=3, pass_id=1)
             np.testing.assert_allclose(a.numpy(), b.numpy().reshape(-1), atol=3e-2)
+
+
+def test_fused_pooled_dispatch_and_blob():
+    """The pooled reference CNN (MaxPool1D after blocks 1-5) is the architecture of
+    csrc/fused_pooled.hip: same parameter blob as the no-pool kernel; other pool patterns are not."""
+    import dataclasses
+
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import fused, generic
+
+    pooled = dataclasses.replace(DEFAULT_SPEC, blocks=tuple(dataclasses.replace(b, pool=(i < 5))
+                                                            for i, b in enumerate(DEFAULT_SPEC.blocks)))
+    two = dataclasses.replace(DEFAULT_SPEC, blocks=tuple(dataclasses.replace(b, pool=(i < 2))
+                                                         for i, b in enumerate(DEFAULT_SPEC.blocks)))
+    assert fused.pooled_supported(pooled) and not fused.supports(pooled)
+    assert not fused.pooled_supported(DEFAULT_SPEC) and not fused.pooled_supported(two)
+    p = R.synthetic_params(pooled, 2)
+    blob = fused.pack_blob(pooled, p)
+    assert blob.numel() == fused.layout()["bytes"]
+    pk = generic.pack(pooled, p)
+    assert torch.equal(pk["pooled_blob"][0], blob)
+    assert "pooled_blob" not in generic.pack(two, R.synthetic_params(two, 2))
+    # the last block feeds the head in fp32 on the fused path: the emulation follows it
+    x = torch.randn(5, 60, 4, generator=torch.Generator().manual_seed(1))
+    a = generic.emulate(pooled, p, x, logits=True)
+    b = generic.emulate(pooled, p, x, logits=True, last_fp32=True)
+    assert torch.equal(a, b)

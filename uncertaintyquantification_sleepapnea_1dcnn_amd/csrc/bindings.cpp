@@ -17,6 +17,11 @@ hipError_t launch_fused_forward(const void* x, const uint8_t* blob, long long bl
                                 const float* dscale, int grid, hipStream_t stream);
 int fused_blob_bytes();
 int fused_lds_bytes();
+hipError_t launch_fused_pooled(const void* x, const uint8_t* blob, long long blob_stride, float* out, int n_win,
+                               int n_pass, int n_member, unsigned window_offset, unsigned pass_offset,
+                               unsigned long long seed, int dropout, int out_logits, const unsigned* thr,
+                               hipStream_t stream);
+int fused_pooled_lds_bytes();
 void fused_layout(int* woffs, int* eoffs, int* dense_off);
 hipError_t launch_uq_reduce(const float* probs, int t_count, int n, float* out, hipStream_t stream);
 hipError_t launch_bootstrap(const float* metrics, const int* y, const int* idx, unsigned seed, int n, int n_boot,
@@ -102,9 +107,11 @@ inline void check(hipError_t e, const char* what) {
   TORCH_CHECK(e == hipSuccess, what, " failed: ", hipGetErrorString(e));
 }
 
-at::Tensor fused_forward(const at::Tensor& x, const at::Tensor& blob, int64_t n_pass, int64_t window_offset,
-                         int64_t pass_offset, int64_t seed, bool dropout, bool out_logits, at::IntArrayRef thr,
-                         at::ArrayRef<double> dscale, int64_t grid) {
+// pooled = false: fused_forward.hip (the reference no-pool CNN); true: fused_pooled.hip (MaxPool1D(2)
+// after blocks 1-5).  Same (N, 60, 4) input, same parameter blob.
+at::Tensor fused_forward_impl(const at::Tensor& x, const at::Tensor& blob, int64_t n_pass, int64_t window_offset,
+                              int64_t pass_offset, int64_t seed, bool dropout, bool out_logits, at::IntArrayRef thr,
+                              at::ArrayRef<double> dscale, int64_t grid, bool pooled) {
   TORCH_CHECK(x.is_cuda() && blob.is_cuda(), "fused_forward: tensors must be on the GPU");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "fused_forward: x must be contiguous bf16");
   TORCH_CHECK(x.dim() == 3 && x.size(1) == 60 && x.size(2) == 4, "fused_forward: x must be (N, 60, 4), got ",
@@ -128,12 +135,33 @@ at::Tensor fused_forward(const at::Tensor& x, const at::Tensor& blob, int64_t n_
     t[i] = static_cast<unsigned>(thr[i]);
     d[i] = static_cast<float>(dscale[i]);
   }
-  check(apneauq::launch_fused_forward(x.data_ptr(), blob.data_ptr<uint8_t>(),
-                                      blob.stride(0), out.data_ptr<float>(), (int)n_win, (int)n_pass, (int)n_member,
-                                      (unsigned)window_offset, (unsigned)pass_offset, (unsigned long long)seed,
-                                      dropout ? 1 : 0, out_logits ? 1 : 0, t, d, (int)grid, cur_stream()),
-        "fused_forward");
+  if (pooled)
+    check(apneauq::launch_fused_pooled(x.data_ptr(), blob.data_ptr<uint8_t>(), blob.stride(0), out.data_ptr<float>(),
+                                       (int)n_win, (int)n_pass, (int)n_member, (unsigned)window_offset,
+                                       (unsigned)pass_offset, (unsigned long long)seed, dropout ? 1 : 0,
+                                       out_logits ? 1 : 0, t, cur_stream()),
+          "fused_pooled_forward");
+  else
+    check(apneauq::launch_fused_forward(x.data_ptr(), blob.data_ptr<uint8_t>(), blob.stride(0), out.data_ptr<float>(),
+                                        (int)n_win, (int)n_pass, (int)n_member, (unsigned)window_offset,
+                                        (unsigned)pass_offset, (unsigned long long)seed, dropout ? 1 : 0,
+                                        out_logits ? 1 : 0, t, d, (int)grid, cur_stream()),
+          "fused_forward");
   return out;
+}
+
+at::Tensor fused_forward(const at::Tensor& x, const at::Tensor& blob, int64_t n_pass, int64_t window_offset,
+                         int64_t pass_offset, int64_t seed, bool dropout, bool out_logits, at::IntArrayRef thr,
+                         at::ArrayRef<double> dscale, int64_t grid) {
+  return fused_forward_impl(x, blob, n_pass, window_offset, pass_offset, seed, dropout, out_logits, thr, dscale, grid,
+                            false);
+}
+
+at::Tensor fused_pooled_forward(const at::Tensor& x, const at::Tensor& blob, int64_t n_pass, int64_t window_offset,
+                                int64_t pass_offset, int64_t seed, bool dropout, bool out_logits, at::IntArrayRef thr,
+                                at::ArrayRef<double> dscale) {
+  return fused_forward_impl(x, blob, n_pass, window_offset, pass_offset, seed, dropout, out_logits, thr, dscale, 0,
+                            true);
 }
 
 at::Tensor uq_reduce(const at::Tensor& probs) {
@@ -742,6 +770,7 @@ std::vector<int64_t> fused_layout() {
   v.push_back(d);
   v.push_back(apneauq::fused_blob_bytes());
   v.push_back(apneauq::fused_lds_bytes());
+  v.push_back(apneauq::fused_pooled_lds_bytes());
   return v;
 }
 
@@ -750,6 +779,8 @@ std::vector<int64_t> fused_layout() {
 TORCH_LIBRARY(apneauq, m) {
   m.def("fused_forward(Tensor x, Tensor blob, int n_pass, int window_offset, int pass_offset, int seed, "
         "bool dropout, bool out_logits, int[] thr, float[] dscale, int grid) -> Tensor");
+  m.def("fused_pooled_forward(Tensor x, Tensor blob, int n_pass, int window_offset, int pass_offset, int seed, "
+        "bool dropout, bool out_logits, int[] thr, float[] dscale) -> Tensor");
   m.def("uq_reduce(Tensor probs) -> Tensor");
   m.def("bootstrap(Tensor metrics, Tensor y, Tensor? idx, int seed, int n_boot) -> Tensor");
   m.def("bootstrap_partial(Tensor metrics, Tensor y, Tensor? idx, int seed, int n_boot, int n_global, int lo) -> Tensor");
@@ -791,6 +822,7 @@ TORCH_LIBRARY(apneauq, m) {
 
 TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
   m.impl("fused_forward", &fused_forward);
+  m.impl("fused_pooled_forward", &fused_pooled_forward);
   m.impl("uq_reduce", &uq_reduce);
   m.impl("bootstrap", &bootstrap);
   m.impl("bootstrap_partial", &bootstrap_partial);

@@ -20,6 +20,7 @@
 //   * block 6's epilogue feeds GAP + Dense(96->1) + sigmoid directly (fp32), never touching LDS.
 //   LDS per workgroup ~75 KiB -> 2 workgroups (8 waves) per CU.
 #include "common.h"
+#include "fused_blob.h"
 
 namespace apneauq {
 namespace fused {
@@ -42,18 +43,6 @@ constexpr int kLdsBytes = kActBytes + kX0Bytes + kHeadBytes;
 constexpr int kThreads = 256;
 static_assert(kActBytes % 16 == 0 && kX0Bytes % 16 == 0, "LDS carve must stay 16-B aligned");
 
-// channel / kernel-size table of the default spec (cnn_baseline_train.py:59-86)
-constexpr int C[7] = {4, 128, 192, 224, 96, 256, 96};
-constexpr int KS[6] = {7, 5, 3, 7, 9, 9};
-
-__host__ __device__ constexpr int ksteps(int l) { return (C[l] * KS[l] + 31) / 32; }
-__host__ __device__ constexpr int wbytes(int l) { return ksteps(l) * (C[l + 1] / 16) * 1024; }
-constexpr int kEpiRows = 8;  // per-channel [s, t' = b*s + t, lo, hi], then the same x 1/(1-rate) (ops/fused.py)
-__host__ __device__ constexpr int ebytes(int l) { return ((kEpiRows * C[l + 1] * 4) + 15) / 16 * 16; }
-__host__ __device__ constexpr int woff(int l) { return l == 0 ? 0 : woff(l - 1) + wbytes(l - 1); }
-__host__ __device__ constexpr int eoff(int l) { return l == 0 ? woff(6) : eoff(l - 1) + ebytes(l - 1); }
-constexpr int kDenseOff = eoff(6);
-constexpr int kBlobBytes = kDenseOff + ((C[6] + 1) * 4 + 15) / 16 * 16;
 
 extern __shared__ __attribute__((aligned(16))) char smem[];  // dynamic LDS, carved below
 

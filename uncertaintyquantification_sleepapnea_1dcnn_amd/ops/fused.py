@@ -29,6 +29,17 @@ def supports(spec: ModelSpec) -> bool:
             and tuple(b.kernel_size for b in spec.blocks) == FUSED_KSIZES and not spec.has_pool)
 
 
+POOLED_PATTERN = (True, True, True, True, True, False)
+
+
+def pooled_supported(spec: ModelSpec) -> bool:
+    """True if ``csrc/fused_pooled.hip`` implements this architecture: the reference CNN with
+    MaxPool1D(2) after blocks 1-5 (the pooling lines of train_deep_ensemble_cnns.py:36-66)."""
+    return (spec.input_length == FUSED_LENGTH and tuple(spec.channels()) == FUSED_CHANNELS
+            and tuple(b.kernel_size for b in spec.blocks) == FUSED_KSIZES
+            and tuple(bool(b.pool) for b in spec.blocks) == POOLED_PATTERN)
+
+
 _WARNED = set()
 
 
@@ -117,8 +128,9 @@ def pack_blob(spec: ModelSpec, p, bn_override: Optional[Sequence] = None) -> tor
     ``bn_override``: optional list of 6 (scale, shift) pairs replacing the running-stat BN affine
     (used by the batch-statistics MC-Dropout parity mode).
     """
-    if not supports(spec):
-        raise ValueError("fused kernel supports only the reference (60, 4) no-pool architecture")
+    if not (supports(spec) or pooled_supported(spec)):
+        raise ValueError("fused kernels support only the reference (60, 4) architecture, without pooling or "
+                         "with MaxPool1D(2) after blocks 1-5")
     lay = layout()
     dev = p["conv1d_1/kernel"].device
     blob = torch.zeros(lay["bytes"], dtype=torch.uint8, device=dev)

@@ -5,7 +5,10 @@ spec can express -- the opt-in ``MaxPool1D(2)`` blocks (the thes
 ``ensemble_cnn`` models), other window shapes such as the north-star "30 s single-channel"
 ``ModelSpec(30, 1)``, other filter counts and odd kernel sizes -- runs here: one MFMA launch per
 block (bias + ReLU + BN(running) + pool + counter-based dropout fused into its epilogue) and one
-GAP + Dense head launch, with bf16 activations between blocks.
+GAP + Dense head launch, with bf16 activations between blocks.  The pooled reference CNN (MaxPool1D
+after blocks 1-5, :func:`fused.pooled_supported`) instead runs the fused whole-network kernel
+``csrc/fused_pooled.hip`` (8 samples per workgroup, activations in LDS, one launch); set
+``APNEAUQ_POOLED_FUSED=0`` to force the layer-wise kernels (A/B runs).
 
 Dropout masks are the same pure function of (seed, layer, pass, window, t, channel) as everywhere
 else (``ops/rng.py``), so results match the fp32 reference's masks exactly and do not depend on
@@ -14,6 +17,7 @@ generic training kernels (``ops/generic_train.py``).
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -49,7 +53,37 @@ def pack(spec: ModelSpec, p) -> Dict[str, object]:
         blocks.append((fr, epi))
     dense_w = p["output_layer/kernel"].float().reshape(-1).to(dev).contiguous()
     dense_b = float(p["output_layer/bias"].float().reshape(-1)[0])
-    return {"blocks": blocks, "dense_w": dense_w, "dense_b": dense_b}
+    out = {"blocks": blocks, "dense_w": dense_w, "dense_b": dense_b}
+    if fused.pooled_supported(spec) and os.environ.get("APNEAUQ_POOLED_FUSED", "1") != "0":
+        out["pooled_blob"] = fused.pack_blob(spec, p).unsqueeze(0)
+    return out
+
+
+_MAX_SAMPLES = 1 << 31  # samples per fused-pooled launch (32-bit sample / tile ids)
+
+
+def _pooled_forward(packed, spec: ModelSpec, x: torch.Tensor, n_pass: int, dropout: bool, seed: int,
+                    window_offset: int, pass_offset: int, logits: bool) -> torch.Tensor:
+    """(n_pass, N) through ``csrc/fused_pooled.hip``; launches split so that one holds < 2^31 samples
+    (masks are keyed by global pass / window ids, so the split does not change the result)."""
+    o = _ext.ops()
+    thr, dsc = fused.dropout_tables(spec)
+    s63 = int(seed) & ((1 << 63) - 1)
+    blob = packed["pooled_blob"]
+    n = x.shape[0]
+    if not dropout:  # deterministic: every pass is identical
+        y = o.fused_pooled_forward(x, blob, 1, int(window_offset), 0, s63, False, bool(logits), thr, dsc)[0, 0]
+        return y.unsqueeze(0).expand(n_pass, n).contiguous()
+    out = torch.empty(n_pass, n, dtype=torch.float32, device=x.device)
+    wc = min(n, _MAX_SAMPLES // 2)
+    pc = max(1, (_MAX_SAMPLES // 2) // wc)
+    for w0 in range(0, n, wc):
+        w1 = min(n, w0 + wc)
+        for p0 in range(0, n_pass, pc):
+            p1 = min(n_pass, p0 + pc)
+            out[p0:p1, w0:w1] = o.fused_pooled_forward(x[w0:w1], blob, p1 - p0, int(window_offset) + w0,
+                                                       int(pass_offset) + p0, s63, True, bool(logits), thr, dsc)[0]
+    return out
 
 
 def _forward_chunk(packed, spec: ModelSpec, x_bf16: torch.Tensor, n_win: int, dropout: bool, seed: int,
@@ -75,6 +109,8 @@ def forward(packed, spec: ModelSpec, x_bf16: torch.Tensor, *, n_pass: int = 1, d
     if n == 0:
         return out
     x = x_bf16.contiguous()
+    if "pooled_blob" in packed:
+        return _pooled_forward(packed, spec, x, n_pass, dropout, seed, window_offset, pass_offset, logits)
     widest = max(ln * c for ln, c in zip(spec.lengths(), spec.channels()))
     per_pass = max(1, n * widest)
     pc = max(1, min(n_pass, _CHUNK_ELEMS // per_pass))
@@ -98,9 +134,14 @@ def forward(packed, spec: ModelSpec, x_bf16: torch.Tensor, *, n_pass: int = 1, d
 
 
 def emulate(spec: ModelSpec, p, x: torch.Tensor, *, dropout: bool = False, seed: int = 0, pass_id: int = 0,
-            sample_ids: Optional[torch.Tensor] = None, logits: bool = False) -> torch.Tensor:
+            sample_ids: Optional[torch.Tensor] = None, logits: bool = False,
+            last_fp32: Optional[bool] = None) -> torch.Tensor:
     """CPU emulation of the generic kernels' arithmetic (bf16 operands and activations, fp32
-    accumulation, folded epilogue) -- the tight oracle for the GPU tests."""
+    accumulation, folded epilogue) -- the tight oracle for the GPU tests.  ``last_fp32``: the last
+    block's output feeds the head in fp32 (the fused kernels; default: whenever :func:`forward`
+    takes the fused pooled kernel for ``spec``)."""
+    if last_fp32 is None:
+        last_fp32 = fused.pooled_supported(spec) and os.environ.get("APNEAUQ_POOLED_FUSED", "1") != "0"
     from ..models.reference import conv1d_same
 
     n = x.shape[0]
@@ -121,6 +162,6 @@ def emulate(spec: ModelSpec, p, x: torch.Tensor, *, dropout: bool = False, seed:
             keep = rng.keep_mask_torch(rng.stream_key(seed, i - 1, pass_id), sample_ids, y.shape[1], y.shape[2],
                                        b.dropout)
             y = torch.where(keep, y, torch.zeros_like(y))
-        h = y.to(torch.bfloat16).float()
+        h = y if (last_fp32 and i == len(spec.blocks)) else y.to(torch.bfloat16).float()
     logit = h.mean(dim=1) @ p["output_layer/kernel"].float().reshape(-1) + p["output_layer/bias"].float().reshape(-1)
     return logit if logits else torch.sigmoid(logit)
