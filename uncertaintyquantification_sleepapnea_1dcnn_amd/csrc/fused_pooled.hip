@@ -15,9 +15,10 @@
 //   * each block's input lives in LDS in per-sample slots of SIN rows: LIN valid rows, then zero
 //     rows that double as the 'same' padding of the next slot (SIN >= LIN + PAD), so the
 //     implicit-GEMM conv needs no bounds checks.  LDS row = GEMM row;
-//   * taps that can never reach a valid input row are skipped: block 5 (3 rows, k = 9) runs taps
-//     3..6 for the 2 rows its pool keeps, block 6 (1 row, k = 9) only the centre tap -- block 6 is
-//     a dense 256 -> 96 layer, 9x fewer MFMAs than the padded conv;
+//   * only the rows the pool keeps are computed where that saves row tiles (block 4: 8 of 12 slot
+//     rows, block 5: 2 of 8), and taps that can never reach a valid input row are skipped: block 5
+//     (3 rows, k = 9) runs taps 3..6 for its 2 kept rows, block 6 (1 row, k = 9) only the centre tap
+//     -- block 6 is a dense 256 -> 96 layer, 9x fewer MFMAs than the padded conv;
 //   * the epilogue pools rows t, t^1 (lanes m, m^1) with one DPP quad permute, applies the
 //     counter-based dropout keyed by the pooled step (ops/rng.py, same masks as generic_conv.hip)
 //     and writes bf16 in place over the block input (a barrier after the K loop; row groups
@@ -47,10 +48,23 @@ constexpr int SIN[6] = {64, 32, 16, 12, 8, 1};
 constexpr int LOUT[6] = {30, 15, 7, 3, 1, 1};   // rows after MaxPool1D(2, valid) (block 6: no pool)
 constexpr int T0[6] = {0, 0, 0, 0, 3, 4};       // taps [T0, T1) reach a valid input row of a kept output row
 constexpr int T1[6] = {7, 5, 3, 7, 7, 5};
-constexpr int RG[6] = {8, 8, 8, 6, 4, 1};       // row tiles per row group
+// GEMM rows computed per sample: all SIN slot rows, except where the pool keeps only a prefix --
+// block 4 computes t < 8 of its 12-row slots (pool keeps t < 6), block 5 t < 2 of 8 (keeps t < 2);
+// a computed row o is slot row (o / OPS) * SIN + o % OPS
+constexpr int OPS[6] = {64, 32, 16, 8, 2, 1};
+constexpr int RG[6] = {8, 8, 8, 4, 1, 1};       // row tiles per row group
 constexpr int NG[6] = {4, 2, 1, 1, 1, 1};       // row groups
-constexpr int WM[6] = {1, 1, 2, 2, 1, 1};       // wave rows (4 / WM wave columns over channel tiles)
-constexpr int NF[6] = {2, 3, 7, 3, 4, 2};       // channel tiles per wave
+constexpr int WM[6] = {1, 1, 1, 1, 1, 1};       // wave rows (4 / WM wave columns over channel tiles)
+constexpr int NF[6] = {2, 3, 3, 1, 4, 2};       // full channel tiles per wave
+// HALF: Cout tiles that do not split 4 ways (224 -> 14, 96 -> 6 = 2 pairs x (2 NF + 1)) -- each wave
+// pair shares its middle tile, one wave per half of the row tiles, so every weight fragment is
+// requested once per workgroup and all waves issue the same MFMA count (2 wave rows loading the
+// same fragments: profiles/pooled_fused_r3.md)
+constexpr bool HALF[6] = {false, false, true, true, false, false};
+// k-steps of weight fragments in flight ahead of the MFMAs.  Depths (3,3,2,4,3,4) and (4,4,3,6,5,6)
+// measured 0.8 % and 1.9 % slower than 1 everywhere (profiles/pooled_fused_r3.md): weight latency is
+// not what bounds this kernel.
+constexpr int PD[6] = {1, 1, 1, 1, 1, 1};
 
 __host__ __device__ constexpr int row_bytes(int c) { return 2 * c + 16; }  // +16 B: conflict-free rows
 constexpr int kHB = 4 * row_bytes(256);                                      // leading zero rows (>= PAD rows of any block)
@@ -80,16 +94,20 @@ struct Geo {
   static constexpr int NRW = RG[L] / WM[L];      // row tiles per wave per group
   static constexpr int SI = FIRST ? kCin * 2 : row_bytes(CIN);
   static constexpr int SOUT = L < 5 ? SIN[L + 1] : 1, SO = row_bytes(COUT);
-  static constexpr int SPG = RG[L] * 16 / SIN[L];  // samples per row group (block 6: all 8)
+  static constexpr int SPG = RG[L] * 16 / OPS[L];  // samples per row group (block 6: all 8)
 };
 
 // compile-time checks of the slot geometry and the in-place hand-over
 template <int L>
 constexpr bool geometry_ok() {
   using G = Geo<L>;
-  if (L < 5 && RG[L] * NG[L] * 16 != kNS * SIN[L]) return false;  // row groups tile the slots
+  if (L < 5 && RG[L] * NG[L] * 16 != kNS * OPS[L]) return false;  // row groups tile the computed rows
+  if (L < 5 && (OPS[L] > SIN[L] || OPS[L] % 2 != 0 || 2 * LOUT[L] > OPS[L])) return false;  // pool pairs
+  if (L == 0 && OPS[L] != SIN[L]) return false;
   if (L == 5 && RG[L] * 16 < kNS) return false;
-  if (G::NWC * NF[L] < G::NCT || RG[L] % WM[L] != 0) return false;  // wave tiling covers the block
+  if (HALF[L] ? (WM[L] != 1 || G::NCT != 2 * (2 * NF[L] + 1) || RG[L] % 2 != 0)
+              : (G::NWC * NF[L] < G::NCT || RG[L] % WM[L] != 0))
+    return false;  // wave tiling covers the block
   if (L > 0 && L < 5 && SIN[L] < LIN[L] + G::PAD) return false;    // zero rows = next slot's padding
   if (L < 5 && (2 * LOUT[L] > SIN[L] || LOUT[L] > G::SOUT)) return false;
   // row group g's output ends before group g+1's first input row (minus the padding)
@@ -133,37 +151,62 @@ __device__ __forceinline__ void pblock(const Ctx X) {
   const char* x0 = smem + kActBytes + kX0Lead * kCin * 2;
   const unsigned* keys = reinterpret_cast<const unsigned*>(smem + kActBytes + kX0Bytes) + L * kNS;
   float* head = reinterpret_cast<float*>(smem + kActBytes + kX0Bytes + kKeyBytes);
-  constexpr int NFL = NF[L], NRW = G::NRW;
+  constexpr bool HF = HALF[L];
+  constexpr int NFL = NF[L], NRW = G::NRW, HRT = NRW / 2;
+  constexpr int NFL_A = NFL + (HF ? 1 : 0);  // weight fragments per wave per k-step
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int m = lane & 15, h = lane >> 4;
   const int wc = wave % G::NWC, wr = wave / G::NWC;
-  const int ct0 = wc * NFL;
-  // channel tiles past NCT (block 6: 6 tiles over 4 x 2) load tile 0 and skip their MFMAs
+  // channel tiles: NFL full ones from ctf (+ the pair's shared middle tile cth with HALF); local row
+  // tile r < HRT is row tile rlo + r, r >= HRT is rhi + r - HRT (HALF: the odd wave of a pair
+  // swaps the halves, so the shared tile always sits in local rows r < HRT, a compile-time range)
+  int ctf, cth = 0, rlo = wr * NRW, rhi = wr * NRW + HRT;
+  if constexpr (HF) {
+    const int pair = wave >> 1, odd = wave & 1;
+    ctf = pair * (2 * NFL + 1) + (odd ? NFL + 1 : 0);
+    cth = pair * (2 * NFL + 1) + NFL;
+    rlo = odd * HRT;
+    rhi = HRT - rlo;
+  } else {
+    ctf = wc * NFL;
+  }
+  auto ct_of = [&](int c) { return (HF && c == NFL) ? cth : ctf + c; };
+  auto ct_ok = [&](int c) { return HF || ctf + c < G::NCT; };  // block 6: 6 tiles over 4 x 2 (wave-uniform)
+  auto nrows = [&](int c) { return (HF && c == NFL) ? HRT : NRW; };  // compile-time after unrolling
   const gbf16x8* wp = reinterpret_cast<const gbf16x8*>(X.blob + woff(L)) + lane;
-  int ctl[NFL];
+  int ctl[NFL_A];  // tiles past NCT load tile 0 and skip their MFMAs
 #pragma unroll
-  for (int c = 0; c < NFL; ++c) ctl[c] = ct0 + c < G::NCT ? ct0 + c : 0;
+  for (int c = 0; c < NFL_A; ++c) ctl[c] = ct_ok(c) ? ct_of(c) : 0;
 
   const gfloat* epi = reinterpret_cast<const gfloat*>(X.blob + eoff(L)) + (DROP ? 4 * G::COUT : 0);
 
 #pragma unroll 1
   for (int g = 0; g < NG[L]; ++g) {
-    const int rt0 = g * RG[L] + wr * NRW;  // this wave's first row tile
-    f32x4 acc[NFL][NRW];
+    const int rg0 = g * RG[L];
+    auto rt_of = [&](int r) { return rg0 + (!HF ? rlo + r : r < HRT ? rlo + r : rhi + r - HRT); };
+    f32x4 acc[NFL_A][NRW];
 #pragma unroll
-    for (int c = 0; c < NFL; ++c)
+    for (int c = 0; c < NFL_A; ++c)
 #pragma unroll
       for (int r = 0; r < NRW; ++r) acc[c][r] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    auto load_a = [&](int s, bf16x8 (&a)[NFL]) {
+    auto load_a = [&](int s, bf16x8 (&a)[NFL_A]) {
 #pragma unroll
-      for (int c = 0; c < NFL; ++c) a[c] = wp[(s * G::NCT + ctl[c]) * 64];
+      for (int c = 0; c < NFL_A; ++c) a[c] = wp[(s * G::NCT + ctl[c]) * 64];
     };
-    const char* bb = G::FIRST ? x0 + (rt0 * 16 + m + 2 * h - G::PAD) * G::SI
-                              : act + (rt0 * 16 + m - G::PAD) * G::SI + 16 * h;
-    auto step = [&](int s, const bf16x8 (&a)[NFL]) {
+    const int lofs = G::FIRST ? (m + 2 * h - G::PAD) * G::SI : (m - G::PAD) * G::SI + 16 * h;
+    const char* bb_lo = (G::FIRST ? x0 : act) + (rg0 + rlo) * 16 * G::SI + lofs;
+    const char* bb_hi = (G::FIRST ? x0 : act) + (rg0 + rhi) * 16 * G::SI + lofs;
+    constexpr bool DENSE = OPS[L] == SIN[L];  // computed row = slot row (else one base per row tile)
+    const char* bbr[NRW];
+#pragma unroll
+    for (int r = 0; r < NRW; ++r) {
+      const int o = rt_of(r) * 16 + m;
+      bbr[r] = act + ((o / OPS[L]) * SIN[L] + o % OPS[L] - G::PAD) * G::SI + 16 * h;
+    }
+    auto step = [&](int s, const bf16x8 (&a)[NFL_A]) {
       int soff = 0;
       if constexpr (!G::FIRST) {
         const int tap = s / G::CB, cb = s - tap * G::CB;
@@ -171,55 +214,63 @@ __device__ __forceinline__ void pblock(const Ctx X) {
       }
 #pragma unroll
       for (int r = 0; r < NRW; ++r) {
+        const char* bb = !DENSE ? bbr[r]
+                         : !HF  ? bb_lo + r * 16 * G::SI
+                                : (r < HRT ? bb_lo : bb_hi) + (r % (HF ? HRT : 1)) * 16 * G::SI;
         bf16x8 b;
         if constexpr (G::FIRST) {
           // k = tap*4 + ci: the lane's 8 k are taps 2h, 2h+1 x 4 channels = two consecutive rows
-          const bf16x4 lo = *reinterpret_cast<const bf16x4*>(bb + r * 16 * G::SI);
-          const bf16x4 hi = *reinterpret_cast<const bf16x4*>(bb + r * 16 * G::SI + 8);
+          const bf16x4 lo = *reinterpret_cast<const bf16x4*>(bb);
+          const bf16x4 hi = *reinterpret_cast<const bf16x4*>(bb + 8);
           b = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         } else {
-          b = *reinterpret_cast<const bf16x8*>(bb + soff + r * 16 * G::SI);
+          b = *reinterpret_cast<const bf16x8*>(bb + soff);
         }
 #pragma unroll
-        for (int c = 0; c < NFL; ++c)
-          if (ct0 + c < G::NCT) acc[c][r] = mfma16(a[c], b, acc[c][r]);  // wave-uniform
+        for (int c = 0; c < NFL_A; ++c)
+          if (ct_ok(c) && r < nrows(c)) acc[c][r] = mfma16(a[c], b, acc[c][r]);  // wave-uniform
       }
     };
 
-    // K loop over k-steps [S0, S1), weight fragments one step ahead (two register stages)
-    constexpr int NSTEP = G::S1 - G::S0, NFULL = NSTEP / 2 * 2;
-    bf16x8 a[2][NFL];
-    load_a(G::S0, a[0]);
-#pragma unroll 1
-    for (int s0 = 0; s0 < NFULL; s0 += 2) {
+    // K loop over k-steps [S0, S1): a ring of NSG register stages, the fragments of step s + PD in
+    // flight under step s's MFMAs (loads past the end are clamped: vmcnt bookkeeping stays exact)
+    constexpr int NSTEP = G::S1 - G::S0, PDL = PD[L] < NSTEP ? PD[L] : NSTEP, NSG = PDL + 1;
+    constexpr int NFULL = NSTEP / NSG * NSG;
+    bf16x8 a[NSG][NFL_A];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < PDL; ++j) load_a(G::S0 + j, a[j]);
+#pragma unroll 1
+    for (int s0 = 0; s0 < NFULL; s0 += NSG) {
+#pragma unroll
+      for (int j = 0; j < NSG; ++j) {
         const int s = s0 + j;
-        load_a(G::S0 + (s + 1 < NSTEP ? s + 1 : NSTEP - 1), a[(j + 1) & 1]);
+        load_a(G::S0 + (s + PDL < NSTEP ? s + PDL : NSTEP - 1), a[(j + PDL) % NSG]);
         __builtin_amdgcn_sched_barrier(0);
         step(G::S0 + s, a[j]);
       }
     }
-    if constexpr (NSTEP & 1) step(G::S0 + NSTEP - 1, a[0]);
+#pragma unroll
+    for (int j = 0; j < NSTEP - NFULL; ++j) step(G::S0 + NFULL + j, a[j]);
 
     // ---- epilogue: bias + ReLU + BN (one fma + med3), pool, dropout; bf16 in place / dense head
     if constexpr (!G::FIRST) __syncthreads();  // every wave finished reading this group's input rows
     float hp = 0.f;                            // HEAD: this lane's share of sample m's logit
 #pragma unroll
-    for (int c = 0; c < NFL; ++c) {
-      if (ct0 + c >= G::NCT) break;  // wave-uniform
-      const int co0 = (ct0 + c) * 16 + 4 * h;
+    for (int c = 0; c < NFL_A; ++c) {
+      if (!ct_ok(c)) break;  // wave-uniform
+      const int co0 = ct_of(c) * 16 + 4 * h;
       const f32x4 sc = *reinterpret_cast<const gf32x4*>(epi + co0);
       const f32x4 sh = *reinterpret_cast<const gf32x4*>(epi + G::COUT + co0);
       const f32x4 lo = *reinterpret_cast<const gf32x4*>(epi + 2 * G::COUT + co0);
       const f32x4 hi = *reinterpret_cast<const gf32x4*>(epi + 3 * G::COUT + co0);
 #pragma unroll
       for (int r = 0; r < NRW; ++r) {
+        if (r >= nrows(c)) break;
         f32x4 v = acc[c][r];
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = __builtin_amdgcn_fmed3f(__builtin_fmaf(v[i], sc[i], sh[i]), lo[i], hi[i]);
-        const int row = (rt0 + r) * 16 + m;
-        const int smp = G::HEAD ? m : row / SIN[L], t = G::HEAD ? 0 : row - smp * SIN[L];
+        const int row = rt_of(r) * 16 + m;
+        const int smp = G::HEAD ? m : row / OPS[L], t = G::HEAD ? 0 : row - smp * OPS[L];
         if constexpr (G::POOL) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i], dpp_mov<0xB1>(v[i]));  // rows t, t^1: lanes m, m^1
@@ -228,8 +279,17 @@ __device__ __forceinline__ void pblock(const Ctx X) {
         const bool keep_row = G::HEAD ? m < kNS : ((t & 1) == 0 && tp < LOUT[L]);
         if constexpr (DROP) {
           const unsigned key = keys[smp < kNS ? smp : 0];
-          const unsigned b01 = dropout_bits2(key, (unsigned)tp, (unsigned)co0);
-          const unsigned b23 = dropout_bits2(key, (unsigned)tp, (unsigned)co0 + 2);
+          unsigned b01, b23;
+          if constexpr (G::POOL) {
+            // lanes m, m^1 hold the same pooled element: each hashes one channel pair, DPP swaps them
+            const unsigned own = dropout_bits2(key, (unsigned)tp, (unsigned)co0 + 2 * (m & 1));
+            const unsigned other = (unsigned)__builtin_amdgcn_update_dpp(0, (int)own, 0xB1, 0xF, 0xF, false);
+            b01 = (m & 1) ? other : own;
+            b23 = (m & 1) ? own : other;
+          } else {
+            b01 = dropout_bits2(key, (unsigned)tp, (unsigned)co0);
+            b23 = dropout_bits2(key, (unsigned)tp, (unsigned)co0 + 2);
+          }
           v[0] = (b01 & 0xFFFFu) >= X.thr ? v[0] : 0.f;
           v[1] = (b01 >> 16) >= X.thr ? v[1] : 0.f;
           v[2] = (b23 & 0xFFFFu) >= X.thr ? v[2] : 0.f;
