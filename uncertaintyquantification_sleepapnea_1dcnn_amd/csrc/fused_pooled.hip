@@ -32,6 +32,8 @@
 namespace apneauq {
 namespace pooled {
 
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
 using fused::C;
 using fused::eoff;
 using fused::kDenseOff;
@@ -263,45 +265,52 @@ __device__ __forceinline__ void pblock(const Ctx X) {
       const f32x4 sh = *reinterpret_cast<const gf32x4*>(epi + G::COUT + co0);
       const f32x4 lo = *reinterpret_cast<const gf32x4*>(epi + 2 * G::COUT + co0);
       const f32x4 hi = *reinterpret_cast<const gf32x4*>(epi + 3 * G::COUT + co0);
+      if constexpr (G::POOL) {
+        // Pool first, per lane pair (rows t, t^1 = lanes m, m^1, the same 4 channels): the BN clamp is
+        // monotone, so max(clamp(u_a), clamp(u_b)) == clamp(max(u_a, u_b)) exactly, u = fma(acc, s, t').
+        // The even lane then finishes channels co0, co0+1 of the pooled element and the odd lane
+        // co0+2, co0+3: half the clamp / dropout / convert / store work per lane.
+        const int odd = m & 1, ch = co0 + 2 * odd;
+        const float lk0 = odd ? lo[2] : lo[0], lk1 = odd ? lo[3] : lo[1];
+        const float hk0 = odd ? hi[2] : hi[0], hk1 = odd ? hi[3] : hi[1];
 #pragma unroll
-      for (int r = 0; r < NRW; ++r) {
-        if (r >= nrows(c)) break;
+        for (int r = 0; r < NRW; ++r) {
+          if (r >= nrows(c)) break;
+          f32x4 u;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) u[i] = __builtin_fmaf(acc[c][r][i], sc[i], sh[i]);
+          const float z0 = odd ? u[0] : u[2], z1 = odd ? u[1] : u[3];  // the partner's channels
+          float x0 = odd ? u[2] : u[0], x1 = odd ? u[3] : u[1];
+          x0 = __builtin_amdgcn_fmed3f(fmaxf(x0, dpp_mov<0xB1>(z0)), lk0, hk0);
+          x1 = __builtin_amdgcn_fmed3f(fmaxf(x1, dpp_mov<0xB1>(z1)), lk1, hk1);
+          const int row = rt_of(r) * 16 + m;
+          const int smp = row / OPS[L], tp = (row - smp * OPS[L]) >> 1;
+          if constexpr (DROP) {
+            const unsigned bits = dropout_bits2(keys[smp], (unsigned)tp, (unsigned)ch);
+            x0 = (bits & 0xFFFFu) >= X.thr ? x0 : 0.f;
+            x1 = (bits >> 16) >= X.thr ? x1 : 0.f;
+          }
+          if (tp < LOUT[L])
+            *reinterpret_cast<bf16x2*>(act + (smp * G::SOUT + tp) * G::SO + ch * 2) = bf16x2{(__bf16)x0, (__bf16)x1};
+        }
+        continue;
+      }
+#pragma unroll
+      for (int r = 0; r < NRW; ++r) {  // HEAD (block 6): no pool, rows m < 8 are the samples
         f32x4 v = acc[c][r];
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = __builtin_amdgcn_fmed3f(__builtin_fmaf(v[i], sc[i], sh[i]), lo[i], hi[i]);
-        const int row = rt_of(r) * 16 + m;
-        const int smp = G::HEAD ? m : row / OPS[L], t = G::HEAD ? 0 : row - smp * OPS[L];
-        if constexpr (G::POOL) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i], dpp_mov<0xB1>(v[i]));  // rows t, t^1: lanes m, m^1
-        }
-        const int tp = G::POOL ? t >> 1 : t;
-        const bool keep_row = G::HEAD ? m < kNS : ((t & 1) == 0 && tp < LOUT[L]);
         if constexpr (DROP) {
-          const unsigned key = keys[smp < kNS ? smp : 0];
-          unsigned b01, b23;
-          if constexpr (G::POOL) {
-            // lanes m, m^1 hold the same pooled element: each hashes one channel pair, DPP swaps them
-            const unsigned own = dropout_bits2(key, (unsigned)tp, (unsigned)co0 + 2 * (m & 1));
-            const unsigned other = (unsigned)__builtin_amdgcn_update_dpp(0, (int)own, 0xB1, 0xF, 0xF, false);
-            b01 = (m & 1) ? other : own;
-            b23 = (m & 1) ? own : other;
-          } else {
-            b01 = dropout_bits2(key, (unsigned)tp, (unsigned)co0);
-            b23 = dropout_bits2(key, (unsigned)tp, (unsigned)co0 + 2);
-          }
+          const unsigned key = keys[m < kNS ? m : 0];
+          const unsigned b01 = dropout_bits2(key, 0u, (unsigned)co0);
+          const unsigned b23 = dropout_bits2(key, 0u, (unsigned)co0 + 2);
           v[0] = (b01 & 0xFFFFu) >= X.thr ? v[0] : 0.f;
           v[1] = (b01 >> 16) >= X.thr ? v[1] : 0.f;
           v[2] = (b23 & 0xFFFFu) >= X.thr ? v[2] : 0.f;
           v[3] = (b23 >> 16) >= X.thr ? v[3] : 0.f;
         }
-        if constexpr (G::HEAD) {
-          const f32x4 dw = *reinterpret_cast<const gf32x4*>(reinterpret_cast<const gfloat*>(X.blob + kDenseOff) + co0);
-          hp += keep_row ? v[0] * dw[0] + v[1] * dw[1] + v[2] * dw[2] + v[3] * dw[3] : 0.f;
-        } else if (keep_row) {
-          *reinterpret_cast<bf16x4*>(act + (smp * G::SOUT + tp) * G::SO + co0 * 2) =
-              bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
-        }
+        const f32x4 dw = *reinterpret_cast<const gf32x4*>(reinterpret_cast<const gfloat*>(X.blob + kDenseOff) + co0);
+        hp += m < kNS ? v[0] * dw[0] + v[1] * dw[1] + v[2] * dw[2] + v[3] * dw[3] : 0.f;
       }
     }
     if constexpr (G::HEAD) {
