@@ -1,8 +1,8 @@
 """Micro-benchmark of the layer-wise HIP path (ops/generic.py) for non-reference architectures:
 MC Dropout T passes over N windows, windows/s; ``--spec reference`` runs the reference
 architecture through the generic kernels for comparison with the fused kernel (bench/fused_micro.py);
-``pooled`` takes the fused pooled kernel (csrc/fused_pooled.hip), ``pooled_layerwise`` the same model on
-the layer-wise kernels."""
+``pooled`` and ``single30`` take the fused multi-sample-tile kernels (csrc/fused_tiled.hip),
+``*_layerwise`` the same models on the layer-wise kernels."""
 import argparse
 import dataclasses
 import json
@@ -31,12 +31,12 @@ def main():
     ap.add_argument("--iters", type=int, default=3)
     a = ap.parse_args()
     res = {}
-    runs = list(SPECS.items()) + [("pooled_layerwise", SPECS["pooled"])]
+    runs = list(SPECS.items()) + [("pooled_layerwise", SPECS["pooled"]), ("single30_layerwise", SPECS["single30"])]
     for name, spec in runs:
         p = {k: v.cuda() for k, v in R.synthetic_params(spec, 1).items()}
         pk = generic.pack(spec, p)
-        if name == "pooled_layerwise":  # the layer-wise kernels on the spec the fused pooled kernel covers
-            pk = {k: v for k, v in pk.items() if k != "pooled_blob"}
+        if name.endswith("_layerwise"):  # the layer-wise kernels on a spec a fused tiled kernel covers
+            pk = {k: v for k, v in pk.items() if k != "tiled_blob"}
         x = torch.randn(a.n, spec.input_length, spec.input_channels, device="cuda").to(torch.bfloat16)
         fn = lambda: generic.forward(pk, spec, x, n_pass=a.T, dropout=True, seed=3)  # noqa: E731
         fn()

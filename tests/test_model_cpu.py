@@ -142,7 +142,8 @@ def test_generic_emulation_matches_reference_pooled():
 
 def test_fused_pooled_dispatch_and_blob():
     """The pooled reference CNN (MaxPool1D after blocks 1-5) is the architecture of
-    csrc/fused_pooled.hip: same parameter blob as the no-pool kernel; other pool patterns are not."""
+    csrc/fused_tiled.hip (with the 30 s single-channel window): same parameter blob as the no-pool
+    kernel; other pool patterns are not."""
     import dataclasses
 
     from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import fused, generic
@@ -151,14 +152,19 @@ def test_fused_pooled_dispatch_and_blob():
                                                             for i, b in enumerate(DEFAULT_SPEC.blocks)))
     two = dataclasses.replace(DEFAULT_SPEC, blocks=tuple(dataclasses.replace(b, pool=(i < 2))
                                                          for i, b in enumerate(DEFAULT_SPEC.blocks)))
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.models.spec import ModelSpec
+
     assert fused.pooled_supported(pooled) and not fused.supports(pooled)
+    single = ModelSpec(30, 1, DEFAULT_SPEC.blocks)
+    assert fused.tiled_net(pooled) == 0 and fused.tiled_net(single) == 1 and fused.tiled_net(DEFAULT_SPEC) is None
+    assert fused.pack_blob(single, R.synthetic_params(single, 1)).numel() == fused.layout()["bytes"]
     assert not fused.pooled_supported(DEFAULT_SPEC) and not fused.pooled_supported(two)
     p = R.synthetic_params(pooled, 2)
     blob = fused.pack_blob(pooled, p)
     assert blob.numel() == fused.layout()["bytes"]
     pk = generic.pack(pooled, p)
-    assert torch.equal(pk["pooled_blob"][0], blob)
-    assert "pooled_blob" not in generic.pack(two, R.synthetic_params(two, 2))
+    assert torch.equal(pk["tiled_blob"][0], blob)
+    assert "tiled_blob" not in generic.pack(two, R.synthetic_params(two, 2))
     # the last block feeds the head in fp32 on the fused path: the emulation follows it
     x = torch.randn(5, 60, 4, generator=torch.Generator().manual_seed(1))
     a = generic.emulate(pooled, p, x, logits=True)

@@ -1,4 +1,4 @@
-"""Kernel time of the fused pooled CNN (csrc/fused_pooled.hip) for MC Dropout T=50 x 16384 windows,
+"""Kernel time of the fused pooled CNN (csrc/fused_tiled.hip) for MC Dropout T=50 x 16384 windows,
 dropout on / off (APNEAUQ_SO_PATH selects a probe build)."""
 import dataclasses
 import json

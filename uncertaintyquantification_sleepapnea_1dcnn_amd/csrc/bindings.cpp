@@ -17,10 +17,10 @@ hipError_t launch_fused_forward(const void* x, const uint8_t* blob, long long bl
                                 const float* dscale, int grid, hipStream_t stream);
 int fused_blob_bytes();
 int fused_lds_bytes();
-hipError_t launch_fused_pooled(const void* x, const uint8_t* blob, long long blob_stride, float* out, int n_win,
-                               int n_pass, int n_member, unsigned window_offset, unsigned pass_offset,
-                               unsigned long long seed, int dropout, int out_logits, const unsigned* thr,
-                               hipStream_t stream);
+hipError_t launch_fused_tiled(int net, const void* x, const uint8_t* blob, long long blob_stride, float* out,
+                              int n_win, int n_pass, int n_member, unsigned window_offset, unsigned pass_offset,
+                              unsigned long long seed, int dropout, int out_logits, const unsigned* thr,
+                              hipStream_t stream);
 int fused_pooled_lds_bytes();
 void fused_layout(int* woffs, int* eoffs, int* dense_off);
 hipError_t launch_uq_reduce(const float* probs, int t_count, int n, float* out, hipStream_t stream);
@@ -107,22 +107,25 @@ inline void check(hipError_t e, const char* what) {
   TORCH_CHECK(e == hipSuccess, what, " failed: ", hipGetErrorString(e));
 }
 
-// pooled = false: fused_forward.hip (the reference no-pool CNN); true: fused_pooled.hip (MaxPool1D(2)
-// after blocks 1-5).  Same (N, 60, 4) input, same parameter blob.
+// net -1: fused_forward.hip (the reference no-pool CNN); 0 / 1: fused_tiled.hip (MaxPool1D(2) after
+// blocks 1-5 / the (30, 1) single-channel window).  Same parameter blob.
 at::Tensor fused_forward_impl(const at::Tensor& x, const at::Tensor& blob, int64_t n_pass, int64_t window_offset,
                               int64_t pass_offset, int64_t seed, bool dropout, bool out_logits, at::IntArrayRef thr,
-                              at::ArrayRef<double> dscale, int64_t grid, bool pooled) {
+                              at::ArrayRef<double> dscale, int64_t grid, int net) {
   TORCH_CHECK(x.is_cuda() && blob.is_cuda(), "fused_forward: tensors must be on the GPU");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "fused_forward: x must be contiguous bf16");
-  TORCH_CHECK(x.dim() == 3 && x.size(1) == 60 && x.size(2) == 4, "fused_forward: x must be (N, 60, 4), got ",
-              x.sizes());
+  const int64_t want_l = net == 1 ? 30 : 60, want_c = net == 1 ? 1 : 4;
+  TORCH_CHECK(x.dim() == 3 && x.size(1) == want_l && x.size(2) == want_c, "fused_forward: x must be (N, ", want_l,
+              ", ", want_c, "), got ", x.sizes());
   TORCH_CHECK(blob.scalar_type() == at::kByte && blob.dim() == 2 && blob.is_contiguous(),
               "fused_forward: blob must be contiguous uint8 (members, bytes)");
   TORCH_CHECK(blob.size(1) == apneauq::fused_blob_bytes(), "fused_forward: blob has ", blob.size(1),
               " bytes per member, kernel expects ", apneauq::fused_blob_bytes());
   TORCH_CHECK(thr.size() == 6 && dscale.size() == 6, "fused_forward: need 6 dropout thresholds/scales");
   TORCH_CHECK(n_pass >= 1, "fused_forward: n_pass >= 1");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(blob.data_ptr()) % 16 == 0,
+  // x: 16-B vector loads except for the single-channel net (element loads into its im2col rows)
+  TORCH_CHECK((net == 1 || reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0) &&
+                  reinterpret_cast<uintptr_t>(blob.data_ptr()) % 16 == 0,
               "fused_forward: 16-B alignment required");
   const int64_t n_win = x.size(0), n_member = blob.size(0);
   TORCH_CHECK(n_pass * n_win < (int64_t(1) << 31), "fused_forward: too many samples for one launch");
@@ -135,12 +138,12 @@ at::Tensor fused_forward_impl(const at::Tensor& x, const at::Tensor& blob, int64
     t[i] = static_cast<unsigned>(thr[i]);
     d[i] = static_cast<float>(dscale[i]);
   }
-  if (pooled)
-    check(apneauq::launch_fused_pooled(x.data_ptr(), blob.data_ptr<uint8_t>(), blob.stride(0), out.data_ptr<float>(),
-                                       (int)n_win, (int)n_pass, (int)n_member, (unsigned)window_offset,
-                                       (unsigned)pass_offset, (unsigned long long)seed, dropout ? 1 : 0,
-                                       out_logits ? 1 : 0, t, cur_stream()),
-          "fused_pooled_forward");
+  if (net >= 0)
+    check(apneauq::launch_fused_tiled(net, x.data_ptr(), blob.data_ptr<uint8_t>(), blob.stride(0),
+                                      out.data_ptr<float>(), (int)n_win, (int)n_pass, (int)n_member,
+                                      (unsigned)window_offset, (unsigned)pass_offset, (unsigned long long)seed,
+                                      dropout ? 1 : 0, out_logits ? 1 : 0, t, cur_stream()),
+          "fused_tiled_forward");
   else
     check(apneauq::launch_fused_forward(x.data_ptr(), blob.data_ptr<uint8_t>(), blob.stride(0), out.data_ptr<float>(),
                                         (int)n_win, (int)n_pass, (int)n_member, (unsigned)window_offset,
@@ -154,14 +157,19 @@ at::Tensor fused_forward(const at::Tensor& x, const at::Tensor& blob, int64_t n_
                          int64_t pass_offset, int64_t seed, bool dropout, bool out_logits, at::IntArrayRef thr,
                          at::ArrayRef<double> dscale, int64_t grid) {
   return fused_forward_impl(x, blob, n_pass, window_offset, pass_offset, seed, dropout, out_logits, thr, dscale, grid,
-                            false);
+                            -1);
 }
 
 at::Tensor fused_pooled_forward(const at::Tensor& x, const at::Tensor& blob, int64_t n_pass, int64_t window_offset,
                                 int64_t pass_offset, int64_t seed, bool dropout, bool out_logits, at::IntArrayRef thr,
                                 at::ArrayRef<double> dscale) {
-  return fused_forward_impl(x, blob, n_pass, window_offset, pass_offset, seed, dropout, out_logits, thr, dscale, 0,
-                            true);
+  return fused_forward_impl(x, blob, n_pass, window_offset, pass_offset, seed, dropout, out_logits, thr, dscale, 0, 0);
+}
+
+at::Tensor fused_single_forward(const at::Tensor& x, const at::Tensor& blob, int64_t n_pass, int64_t window_offset,
+                                int64_t pass_offset, int64_t seed, bool dropout, bool out_logits, at::IntArrayRef thr,
+                                at::ArrayRef<double> dscale) {
+  return fused_forward_impl(x, blob, n_pass, window_offset, pass_offset, seed, dropout, out_logits, thr, dscale, 0, 1);
 }
 
 at::Tensor uq_reduce(const at::Tensor& probs) {
@@ -781,6 +789,8 @@ TORCH_LIBRARY(apneauq, m) {
         "bool dropout, bool out_logits, int[] thr, float[] dscale, int grid) -> Tensor");
   m.def("fused_pooled_forward(Tensor x, Tensor blob, int n_pass, int window_offset, int pass_offset, int seed, "
         "bool dropout, bool out_logits, int[] thr, float[] dscale) -> Tensor");
+  m.def("fused_single_forward(Tensor x, Tensor blob, int n_pass, int window_offset, int pass_offset, int seed, "
+        "bool dropout, bool out_logits, int[] thr, float[] dscale) -> Tensor");
   m.def("uq_reduce(Tensor probs) -> Tensor");
   m.def("bootstrap(Tensor metrics, Tensor y, Tensor? idx, int seed, int n_boot) -> Tensor");
   m.def("bootstrap_partial(Tensor metrics, Tensor y, Tensor? idx, int seed, int n_boot, int n_global, int lo) -> Tensor");
@@ -823,6 +833,7 @@ TORCH_LIBRARY(apneauq, m) {
 TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
   m.impl("fused_forward", &fused_forward);
   m.impl("fused_pooled_forward", &fused_pooled_forward);
+  m.impl("fused_single_forward", &fused_single_forward);
   m.impl("uq_reduce", &uq_reduce);
   m.impl("bootstrap", &bootstrap);
   m.impl("bootstrap_partial", &bootstrap_partial);

@@ -33,11 +33,23 @@ POOLED_PATTERN = (True, True, True, True, True, False)
 
 
 def pooled_supported(spec: ModelSpec) -> bool:
-    """True if ``csrc/fused_pooled.hip`` implements this architecture: the reference CNN with
-    MaxPool1D(2) after blocks 1-5 (the pooling lines of train_deep_ensemble_cnns.py:36-66)."""
+    """True if ``csrc/fused_tiled.hip`` (PooledNet) implements this architecture: the reference CNN
+    with MaxPool1D(2) after blocks 1-5 (the pooling lines of train_deep_ensemble_cnns.py:36-66)."""
     return (spec.input_length == FUSED_LENGTH and tuple(spec.channels()) == FUSED_CHANNELS
             and tuple(b.kernel_size for b in spec.blocks) == FUSED_KSIZES
             and tuple(bool(b.pool) for b in spec.blocks) == POOLED_PATTERN)
+
+
+def single30_supported(spec: ModelSpec) -> bool:
+    """True if ``csrc/fused_tiled.hip`` (Single30Net) implements this architecture: the reference
+    filters / kernel sizes on the north star's 30 s single-channel window, no pooling."""
+    return (spec.input_length == 30 and tuple(spec.channels()) == (1,) + FUSED_CHANNELS[1:]
+            and tuple(b.kernel_size for b in spec.blocks) == FUSED_KSIZES and not spec.has_pool)
+
+
+def tiled_net(spec: ModelSpec) -> Optional[int]:
+    """Net id of ``csrc/fused_tiled.hip`` for this spec (0 pooled, 1 single-channel 30 s), else None."""
+    return 0 if pooled_supported(spec) else 1 if single30_supported(spec) else None
 
 
 _WARNED = set()
@@ -128,9 +140,9 @@ def pack_blob(spec: ModelSpec, p, bn_override: Optional[Sequence] = None) -> tor
     ``bn_override``: optional list of 6 (scale, shift) pairs replacing the running-stat BN affine
     (used by the batch-statistics MC-Dropout parity mode).
     """
-    if not (supports(spec) or pooled_supported(spec)):
-        raise ValueError("fused kernels support only the reference (60, 4) architecture, without pooling or "
-                         "with MaxPool1D(2) after blocks 1-5")
+    if not (supports(spec) or tiled_net(spec) is not None):
+        raise ValueError("fused kernels support only the reference filters / kernel sizes on a (60, 4) window "
+                         "(without pooling or with MaxPool1D(2) after blocks 1-5) or a (30, 1) window")
     lay = layout()
     dev = p["conv1d_1/kernel"].device
     blob = torch.zeros(lay["bytes"], dtype=torch.uint8, device=dev)

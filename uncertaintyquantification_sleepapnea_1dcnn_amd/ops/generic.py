@@ -5,10 +5,10 @@ spec can express -- the opt-in ``MaxPool1D(2)`` blocks (the thes
 ``ensemble_cnn`` models), other window shapes such as the north-star "30 s single-channel"
 ``ModelSpec(30, 1)``, other filter counts and odd kernel sizes -- runs here: one MFMA launch per
 block (bias + ReLU + BN(running) + pool + counter-based dropout fused into its epilogue) and one
-GAP + Dense head launch, with bf16 activations between blocks.  The pooled reference CNN (MaxPool1D
-after blocks 1-5, :func:`fused.pooled_supported`) instead runs the fused whole-network kernel
-``csrc/fused_pooled.hip`` (8 samples per workgroup, activations in LDS, one launch); set
-``APNEAUQ_POOLED_FUSED=0`` to force the layer-wise kernels (A/B runs).
+GAP + Dense head launch, with bf16 activations between blocks.  Two variants of the reference CNN
+instead run a fused whole-network kernel (``csrc/fused_tiled.hip``, multi-sample tiles, activations
+in LDS, one launch; :func:`fused.tiled_net`): MaxPool1D after blocks 1-5, and the north star's 30 s
+single-channel window.  ``APNEAUQ_TILED_FUSED=0`` forces the layer-wise kernels (A/B runs).
 
 Dropout masks are the same pure function of (seed, layer, pass, window, t, channel) as everywhere
 else (``ops/rng.py``), so results match the fp32 reference's masks exactly and do not depend on
@@ -54,25 +54,30 @@ def pack(spec: ModelSpec, p) -> Dict[str, object]:
     dense_w = p["output_layer/kernel"].float().reshape(-1).to(dev).contiguous()
     dense_b = float(p["output_layer/bias"].float().reshape(-1)[0])
     out = {"blocks": blocks, "dense_w": dense_w, "dense_b": dense_b}
-    if fused.pooled_supported(spec) and os.environ.get("APNEAUQ_POOLED_FUSED", "1") != "0":
-        out["pooled_blob"] = fused.pack_blob(spec, p).unsqueeze(0)
+    if _tiled_enabled(spec):
+        out["tiled_blob"] = fused.pack_blob(spec, p).unsqueeze(0)
     return out
 
 
-_MAX_SAMPLES = 1 << 31  # samples per fused-pooled launch (32-bit sample / tile ids)
+def _tiled_enabled(spec: ModelSpec) -> bool:
+    return fused.tiled_net(spec) is not None and os.environ.get("APNEAUQ_TILED_FUSED", "1") != "0"
 
 
-def _pooled_forward(packed, spec: ModelSpec, x: torch.Tensor, n_pass: int, dropout: bool, seed: int,
-                    window_offset: int, pass_offset: int, logits: bool) -> torch.Tensor:
-    """(n_pass, N) through ``csrc/fused_pooled.hip``; launches split so that one holds < 2^31 samples
+_MAX_SAMPLES = 1 << 31  # samples per fused-tiled launch (32-bit sample / tile ids)
+
+
+def _tiled_forward(packed, spec: ModelSpec, x: torch.Tensor, n_pass: int, dropout: bool, seed: int,
+                   window_offset: int, pass_offset: int, logits: bool) -> torch.Tensor:
+    """(n_pass, N) through ``csrc/fused_tiled.hip``; launches split so that one holds < 2^31 samples
     (masks are keyed by global pass / window ids, so the split does not change the result)."""
     o = _ext.ops()
+    launch = o.fused_pooled_forward if fused.tiled_net(spec) == 0 else o.fused_single_forward
     thr, dsc = fused.dropout_tables(spec)
     s63 = int(seed) & ((1 << 63) - 1)
-    blob = packed["pooled_blob"]
+    blob = packed["tiled_blob"]
     n = x.shape[0]
     if not dropout:  # deterministic: every pass is identical
-        y = o.fused_pooled_forward(x, blob, 1, int(window_offset), 0, s63, False, bool(logits), thr, dsc)[0, 0]
+        y = launch(x, blob, 1, int(window_offset), 0, s63, False, bool(logits), thr, dsc)[0, 0]
         return y.unsqueeze(0).expand(n_pass, n).contiguous()
     out = torch.empty(n_pass, n, dtype=torch.float32, device=x.device)
     wc = min(n, _MAX_SAMPLES // 2)
@@ -81,8 +86,8 @@ def _pooled_forward(packed, spec: ModelSpec, x: torch.Tensor, n_pass: int, dropo
         w1 = min(n, w0 + wc)
         for p0 in range(0, n_pass, pc):
             p1 = min(n_pass, p0 + pc)
-            out[p0:p1, w0:w1] = o.fused_pooled_forward(x[w0:w1], blob, p1 - p0, int(window_offset) + w0,
-                                                       int(pass_offset) + p0, s63, True, bool(logits), thr, dsc)[0]
+            out[p0:p1, w0:w1] = launch(x[w0:w1], blob, p1 - p0, int(window_offset) + w0, int(pass_offset) + p0, s63,
+                                       True, bool(logits), thr, dsc)[0]
     return out
 
 
@@ -109,8 +114,8 @@ def forward(packed, spec: ModelSpec, x_bf16: torch.Tensor, *, n_pass: int = 1, d
     if n == 0:
         return out
     x = x_bf16.contiguous()
-    if "pooled_blob" in packed:
-        return _pooled_forward(packed, spec, x, n_pass, dropout, seed, window_offset, pass_offset, logits)
+    if "tiled_blob" in packed:
+        return _tiled_forward(packed, spec, x, n_pass, dropout, seed, window_offset, pass_offset, logits)
     widest = max(ln * c for ln, c in zip(spec.lengths(), spec.channels()))
     per_pass = max(1, n * widest)
     pc = max(1, min(n_pass, _CHUNK_ELEMS // per_pass))
@@ -139,9 +144,9 @@ def emulate(spec: ModelSpec, p, x: torch.Tensor, *, dropout: bool = False, seed:
     """CPU emulation of the generic kernels' arithmetic (bf16 operands and activations, fp32
     accumulation, folded epilogue) -- the tight oracle for the GPU tests.  ``last_fp32``: the last
     block's output feeds the head in fp32 (the fused kernels; default: whenever :func:`forward`
-    takes the fused pooled kernel for ``spec``)."""
+    takes a fused kernel for ``spec``)."""
     if last_fp32 is None:
-        last_fp32 = fused.pooled_supported(spec) and os.environ.get("APNEAUQ_POOLED_FUSED", "1") != "0"
+        last_fp32 = _tiled_enabled(spec)
     from ..models.reference import conv1d_same
 
     n = x.shape[0]
