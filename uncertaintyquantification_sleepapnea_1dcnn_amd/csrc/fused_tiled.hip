@@ -144,7 +144,8 @@ constexpr bool geometry_ok() {
   if (L >= 1 && N::NG[L] > 1 && G::SPG * G::SOUT * G::SO > (G::SPG * N::SIN[L] - G::PAD) * G::SI) return false;
   if (L >= 1 && N::NS * N::SIN[L] * G::SI > Lay<N>::max_act()) return false;
   // GAP head: a wave's rows are whole samples (two row tiles each)
-  if (L == 5 && !rowhead && (N::OPS[5] != 32 || N::NG[5] != 1 || N::HALF[5] || G::NRW % 2 != 0)) return false;
+  if (L == 5 && !rowhead && (N::OPS[5] % 16 != 0 || N::NG[5] != 1 || N::HALF[5] || G::NRW % (N::OPS[5] / 16) != 0))
+    return false;
   return true;
 }
 template <class N>
@@ -301,7 +302,8 @@ __device__ __forceinline__ void block(const Ctx X) {
 
     // ---- epilogue: bias + ReLU + BN (one fma + med3), pool, dropout; bf16 in place / dense head
     if constexpr (!G::FIRST) __syncthreads();  // every wave finished reading this group's input rows
-    constexpr int NHP = (ROWHEAD || NRW < 2) ? 1 : NRW / 2;
+    constexpr int RPS = OPSL / 16 > 0 ? OPSL / 16 : 1;  // GAP head: row tiles per sample
+    constexpr int NHP = (ROWHEAD || NRW < RPS) ? 1 : NRW / RPS;
     float hp[NHP];  // HEAD: logit partials (ROWHEAD: of sample m; GAP: per sample of the wave)
 #pragma unroll
     for (int i = 0; i < NHP; ++i) hp[i] = 0.f;
@@ -358,9 +360,9 @@ __device__ __forceinline__ void block(const Ctx X) {
           const int row = rt_of(r) * 16 + m;
           const int smp = row / OPSL, t = row - smp * OPSL;
           if constexpr (DROP) drop4(v, keys[smp], (unsigned)t, (unsigned)co0, X.thr);
-          if constexpr (G::HEAD) {  // GAP: this lane's share of sample (r / 2) of the wave's rows
+          if constexpr (G::HEAD) {  // GAP: this lane's share of sample (r / RPS) of the wave's rows
             const float gsum = v[0] * dw[0] + v[1] * dw[1] + v[2] * dw[2] + v[3] * dw[3];
-            hp[r / 2] += t < N::LOUT[L] ? gsum : 0.f;
+            hp[r / RPS] += t < N::LOUT[L] ? gsum : 0.f;
           } else if (t < N::LOUT[L]) {
             *reinterpret_cast<bf16x4*>(act + (smp * G::SOUT + t) * G::SO + co0 * 2) =
                 bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
@@ -374,13 +376,13 @@ __device__ __forceinline__ void block(const Ctx X) {
       p += __shfl_xor(p, 32, kWave);
       if (h == 0 && m < NS) head[wave * NS + m] = p;
     } else if constexpr (G::HEAD) {
-      // per sample of the wave: sum over its 32 rows (2 tiles x 16 lanes) and the 4 channel quarters
+      // per sample of the wave: sum over its rows (RPS tiles x 16 lanes) and the 4 channel quarters
 #pragma unroll
-      for (int i = 0; i < NRW / 2; ++i) {
+      for (int i = 0; i < NHP; ++i) {
         float p = group16_sum(hp[i]);
         p += __shfl_xor(p, 16, kWave);
         p += __shfl_xor(p, 32, kWave);
-        if (lane == 0) head[(rt_of(2 * i) / 2) * G::NWC + wc] = p;  // [sample][wave column]
+        if (lane == 0) head[(rt_of(RPS * i) / RPS) * G::NWC + wc] = p;  // [sample][wave column]
       }
     } else {
       // the zero rows LOUT .. SOUT-1 of this group's output slots (the next block's padding)
@@ -439,15 +441,17 @@ __global__ __launch_bounds__(kThreads, 2) void fused_tiled_kernel(Args A) {
   } else {
     // NS input windows: L x CIN0 bf16 + zero rows per X0ROWS-row slot, one 16-B chunk per thread
     constexpr int CPS = N::X0ROWS * N::CIN0 * 2 / 16, CVAL = N::L * N::CIN0 * 2 / 16;  // chunks per slot / valid
-    static_assert(NS * CPS == kThreads && N::L * N::CIN0 * 2 % 16 == 0, "one x0 chunk per thread");
-    const int sl = threadIdx.x / CPS, chk = threadIdx.x % CPS;
-    const long long gs = (long long)tile * NS + sl;
-    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (chk < CVAL && gs < samples) {
-      const int win = (int)(gs % A.n_win);
-      v = reinterpret_cast<const f32x4*>(A.x + (long long)win * (N::L * N::CIN0))[chk];
+    static_assert(NS * CPS <= kThreads && N::L * N::CIN0 * 2 % 16 == 0, "one x0 chunk per thread");
+    if (threadIdx.x < NS * CPS) {
+      const int sl = threadIdx.x / CPS, chk = threadIdx.x % CPS;
+      const long long gs = (long long)tile * NS + sl;
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (chk < CVAL && gs < samples) {
+        const int win = (int)(gs % A.n_win);
+        v = reinterpret_cast<const f32x4*>(A.x + (long long)win * (N::L * N::CIN0))[chk];
+      }
+      reinterpret_cast<f32x4*>(x0 + (Y::kX0Lead + sl * N::X0ROWS) * Y::kX0RowB)[chk] = v;
     }
-    reinterpret_cast<f32x4*>(x0 + (Y::kX0Lead + sl * N::X0ROWS) * Y::kX0RowB)[chk] = v;
   }
   // per-(block, sample) dropout keys: the same (seed, layer, pass, window) streams as every path
   if (DROP && threadIdx.x < 6 * NS) {
@@ -532,7 +536,9 @@ hipError_t launch(const void* x, const uint8_t* blob, long long blob_stride, flo
 
 int fused_pooled_lds_bytes() { return tiled::Lay<tiled::PooledNet>::kLdsBytes; }
 
-// net 0: the pooled (60, 4) CNN; net 1: the (30, 1) single-channel CNN
+// net 0: the pooled (60, 4) CNN; net 1: the (30, 1) single-channel CNN.  (The (60, 4) no-pool CNN on
+// this template -- 2 samples x 64 rows, results within 2e-7 of fused_forward.hip -- ran MCD T=50 x 16384
+// in 71.2 ms against 66.2 ms there: profiles/pooled_fused_r3.md.)
 hipError_t launch_fused_tiled(int net, const void* x, const uint8_t* blob, long long blob_stride, float* out,
                               int n_win, int n_pass, int n_member, unsigned window_offset, unsigned pass_offset,
                               unsigned long long seed, int dropout, int out_logits, const unsigned* thr,
