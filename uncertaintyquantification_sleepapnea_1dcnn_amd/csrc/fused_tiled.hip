@@ -307,6 +307,13 @@ __device__ __forceinline__ void block(const Ctx X) {
     float hp[NHP];  // HEAD: logit partials (ROWHEAD: of sample m; GAP: per sample of the wave)
 #pragma unroll
     for (int i = 0; i < NHP; ++i) hp[i] = 0.f;
+    // dropout keys of this lane's rows, read from LDS once for all channel tiles
+    unsigned keyr[NRW];
+#pragma unroll
+    for (int r = 0; r < NRW; ++r) {
+      const int row = rt_of(r) * 16 + m;
+      keyr[r] = DROP ? keys[ROWHEAD ? (m < NS ? m : 0) : row / OPSL] : 0u;
+    }
 #pragma unroll
     for (int c = 0; c < NFL_A; ++c) {
       if (!ct_ok(c)) break;  // wave-uniform
@@ -336,7 +343,7 @@ __device__ __forceinline__ void block(const Ctx X) {
           const int row = rt_of(r) * 16 + m;
           const int smp = row / OPSL, tp = (row - smp * OPSL) >> 1;
           if constexpr (DROP) {
-            const unsigned bits = dropout_bits2(keys[smp], (unsigned)tp, (unsigned)ch);
+            const unsigned bits = dropout_bits2(keyr[r], (unsigned)tp, (unsigned)ch);
             x0v = (bits & 0xFFFFu) >= X.thr ? x0v : 0.f;
             x1v = (bits >> 16) >= X.thr ? x1v : 0.f;
           }
@@ -354,12 +361,12 @@ __device__ __forceinline__ void block(const Ctx X) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = __builtin_amdgcn_fmed3f(__builtin_fmaf(v[i], sc[i], sh[i]), lo[i], hi[i]);
         if constexpr (ROWHEAD) {  // one row per sample: rows m < NS are the samples
-          if constexpr (DROP) drop4(v, keys[m < NS ? m : 0], 0u, (unsigned)co0, X.thr);
+          if constexpr (DROP) drop4(v, keyr[r], 0u, (unsigned)co0, X.thr);
           hp[0] += m < NS ? v[0] * dw[0] + v[1] * dw[1] + v[2] * dw[2] + v[3] * dw[3] : 0.f;
         } else {
           const int row = rt_of(r) * 16 + m;
           const int smp = row / OPSL, t = row - smp * OPSL;
-          if constexpr (DROP) drop4(v, keys[smp], (unsigned)t, (unsigned)co0, X.thr);
+          if constexpr (DROP) drop4(v, keyr[r], (unsigned)t, (unsigned)co0, X.thr);
           if constexpr (G::HEAD) {  // GAP: this lane's share of sample (r / RPS) of the wave's rows
             const float gsum = v[0] * dw[0] + v[1] * dw[1] + v[2] * dw[2] + v[3] * dw[3];
             hp[r / RPS] += t < N::LOUT[L] ? gsum : 0.f;

@@ -133,7 +133,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& A, f32x4 (&acc)[kC
       }
       if (A.pool) {  // MaxPool1D(2, valid) after BN: rows t and t^1 live in lanes l and l^1
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i], __shfl_xor(v[i], 1, kWave));
+        for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i], dpp_mov<0xB1>(v[i]));  // DPP quad_perm [1,0,3,2]
       }
       if (A.dropout) {
         const unsigned b01 = dropout_bits2(key, (unsigned)tout, (unsigned)co0);
