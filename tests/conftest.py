@@ -22,3 +22,17 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture
+def deterministic():
+    """Deterministic HIP training (``ops/train_ops.set_deterministic``): every cross-workgroup sum of
+    the reference-architecture and generic training kernels in a fixed order, so equivalent step
+    sequences (eager / graph replay / member-batched / concurrent) give bitwise-identical results."""
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import _ext, train_ops
+
+    _ext.require()
+    old = train_ops.DETERMINISTIC
+    train_ops.set_deterministic(True)
+    yield
+    train_ops.set_deterministic(old)

@@ -138,12 +138,26 @@ def test_uq_api_sharded_equals_single_process(bn_mode):
 
 
 def _boot_sharded(rank, world, parity):
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.uq import distributed as D
     from uncertaintyquantification_sleepapnea_1dcnn_amd.uq import uq_techniques as U
 
-    rs = np.random.RandomState(5)
-    p = rs.rand(6, 41).astype(np.float32)
-    y = (rs.rand(41) > 0.6).astype(np.int64)
-    return U.bootstrap_metrics(p, y, 17, random_state=9, parity=parity, device="cpu")
+    calls = []
+    real = D.bootstrap_sharded
+
+    def spy(*a, **k):  # the sharded branch (partial sums + all-reduce) must be the one that ran
+        calls.append(1)
+        return real(*a, **k)
+
+    D.bootstrap_sharded = spy
+    try:
+        rs = np.random.RandomState(5)
+        p = rs.rand(6, 41).astype(np.float32)
+        y = (rs.rand(41) > 0.6).astype(np.int64)
+        out = U.bootstrap_metrics(p, y, 17, random_state=9, parity=parity, device="cpu", distributed=True)
+    finally:
+        D.bootstrap_sharded = real
+    assert calls == [1], calls
+    return out
 
 
 @pytest.mark.parametrize("parity", [True, False])

@@ -125,45 +125,46 @@ def test_hip_training_reduces_loss():
     assert h.history["val_accuracy"][-1] > 0.8
 
 
-def test_graphed_training_step_matches_eager(monkeypatch):
+def _four_steps(monkeypatch, graph, x, y):
+    monkeypatch.setenv("APNEAUQ_TRAIN_GRAPH", graph)
+    m = AlarconCNN1D(seed=3, device="cuda")
+    losses = [float(m.train_step(x[i * 64:(i + 1) * 64], y[i * 64:(i + 1) * 64])) for i in range(4)]
+    if graph == "1":
+        assert 64 in getattr(m, "_train_graphs", {})  # the graph path really ran
+    return losses, m.store.flat.clone(), m.store.stats.clone(), (m.optimizer.iterations, m._train_step_counter)
+
+
+def test_graphed_training_step_matches_eager(monkeypatch, deterministic):
     """The HIP-graph replay of the training step (device-side dropout pass / Adam step counters)
-    follows the eager HIP step: same losses and (up to fp32 atomic summation order) same weights."""
-    _ext.require()
+    IS the eager HIP step: in deterministic mode 4 steps give bitwise-identical losses, weights and
+    BN statistics.  In atomic mode only step 1 is compared (identical weights, masks and inputs):
+    later steps inherit the fp32 summation order of the atomics."""
     from uncertaintyquantification_sleepapnea_1dcnn_amd.data.synthetic import synthetic_windows
 
     x, y, _ = synthetic_windows(256, seed=5)
     x = torch.as_tensor(x, dtype=torch.float32).cuda()
     y = torch.as_tensor(y, dtype=torch.float32).cuda()
-    runs = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("APNEAUQ_TRAIN_GRAPH", mode)
-        m = AlarconCNN1D(seed=3, device="cuda")
-        losses = [float(m.train_step(x[i * 64:(i + 1) * 64], y[i * 64:(i + 1) * 64])) for i in range(4)]
-        runs[mode] = (losses, m.store.flat.clone(), m.optimizer.iterations, m._train_step_counter)
-        if mode == "1":
-            assert 64 in getattr(m, "_train_graphs", {})  # the graph path really ran
-    (le, we, ie, ce), (lg, wg, ig, cg) = runs["0"], runs["1"]
-    assert (ie, ce) == (ig, cg) == (4, 4)
-    assert abs(lg[0] - le[0]) < 1e-4 * abs(le[0])  # step 1: identical weights, masks, inputs
-    np.testing.assert_allclose(lg, le, rtol=5e-3, atol=1e-3)  # fp32 atomics: order-dependent sums
-    # Adam moves every weight by ~lr whatever its gradient size, so a near-zero gradient whose sign
-    # depends on the atomic summation order moves by +-lr: compare whole-vector norms, not max-abs
-    w0 = AlarconCNN1D(seed=3, device="cuda").store.flat
-    rel = ((wg - we).norm() / (we - w0).norm()).item()
-    assert rel < 0.2, rel
+    le, we, se, ce = _four_steps(monkeypatch, "0", x, y)
+    lg, wg, sg, cg = _four_steps(monkeypatch, "1", x, y)
+    assert ce == cg == (4, 4)
+    assert lg == le
+    assert torch.equal(wg, we) and torch.equal(sg, se)
+    train_ops.set_deterministic(False)
+    la, _, _, _ = _four_steps(monkeypatch, "0", x, y)
+    lb, _, _, _ = _four_steps(monkeypatch, "1", x, y)
+    assert abs(lb[0] - la[0]) < 1e-4 * abs(la[0])
 
 
-def test_fit_concurrent_on_streams_matches_sequential():
+def test_fit_concurrent_on_streams_matches_sequential(deterministic):
     """Three members trained concurrently (training/trainer.py:fit_concurrent), on HIP streams and as
-    member-batched launches, track back-to-back fits (atomics make the kernels order-nondeterministic,
-    so loss histories are compared to 2 %), and train_ensemble on one GPU uses the concurrent path."""
+    member-batched launches, ARE back-to-back fits in deterministic mode (bitwise-identical loss
+    histories and weights), and train_ensemble on one GPU uses the concurrent path."""
     import os
     import tempfile
 
     from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel.ensemble import load_ensemble_prefix, train_ensemble
     from uncertaintyquantification_sleepapnea_1dcnn_amd.training.trainer import fit_concurrent
 
-    _ext.require()
     g = torch.Generator().manual_seed(2)
     x = torch.randn(3072, 60, 4, generator=g)
     y = (x[:, :, 0].mean(1) > 0).float()
@@ -173,8 +174,9 @@ def test_fit_concurrent_on_streams_matches_sequential():
     for batched in (False, True):
         con = [AlarconCNN1D(seed=20 + i, device="cuda") for i in range(3)]
         h_con = fit_concurrent(con, x, y, batched=batched, **kw)
-        for hs, hc in zip(h_seq, h_con):
-            np.testing.assert_allclose(hc.history["loss"], hs.history["loss"], rtol=2e-2)
+        for hs, hc, ms, mc in zip(h_seq, h_con, seq, con):
+            assert hc.history["loss"] == hs.history["loss"], (batched, hc.history["loss"], hs.history["loss"])
+            assert torch.equal(mc.store.flat, ms.store.flat), batched
     with tempfile.TemporaryDirectory() as d:
         paths = train_ensemble(x.numpy(), y.numpy(), num_models=3, save_dir=d, prefix="m", name_offset=0, epochs=2,
                                batch_size=512, verbose=0, epoch_backup=False)
@@ -182,7 +184,7 @@ def test_fit_concurrent_on_streams_matches_sequential():
         assert len(load_ensemble_prefix(os.path.join(d, "m"), 3, device="cuda")) == 3
 
 
-def test_bf16_hip_training_matches_fp32_training(monkeypatch):
+def test_bf16_hip_training_matches_fp32_training(monkeypatch, deterministic):
     """bf16 HIP training tracks fp32 training: same data, seed and Keras loop (10 epochs,
     batch 1024, validation_split=0.1 -> tail slice).  Every epoch's training loss agrees within 2 %
     and the best val AUC within 0.01.  (Val LOSS is not compared: on the tail slice it is evaluated
@@ -203,8 +205,8 @@ def test_bf16_hip_training_matches_fp32_training(monkeypatch):
         res[backend] = m.fit(x, y.astype(np.float32), batch_size=1024, epochs=10, validation_split=0.1,
                              verbose=0).history
     hh, ht = res["hip"], res["torch"]
-    # 2 % relative, plus 2e-3 absolute for the late epochs (loss ~0.06), where one epoch's atomics-order
-    # noise alone moves the bf16 loss by ~1e-3 (r2 session 3: 0.0012 = 2.05 % at epoch 8)
+    # 2 % relative, plus 2e-3 absolute for the late epochs (loss ~0.06), where bf16 rounding alone moves
+    # the loss by ~1e-3 (r2 session 3: 0.0012 = 2.05 % at epoch 8; deterministic mode: reproducible)
     np.testing.assert_allclose(hh["loss"], ht["loss"], rtol=0.02, atol=2e-3)
     assert 0.9 < ht["val_auc"][-1] < 0.9999, ht["val_auc"]
     # val AUC on the tail slice swings by a few 1e-2 from epoch to epoch in BOTH backends (moving-average
@@ -214,57 +216,65 @@ def test_bf16_hip_training_matches_fp32_training(monkeypatch):
     assert abs(hh["val_auc"][-1] - ht["val_auc"][-1]) < 0.05, (hh["val_auc"], ht["val_auc"])
 
 
-def test_member_batched_step_matches_single_graphs():
-    """GraphedEnsembleStep (one member-batched launch per layer for 3 members) follows each member's
-    own graphed step: same first-step losses, and (up to fp32 atomic summation order) same losses
-    and weights after 4 steps on member-specific batches; the host / device counters advance alike."""
-    _ext.require()
-    from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import train_ops
+def _member_steps(x, y, batched: bool):
+    ms = [AlarconCNN1D(seed=10 + i, device="cuda") for i in range(3)]
+    ls = [[], [], []]
+    if batched:
+        st = train_ops.GraphedEnsembleStep(ms, 64)
+        for s in range(4):
+            out = st([x[i, s] for i in range(3)], [y[i, s] for i in range(3)])
+            for i, (loss, p) in enumerate(out):
+                ls[i].append(float(loss))
+                assert p.shape == (64,) and bool(((p > 0) & (p < 1)).all())
+    else:
+        ls = [[float(m.train_step(x[i, s], y[i, s])) for s in range(4)] for i, m in enumerate(ms)]
+    return ms, ls
 
+
+def test_member_batched_step_matches_single_graphs(deterministic):
+    """GraphedEnsembleStep (one member-batched launch per layer for 3 members) IS each member's own
+    graphed step: in deterministic mode 4 steps on member-specific batches give bitwise-identical
+    losses, weights and BN statistics, and the host / device counters advance alike.  Atomic mode:
+    the first-step losses agree (later steps inherit the atomics' summation order)."""
     g = torch.Generator().manual_seed(8)
     x = torch.randn(3, 4, 64, 60, 4, generator=g).cuda()
     y = (torch.rand(3, 4, 64, generator=g) < 0.4).float().cuda()
-    single = [AlarconCNN1D(seed=10 + i, device="cuda") for i in range(3)]
-    ls = [[float(m.train_step(x[i, s], y[i, s])) for s in range(4)] for i, m in enumerate(single)]
-    batched = [AlarconCNN1D(seed=10 + i, device="cuda") for i in range(3)]
-    st = train_ops.GraphedEnsembleStep(batched, 64)
-    lb = [[], [], []]
-    for s in range(4):
-        out = st([x[i, s] for i in range(3)], [y[i, s] for i in range(3)])
-        for i, (loss, p) in enumerate(out):
-            lb[i].append(float(loss))
-            assert p.shape == (64,) and bool(((p > 0) & (p < 1)).all())
+    single, ls = _member_steps(x, y, False)
+    batched, lb = _member_steps(x, y, True)
     for i in range(3):
         assert (batched[i].optimizer.iterations, batched[i]._train_step_counter) == (4, 4)
-        assert abs(lb[i][0] - ls[i][0]) < 1e-4 * abs(ls[i][0])
-        np.testing.assert_allclose(lb[i], ls[i], rtol=5e-3, atol=1e-3)
-        w0 = AlarconCNN1D(seed=10 + i, device="cuda").store.flat
-        rel = ((batched[i].store.flat - single[i].store.flat).norm() / (single[i].store.flat - w0).norm()).item()
-        assert rel < 0.2, rel
+        assert lb[i] == ls[i], (i, lb[i], ls[i])
+        assert torch.equal(batched[i].store.flat, single[i].store.flat), i
+        assert torch.equal(batched[i].store.stats, single[i].store.stats), i
     # members stay independent: member 1 with another seed's weights differs from member 0
     assert abs(lb[0][0] - lb[1][0]) > 1e-3
+    train_ops.set_deterministic(False)
+    _, la = _member_steps(x, y, False)
+    _, lc = _member_steps(x, y, True)
+    for i in range(3):
+        assert abs(lc[i][0] - la[i][0]) < 1e-4 * abs(la[i][0])
 
 
-def test_fit_concurrent_batched_matches_streams():
+def test_fit_concurrent_batched_matches_streams(deterministic):
     """fit_concurrent's member-batched mode (one GraphedEnsembleStep per round, tail batches and
-    members that stop early included) tracks the stream mode epoch by epoch."""
+    members that stop early included) equals the stream mode epoch by epoch, bitwise in
+    deterministic mode."""
     from uncertaintyquantification_sleepapnea_1dcnn_amd.training.callbacks import EarlyStopping
     from uncertaintyquantification_sleepapnea_1dcnn_amd.training.trainer import fit_concurrent
 
-    _ext.require()
     g = torch.Generator().manual_seed(4)
     x = torch.randn(1100, 60, 4, generator=g)
     y = (x[:, :, 0].mean(1) > 0).float()
-    hs = {}
+    hs, ws = {}, {}
     for mode in (False, True):
         ms = [AlarconCNN1D(seed=30 + i, device="cuda") for i in range(3)]
         cbs = [[EarlyStopping(monitor="loss", patience=0, min_delta=10.0)] if i == 2 else [] for i in range(3)]
         hs[mode] = fit_concurrent(ms, x, y, batched=mode, batch_size=256, epochs=3, verbose=0, shuffle=True,
                                   callbacks=cbs)
-    for a, b in zip(hs[False], hs[True]):
-        la, lb = a.history["loss"], b.history["loss"]
-        assert len(la) == len(lb)
-        np.testing.assert_allclose(lb, la, rtol=2e-2)
+        ws[mode] = [m.store.flat.clone() for m in ms]
+    for a, b, wa, wb in zip(hs[False], hs[True], ws[False], ws[True]):
+        assert a.history["loss"] == b.history["loss"], (a.history["loss"], b.history["loss"])
+        assert torch.equal(wa, wb)
     assert len(hs[True][2].history["loss"]) < 3  # the early-stopped member left the batched rounds
 
 

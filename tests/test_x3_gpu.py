@@ -133,3 +133,52 @@ def test_mcd_batch_window_chunked_equals_one_shot():
     torch.testing.assert_close(res[1][0], res[0][0], atol=1e-6, rtol=0)
     for k in res[0][1]:
         torch.testing.assert_close(res[1][1][k], res[0][1][k], atol=1e-6, rtol=1e-6)
+
+
+def _scaled_params(seed, dev, case):
+    """Weights whose BN affines put every split activation far outside the fp16 comfort range:
+    "huge": |a| ~ 1e4 (up to ~1e5 with the dropout rescale, beyond fp16's 65504); "tiny": |a| ~ 1e-6
+    (below fp16's 6e-5 normal range, where the lo half would be lost).  Conv biases / moving stats are
+    chosen so that every block keeps that scale, and the dense kernel brings the logits back to O(1)."""
+    p = _params(seed, dev)
+    for i in range(1, 7):
+        g, mv = p[f"batchnorm_{i}/gamma"], p[f"batchnorm_{i}/moving_variance"]
+        p[f"batchnorm_{i}/moving_mean"].zero_()
+        if case == "huge":
+            g.fill_(1e4)
+            mv.fill_(1.0 if i == 1 else 1e8)  # running BN: R_l ~ 1e4 -> a_l ~ 1e4
+        else:
+            g.fill_(1e-6 if i == 1 else SPEC.bn_epsilon ** 0.5)  # a_1 ~ 1e-6; then a_l ~ R_l ~ 1e-6
+            mv.fill_(1.0 if i == 1 else 0.0)
+            p[f"batchnorm_{i}/beta"].zero_()
+            p[f"conv1d_{i}/bias"].zero_()
+    p["output_layer/kernel"].mul_(1e-4 if case == "huge" else 1e6)
+    return p
+
+
+@pytest.mark.parametrize("case", ["huge", "tiny"])
+def test_range_safe_activation_split(case):
+    """the fp16 hi/lo split of each block's input is prescaled by a power of two
+    derived from the tracked channel maxima of the block's ReLU output (ops/x3.py, x3_aff), so BN
+    gamma = 1e4 and 1e-6-scale activations keep the fp32-faithful precision: Deep-Ensemble logits within
+    1e-5 relative, batch-BN MC Dropout within the usual 1e-5 |dp|."""
+    _ext.require()
+    dev = torch.device("cuda")
+    x = _x(48, 21)
+    p = _scaled_params(31, dev, case)
+    model = x3.X3Model(SPEC, [p])
+    lg = x3.forward_running(model, x.to(dev), logits=True)[0, 0].cpu()
+    r, _ = _ref(p, x, return_logits=True)
+    assert torch.isfinite(lg).all()
+    rel = ((lg - r).abs() / r.abs().clamp_min(1e-3)).max().item()
+    assert rel <= 1e-5, f"{case}: DE logits max relative error {rel:.3e}"
+    pb = _scaled_params(31, dev, case)
+    pc = {k: v.detach().cpu().clone() for k, v in pb.items()}
+    ph = x3.mcd_batch(x3.X3Model(SPEC, [pb]), x.to(dev), 2, seed=3, pass_base=0, update_moving=False)
+    ids = torch.arange(x.shape[0])
+    for t in range(2):
+        ref = R.forward(SPEC, pc, x, dropout=True, bn_batch_stats=True, update_moving=False, seed=3, pass_id=t,
+                        sample_ids=ids).reshape(-1)
+        d = (ph[t].cpu() - ref).abs().max().item()
+        assert d <= BOUND, f"{case}: batch-BN MC Dropout pass {t}: max |dp| {d:.3e}"
+        assert 0.02 < ref.std().item(), "the logits must not be saturated (the test would be vacuous)"

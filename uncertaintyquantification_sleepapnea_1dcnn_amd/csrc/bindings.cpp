@@ -42,10 +42,11 @@ hipError_t train_stream_keys(unsigned* keys, const int* c, int n, unsigned long 
 hipError_t launch_generic_conv(const void* x, const void* wfrag, const float* epi, void* y, int n, int L, int cin,
                                int cout, int cout_pad, int ksize, int pool, int dropout, unsigned thr, int layer,
                                int n_win, unsigned pass_offset, unsigned window_offset, unsigned long long seed,
-                               hipStream_t stream, int mode, int in_rs, int in_off, float* stats, long long x_rows);
-hipError_t launch_gt_bn_finalize(const float* st, int C, float inv_count, const float* gamma, const float* beta,
-                                 float eps, float momentum, float* mmean, float* mvar, int update, float* bn,
-                                 hipStream_t stream);
+                               hipStream_t stream, int mode, int in_rs, int in_off, float* stats, long long x_rows,
+                               int det_slots);
+hipError_t launch_gt_bn_finalize(const float* st, int nslots, int C, float inv_count, const float* gamma,
+                                 const float* beta, float eps, float momentum, float* mmean, float* mvar, int update,
+                                 float* bn, hipStream_t stream);
 hipError_t launch_gt_apply(const void* z, const float* bn, void* out, int n, int L, int C, int pool, int out_rs,
                            int out_off, int dropout, unsigned thr, float inv_keep, unsigned skey,
                            unsigned window_offset, hipStream_t stream, const unsigned* skey_dev);
@@ -53,17 +54,18 @@ hipError_t launch_gt_bwd(int dz_mode, const void* z, const float* bn, const void
                          const float* w, float invL, int n, int L, int C, int pool, int dropout, unsigned thr,
                          float inv_keep, unsigned skey, unsigned window_offset, float* bst, const float* coef,
                          const float* gamma, void* dz, int dz_rs, int dz_off, float* gbias, hipStream_t stream,
-                         const unsigned* skey_dev);
-hipError_t launch_gt_bwd_finalize(const float* bst, int C, float inv_count, float* coef, float* ggamma, float* gbeta,
-                                  hipStream_t stream);
+                         const unsigned* skey_dev, int det_slots);
+hipError_t launch_gt_bwd_finalize(const float* bst, int nslots, int C, float inv_count, float* coef, float* ggamma,
+                                  float* gbeta, hipStream_t stream);
 hipError_t launch_metrics_update(const float* p, const float* y, long long n, const float* thr, int n_thr,
                                  unsigned long long* counts, hipStream_t stream);
 hipError_t launch_generic_head(const void* y, const float* w, float b, int n, int L, int C, int out_logits, float* out,
                                hipStream_t stream);
 hipError_t launch_gt_wgrad(const void* x, long long x_rows, const void* dz, long long R, int cin, int cout, int k,
-                           float* gw, hipStream_t st);
+                           float* gw, hipStream_t st, float* part, long long part_floats);
 hipError_t launch_gt_head(const void* h, const float* w, const float* b, const float* y, float* prob, float* dlog,
-                          float* loss, float* gw, float* gb, int n, int L, int C, float inv_gb, hipStream_t st);
+                          float* loss, float* gw, float* gb, int n, int L, int C, float inv_gb, hipStream_t st,
+                          float* part, long long part_floats);
 int gt_pack_max_blocks();
 long long train_wgrad_part_floats(int B);
 int train_det_floats(int B);
@@ -435,11 +437,11 @@ at::Tensor train_args_dev(const std::vector<at::Tensor>& ctxs, int64_t device) {
   for (const auto& c : ctxs) v.push_back(args_from_ctx(c, -1));
   const auto& a = v[0];
   for (const auto& x : v) {
-    TORCH_CHECK(x.B == a.B && x.n_win == a.n_win && x.groups == 1 && x.st_groups == a.st_groups && x.det == nullptr &&
+    TORCH_CHECK(x.B == a.B && x.n_win == a.n_win && x.groups == 1 && x.st_groups == a.st_groups && (x.det == nullptr) == (a.det == nullptr) &&
                     !x.shared0 && (x.tab == nullptr) == (a.tab == nullptr) && x.wpart != nullptr &&
                     (x.hpart == nullptr) == (a.hpart == nullptr) && x.pass_dev != nullptr,
-                "train_args_dev: member contexts must share batch size, stats groups and modes (atomic, device "
-                "counters, wgrad partials)");
+                "train_args_dev: member contexts must share batch size, stats groups and modes (atomic or "
+                "deterministic, device counters, wgrad partials)");
   }
   auto cpu = at::empty({M * (int64_t)sizeof(apneauq::train::Args)}, at::TensorOptions().dtype(at::kByte));
   std::memcpy(cpu.data_ptr(), v.data(), M * sizeof(apneauq::train::Args));
@@ -500,7 +502,7 @@ at::Tensor generic_conv(const at::Tensor& x, const at::Tensor& wfrag, const at::
   check(apneauq::launch_generic_conv(x.data_ptr(), wfrag.data_ptr(), epi.data_ptr<float>(), y.data_ptr(), (int)n, (int)L,
                                      (int)cin, (int)cout, (int)cout_pad, (int)ksize, pool ? 1 : 0, dropout ? 1 : 0,
                                      (unsigned)thr, (int)layer, (int)n_win, (unsigned)pass_offset, (unsigned)window_offset,
-                                     (unsigned long long)seed, cur_stream(), 0, (int)L, 0, nullptr, n * L),
+                                     (unsigned long long)seed, cur_stream(), 0, (int)L, 0, nullptr, n * L, 0),
         "generic_conv");
   return y;
 }
@@ -523,7 +525,7 @@ constexpr int64_t kGtSlots = 16;
 // in_off - pad .. in_off + L - 1 + pad of each sample, all of which must exist.
 void gt_conv(const at::Tensor& x, const at::Tensor& wfrag, const c10::optional<at::Tensor>& bias, at::Tensor& y,
              const c10::optional<at::Tensor>& stats, int64_t n, int64_t L, int64_t cin, int64_t cout, int64_t ksize,
-             int64_t mode, int64_t in_rs, int64_t in_off) {
+             int64_t mode, int64_t in_rs, int64_t in_off, bool det) {
   TORCH_CHECK(mode == 1 || mode == 2, "gt_conv: mode must be 1 (train) or 2 (linear)");
   TORCH_CHECK(ksize % 2 == 1 && cout % 4 == 0 && cout <= 1024 && n >= 0 && L >= 1, "gt_conv: bad shape");
   TORCH_CHECK(wfrag.is_cuda() && wfrag.scalar_type() == at::kBFloat16 && wfrag.is_contiguous() && wfrag.dim() == 4 &&
@@ -543,11 +545,13 @@ void gt_conv(const at::Tensor& x, const at::Tensor& wfrag, const c10::optional<a
     bp = bias->data_ptr<float>();
     sp = stats->data_ptr<float>();
   }
+  // deterministic mode: one plain-store slot per (workgroup, wave row); the launcher checks the count
+  const int det_slots = (mode == 1 && det) ? (int)(stats->numel() / (2 * cout)) : 0;
   TORCH_CHECK(n * L < (int64_t(1) << 31), "gt_conv: too many rows");
   const at::DeviceGuard guard(y.device());
   check(apneauq::launch_generic_conv(x.data_ptr(), wfrag.data_ptr(), bp, y.data_ptr(), (int)n, (int)L, (int)cin,
                                      (int)cout, (int)(wfrag.size(1) * 16), (int)ksize, 0, 0, 0u, 0, 1, 0u, 0u, 0ull,
-                                     cur_stream(), (int)mode, (int)in_rs, (int)in_off, sp, x.numel() / cin),
+                                     cur_stream(), (int)mode, (int)in_rs, (int)in_off, sp, x.numel() / cin, det_slots),
         "gt_conv");
 }
 
@@ -558,7 +562,9 @@ void gt_bn_finalize(const at::Tensor& st, int64_t C, double inv_count, const at:
               "gt_bn_finalize: per-channel tensors must have C elements");
   need_f32(bn, 4 * C, "gt_bn_finalize bn");
   const at::DeviceGuard guard(bn.device());
-  check(apneauq::launch_gt_bn_finalize(st.data_ptr<float>(), (int)C, (float)inv_count, gamma.data_ptr<float>(),
+  // every slot of the table is summed (in a fixed order): kGtSlots atomic copies or the deterministic slots
+  check(apneauq::launch_gt_bn_finalize(st.data_ptr<float>(), (int)(st.numel() / (2 * C)), (int)C, (float)inv_count,
+                                       gamma.data_ptr<float>(),
                                        beta.data_ptr<float>(), (float)eps, (float)momentum, mmean.data_ptr<float>(),
                                        mvar.data_ptr<float>(), update ? 1 : 0, bn.data_ptr<float>(), cur_stream()),
         "gt_bn_finalize");
@@ -595,7 +601,7 @@ void gt_bwd(bool dz_mode, const at::Tensor& z, const at::Tensor& bn, const c10::
             int64_t C, bool pool, bool dropout, int64_t thr, double inv_keep, int64_t skey, int64_t window_offset,
             const c10::optional<at::Tensor>& bst, const c10::optional<at::Tensor>& coef,
             const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& dz, int64_t dz_rs, int64_t dz_off,
-            const c10::optional<at::Tensor>& gbias, const c10::optional<at::Tensor>& skey_dev) {
+            const c10::optional<at::Tensor>& gbias, const c10::optional<at::Tensor>& skey_dev, bool det) {
   TORCH_CHECK(C % 4 == 0 && C <= 1024 && L >= 1, "gt_bwd: bad shape");
   const int64_t lout = pool ? L / 2 : L;
   need_rows(z, n * L, C, "gt_bwd z");
@@ -632,11 +638,13 @@ void gt_bwd(bool dz_mode, const at::Tensor& z, const at::Tensor& bn, const c10::
     dzp = dz->data_ptr();
     gbp = gbias->data_ptr<float>();
   }
+  // deterministic mode: workgroup b writes slot b (the grid is capped to the slot count)
+  const int det_slots = !det ? 0 : (int)(dz_mode ? gbias->numel() / C : bst->numel() / (2 * C));
   const at::DeviceGuard guard(z.device());
   check(apneauq::launch_gt_bwd(dz_mode ? 1 : 0, z.data_ptr(), bn.data_ptr<float>(), dhp, dlp, wp, (float)invL, (int)n,
                                (int)L, (int)C, pool ? 1 : 0, dropout ? 1 : 0, (unsigned)thr, (float)inv_keep,
                                (unsigned)skey, (unsigned)window_offset, bp, cp, gp, dzp, (int)dz_rs, (int)dz_off, gbp,
-                               cur_stream(), skey_dev_ptr(skey_dev)),
+                               cur_stream(), skey_dev_ptr(skey_dev), det_slots),
         "gt_bwd");
 }
 
@@ -647,38 +655,51 @@ void gt_bwd_finalize(const at::Tensor& bst, int64_t C, double inv_count, at::Ten
   TORCH_CHECK(ggamma.is_cuda() && ggamma.scalar_type() == at::kFloat && ggamma.numel() == C && gbeta.numel() == C,
               "gt_bwd_finalize: grads must have C elements");
   const at::DeviceGuard guard(coef.device());
-  check(apneauq::launch_gt_bwd_finalize(bst.data_ptr<float>(), (int)C, (float)inv_count, coef.data_ptr<float>(),
+  check(apneauq::launch_gt_bwd_finalize(bst.data_ptr<float>(), (int)(bst.numel() / (2 * C)), (int)C, (float)inv_count,
+                                        coef.data_ptr<float>(),
                                         ggamma.data_ptr<float>(), gbeta.data_ptr<float>(), cur_stream()),
         "gt_bwd_finalize");
 }
 
 // Generic wgrad (csrc/generic_wgrad.hip): gw (k, cin, cout) fp32 += sum_R x[R + tap] dz[R]; gw pre-zeroed.
-void gt_wgrad(const at::Tensor& x, const at::Tensor& dz, int64_t R, int64_t cin, int64_t cout, int64_t k, at::Tensor& gw) {
+// part (deterministic mode): fp32 scratch for the per-row-group partials, summed in order into gw.
+void gt_wgrad(const at::Tensor& x, const at::Tensor& dz, int64_t R, int64_t cin, int64_t cout, int64_t k, at::Tensor& gw,
+              const c10::optional<at::Tensor>& part) {
   need_rows(x, R + k - 1, cin, "gt_wgrad x");
   need_rows(dz, R, cout, "gt_wgrad dz");
   need_f32(gw, k * cin * cout, "gt_wgrad gw");
   TORCH_CHECK(k >= 1 && k <= 15 && cin >= 1 && cout >= 1, "gt_wgrad: 1 <= k <= 15");
   const at::DeviceGuard guard(x.device());
+  float* pp = nullptr;
+  if (part.has_value() && part->defined()) {
+    need_f32(*part, k * cin * cout, "gt_wgrad part");
+    pp = part->data_ptr<float>();
+  }
   check(apneauq::launch_gt_wgrad(x.data_ptr(), x.numel() / cin, dz.data_ptr(), R, (int)cin, (int)cout, (int)k,
-                                 gw.data_ptr<float>(), cur_stream()),
+                                 gw.data_ptr<float>(), cur_stream(), pp, pp ? part->numel() : 0),
         "gt_wgrad");
 }
 
 // Generic head (csrc/generic_wgrad.hip): GAP + Dense + BCE + dlogit + dense grads, n samples.
 void gt_head(const at::Tensor& h, const at::Tensor& w, const at::Tensor& b, const at::Tensor& y, at::Tensor& prob,
              at::Tensor& dlog, at::Tensor& loss, at::Tensor& gw, at::Tensor& gb, int64_t n, int64_t L, int64_t C,
-             double inv_gb) {
+             double inv_gb, const c10::optional<at::Tensor>& part) {
   need_rows(h, n * L, C, "gt_head h");
   need_f32(w, C, "gt_head w");
   for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&b, &loss, &gb}) need_f32(*t, 1, "gt_head scalar");
   for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&y, &prob, &dlog}) need_f32(*t, n, "gt_head per-sample");
   need_f32(gw, C, "gt_head gw");
   TORCH_CHECK(C >= 1 && C <= 4096 && L >= 1, "gt_head: bad shape");
+  float* pp = nullptr;  // deterministic mode: per-workgroup records, summed in order
+  if (part.has_value() && part->defined()) {
+    need_f32(*part, ((n + 3) / 4) * (C + 2), "gt_head part");
+    pp = part->data_ptr<float>();
+  }
   const at::DeviceGuard guard(h.device());
   check(apneauq::launch_gt_head(h.data_ptr(), w.data_ptr<float>(), b.data_ptr<float>(), y.data_ptr<float>(),
                                 prob.data_ptr<float>(), dlog.data_ptr<float>(), loss.data_ptr<float>(),
                                 gw.data_ptr<float>(), gb.data_ptr<float>(), (int)n, (int)L, (int)C, (float)inv_gb,
-                                cur_stream()),
+                                cur_stream(), pp, pp ? part->numel() : 0),
         "gt_head");
 }
 
@@ -815,18 +836,19 @@ TORCH_LIBRARY(apneauq, m) {
   m.def("generic_head(Tensor y, Tensor w, float b, bool logits) -> Tensor");
   m.def("metrics_update(Tensor p, Tensor y, Tensor thr, Tensor(a!) counts) -> ()");
   m.def("gt_conv(Tensor x, Tensor wfrag, Tensor? bias, Tensor(a!) y, Tensor(b!)? stats, int n, int L, int cin, "
-        "int cout, int ksize, int mode, int in_rs, int in_off) -> ()");
+        "int cout, int ksize, int mode, int in_rs, int in_off, bool det=False) -> ()");
   m.def("gt_bn_finalize(Tensor st, int C, float inv_count, Tensor gamma, Tensor beta, float eps, float momentum, "
         "Tensor(a!) mmean, Tensor(b!) mvar, bool update, Tensor(c!) bn) -> ()");
   m.def("gt_apply(Tensor z, Tensor bn, Tensor(a!) out, int n, int L, int C, bool pool, int out_rs, int out_off, "
         "bool dropout, int thr, float inv_keep, int skey, int window_offset, Tensor? skey_dev=None) -> ()");
   m.def("gt_bwd(bool dz_mode, Tensor z, Tensor bn, Tensor? dh, Tensor? dlog, Tensor? w, float invL, int n, int L, "
         "int C, bool pool, bool dropout, int thr, float inv_keep, int skey, int window_offset, Tensor(a!)? bst, "
-        "Tensor? coef, Tensor? gamma, Tensor(b!)? dz, int dz_rs, int dz_off, Tensor(c!)? gbias, Tensor? skey_dev=None) -> ()");
+        "Tensor? coef, Tensor? gamma, Tensor(b!)? dz, int dz_rs, int dz_off, Tensor(c!)? gbias, Tensor? skey_dev=None, "
+        "bool det=False) -> ()");
   m.def("gt_bwd_finalize(Tensor bst, int C, float inv_count, Tensor(a!) coef, Tensor(b!) ggamma, Tensor(c!) gbeta) -> ()");
-  m.def("gt_wgrad(Tensor x, Tensor dz, int R, int cin, int cout, int k, Tensor(a!) gw) -> ()");
+  m.def("gt_wgrad(Tensor x, Tensor dz, int R, int cin, int cout, int k, Tensor(a!) gw, Tensor(b!)? part=None) -> ()");
   m.def("gt_head(Tensor h, Tensor w, Tensor b, Tensor y, Tensor(a!) prob, Tensor(b!) dlog, Tensor(c!) loss, "
-        "Tensor(d!) gw, Tensor(e!) gb, int n, int L, int C, float inv_gb) -> ()");
+        "Tensor(d!) gw, Tensor(e!) gb, int n, int L, int C, float inv_gb, Tensor(f!)? part=None) -> ()");
   m.def("gt_pack(Tensor[] w, Tensor(a!)[] fwd, Tensor(b!)[] dgr, int[] k, int[] cin, int[] cout) -> ()");
 }
 

@@ -75,6 +75,12 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
 // Sum over the 16 lanes of a 16-lane group (lanes sharing lane>>4 = one DPP row), every lane gets
 // the sum: two quad permutes and two row rotations as v_add_f32_dpp on the VALU.  (__shfl_xor lowers
 // to ds_swizzle / ds_bpermute: four dependent LDS round trips per sum; the x3 batch-BN MC Dropout
@@ -88,6 +94,15 @@ __device__ __forceinline__ float group16_sum(float v) {
   v += dpp_mov<0x4E>(v);   // quad_perm [2, 3, 0, 1]
   v += dpp_mov<0x124>(v);  // row_ror 4
   v += dpp_mov<0x128>(v);  // row_ror 8
+  return v;
+}
+
+// Max over the 16 lanes of a 16-lane group, every lane gets it (DPP as group16_sum).
+__device__ __forceinline__ float group16_max(float v) {
+  v = fmaxf(v, dpp_mov<0xB1>(v));
+  v = fmaxf(v, dpp_mov<0x4E>(v));
+  v = fmaxf(v, dpp_mov<0x124>(v));
+  v = fmaxf(v, dpp_mov<0x128>(v));
   return v;
 }
 

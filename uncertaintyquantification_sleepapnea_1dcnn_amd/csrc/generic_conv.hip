@@ -40,7 +40,9 @@ struct ConvArgs {
   unsigned pass_offset, window_offset;
   unsigned long long seed;
   int in_rs, in_off;      // input row addressing: sample n, step t at row n * in_rs + in_off + t
-  float* stats;           // kTrain: BN moment sums (kStatSlots, 2, Cout)
+  float* stats;           // kTrain: BN moment sums (kStatSlots, 2, Cout); deterministic mode: (2 grid.x, 2, Cout),
+                          // one slot per (workgroup, wave row) written with plain stores
+  int det;
   long long x_rows;       // rows of the input buffer (staging bound)
   int lds_rows, lds_stride;  // conv_lds_kernel: staged rows, bytes per LDS row
 };
@@ -60,7 +62,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& A, f32x4 (&acc)[kC
                                               int m, int h) {
   if constexpr (MODE != kInfer) {
     // training / dgrad epilogue: no pool, no dropout; y is (N, L, Cout)
-    float* st = A.stats + (blockIdx.x % kStatSlots) * 2 * A.cout;
+    float* st = A.stats + (long long)(A.det ? blockIdx.x * 2 + (threadIdx.x >> 7) : blockIdx.x % kStatSlots) * 2 * A.cout;
 #pragma unroll
     for (int c = 0; c < kCT; ++c) {
       const int ct = ct0 + c;
@@ -97,10 +99,15 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& A, f32x4 (&acc)[kC
           s2[i] = group16_sum(s2[i]);
         }
         if (m == 0 && cok) {
+          if (A.det) {
+            *reinterpret_cast<f32x4*>(st + co0) = f32x4{s1[0], s1[1], s1[2], s1[3]};
+            *reinterpret_cast<f32x4*>(st + A.cout + co0) = f32x4{s2[0], s2[1], s2[2], s2[3]};
+          } else {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            atomicAdd(st + co0 + i, s1[i]);
-            atomicAdd(st + A.cout + co0 + i, s2[i]);
+            for (int i = 0; i < 4; ++i) {
+              atomicAdd(st + co0 + i, s1[i]);
+              atomicAdd(st + A.cout + co0 + i, s2[i]);
+            }
           }
         }
       }
@@ -369,7 +376,8 @@ __global__ __launch_bounds__(256) void head_kernel(const __bf16* y, const float*
 hipError_t launch_generic_conv(const void* x, const void* wfrag, const float* epi, void* y, int n, int L, int cin,
                                int cout, int cout_pad, int ksize, int pool, int dropout, unsigned thr, int layer,
                                int n_win, unsigned pass_offset, unsigned window_offset, unsigned long long seed,
-                               hipStream_t stream, int mode, int in_rs, int in_off, float* stats, long long x_rows) {
+                               hipStream_t stream, int mode, int in_rs, int in_off, float* stats, long long x_rows,
+                               int det_slots) {
   generic::ConvArgs A;
   A.x = reinterpret_cast<const __bf16*>(x);
   A.wfrag = reinterpret_cast<const bf16x8*>(wfrag);
@@ -405,6 +413,8 @@ hipError_t launch_generic_conv(const void* x, const void* wfrag, const float* ep
   if (rows == 0) return hipSuccess;
   constexpr int kRowsWG = 2 * generic::kRT * 16, kChWG = 2 * generic::kCT;  // 128 rows x 8 channel tiles
   const dim3 grid((unsigned)((rows + kRowsWG - 1) / kRowsWG), (unsigned)((cout_pad / 16 + kChWG - 1) / kChWG));
+  A.det = mode == generic::kTrain && det_slots > 0;
+  if (A.det && (long long)grid.x * 2 > det_slots) return hipErrorInvalidValue;  // one slot per (workgroup, wave row)
   // LDS staging when every row a workgroup can touch fits: 128 output rows span at most
   // 127 + ceil(127 / Lp) * max(0, in_rs - Lp) input rows, plus the 2 * pad halo
   const long long extra = (long long)(127 + A.Lp - 1) / A.Lp * (A.in_rs > A.Lp ? A.in_rs - A.Lp : 0);

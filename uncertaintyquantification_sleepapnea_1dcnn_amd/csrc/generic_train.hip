@@ -25,15 +25,44 @@ namespace gtrain {
 
 constexpr int kSlots = 16;  // == generic::kStatSlots
 
-__global__ void bn_finalize_kernel(const float* st, int C, float inv_count, const float* gamma, const float* beta,
-                                   float eps, float momentum, float* mmean, float* mvar, int update, float* bn) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s1 = 0.0, s2 = 0.0;
-  for (int s = 0; s < kSlots; ++s) {
-    s1 += st[s * 2 * C + c];
-    s2 += st[s * 2 * C + C + c];
+// Ordered sums of the two C-wide rows of every slot of an (nslots, 2, C) table, 16 channels x 16 slot
+// lanes per 256-thread block: lane j adds slots j, j + 16, ... in order (fp64), then the block's first
+// 16 threads add the 16 lane sums in order.  The association depends on nslots only, so the result is
+// bitwise reproducible for a fixed slot layout: atomic mode (kSlots interleaved copies, each itself an
+// atomic sum) and deterministic mode (one slot per producing workgroup, written with plain stores).
+__device__ __forceinline__ bool slot_pair_sums(const float* st, int nslots, int C, double (&red)[2][256], double& s1,
+                                               double& s2, int& c) {
+  const int chl = threadIdx.x & 15, lane = threadIdx.x >> 4;
+  c = blockIdx.x * 16 + chl;
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    for (int s = lane; s < nslots; s += 16) {
+      a += (double)st[(long long)s * 2 * C + c];
+      b += (double)st[(long long)s * 2 * C + C + c];
+    }
   }
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = b;
+  __syncthreads();
+  s1 = 0.0;
+  s2 = 0.0;
+  if (threadIdx.x >= 16 || c >= C) return false;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    s1 += red[0][j * 16 + chl];
+    s2 += red[1][j * 16 + chl];
+  }
+  return true;
+}
+
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* st, int nslots, int C, float inv_count,
+                                                          const float* gamma, const float* beta, float eps,
+                                                          float momentum, float* mmean, float* mvar, int update,
+                                                          float* bn) {
+  __shared__ double red[2][256];
+  double s1, s2;
+  int c;
+  if (!slot_pair_sums(st, nslots, C, red, s1, s2, c)) return;
   const double meand = s1 * inv_count;
   const float mean = (float)meand;
   const float var = (float)fmax(s2 * inv_count - meand * meand, 0.0);
@@ -118,6 +147,7 @@ struct BwdArgs {
   __bf16* dz;          // bwd_dz: row (n, t) at n * dz_rs + dz_off + t
   int dz_rs, dz_off;
   float* gbias;        // bwd_dz: bias-gradient slots (kSlots, C), summed by the host
+  int det;             // deterministic mode: block b writes slot b with plain stores (grid <= slots)
 };
 
 // Gradient w.r.t. the BN output y at pre-pool row (ns, t), channels c .. c+3.
@@ -219,33 +249,41 @@ __global__ __launch_bounds__(256) void bwd_kernel(BwdArgs A) {
   }
   block_reduce8(lds, acc, G, rpb);
   if (threadIdx.x < G) {
+    const int slot = A.det ? blockIdx.x : blockIdx.x % kSlots;
     if constexpr (!DZ) {
-      float* st = A.bst + (blockIdx.x % kSlots) * 2 * A.C;
+      float* st = A.bst + (long long)slot * 2 * A.C;
+      if (A.det) {
+        *reinterpret_cast<f32x4*>(st + c) = f32x4{acc[0], acc[1], acc[2], acc[3]};
+        *reinterpret_cast<f32x4*>(st + A.C + c) = f32x4{acc[4], acc[5], acc[6], acc[7]};
+      } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        atomicAdd(st + c + j, acc[j]);
-        atomicAdd(st + A.C + c + j, acc[4 + j]);
+        for (int j = 0; j < 4; ++j) {
+          atomicAdd(st + c + j, acc[j]);
+          atomicAdd(st + A.C + c + j, acc[4 + j]);
+        }
       }
     } else {
+      float* gb = A.gbias + (long long)slot * A.C + c;
+      if (A.det) {
+        *reinterpret_cast<f32x4*>(gb) = f32x4{acc[0], acc[1], acc[2], acc[3]};
+      } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) atomicAdd(A.gbias + (blockIdx.x % kSlots) * A.C + c + j, acc[j]);
+        for (int j = 0; j < 4; ++j) atomicAdd(gb + j, acc[j]);
+      }
     }
   }
 }
 
-__global__ void bwd_finalize_kernel(const float* bst, int C, float inv_count, float* coef, float* ggamma,
-                                    float* gbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float s1 = 0.f, s2 = 0.f;
-  for (int s = 0; s < kSlots; ++s) {
-    s1 += bst[s * 2 * C + c];
-    s2 += bst[s * 2 * C + C + c];
-  }
-  gbeta[c] = s1;
-  ggamma[c] = s2;
-  coef[c] = s1 * inv_count;
-  coef[C + c] = s2 * inv_count;
+__global__ __launch_bounds__(256) void bwd_finalize_kernel(const float* bst, int nslots, int C, float inv_count,
+                                                           float* coef, float* ggamma, float* gbeta) {
+  __shared__ double red[2][256];
+  double s1, s2;
+  int c;
+  if (!slot_pair_sums(bst, nslots, C, red, s1, s2, c)) return;
+  gbeta[c] = (float)s1;
+  ggamma[c] = (float)s2;
+  coef[c] = (float)(s1 * inv_count);
+  coef[C + c] = (float)(s2 * inv_count);
 }
 
 inline int elem_grid(long long items, int per_block) {
@@ -255,11 +293,11 @@ inline int elem_grid(long long items, int per_block) {
 
 }  // namespace gtrain
 
-hipError_t launch_gt_bn_finalize(const float* st, int C, float inv_count, const float* gamma, const float* beta,
-                                 float eps, float momentum, float* mmean, float* mvar, int update, float* bn,
-                                 hipStream_t stream) {
-  hipLaunchKernelGGL(gtrain::bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, st, C, inv_count, gamma,
-                     beta, eps, momentum, mmean, mvar, update, bn);
+hipError_t launch_gt_bn_finalize(const float* st, int nslots, int C, float inv_count, const float* gamma,
+                                 const float* beta, float eps, float momentum, float* mmean, float* mvar, int update,
+                                 float* bn, hipStream_t stream) {
+  hipLaunchKernelGGL(gtrain::bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, stream, st, nslots, C, inv_count,
+                     gamma, beta, eps, momentum, mmean, mvar, update, bn);
   return hipGetLastError();
 }
 
@@ -293,7 +331,7 @@ hipError_t launch_gt_bwd(int dz_mode, const void* z, const float* bn, const void
                          const float* w, float invL, int n, int L, int C, int pool, int dropout, unsigned thr,
                          float inv_keep, unsigned skey, unsigned window_offset, float* bst, const float* coef,
                          const float* gamma, void* dz, int dz_rs, int dz_off, float* gbias, hipStream_t stream,
-                         const unsigned* skey_dev) {
+                         const unsigned* skey_dev, int det_slots) {
   gtrain::BwdArgs A;
   A.skey_dev = skey_dev;
   A.z = reinterpret_cast<const __bf16*>(z);
@@ -319,10 +357,13 @@ hipError_t launch_gt_bwd(int dz_mode, const void* z, const float* bn, const void
   A.dz_rs = dz_rs;
   A.dz_off = dz_off;
   A.gbias = gbias;
+  A.det = det_slots > 0;
   const int rpb = 256 / (C / 4);
   const long long rows = (long long)n * L;
   if (rows == 0) return hipSuccess;
-  const dim3 grid(gtrain::elem_grid(rows, rpb * 4));  // ~4 rows per thread
+  int g = gtrain::elem_grid(rows, rpb * 4);  // ~4 rows per thread
+  if (A.det && g > det_slots) g = det_slots;  // one slot per block (grid-stride rows)
+  const dim3 grid(g);
   if (dz_mode)
     hipLaunchKernelGGL(gtrain::bwd_kernel<true>, grid, dim3(256), 0, stream, A);
   else
@@ -330,10 +371,10 @@ hipError_t launch_gt_bwd(int dz_mode, const void* z, const float* bn, const void
   return hipGetLastError();
 }
 
-hipError_t launch_gt_bwd_finalize(const float* bst, int C, float inv_count, float* coef, float* ggamma, float* gbeta,
-                                  hipStream_t stream) {
-  hipLaunchKernelGGL(gtrain::bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, bst, C, inv_count,
-                     coef, ggamma, gbeta);
+hipError_t launch_gt_bwd_finalize(const float* bst, int nslots, int C, float inv_count, float* coef, float* ggamma,
+                                  float* gbeta, hipStream_t stream) {
+  hipLaunchKernelGGL(gtrain::bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, stream, bst, nslots, C,
+                     inv_count, coef, ggamma, gbeta);
   return hipGetLastError();
 }
 

@@ -62,6 +62,7 @@ struct WgArgs {
   int cin, cout, k;
   int n_ci, n_co;    // ci tiles (16) / co blocks (4 * NCO tiles) of the grid
   int chunks_per_wg;
+  float* part;       // deterministic mode: (row groups, k * cin * cout) partials, plain stores (nullptr: atomics)
 };
 
 // IM2COL: M = kk = tap * cin + ci < 32 (two 16-row A tiles), one "tap".
@@ -227,7 +228,11 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(WgArgs A) {
             ci = ci0 + m;
             if (ci >= A.cin) continue;
           }
-          atomicAdd(A.gw + ((long long)tap * A.cin + ci) * A.cout + co, acc[t][mi][c][i]);
+          const long long e = ((long long)tap * A.cin + ci) * A.cout + co;
+          if (A.part != nullptr)
+            A.part[(long long)rg * A.k * A.cin * A.cout + e] = acc[t][mi][c][i];
+          else
+            atomicAdd(A.gw + e, acc[t][mi][c][i]);
         }
       }
   }
@@ -250,6 +255,7 @@ struct HeadArgs {
   float* gb;         // (1)
   int n, L, C;
   float inv_gb;
+  float* part;       // deterministic mode: per-workgroup records [loss, dense bias, dense weights (C)]
 };
 
 __global__ __launch_bounds__(256) void head_kernel(HeadArgs A) {
@@ -277,21 +283,74 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs A) {
     if (lane == 0) {
       A.prob[s] = p;
       A.dlog[s] = dl;
-      atomicAdd(A.loss, fmaxf(z, 0.f) - z * yv + log1pf(__expf(-fabsf(z))));
     }
   } else {
     for (int c = lane; c < A.C; c += 64) gap[c] = 0.f;
   }
   float* dls = hsm + 4 * A.C;
-  if (lane == 0) dls[wave] = dl;
+  float* wloss = dls + 4;
+  if (lane == 0) {
+    dls[wave] = dl;
+    wloss[wave] = s < A.n ? fmaxf(z, 0.f) - z * A.y[s] + log1pf(__expf(-fabsf(z))) : 0.f;
+  }
   __syncthreads();
+  float* rec = A.part != nullptr ? A.part + (long long)blockIdx.x * (A.C + 2) : nullptr;
   for (int c = threadIdx.x; c < A.C; c += 256) {
     float g = 0.f;
 #pragma unroll
     for (int w2 = 0; w2 < 4; ++w2) g += dls[w2] * hsm[w2 * A.C + c];
-    atomicAdd(A.gw + c, g);
+    if (rec != nullptr)
+      rec[2 + c] = g;
+    else
+      atomicAdd(A.gw + c, g);
   }
-  if (threadIdx.x == 0) atomicAdd(A.gb, dls[0] + dls[1] + dls[2] + dls[3]);
+  if (threadIdx.x == 0) {
+    const float lsum = (wloss[0] + wloss[1]) + (wloss[2] + wloss[3]);
+    const float bsum = (dls[0] + dls[1]) + (dls[2] + dls[3]);
+    if (rec != nullptr) {
+      rec[0] = lsum;
+      rec[1] = bsum;
+    } else {
+      atomicAdd(A.loss, lsum);
+      atomicAdd(A.gb, bsum);
+    }
+  }
+}
+
+// Deterministic mode: column sums of an (nrows, ncols) fp32 partial table in a fixed order, 16 columns x
+// 16 row lanes per block (lane j adds rows j, j + 16, ... in fp64, then 16 lane sums in order), written
+// to up to three consecutive column segments.
+struct RedSeg {
+  float* ptr;
+  long long cols;
+};
+struct RedDst {
+  RedSeg seg[3];
+};
+
+__global__ __launch_bounds__(256) void ordered_reduce_kernel(const float* __restrict__ part, int nrows, long long ncols,
+                                                             RedDst d) {
+  __shared__ double red[256];
+  const int cl = threadIdx.x & 15, lane = threadIdx.x >> 4;
+  const long long c = (long long)blockIdx.x * 16 + cl;
+  double a = 0.0;
+  if (c < ncols)
+    for (int r = lane; r < nrows; r += 16) a += (double)part[(long long)r * ncols + c];
+  red[threadIdx.x] = a;
+  __syncthreads();
+  if (threadIdx.x >= 16 || c >= ncols) return;
+  double s = 0.0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) s += red[j * 16 + cl];
+  long long k = c;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    if (k < d.seg[q].cols) {
+      d.seg[q].ptr[k] = (float)s;
+      return;
+    }
+    k -= d.seg[q].cols;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -363,8 +422,16 @@ static hipError_t wg_dispatch(const gwgrad::WgArgs& A, int grid, bool im2col, hi
 }
 
 // gw must be zeroed by the caller (the step zeroes the whole flat gradient).
+static hipError_t ordered_reduce(const float* part, int nrows, long long ncols, gwgrad::RedDst d, hipStream_t st) {
+  hipLaunchKernelGGL(gwgrad::ordered_reduce_kernel, dim3((unsigned)((ncols + 15) / 16)), dim3(256), 0, st, part, nrows,
+                     ncols, d);
+  return hipGetLastError();
+}
+
+// part (deterministic mode, nullable): room for part_floats partials; the row groups are capped so that
+// each writes its own (k, cin, cout) slice, then an ordered reduce writes gw.
 hipError_t launch_gt_wgrad(const void* x, long long x_rows, const void* dz, long long R, int cin, int cout, int k,
-                           float* gw, hipStream_t st) {
+                           float* gw, hipStream_t st, float* part, long long part_floats) {
   if (R <= 0) return hipSuccess;
   if (k < 1 || k > 15 || cin < 1 || cout < 1) return hipErrorInvalidValue;
   if (x_rows < R + k - 1) return hipErrorInvalidValue;  // every tap's rows must exist
@@ -377,6 +444,7 @@ hipError_t launch_gt_wgrad(const void* x, long long x_rows, const void* dz, long
   A.cin = cin;
   A.cout = cout;
   A.k = k;
+  A.part = part;
   const bool im2col = cin * k <= 32;
   // co tiles per wave: the fewest padded tile slots (4 waves x NCO per block), then the largest NCO; the
   // accumulators (k x NCO tiles) are capped so a workgroup keeps >= 2 waves per SIMD
@@ -403,26 +471,44 @@ hipError_t launch_gt_wgrad(const void* x, long long x_rows, const void* dz, long
   long long rg = 2048 / blocks;
   if (rg < 1) rg = 1;
   if (rg > (chunks + minc - 1) / minc) rg = (chunks + minc - 1) / minc;
+  const long long wfl = (long long)k * cin * cout;
+  if (part != nullptr && rg > part_floats / wfl) rg = part_floats / wfl;  // one partial slice per row group
   if (rg < 1) rg = 1;
   A.chunks_per_wg = (int)((chunks + rg - 1) / rg);
   rg = (chunks + A.chunks_per_wg - 1) / A.chunks_per_wg;
   const long long grid = blocks * rg;
   if (grid > 0x7FFFFFFF) return hipErrorInvalidValue;
+  if (part != nullptr && rg * wfl > part_floats) return hipErrorInvalidValue;
+  hipError_t e;
   switch (nco) {
-    case 1: return wg_dispatch<1>(A, (int)grid, im2col, st);
-    case 2: return wg_dispatch<2>(A, (int)grid, im2col, st);
-    case 3: return wg_dispatch<3>(A, (int)grid, im2col, st);
-    default: return wg_dispatch<4>(A, (int)grid, im2col, st);
+    case 1: e = wg_dispatch<1>(A, (int)grid, im2col, st); break;
+    case 2: e = wg_dispatch<2>(A, (int)grid, im2col, st); break;
+    case 3: e = wg_dispatch<3>(A, (int)grid, im2col, st); break;
+    default: e = wg_dispatch<4>(A, (int)grid, im2col, st); break;
   }
+  if (e != hipSuccess || part == nullptr) return e;
+  gwgrad::RedDst d = {};
+  d.seg[0] = {gw, wfl};
+  return ordered_reduce(part, (int)rg, wfl, d, st);
 }
 
+// part (deterministic mode, nullable): ceil(n / 4) * (C + 2) floats of per-workgroup records.
 hipError_t launch_gt_head(const void* h, const float* w, const float* b, const float* y, float* prob, float* dlog,
-                          float* loss, float* gw, float* gb, int n, int L, int C, float inv_gb, hipStream_t st) {
+                          float* loss, float* gw, float* gb, int n, int L, int C, float inv_gb, hipStream_t st,
+                          float* part, long long part_floats) {
   if (n <= 0) return hipSuccess;
-  gwgrad::HeadArgs A{reinterpret_cast<const __bf16*>(h), w, b, y, prob, dlog, loss, gw, gb, n, L, C, inv_gb};
-  const size_t lds = (4 * (size_t)C + 4) * sizeof(float);
-  hipLaunchKernelGGL(gwgrad::head_kernel, dim3((n + 3) / 4), dim3(256), lds, st, A);
-  return hipGetLastError();
+  const int nblk = (n + 3) / 4;
+  if (part != nullptr && (long long)nblk * (C + 2) > part_floats) return hipErrorInvalidValue;
+  gwgrad::HeadArgs A{reinterpret_cast<const __bf16*>(h), w, b, y, prob, dlog, loss, gw, gb, n, L, C, inv_gb, part};
+  const size_t lds = (4 * (size_t)C + 8) * sizeof(float);
+  hipLaunchKernelGGL(gwgrad::head_kernel, dim3(nblk), dim3(256), lds, st, A);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || part == nullptr) return e;
+  gwgrad::RedDst d = {};
+  d.seg[0] = {loss, 1};
+  d.seg[1] = {gb, 1};
+  d.seg[2] = {gw, C};
+  return ordered_reduce(part, nblk, C + 2, d, st);
 }
 
 int gt_pack_max_blocks() { return gwgrad::kMaxBlocks; }

@@ -1697,9 +1697,7 @@ struct DetDst {
   DetSeg seg[4];
 };
 
-__global__ __launch_bounds__(256) void det_reduce_kernel(const float* __restrict__ part, int n, int w, DetDst d) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= w) return;
+__device__ __forceinline__ void det_reduce_col(const float* __restrict__ part, int n, int w, const DetDst& d, int c) {
   double acc = 0.0;
   int i = 0;
   for (; i + 4 <= n; i += 4) {  // fixed association: ((r0 + r1) + (r2 + r3)) per group of four rows
@@ -1720,6 +1718,33 @@ __global__ __launch_bounds__(256) void det_reduce_kernel(const float* __restrict
     }
     k -= d.seg[q].cols;
   }
+}
+
+__global__ __launch_bounds__(256) void det_reduce_kernel(const float* __restrict__ part, int n, int w, DetDst d) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < w) det_reduce_col(part, n, w, d, c);
+}
+
+// member-batched: member blockIdx.z's partial table and destinations (from its Args) of the reduce that
+// follows op 0 (forward of layer l: the moments of block l), 1 (head: loss, dense grads, block-6
+// backward sums) or 2 (dgrad of layer l: backward sums of block l - 1); same association as the
+// single-model det_reduce_kernel, so member-batched deterministic steps equal single-model ones bitwise
+__global__ __launch_bounds__(256) void det_reduce_mb_kernel(const Args* __restrict__ Am, int op, int l, int n, int w) {
+  const Args& A = Am[blockIdx.z];
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= w) return;
+  DetDst d = {};
+  if (op == 0) {
+    d.seg[0] = {A.L[l].st, w, 1};
+  } else if (op == 1) {
+    d.seg[0] = {A.loss_sum, 1, 0};
+    d.seg[1] = {A.g_dense_b, 1, 0};
+    d.seg[2] = {A.g_dense_w, C[6], 0};
+    d.seg[3] = {A.L[5].bst, 2 * C[6], 1};
+  } else {
+    d.seg[0] = {A.L[l - 1].bst, w, 1};
+  }
+  det_reduce_col(A.det, n, w, d, c);
 }
 
 template <bool MB>
@@ -1961,7 +1986,9 @@ static void wg_launch(const Args& A, const Args* Am, int M, hipStream_t st) {
   using W = train::WgCfg<l>;
   const int nci = (l == 0) ? 1 : train::C[l] / W::CIB;
   const int nco = train::C[l + 1] / W::COB;
-  const int rgs = wg_rgs<l>(A.B, M);
+  // deterministic mode: the single-model row grouping (M = 1), so a member-batched step sums every
+  // gradient in the same order as the member's own step
+  const int rgs = wg_rgs<l>(A.B, A.det != nullptr ? 1 : M);
   hipLaunchKernelGGL(HIP_KERNEL_NAME(train::wgrad_kernel<l, MB>), dim3(nci * nco * rgs, 1, M), dim3(256), lds_wgrad<l>(),
                      st, A, Am);
   if (A.wpart != nullptr) {
@@ -2024,16 +2051,38 @@ hipError_t train_launch_finalize(const Args& A, int update_moving, int grads, hi
 // A0 = member 0's Args (host copy: sizes and flags, identical for every member), Am = the device array of
 // all M members' Args.  op: 0 fwd(layer) | 1 head(flag = backward) | 2 dgrad(layer) | 3 wgrad(layer)
 // | 4 finalize(layer = update_moving, flag = grads) | 5 forward rows of the parameter table.
-// Atomic-mode single-device training only (no deterministic partials, no shared block 1).
+// Single-device training only (no shared block 1).  Deterministic mode (every member with partial
+// tables, A0.det set): each reduction is followed by det_reduce_mb_kernel over all members.
+static hipError_t det_reduce_mb(const Args* Am, int M, int op, int l, int n, int w, hipStream_t st) {
+  hipLaunchKernelGGL(train::det_reduce_mb_kernel, dim3((w + 255) / 256, 1, M), dim3(256), 0, st, Am, op, l, n, w);
+  return hipGetLastError();
+}
+
 hipError_t train_launch_mb(const Args& A0, const Args* Am, int M, int op, int layer, int flag, hipStream_t st) {
-  if (M < 1 || M > 65535 || Am == nullptr || A0.det != nullptr || A0.shared0 || A0.groups != 1) return hipErrorInvalidValue;
+  if (M < 1 || M > 65535 || Am == nullptr || A0.shared0 || A0.groups != 1) return hipErrorInvalidValue;
+  const bool det = A0.det != nullptr;
+  if (det && A0.tab != nullptr) return hipErrorInvalidValue;
   switch (op) {
-    case 0: return fwd_launch<true>(A0, Am, M, layer, fwd_grid(A0.B), st);
-    case 1:
+    case 0: {
+      const hipError_t e = fwd_launch<true>(A0, Am, M, layer, fwd_grid(A0.B), st);
+      if (e != hipSuccess || !det) return e;
+      return det_reduce_mb(Am, M, 0, layer, fwd_grid(A0.B), 2 * train::C[layer + 1], st);
+    }
+    case 1: {
       hipLaunchKernelGGL(train::head_kernel<true>, dim3((A0.B + 3) / 4, 1, M), dim3(256), (8 * train::C[6] + 2) * 4, st, A0,
                          Am, flag);
-      return hipGetLastError();
-    case 2: return dgrad_launch<true>(A0, Am, M, layer, st);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess || !det || !flag) return e;
+      return det_reduce_mb(Am, M, 1, 0, A0.B, train::kHeadRec, st);
+    }
+    case 2: {
+      const hipError_t e = dgrad_launch<true>(A0, Am, M, layer, st);
+      if (e != hipSuccess || !det) return e;
+      static constexpr int wm[6] = {0, train::Tiling<train::C[1]>::WM, train::Tiling<train::C[2]>::WM,
+                                    train::Tiling<train::C[3]>::WM, train::Tiling<train::C[4]>::WM,
+                                    train::Tiling<train::C[5]>::WM};
+      return det_reduce_mb(Am, M, 2, layer, ((A0.B + 1) / 2) * wm[layer], 2 * train::C[layer], st);
+    }
     case 3: return wgrad_launch<true>(A0, Am, M, layer, st);
     case 4:
       hipLaunchKernelGGL(train::bn_finalize_kernel<true>, dim3(6, 1, M), dim3(256), 0, st, A0, Am, layer, flag);

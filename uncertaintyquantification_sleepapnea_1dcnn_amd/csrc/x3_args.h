@@ -6,25 +6,28 @@ namespace apneauq {
 namespace x3 {
 
 struct LayerArgs {
-  const float* in;        // R_{l-1}: [samples_in][60][CIN] fp32; sign bit = dropped (unless hash_in)
-  float* out;             // R_l [samples][60][COUT] fp32 (sign = dropped); block 6: sums [samples][2][COUT]
+  const float* in;        // R_{l-1}: [samples_in][60][CIN] fp32 ReLU output (before BN and dropout)
+  float* out;             // R_l [samples][60][COUT] fp32; block 6: masked sums [samples][2][COUT]
   const void* wfrag;      // [G][chunk][tap][ct][hi|lo][64 lanes][8] fp16
   long long w_gstride;    // 16-B fragments per weight group (0: one set shared by all groups)
   const float* bias;      // [G][COUT]
   const float* wscale;    // [G] 2^-sw (exact) undoing the host weight pre-scale
   int p_gstride;          // bias floats per weight group (0: shared; then wscale[0] too)
-  const float* aff_in;    // [G][2][CIN] BN affine of block l-1 (scale | shift) x 1/(1-p_{l-1})
+  const float* aff_in;    // [G][2][CIN] BN affine of block l-1 (scale | shift) x 1/(1-p_{l-1}) x 2^sa
   int aff_gstride;        // floats per group (0: shared)
+  const float* ascale;    // [G] 2^-sa undoing the activation prescale folded into aff_in (nullptr: 1);
+                          // indexed like aff_in (aff_gstride 0: one value)
+  unsigned* rmax;         // [G][COUT] running max of R_l (fp32 bits, R_l >= 0; nullptr: not tracked)
+  int rmax_gstride;       // COUT: one row per group; 0: one row shared by all groups (passes sharing an affine)
   double* stats;          // [G][16 slots][2][COUT] moment sums of R_l (nullptr: none)
   int n_win;              // windows per group
   int groups;
   int tiles_per_group;    // informational (the kernel derives its tiling from n_win, groups and its tile size)
   int total_tiles;
   int in_shared;          // input indexed by window only (block-1 output shared by all passes)
-  int hash_in;            // input dropout drawn from the counter hash (block-1 output carries no sign mask)
-  unsigned thr_in;        // 16-bit drop threshold of block l-1 (hash_in)
-  unsigned thr_out;       // 16-bit drop threshold of block l (0: no dropout)
-  int layer;              // 0-based index of this block (dropout stream of the output mask)
+  unsigned thr_in;        // 16-bit drop threshold of block l-1, whose mask the staging draws (0: no dropout)
+  unsigned thr_out;       // 16-bit drop threshold of block l (block 6 only: its masked sums; 0: no dropout)
+  int layer;              // 0-based index of this block (dropout streams: layer - 1 in, layer out)
   unsigned pass_base;     // dropout pass id of group 0
   unsigned window_offset;
   unsigned long long seed;
@@ -36,6 +39,7 @@ struct L1Args {
   const float* b;      // [G][128]
   float* out;          // [G][n_win][60][128]
   double* stats;       // [G][16][2][128] or nullptr
+  unsigned* rmax;      // [G][128] max of R_1 (fp32 bits) or nullptr
   int n_win, groups, blocks_per_group;
 };
 
@@ -46,6 +50,8 @@ struct AffArgs {
   float* mmean;
   float* mvar;
   float* aff;            // [G][2][C]
+  const unsigned* rmax;  // [G][C] max of the block's ReLU output (nullptr: no activation prescale)
+  float* ascale;         // [G] out: 2^-sa, the inverse of the power-of-two prescale folded into aff
   int C, groups, p_gstride, update;
   int repeat;            // moving updates per stats group (block 1 moments are shared by all passes)
   double inv_count;

@@ -44,8 +44,9 @@ int num_cus(const at::Tensor& t) {
 void x3_layer(int64_t layer, const at::Tensor& in, at::Tensor& out, const at::Tensor& wfrag, int64_t w_gstride,
               const at::Tensor& bias, const at::Tensor& wscale, int64_t p_gstride, const at::Tensor& aff_in,
               int64_t aff_gstride, const c10::optional<at::Tensor>& stats, int64_t n_win, int64_t groups,
-              bool in_shared, bool hash_in, int64_t thr_in, int64_t thr_out, int64_t seed, int64_t pass_base,
-              int64_t window_offset, int64_t grid) {
+              bool in_shared, int64_t thr_in, int64_t thr_out, int64_t seed, int64_t pass_base,
+              int64_t window_offset, int64_t grid, const c10::optional<at::Tensor>& ascale,
+              const c10::optional<at::Tensor>& rmax) {
   TORCH_CHECK(layer >= 1 && layer <= 5, "x3_layer: layer must be 1..5 (block 2..6)");
   TORCH_CHECK(n_win >= 1 && groups >= 1, "x3_layer: empty launch");
   const int cin = kCh[layer], cout = kCh[layer + 1], ks = kKs[layer];
@@ -70,6 +71,19 @@ void x3_layer(int64_t layer, const at::Tensor& in, at::Tensor& out, const at::Te
     st = stats->data_ptr<double>();
   }
   TORCH_CHECK(thr_in >= 0 && thr_in <= 65536 && thr_out >= 0 && thr_out <= 65536, "x3_layer: thresholds");
+  const float* asp = nullptr;
+  if (ascale.has_value() && ascale->defined()) {
+    need(*ascale, at::kFloat, aff_gstride ? groups : 1, "x3_layer: ascale");
+    asp = ascale->data_ptr<float>();
+  }
+  unsigned* rmp = nullptr;
+  if (rmax.has_value() && rmax->defined()) {
+    TORCH_CHECK(layer < 5, "x3_layer: block 6 has no split consumer (no rmax)");
+    need(*rmax, at::kInt, cout, "x3_layer: rmax");
+    // exactly one row per group, or one row shared by every group (passes sharing one affine)
+    TORCH_CHECK(rmax->numel() == groups * cout || rmax->numel() == cout, "x3_layer: rmax must hold groups x Cout or Cout");
+    rmp = reinterpret_cast<unsigned*>(rmax->data_ptr<int>());
+  }
   const at::DeviceGuard guard(in.device());
   apneauq::x3::LayerArgs A;
   A.in = in.data_ptr<float>();
@@ -82,12 +96,14 @@ void x3_layer(int64_t layer, const at::Tensor& in, at::Tensor& out, const at::Te
   A.aff_in = aff_in.data_ptr<float>();
   A.aff_gstride = (int)aff_gstride;
   A.stats = st;
+  A.ascale = asp;
+  A.rmax = rmp;
+  A.rmax_gstride = (rmp != nullptr && rmax->numel() == groups * cout) ? cout : 0;
   A.n_win = (int)n_win;
   A.groups = (int)groups;
   A.tiles_per_group = (int)tpg;
   A.total_tiles = (int)(tpg * groups);
   A.in_shared = in_shared ? 1 : 0;
-  A.hash_in = hash_in ? 1 : 0;
   A.thr_in = (unsigned)thr_in;
   A.thr_out = (unsigned)thr_out;
   A.layer = (int)layer;
@@ -100,7 +116,7 @@ void x3_layer(int64_t layer, const at::Tensor& in, at::Tensor& out, const at::Te
 }
 
 void x3_l1(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b, at::Tensor& out,
-           const c10::optional<at::Tensor>& stats, int64_t n_win, int64_t groups) {
+           const c10::optional<at::Tensor>& stats, int64_t n_win, int64_t groups, const c10::optional<at::Tensor>& rmax) {
   TORCH_CHECK(n_win >= 1 && groups >= 1, "x3_l1: empty launch");
   need(x, at::kFloat, n_win * 60 * 4, "x3_l1: x");
   need(w, at::kFloat, groups * 7 * 4 * 128, "x3_l1: w");
@@ -111,17 +127,23 @@ void x3_l1(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b, at::Te
     need(*stats, at::kDouble, groups * apneauq::x3::kStatSlots * 2 * 128, "x3_l1: stats");
     st = stats->data_ptr<double>();
   }
+  unsigned* rmp = nullptr;
+  if (rmax.has_value() && rmax->defined()) {
+    need(*rmax, at::kInt, groups * 128, "x3_l1: rmax");
+    rmp = reinterpret_cast<unsigned*>(rmax->data_ptr<int>());
+  }
   const int64_t bpg = (n_win + apneauq::x3::kL1Win - 1) / apneauq::x3::kL1Win;
   TORCH_CHECK(bpg * groups < (int64_t(1) << 31), "x3_l1: too many blocks");
   const at::DeviceGuard guard(x.device());
-  apneauq::x3::L1Args A{x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(), out.data_ptr<float>(), st,
+  apneauq::x3::L1Args A{x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(), out.data_ptr<float>(), st, rmp,
                         (int)n_win, (int)groups, (int)bpg};
   check(apneauq::x3_launch_l1(A, cur_stream()), "x3_l1");
 }
 
 void x3_aff(const c10::optional<at::Tensor>& stats, const at::Tensor& gamma, const at::Tensor& beta, at::Tensor& mmean,
             at::Tensor& mvar, at::Tensor& aff, int64_t C, int64_t groups, int64_t p_gstride, bool update,
-            int64_t repeat, double inv_count, double eps, double momentum, double dsc) {
+            int64_t repeat, double inv_count, double eps, double momentum, double dsc,
+            const c10::optional<at::Tensor>& rmax, const c10::optional<at::Tensor>& ascale) {
   TORCH_CHECK(C >= 1 && C <= 4096 && groups >= 1, "x3_aff: bad sizes");
   TORCH_CHECK(p_gstride == 0 || p_gstride == C, "x3_aff: p_gstride must be 0 or C");
   const int64_t pg = p_gstride ? groups : 1;
@@ -136,9 +158,18 @@ void x3_aff(const c10::optional<at::Tensor>& stats, const at::Tensor& gamma, con
     st = stats->data_ptr<double>();
   }
   TORCH_CHECK(!update || st != nullptr, "x3_aff: the moving update needs batch moments");
+  const unsigned* rmp = nullptr;
+  float* asp = nullptr;
+  if (rmax.has_value() && rmax->defined()) {  // range-safe prescale: needs the output of 2^-sa too
+    TORCH_CHECK(ascale.has_value() && ascale->defined(), "x3_aff: rmax needs ascale");
+    need(*rmax, at::kInt, groups * C, "x3_aff: rmax");
+    need(*ascale, at::kFloat, groups, "x3_aff: ascale");
+    rmp = reinterpret_cast<const unsigned*>(rmax->data_ptr<int>());
+    asp = ascale->data_ptr<float>();
+  }
   const at::DeviceGuard guard(gamma.device());
   apneauq::x3::AffArgs A{st, gamma.data_ptr<float>(), beta.data_ptr<float>(), mmean.data_ptr<float>(),
-                         mvar.data_ptr<float>(), aff.data_ptr<float>(), (int)C, (int)groups, (int)p_gstride,
+                         mvar.data_ptr<float>(), aff.data_ptr<float>(), rmp, asp, (int)C, (int)groups, (int)p_gstride,
                          update ? 1 : 0, (int)repeat, inv_count, (float)eps, (float)momentum, (float)dsc};
   check(apneauq::x3_launch_aff(A, cur_stream()), "x3_aff");
 }
@@ -169,10 +200,13 @@ int64_t x3_lds(int64_t layer) { return apneauq::x3_lds_bytes((int)layer); }
 TORCH_LIBRARY_FRAGMENT(apneauq, m) {
   m.def("x3_layer(int layer, Tensor input, Tensor(a!) out, Tensor wfrag, int w_gstride, Tensor bias, Tensor wscale, "
         "int p_gstride, Tensor aff_in, int aff_gstride, Tensor(b!)? stats, int n_win, int groups, bool in_shared, "
-        "bool hash_in, int thr_in, int thr_out, int seed, int pass_base, int window_offset, int grid) -> ()");
-  m.def("x3_l1(Tensor x, Tensor w, Tensor b, Tensor(a!) out, Tensor(b!)? stats, int n_win, int groups) -> ()");
+        "int thr_in, int thr_out, int seed, int pass_base, int window_offset, int grid, Tensor? ascale=None, "
+        "Tensor(c!)? rmax=None) -> ()");
+  m.def("x3_l1(Tensor x, Tensor w, Tensor b, Tensor(a!) out, Tensor(b!)? stats, int n_win, int groups, "
+        "Tensor(c!)? rmax=None) -> ()");
   m.def("x3_aff(Tensor? stats, Tensor gamma, Tensor beta, Tensor(a!) mmean, Tensor(b!) mvar, Tensor(c!) aff, int C, "
-        "int groups, int p_gstride, bool update, int repeat, float inv_count, float eps, float momentum, float dsc) -> ()");
+        "int groups, int p_gstride, bool update, int repeat, float inv_count, float eps, float momentum, float dsc, "
+        "Tensor? rmax=None, Tensor(d!)? ascale=None) -> ()");
   m.def("x3_head(Tensor sums, Tensor aff, int aff_gstride, Tensor dw, Tensor db, int p_gstride, Tensor(a!) out, "
         "int n_win, int groups, bool logits) -> ()");
   m.def("x3_lds(int layer) -> int", &x3_lds);

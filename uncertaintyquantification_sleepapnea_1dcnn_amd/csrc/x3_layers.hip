@@ -19,8 +19,9 @@
 // Data flow (one launch per layer; the window set stays resident in HBM):
 //   l1_kernel      R_1 = relu(conv(x) + b) fp32 (+ batch moments)           [G1][N][60][128]
 //   aff_kernel     per-group BN affine of block l (batch moments or moving stats), pre-scaled by 1/(1-p)
-//   layer_kernel   stage A_{l-1} = dropout(BN(R_{l-1})) as fp16 hi/lo into LDS, conv on MFMA,
-//                  epilogue: bias + ReLU + moments + dropout mask of block l (sign bit of R_l, fp32)
+//   layer_kernel   stage A_{l-1} = dropout(BN(R_{l-1})) as fp16 hi/lo into LDS (the mask of block l-1
+//                  drawn from the counter hash here, by the loader waves), conv on MFMA,
+//                  epilogue: bias + ReLU + moments, R_l stored fp32
 //                  block 6: per-sample masked channel sums  S1 = sum_t keep*R,  S0 = sum_t keep
 //   head_kernel    logit = b + (1/60) sum_c w_c (s_c S1_c + t_c S0_c)  (BN 6 + dropout 6 + GAP + Dense
 //                  are linear per channel), p = sigmoid(logit)
@@ -50,20 +51,9 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const f16x8 gf16x8;
 
 // Staging waves of a layer without loader waves: the HBM loads of the next chunk are issued by MFMA
-// waves 0..SW-1 only (one per SIMD), so that the partner wave keeps the matrix pipe busy while the
-// stager's in-order vmcnt holds it at its next weight-fragment wait.  APNEAUQ_X3_SW=0: every wave stages.
-#ifndef APNEAUQ_X3_SW
-#define APNEAUQ_X3_SW 4
-#endif
-// Timing-only ablation probes (0 in the library build; nonzero values compute garbage):
-// 1 = no input staging (loads + LDS writes), 2 = no epilogue stores, 4 = no MFMAs,
-// 8 = weight fragments re-read from k-step 0 (L1-resident: no L2 weight stream)
-#ifndef APNEAUQ_X3_RG  // row tiles per MFMA issue group (0: per-layer default; probes force 1 / 2)
-#define APNEAUQ_X3_RG 0
-#endif
-#ifndef APNEAUQ_X3_ABL
-#define APNEAUQ_X3_ABL 0
-#endif
+// waves 0..kStagers-1 only (one per SIMD), so that the partner wave keeps the matrix pipe busy while the
+// stager's in-order vmcnt holds it at its next weight-fragment wait.
+constexpr int kStagers = 4;
 constexpr int kL = 60, kSR = 64, kHalo = 4;
 // A chunk = CK input channels (32 or 64) of the tile's rows; LDS row: hi 2CK B | lo 2CK B | pad 32 B
 // (row stride 2 mod 4 16-B slots for either CK).  Layers with few taps take 64-channel chunks: twice the
@@ -72,7 +62,8 @@ __host__ __device__ constexpr int row_bytes(int ck) { return 4 * ck + 32; }
 // per tile of S samples (S x 64 GEMM rows): LDS rows, chunk-buffer bytes, staged rows, 16-B staging units
 __host__ __device__ constexpr int lds_rows(int S) { return kHalo + S * kSR + kHalo; }
 __host__ __device__ constexpr int buf_bytes(int S, int ck) { return lds_rows(S) * row_bytes(ck); }
-__host__ __device__ constexpr int lds_bytes(int S, int cout, int ck) { return 2 * buf_bytes(S, ck) + 2 * cout * 8; }
+// + per-workgroup fp64 moment sums [2][COUT] and the R_l channel maxima [COUT] (u32)
+__host__ __device__ constexpr int lds_bytes(int S, int cout, int ck) { return 2 * buf_bytes(S, ck) + 2 * cout * 8 + cout * 4; }
 
 // global-address-space load (keeps global_load_*, never flat_*)
 template <typename T>
@@ -89,13 +80,7 @@ __device__ __forceinline__ int opaque_tid() {
 }
 
 __device__ __forceinline__ f32x4 mfma(const f16x8& a, const f16x8& b, const f32x4& c) {
-#if (APNEAUQ_X3_ABL & 4)
-  f32x4 r = c;
-  asm volatile("" : "+v"(r) : "v"(a), "v"(b));
-  return r;
-#else
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
-#endif
 }
 
 // LDS hazard barrier: orders LDS traffic only (global loads in flight stay in flight)
@@ -127,7 +112,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
   constexpr int kCK = CK, kRowB = row_bytes(CK), NQ = CK / 32, kQ = CK / 4;  // 32-ch sub-chunks, quads / row
   constexpr int kS = S, kBufB = buf_bytes(S, CK), kValidRows = S * kL, kUnits = kValidRows * kQ;
   // staging waves: the LW loader waves, else MFMA waves 0..SW-1 (one per SIMD by default)
-  constexpr int SW = LW > 0 ? LW : (APNEAUQ_X3_SW > 0 && APNEAUQ_X3_SW < NW) ? APNEAUQ_X3_SW : NW;
+  constexpr int SW = LW > 0 ? LW : (kStagers < NW ? kStagers : NW);
   constexpr int kSBase = LW > 0 ? NWM * 64 : 0;              // first staging thread
   constexpr int kST = SW * 64;                                // staging threads
   constexpr int kNU = (kUnits + kST - 1) / kST;              // 16-B staging units per staging thread
@@ -136,8 +121,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
   constexpr int NSTEP = NCH * NQ * KS;  // k-steps (32 input channels x one tap) per tile
   // MFMA issue order: row tiles in groups of RG so that >= 4 accumulators rotate (dependent-issue
   // latency); B fragments double-buffered one group ahead when the accumulators leave room
-  constexpr int RG = APNEAUQ_X3_RG > 0 ? APNEAUQ_X3_RG
-                     : NCT >= 4                        ? 1
+  constexpr int RG = NCT >= 4                        ? 1
                      : (NCT >= 3 && NCT * NRT > 16)    ? 1
                      : NCT == 1                        ? 4
                                                        : 2;
@@ -148,6 +132,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
   static_assert(NCTA % WN == 0 && (4 * S) % WM == 0, "wave tiling");
   static_assert(NRT % 4 == 0, "whole 64-row sample slots per wave row (epilogue keys, block 6 sums)");
   double* st = reinterpret_cast<double*>(smem + 2 * kBufB);  // [2][COUT] per-workgroup moment sums
+  unsigned* lmax = reinterpret_cast<unsigned*>(st + 2 * COUT);  // [COUT] channel maxima of R_l (fp32 bits)
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -158,6 +143,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
 
   for (int i = tid; i < 2 * kBufB / 16; i += kThreads) reinterpret_cast<f32x4*>(smem)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int i = tid; i < 2 * COUT; i += kThreads) st[i] = 0.0;
+  for (int i = tid; i < COUT; i += kThreads) lmax[i] = 0u;
   __syncthreads();
 
   const int wg = xcd_wg();
@@ -171,7 +157,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
   // ---- staging: staging thread i = tid - kSBase keeps the 16-B units (row ri = i/8 + kST/8 u,
   // channel quad q = i % 8) of every chunk
   const bool loader = LW > 0 && wave >= NWM;
-  const bool stager = (LW > 0 ? loader : wave < SW) && (APNEAUQ_X3_ABL & 1) == 0;
+  const bool stager = LW > 0 ? loader : wave < SW;
   // staging register set: the chunk's 16-B units + the BN affine (scale, shift) x 1/(1-p) of the
   // thread's 4 channels
   struct Stage {
@@ -179,6 +165,12 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
     f32x4 a, b;
   };
   Stage s0;
+  // dropout keys of the current staging tile's S samples (the input's mask is drawn from the counter
+  // hash of block l-1 here, at the consumer: the producer's epilogue then runs no hash at all, and the
+  // loader waves' hashing overlaps the MFMA waves); recomputed when the staged tile changes
+  const bool hash_in = A.thr_in != 0u;
+  int key_tile = -1;
+  unsigned skeys[kS];
   auto load_chunk = [&](int tile, int c, Stage& R) {
     const int tid = opaque_tid() - kSBase, q = tid % kQ;
     const int g = tile / tpg;
@@ -203,8 +195,12 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
     const int tid = opaque_tid() - kSBase, q = tid % kQ;
     const int g = tile / tpg;
     const int w0 = (tile - g * tpg) * kS;
-    unsigned skey = 0;
-    if (A.hash_in) skey = stream_key(A.seed, A.layer - 1, A.pass_base + g);
+    if (hash_in && tile != key_tile) {  // workgroup-uniform
+      const unsigned skey = stream_key(A.seed, A.layer - 1, A.pass_base + g);
+#pragma unroll
+      for (int s = 0; s < kS; ++s) skeys[s] = sample_key(skey, A.window_offset + w0 + s);
+      key_tile = tile;
+    }
 #pragma unroll
     for (int u = 0; u < kNU; ++u) {
       const int ri = tid / kQ + (kST / kQ) * u;
@@ -212,8 +208,10 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
       const int s = ri / kL, t = ri - s * kL, w = w0 + s;
       const f32x4 v = R.v[u];
       bool keep[4];
-      if (A.hash_in) {
-        const unsigned k = sample_key(skey, A.window_offset + w);
+      if (hash_in) {
+        unsigned k = skeys[0];
+#pragma unroll
+        for (int j = 1; j < kS; ++j) k = s == j ? skeys[j] : k;
         const unsigned b01 = dropout_bits2(k, t, c * kCK + 4 * q);
         const unsigned b23 = dropout_bits2(k, t, c * kCK + 4 * q + 2);
         keep[0] = (b01 & 0xFFFFu) >= A.thr_in;
@@ -228,9 +226,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
       f16x4 hi, lo;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const unsigned bits = __float_as_uint(v[i]);
-        const bool k = valid && keep[i] && (bits >> 31) == 0u;
-        const float a = k ? __builtin_fmaf(__uint_as_float(bits & 0x7FFFFFFFu), R.a[i], R.b[i]) : 0.f;
+        const float a = (valid && keep[i]) ? __builtin_fmaf(v[i], R.a[i], R.b[i]) : 0.f;
         hi[i] = (_Float16)a;
         lo[i] = (_Float16)(a - (float)hi[i]);
       }
@@ -272,7 +268,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
       const int q2 = kk / KS, j = kk - q2 * KS;  // 32-channel sub-chunk, tap
       const char* bb = buf + bofs + q2 * 64;
       const int s = c * NQ * KS + kk;
-      const gf16x8* np = (APNEAUQ_X3_ABL & 8) ? wcur : (s + 1 < NSTEP) ? wcur + (long long)(s + 1) * FRAG_STEP : wnxt;
+      const gf16x8* np = (s + 1 < NSTEP) ? wcur + (long long)(s + 1) * FRAG_STEP : wnxt;
       // all NCT weight fragments resident, the next k-step's issued first (a full tap of MFMAs hides its
       // L2 latency); B fragments double-buffered one row tile ahead when registers allow.  The
       // sched_barriers pin that issue order (left alone, the scheduler sinks each load to its use).
@@ -332,9 +328,13 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
     const int lane = opaque_tid() & 63, m = lane & 15, h = lane >> 4;
     const int g = tile / tpg;
     const int w0 = (tile - g * tpg) * kS;
-    const float ws = A.wscale[A.p_gstride ? g : 0];
+    // weight prescale 2^-sw and activation prescale 2^-sa (range-safe fp16 split of the input), both exact
+    const float ws = A.wscale[A.p_gstride ? g : 0] * (A.ascale != nullptr ? A.ascale[A.aff_gstride ? g : 0] : 1.f);
+    const bool track = !LAST && A.rmax != nullptr;
     const float* bias = A.bias + (long long)g * A.p_gstride;
-    const bool drop = A.thr_out != 0u;
+    // only block 6 draws its output mask here (the masked per-sample sums); blocks 2..5 store the plain
+    // ReLU output and their consumer draws the mask while staging it
+    const bool drop = LAST && A.thr_out != 0u;
     // a wave's row tiles cover whole 64-row sample slots (NRT % 4 == 0): the sample of row tile rt is
     // wave-uniform, so its dropout key is computed once per sample (scalar ALU), not per (ct, rt, lane)
     unsigned skeys[NRT / 4];
@@ -349,7 +349,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
     for (int ct = 0; ct < NCT; ++ct) {
       const int co0 = (ct0 + ct) * 16 + 4 * h;
       const f32x4 b4 = gld<f32x4>(bias + co0);
-      f32x4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1, k1 = s1, k0 = s1;
+      f32x4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1, k1 = s1, k0 = s1, mx = s1;
 #pragma unroll
       for (int rt = 0; rt < NRT; ++rt) {
         const int s = (rt0 + rt) >> 2, t = (((rt0 + rt) & 3) << 4) + m, w = w0 + s;
@@ -372,20 +372,15 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
           for (int e = 0; e < 4; ++e) {
             s1[e] += r[e];
             s2[e] = __builtin_fmaf(r[e], r[e], s2[e]);
+            if (!LAST) mx[e] = fmaxf(mx[e], r[e]);
             if constexpr (LAST) {
               k1[e] += keep[e] ? r[e] : 0.f;
               k0[e] += keep[e] ? 1.f : 0.f;
             }
           }
           if constexpr (!LAST) {
-            f32x4 o;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = __uint_as_float(__float_as_uint(r[e]) | (keep[e] ? 0u : 0x80000000u));
             const long long sample = (long long)g * A.n_win + w;
-            if constexpr ((APNEAUQ_X3_ABL & 2) == 0)
-              *reinterpret_cast<f32x4*>(A.out + (sample * kL + t) * COUT + co0) = o;
-            else
-              asm volatile("" :: "v"(o));
+            *reinterpret_cast<f32x4*>(A.out + (sample * kL + t) * COUT + co0) = r;
           }
         }
         if constexpr (LAST) {
@@ -407,6 +402,13 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
         }
       }
       // reduce over the 16 rows of each lane group (lanes sharing h hold the same 4 channels)
+      if (track) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float a = group16_max(mx[e]);
+          if (m == 0) atomicMax(&lmax[co0 + e], __float_as_uint(a));  // R_l >= 0: bit order = value order
+        }
+      }
       if (A.stats != nullptr) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -427,6 +429,12 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
       for (int i = tid; i < 2 * COUT; i += kThreads) {
         atomicAdd(dst + i, st[i]);
         st[i] = 0.0;
+      }
+    }
+    if (!LAST && A.rmax != nullptr) {
+      for (int i = tid; i < COUT; i += kThreads) {
+        if (lmax[i] != 0u) atomicMax(A.rmax + (long long)g * A.rmax_gstride + i, lmax[i]);
+        lmax[i] = 0u;
       }
     }
     __syncthreads();
@@ -526,7 +534,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) 
 // per 256-thread block (thread = one output channel x one half of the time steps), + batch moments.
 __global__ __launch_bounds__(256) void l1_kernel(const L1Args A) {
   __shared__ float xs[kL1Win][kL + 6][4];
-  __shared__ float red[2][2][128];
+  __shared__ float red[2][3][128];
   const int g = blockIdx.x / A.blocks_per_group;
   const int w0 = (blockIdx.x - g * A.blocks_per_group) * kL1Win;
   const int tid = threadIdx.x, c = tid & 127, half = tid >> 7;
@@ -542,7 +550,7 @@ __global__ __launch_bounds__(256) void l1_kernel(const L1Args A) {
     for (int ci = 0; ci < 4; ++ci) wr[j][ci] = A.w[(((long long)g * 7 + j) * 4 + ci) * 128 + c];
   const float bc = A.b[g * 128 + c];
   __syncthreads();
-  float s1 = 0.f, s2 = 0.f;
+  float s1 = 0.f, s2 = 0.f, mx = 0.f;
   for (int s = 0; s < kL1Win; ++s) {
     const int w = w0 + s;
     if (w >= A.n_win) break;
@@ -557,16 +565,21 @@ __global__ __launch_bounds__(256) void l1_kernel(const L1Args A) {
       o[t * 128] = v;
       s1 += v;
       s2 = __builtin_fmaf(v, v, s2);
+      mx = fmaxf(mx, v);
     }
   }
-  if (A.stats != nullptr) {
+  if (A.stats != nullptr || A.rmax != nullptr) {  // block-uniform
     red[half][0][c] = s1;
     red[half][1][c] = s2;
+    red[half][2][c] = mx;
     __syncthreads();
     if (tid < 128) {
-      double* dst = A.stats + ((long long)g * kStatSlots + (blockIdx.x % kStatSlots)) * 2 * 128;
-      atomicAdd(dst + c, (double)red[0][0][c] + (double)red[1][0][c]);
-      atomicAdd(dst + 128 + c, (double)red[0][1][c] + (double)red[1][1][c]);
+      if (A.stats != nullptr) {
+        double* dst = A.stats + ((long long)g * kStatSlots + (blockIdx.x % kStatSlots)) * 2 * 128;
+        atomicAdd(dst + c, (double)red[0][0][c] + (double)red[1][0][c]);
+        atomicAdd(dst + 128 + c, (double)red[0][1][c] + (double)red[1][1][c]);
+      }
+      if (A.rmax != nullptr) atomicMax(A.rmax + (long long)g * 128 + c, __float_as_uint(fmaxf(red[0][2][c], red[1][2][c])));
     }
   }
 }
@@ -576,35 +589,65 @@ __global__ __launch_bounds__(256) void l1_kernel(const L1Args A) {
 // are the biased batch moments of group g (stats != nullptr) or the moving statistics.  With
 // update != 0 the Keras moving averages are updated once per group in group order (one MC-Dropout
 // pass after the other, the side effect of model(x, training=True)).
-__global__ void aff_kernel(const AffArgs A) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= A.C) return;
+//
+// Range-safe fp16 split (rmax != nullptr): the consumer splits a = aff(R) into fp16 hi + lo, which
+// needs |a| < 65504 (hi finite) and |a| >> 2^-14 (lo normal).  R >= 0 is bounded by the tracked
+// channel maxima, so max |a| over the group is max_c max(|rmax_c s_c + t_c|, |t_c|) (an affine map
+// takes its extremes at the ends of [0, rmax]); the affine is pre-scaled by the exact power of two
+// 2^sa that puts that maximum in [2^13, 2^14), and ascale[g] = 2^-sa lets the consumer's epilogue undo
+// it.  One workgroup; the groups run in order (the moving updates of consecutive passes chain).
+__global__ __launch_bounds__(256) void aff_kernel(const AffArgs A) {
+  __shared__ float red[4];
+  const int tid = threadIdx.x;
   for (int g = 0; g < A.groups; ++g) {
-    const long long po = (long long)g * A.p_gstride + c;
-    float mean, var;
-    if (A.stats != nullptr) {
-      const double* p = A.stats + (long long)g * kStatSlots * 2 * A.C + c;
-      double a = 0.0, b = 0.0;
-      for (int s = 0; s < kStatSlots; ++s) {
-        a += p[s * 2 * A.C];
-        b += p[s * 2 * A.C + A.C];
-      }
-      const double mu = a * A.inv_count;
-      mean = (float)mu;
-      var = (float)fmax(b * A.inv_count - mu * mu, 0.0);
-      if (A.update) {
-        for (int r = 0; r < A.repeat; ++r) {
-          A.mmean[po] = A.mmean[po] * A.momentum + mean * (1.f - A.momentum);
-          A.mvar[po] = A.mvar[po] * A.momentum + var * (1.f - A.momentum);
+    float amax = 0.f;
+    for (int c = tid; c < A.C; c += 256) {
+      const long long po = (long long)g * A.p_gstride + c;
+      float mean, var;
+      if (A.stats != nullptr) {
+        const double* p = A.stats + (long long)g * kStatSlots * 2 * A.C + c;
+        double a = 0.0, b = 0.0;
+        for (int s = 0; s < kStatSlots; ++s) {
+          a += p[s * 2 * A.C];
+          b += p[s * 2 * A.C + A.C];
         }
+        const double mu = a * A.inv_count;
+        mean = (float)mu;
+        var = (float)fmax(b * A.inv_count - mu * mu, 0.0);
+        if (A.update) {
+          for (int r = 0; r < A.repeat; ++r) {
+            A.mmean[po] = A.mmean[po] * A.momentum + mean * (1.f - A.momentum);
+            A.mvar[po] = A.mvar[po] * A.momentum + var * (1.f - A.momentum);
+          }
+        }
+      } else {
+        mean = A.mmean[po];
+        var = A.mvar[po];
       }
-    } else {
-      mean = A.mmean[po];
-      var = A.mvar[po];
+      const float sc = A.gamma[po] / sqrtf(var + A.eps);
+      const float s_ = sc * A.dsc, t_ = (A.beta[po] - mean * sc) * A.dsc;
+      A.aff[((long long)g * 2) * A.C + c] = s_;
+      A.aff[((long long)g * 2 + 1) * A.C + c] = t_;
+      if (A.rmax != nullptr) {
+        const float rm = __uint_as_float(A.rmax[(long long)g * A.C + c]);
+        amax = fmaxf(amax, fmaxf(fabsf(__builtin_fmaf(rm, s_, t_)), fabsf(t_)));
+      }
     }
-    const float sc = A.gamma[po] / sqrtf(var + A.eps);
-    A.aff[((long long)g * 2) * A.C + c] = sc * A.dsc;
-    A.aff[((long long)g * 2 + 1) * A.C + c] = (A.beta[po] - mean * sc) * A.dsc;
+    if (A.rmax == nullptr) continue;  // kernel-uniform
+    amax = wave_max(amax);
+    if ((tid & 63) == 0) red[tid >> 6] = amax;
+    __syncthreads();
+    amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    __syncthreads();  // red is rewritten by the next group
+    int e = 0;
+    if (amax > 0.f && amax < INFINITY) frexpf(amax, &e);  // amax = m 2^e, m in [0.5, 1)
+    const int sa = min(100, max(-100, 14 - e));  // amax 2^sa in [2^13, 2^14)
+    const float up = ldexpf(1.f, sa);
+    for (int c = tid; c < A.C; c += 256) {  // the values this thread wrote above
+      A.aff[((long long)g * 2) * A.C + c] *= up;
+      A.aff[((long long)g * 2 + 1) * A.C + c] *= up;
+    }
+    if (tid == 0) A.ascale[g] = ldexpf(1.f, -sa);
   }
 }
 
@@ -655,16 +698,12 @@ hipError_t launch_layer(const LayerArgs& A, int grid, hipStream_t stream) {
 // budget of 8 waves (loaders at 2-sample tiles: slower; at 4: 99 VGPRs spilled).  64-channel chunks for
 // blocks 3 and 6 (block 2 would spill; Cin 224 / 96 are not multiples of 64).  Measurements:
 // profiles/x3_epilogue_ab_r3.md.
-#ifndef APNEAUQ_X3_LW  // probe: loader waves per layer (-1 = table)
-#define APNEAUQ_X3_LW -1
-#endif
-#define APNEAUQ_X3_LOADERS(n) (APNEAUQ_X3_LW < 0 ? (n) : APNEAUQ_X3_LW)
-#define APNEAUQ_X3_LAYERS(X)                                    \
-  X(1, 128, 192, 5, 4, 2, 4, false, APNEAUQ_X3_LOADERS(0), 32)  \
-  X(2, 192, 224, 3, 2, 1, 7, false, APNEAUQ_X3_LOADERS(4), 64)  \
-  X(3, 224, 96, 7, 4, 4, 2, false, APNEAUQ_X3_LOADERS(4), 32)   \
-  X(4, 96, 256, 9, 2, 1, 8, false, APNEAUQ_X3_LOADERS(4), 32)   \
-  X(5, 256, 96, 9, 4, 4, 2, true, APNEAUQ_X3_LOADERS(4), 64)
+#define APNEAUQ_X3_LAYERS(X)               \
+  X(1, 128, 192, 5, 4, 2, 4, false, 0, 32) \
+  X(2, 192, 224, 3, 2, 1, 7, false, 4, 64) \
+  X(3, 224, 96, 7, 4, 4, 2, false, 4, 32)  \
+  X(4, 96, 256, 9, 2, 1, 8, false, 4, 32)  \
+  X(5, 256, 96, 9, 4, 4, 2, true, 4, 64)
 
 int x3_lds_bytes(int layer) {
 #define APNEAUQ_X3_LDS(L, CI, CO, K, S, WM, WN, LAST, LW, CK) \
@@ -699,7 +738,7 @@ hipError_t x3_launch_l1(const x3::L1Args& A, hipStream_t stream) {
 }
 
 hipError_t x3_launch_aff(const x3::AffArgs& A, hipStream_t stream) {
-  hipLaunchKernelGGL(x3::aff_kernel, dim3((A.C + 255) / 256), dim3(256), 0, stream, A);
+  hipLaunchKernelGGL(x3::aff_kernel, dim3(1), dim3(256), 0, stream, A);
   return hipGetLastError();
 }
 

@@ -41,6 +41,15 @@ from . import _ext, fused, generic, rng
 
 TRAIN_PASS_BASE = 1 << 30  # == training/step.py
 SLOTS = 16  # == kStatSlots (csrc/generic_conv.hip, csrc/generic_train.hip)
+DET_BWD_SLOTS = 256  # deterministic mode: workgroups (= partial slots) of each backward-sum launch
+DET_WGRAD_GROUPS = 16  # deterministic mode: row groups (= partial slices) of each wgrad launch
+
+
+def deterministic() -> bool:
+    """The generic path follows the package-wide switch (``ops/train_ops.set_deterministic``)."""
+    from . import train_ops
+
+    return bool(train_ops.DETERMINISTIC)
 
 
 def supports(spec: ModelSpec) -> bool:
@@ -58,12 +67,16 @@ def supports(spec: ModelSpec) -> bool:
 class GenericTrainWorkspace:
     """Device buffers of one model for batches of up to ``batch`` windows."""
 
-    def __init__(self, model, batch: int, with_backward: bool = True):
+    def __init__(self, model, batch: int, with_backward: bool = True, det: Optional[bool] = None):
         spec: ModelSpec = model.spec
         dev = model.store.device
         self.model = model
         self.B = int(batch)
         self.with_backward = with_backward
+        # deterministic mode (SURVEY §5): every cross-workgroup sum -- BN moments, backward sums, bias,
+        # weight and head gradients -- goes through per-workgroup partial slots written with plain
+        # stores and added in a fixed order (csrc/generic_*.hip ``det``), instead of fp32 atomics
+        self.det = deterministic() if det is None else bool(det)
         B, bf = self.B, torch.bfloat16
         self.L = spec.lengths()
         self.ch = spec.channels()
@@ -75,7 +88,9 @@ class GenericTrainWorkspace:
         self.xin = [torch.zeros(2 * self.pads[l] + B * self.rs[l], self.ch[l], dtype=bf, device=dev) for l in range(nl)]
         self.z = [torch.empty(B * self.L[l], self.ch[l + 1], dtype=bf, device=dev) for l in range(nl)]
         self.hlast = torch.empty(B * self.L[-1], self.ch[-1], dtype=bf, device=dev)
-        sizes = [SLOTS * 2 * self.ch[l + 1] for l in range(nl)]
+        # forward moment slots: (slots, 2, C); deterministic: one per (conv workgroup of 128 rows, wave row)
+        fslots = [2 * -(-B * self.L[l] // 128) if self.det else SLOTS for l in range(nl)]
+        sizes = [fslots[l] * 2 * self.ch[l + 1] for l in range(nl)]
         self.st_all = torch.zeros(sum(sizes), device=dev)
         self.st = list(torch.split(self.st_all, sizes))
         self.bn = [torch.zeros(4 * self.ch[l + 1], device=dev) for l in range(nl)]
@@ -84,11 +99,18 @@ class GenericTrainWorkspace:
             self.dzp = [torch.zeros(B * self.rs[l], self.ch[l + 1], dtype=bf, device=dev) for l in range(nl)]
             self.dh = [torch.empty(B * self.L[l], self.ch[l], dtype=bf, device=dev) if l > 0 else None
                        for l in range(nl)]
-            self.bst_all = torch.zeros(sum(sizes), device=dev)
-            self.bst = list(torch.split(self.bst_all, sizes))
-            # bias-gradient slots (SLOTS, C) per block, zeroed with bst_all
-            self.dbs_all = torch.zeros(sum(sizes) // 2, device=dev)
-            self.dbs = [t.view(SLOTS, -1) for t in torch.split(self.dbs_all, [s // 2 for s in sizes])]
+            bslots = DET_BWD_SLOTS if self.det else SLOTS
+            bsizes = [bslots * 2 * self.ch[l + 1] for l in range(nl)]
+            self.bst_all = torch.zeros(sum(bsizes), device=dev)
+            self.bst = list(torch.split(self.bst_all, bsizes))
+            # bias-gradient slots (slots, C) per block, zeroed with bst_all
+            self.dbs_all = torch.zeros(sum(bsizes) // 2, device=dev)
+            self.dbs = [t.view(bslots, -1) for t in torch.split(self.dbs_all, [s // 2 for s in bsizes])]
+            # deterministic mode: wgrad row-group partials (shared by the sequential wgrad launches) and
+            # the head's per-workgroup records
+            wmax = max(self.ks[l] * self.ch[l] * self.ch[l + 1] for l in range(nl))
+            self.wpart = torch.empty(DET_WGRAD_GROUPS * wmax, device=dev) if self.det else None
+            self.hpart = torch.empty(-(-B // 4) * (self.ch[-1] + 2), device=dev) if self.det else None
             self.coef = [torch.zeros(2 * self.ch[l + 1], device=dev) for l in range(nl)]
             self.y = torch.zeros(B, device=dev)
             self.prob = torch.zeros(B, device=dev)
@@ -139,7 +161,7 @@ def _frag(w: torch.Tensor) -> torch.Tensor:
 def _get_ws(model, batch: int, with_backward: bool = True) -> GenericTrainWorkspace:
     attr = "_gtrain_ws" if with_backward else "_gfwd_ws"
     ws = getattr(model, attr, None)
-    if ws is None or ws.B < batch:
+    if ws is None or ws.B < batch or ws.det != deterministic():
         ws = GenericTrainWorkspace(model, batch, with_backward=with_backward)
         setattr(model, attr, ws)
     return ws
@@ -158,7 +180,7 @@ def _forward(ws: GenericTrainWorkspace, n: int, global_n: int, seed: int, pass_i
         i = l + 1
         cin, cout, L = ws.ch[l], ws.ch[l + 1], ws.L[l]
         o.gt_conv(ws.xin[l], wf[l], v[f"conv1d_{i}/bias"], ws.z[l], ws.st[l], n, L, cin, cout, ws.ks[l], 1,
-                  ws.rs[l], 2 * ws.pads[l])
+                  ws.rs[l], 2 * ws.pads[l], ws.det)
         if sync is not None:
             sync(ws.st[l])
         o.gt_bn_finalize(ws.st[l], cout, 1.0 / (global_n * L), v[f"batchnorm_{i}/gamma"], v[f"batchnorm_{i}/beta"],
@@ -196,7 +218,7 @@ def _grads(model, ws: GenericTrainWorkspace, y: torch.Tensor, n: int, gb: int, p
     ws.head_loss.zero_()
     ws.y[:n].copy_(y.reshape(-1))
     o.gt_head(h, wdense, v["output_layer/bias"], ws.y, ws.prob, ws.dlog, ws.head_loss, g["output_layer/kernel"],
-              g["output_layer/bias"], n, ws.L[-1], ws.ch[-1], 1.0 / gb)
+              g["output_layer/bias"], n, ws.L[-1], ws.ch[-1], 1.0 / gb, ws.hpart)
     dlog = ws.dlog
     ws.bst_all.zero_()
     ws.dbs_all.zero_()
@@ -211,19 +233,19 @@ def _grads(model, ws: GenericTrainWorkspace, y: torch.Tensor, n: int, gb: int, p
         else:
             up = dict(dh=ws.dh[l + 1], dlog=None, w=None, invL=1.0)
         o.gt_bwd(False, ws.z[l], ws.bn[l], up["dh"], up["dlog"], up["w"], up["invL"], n, L, cout, bool(b.pool), drop,
-                 thr, ik, skey, int(window_offset), ws.bst[l], None, None, None, 0, 0, None, kd)
+                 thr, ik, skey, int(window_offset), ws.bst[l], None, None, None, 0, 0, None, kd, ws.det)
         if sync is not None:
             sync(ws.bst[l])
         o.gt_bwd_finalize(ws.bst[l], cout, 1.0 / (gb * L), ws.coef[l], g[f"batchnorm_{i}/gamma"],
                           g[f"batchnorm_{i}/beta"])
         o.gt_bwd(True, ws.z[l], ws.bn[l], up["dh"], up["dlog"], up["w"], up["invL"], n, L, cout, bool(b.pool), drop,
                  thr, ik, skey, int(window_offset), None, ws.coef[l], v[f"batchnorm_{i}/gamma"], ws.dzp[l], ws.rs[l], p,
-                 ws.dbs[l], kd)
+                 ws.dbs[l], kd, ws.det)
         torch.sum(ws.dbs[l], 0, out=g[f"conv1d_{i}/bias"])
         if l > 0:
             o.gt_conv(ws.dzp[l], wd[l], None, ws.dh[l], None, n, L, cout, cin, k, 2, ws.rs[l], p)
         # wgrad: dW[tap] = Xpad[tap : tap + R]^T dZpad (R = n * rs rows), split-K MFMA into the zeroed grad
-        o.gt_wgrad(ws.xin[l], ws.dzp[l], n * ws.rs[l], cin, cout, k, g[f"conv1d_{i}/kernel"])
+        o.gt_wgrad(ws.xin[l], ws.dzp[l], n * ws.rs[l], cin, cout, k, g[f"conv1d_{i}/kernel"], ws.wpart)
 
 
 def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, sync: Optional[Callable] = None,
@@ -264,6 +286,7 @@ class GraphedGenericStep:
         dev = model.store.device
         spec = model.spec
         self.ws = GenericTrainWorkspace(model, self.batch)
+        self.det = self.ws.det
         self.x_in = torch.zeros(self.batch, spec.input_length, spec.input_channels, device=dev)
         self.y_in = torch.zeros(self.batch, device=dev)
         self.keys = torch.zeros(len(spec.blocks), dtype=torch.int32, device=dev)
@@ -319,7 +342,7 @@ def graph_train_step(model, x: torch.Tensor, y: torch.Tensor):
         g = model._gtrain_graphs = {}
     n = int(x.shape[0])
     cur = g.get(n)
-    if cur is None or not train_ops._same_bound(cur.bound, train_ops.bound_key(model)):
+    if cur is None or not train_ops._same_bound(cur.bound, train_ops.bound_key(model)) or cur.det != deterministic():
         g[n] = cur = GraphedGenericStep(model, n)
     return cur(x, y)
 

@@ -270,13 +270,13 @@ def capture_graph(body, dev):
     """Capture ``body()`` (HIP launches only) as a graph on a side stream.
 
     A garbage collection during the capture can destroy an OLD graph, which HIP refuses while a stream
-    is capturing (abort), so collection is paused.  No device synchronisation after the capture: the
-    stale first-replay inputs once seen on the generic path (round 2: ~1 in 40 captures, hidden by a
-    post-capture synchronize) came with a per-step host-written dropout-key array; the step now
-    derives its keys on the device from its counters (``stream_keys``), and 40 + 40 fresh captures
-    of both training paths give step-1 losses identical to the eager step without the synchronize
-    (``tools/probes/capture_race.py``, ``profiles/capture_race_r3.txt``).  ``APNEAUQ_CAPTURE_SYNC=1``
-    restores it."""
+    is capturing (abort), so collection is paused.  The device is synchronised once after the capture
+    (a one-time cost per graph): the stale first-replay inputs once seen on the generic path (round 2:
+    ~1 in 40 captures) came with a per-step host-written dropout-key array that the steps no longer
+    use (keys are derived on the device from the counters, ``stream_keys``; 40 + 40 fresh captures of
+    the single-model paths replayed correctly without it, ``profiles/capture_race_r3.txt``), but the
+    member-batched capture (multi-stream groups, a device Args array uploaded right before capture)
+    was never probed, so the synchronize stays on.  ``APNEAUQ_CAPTURE_SYNC=0`` drops it."""
     import gc
 
     graph = torch.cuda.CUDAGraph()
@@ -293,7 +293,7 @@ def capture_graph(body, dev):
         if was:
             gc.enable()
     torch.cuda.current_stream(dev).wait_stream(side)
-    if os.environ.get("APNEAUQ_CAPTURE_SYNC", "0") == "1":
+    if os.environ.get("APNEAUQ_CAPTURE_SYNC", "1") != "0":
         torch.cuda.synchronize(dev)
     return graph
 
@@ -422,8 +422,9 @@ class GraphedEnsembleStep:
         self.ws, self.ctx, self.x_in, self.y_in = [], [], [], []
         # every member's device counters [dropout step, Adam iterations] are rows of one tensor: one bump
         self.counters = torch.zeros(M, 2, dtype=torch.int32, device=dev)
+        self.deterministic = DETERMINISTIC
         for i, m in enumerate(self.models):
-            ws = TrainWorkspace(m, n)
+            ws = TrainWorkspace(m, n, deterministic=self.deterministic)
             ws.counters = self.counters[i]
             self.ws.append(ws)
             self.x_in.append(ws.x[HALO: HALO + SR * n].view(n, SR, ws.ch[0])[:, :60])
@@ -451,7 +452,7 @@ class GraphedEnsembleStep:
         o, M, n = _ext.ops(), len(self.models), self.batch
         bufs = []
         for ws in self.ws:
-            bufs += [ws.st_all, ws.bst_all, ws.grad, ws.loss, ws.hpart]
+            bufs += [ws.st_all, ws.bst_all, ws.grad, ws.loss] + ([ws.hpart] if ws.det is None else [])
         zmax = 60  # csrc/adam.hip kZeroMax = 64 buffers per launch
         for b0 in range(0, len(bufs), zmax):
             o.zero_buffers(bufs[b0:b0 + zmax])
@@ -499,7 +500,8 @@ class GraphedEnsembleStep:
 
     def valid_for(self, models) -> bool:
         return (len(models) == len(self.models) and all(a is b for a, b in zip(models, self.models)) and
-                all(_same_bound(b, bound_key(m)) for b, m in zip(self.bound, self.models)) and not DETERMINISTIC)
+                all(_same_bound(b, bound_key(m)) for b, m in zip(self.bound, self.models)) and
+                self.deterministic == DETERMINISTIC)
 
     def __call__(self, xs, ys):
         """One step of every member on its own batch (lists of (n, 60, 4) / (n,) device tensors);
@@ -520,9 +522,10 @@ class GraphedEnsembleStep:
 
 def ensemble_supported(models) -> bool:
     """True when :class:`GraphedEnsembleStep` can batch these members: HIP backend on one GPU, the
-    reference architecture, single-device training (no data parallelism), atomic (non-deterministic)
-    mode and graph replay enabled."""
-    if not models or DETERMINISTIC or os.environ.get("APNEAUQ_TRAIN_GRAPH", "1") == "0":
+    reference architecture, single-device training (no data parallelism) and graph replay enabled
+    (atomic or deterministic mode: the deterministic member-batched step equals each member's own
+    deterministic step bitwise)."""
+    if not models or os.environ.get("APNEAUQ_TRAIN_GRAPH", "1") == "0":
         return False
     if os.environ.get("APNEAUQ_TRAIN_BACKEND", "auto") not in ("auto", "hip"):
         return False

@@ -14,7 +14,8 @@ tiles; BN apply, dropout, GAP, Dense and sigmoid are fp32.  Workloads:
   (``uq_techniques.py:29``) or standard MC Dropout (dropout on).
 
 Weights are packed once per model set (:class:`X3Model`); activations live in HBM between the six
-layer launches (fp32, the dropout mask of a block in the sign bit of its ReLU output).
+layer launches (fp32 ReLU outputs; the dropout mask of block l is drawn from the counter hash by the
+block that stages it, block l + 1).
 """
 from __future__ import annotations
 
@@ -32,7 +33,10 @@ STAT_SLOTS = 16  # csrc/x3_args.h kStatSlots
 TILE = 4         # samples per layer-kernel tile
 CK = 32          # input channels per staged chunk
 # bytes of activation workspace per sample: ping-pong fp32 buffers of 192 + 256 channels x 60 steps
+# (+ the block-1 output: per window for batch-BN MC Dropout, per window and member for the Deep Ensemble;
+# budgeted per sample, the conservative bound)
 BYTES_PER_SAMPLE = 60 * (192 + 256) * 4
+R1_BYTES = 60 * 128 * 4
 
 
 def supports(spec: ModelSpec) -> bool:
@@ -121,16 +125,18 @@ class X3Model:
         self._ws: Dict[tuple, "_Workspace"] = {}
 
     def workspace(self, samples: int, n_r1: int, groups: int) -> "_Workspace":
-        key = (samples, n_r1, groups)
-        ws = self._ws.get(key)
-        if ws is None:
-            self._ws.clear()  # one workspace at a time (the buffers are large)
-            ws = self._ws[key] = _Workspace(self.device, samples, n_r1, groups)
+        """One workspace at a time (the buffers are large), kept while it is big enough: a call with
+        fewer samples / windows / groups (a tail batch) reuses it instead of reallocating."""
+        ws = self._ws.get("ws")
+        if ws is None or ws.samples < samples or ws.n_r1 < n_r1 or ws.groups < groups:
+            self._ws.clear()
+            ws = self._ws["ws"] = _Workspace(self.device, samples, n_r1, groups)
         return ws
 
 
 class _Workspace:
     def __init__(self, dev, samples: int, n_r1: int, groups: int):
+        self.samples, self.n_r1, self.groups = int(samples), int(n_r1), max(int(groups), 1)
         f32 = dict(dtype=torch.float32, device=dev)
         self.r1 = torch.empty(n_r1 * 60 * CH[1], **f32)
         self.buf = [torch.empty(samples * 60 * 192, **f32), torch.empty(samples * 60 * 256, **f32)]
@@ -139,6 +145,10 @@ class _Workspace:
         self.stats = [torch.zeros(max(groups, 1) * STAT_SLOTS * 2 * CH[l + 1], dtype=torch.float64, device=dev)
                       for l in range(6)]
         self.aff = [torch.empty(max(groups, 1) * 2 * CH[l + 1], **f32) for l in range(6)]
+        # range-safe fp16 split of block l+2's input: channel maxima of R_l (fp32 bits) and the inverse
+        # power-of-two prescale folded into aff[l] (blocks 1..5; block 6 feeds the fp32 head)
+        self.rmax = [torch.zeros(max(groups, 1) * CH[l + 1], dtype=torch.int32, device=dev) for l in range(5)]
+        self.ascale = [torch.ones(max(groups, 1), **f32) for l in range(5)]
 
 
 def _ops():
@@ -147,6 +157,15 @@ def _ops():
 
 def _dsc(rate: float) -> float:
     return 1.0 / (1.0 - rate) if rate < 1.0 else 0.0
+
+
+def _sync_max(sync: Callable, t: torch.Tensor) -> None:
+    """All ranks must prescale a block's activations alike (identical fp16 splits on every shard): MAX
+    all-reduce of the channel maxima (non-negative fp32 bit patterns order like the int32 values)."""
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized():
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
 
 
 def _sync_stats(sync: Callable, st: torch.Tensor, groups: int, c: int) -> None:
@@ -161,14 +180,14 @@ def _sync_stats(sync: Callable, st: torch.Tensor, groups: int, c: int) -> None:
 
 def _max_samples(dev, per_sample: int, frac: float = 0.45) -> int:
     """Samples (windows x passes / members) per layer launch: at most ``frac`` of the free HBM and at most
-    ``APNEAUQ_X3_WS_GB`` (default 16 GB) of activation workspace, so that the engine co-resides with
+    ``APNEAUQ_X3_WS_GB`` (default 20 GB) of activation workspace, so that the engine co-resides with
     other work (one 50-pass chunk of 16384 windows would hold ~88 GB).  Batch-BN MC Dropout over 16384
     windows, T = 50: 219.2-220.3 ms in one chunk (100 GB cap), 219.6-220.0 ms in 12-GB chunks
     (``profiles/x3_epilogue_ab_r3.md``): pass chunks of >= 30 k samples keep the launches full."""
     import os
 
     free = torch.cuda.mem_get_info(dev)[0]
-    cap = float(os.environ.get("APNEAUQ_X3_WS_GB", "16")) * 2 ** 30
+    cap = float(os.environ.get("APNEAUQ_X3_WS_GB", "20")) * 2 ** 30
     return max(1, int(min(free * frac, cap)) // per_sample)
 
 
@@ -188,7 +207,7 @@ def mcd_batch(model: X3Model, x: torch.Tensor, n_pass: int, seed: int, pass_base
     n = x.shape[0]
     gn = int(global_n or n)
     if max_samples is None:
-        max_samples = _max_samples(model.device, BYTES_PER_SAMPLE)
+        max_samples = _max_samples(model.device, BYTES_PER_SAMPLE + R1_BYTES)
         if sync is not None:  # identical chunking on every rank
             t = torch.tensor([float(max_samples)], dtype=torch.float64, device=model.device)
             import torch.distributed as dist
@@ -216,11 +235,14 @@ def mcd_batch(model: X3Model, x: torch.Tensor, n_pass: int, seed: int, pass_base
     out = torch.empty(n_pass, n, dtype=torch.float32, device=model.device)
     # block 1 once: no dropout precedes it, so every pass sees the same R_1 and the same moments
     ws.stats[0].zero_()
-    o.x3_l1(x, model.w1, model.b1, ws.r1, ws.stats[0], n, 1)
+    ws.rmax[0][: CH[1]].zero_()
+    o.x3_l1(x, model.w1, model.b1, ws.r1, ws.stats[0], n, 1, ws.rmax[0][: CH[1]])
     if sync is not None:
         _sync_stats(sync, ws.stats[0], 1, CH[1])
+        _sync_max(sync, ws.rmax[0][: CH[1]])
     g, b, mm, mv = model.bn[0]
-    o.x3_aff(ws.stats[0], g, b, mm, mv, ws.aff[0], CH[1], 1, 0, bool(update_moving), n_pass, inv_count, eps, mom, dsc[0])
+    o.x3_aff(ws.stats[0], g, b, mm, mv, ws.aff[0], CH[1], 1, 0, bool(update_moving), n_pass, inv_count, eps, mom, dsc[0],
+             ws.rmax[0][: CH[1]], ws.ascale[0][:1])
     for t0 in range(0, n_pass, chunk):
         tc = min(chunk, n_pass - t0)
         pb = int(pass_base) + t0
@@ -228,15 +250,21 @@ def mcd_batch(model: X3Model, x: torch.Tensor, n_pass: int, seed: int, pass_base
             c = CH[l + 1]
             st = ws.stats[l]
             st[: tc * STAT_SLOTS * 2 * c].zero_()
+            rm = ws.rmax[l][: tc * c] if l < 5 else None
+            if rm is not None:
+                rm.zero_()
             src = ws.r1 if l == 1 else ws.buf[(l - 2) % 2]
             dst = ws.sums if l == 5 else ws.buf[(l - 1) % 2]
             o.x3_layer(l, src, dst, model.wfrag[l], 0, model.bias[l], model.wscale[l], 0, ws.aff[l - 1],
-                       0 if l == 1 else 2 * CH[l], st, n, tc, l == 1, l == 1, thr[l - 1], thr[l], seed, pb,
-                       int(window_offset), int(grid))
+                       0 if l == 1 else 2 * CH[l], st, n, tc, l == 1, thr[l - 1], thr[l], seed, pb,
+                       int(window_offset), int(grid), ws.ascale[l - 1], rm)
             if sync is not None:
                 _sync_stats(sync, st, tc, c)
+                if rm is not None:
+                    _sync_max(sync, rm)
             g, b, mm, mv = model.bn[l]
-            o.x3_aff(st, g, b, mm, mv, ws.aff[l], c, tc, 0, bool(update_moving), 1, inv_count, eps, mom, dsc[l])
+            o.x3_aff(st, g, b, mm, mv, ws.aff[l], c, tc, 0, bool(update_moving), 1, inv_count, eps, mom, dsc[l],
+                     rm, ws.ascale[l][:tc] if rm is not None else None)
         o.x3_head(ws.sums, ws.aff[5], 2 * CH[6], model.dw, model.db, 0, ws.out, n, tc, False)
         out[t0: t0 + tc].copy_(ws.out[: tc * n].view(tc, n))
     return out
@@ -269,23 +297,28 @@ def _mcd_batch_windowed(model: X3Model, x: torch.Tensor, n_pass: int, seed: int,
     def run(s: int, e: int, upto: int, pb: int, stats_layer: int) -> None:
         """Blocks 1..upto+1 over windows [s, e) of pass pb; moments of block stats_layer+1 into its slots."""
         m = e - s
-        o.x3_l1(x[s:e], model.w1, model.b1, ws.r1, ws.stats[0] if stats_layer == 0 else None, m, 1)
+        o.x3_l1(x[s:e], model.w1, model.b1, ws.r1, ws.stats[0] if stats_layer == 0 else None, m, 1,
+                ws.rmax[0][: CH[1]] if stats_layer == 0 else None)
         for l in range(1, upto + 1):
             src = ws.r1 if l == 1 else ws.buf[(l - 2) % 2]
             dst = ws.sums if l == 5 else ws.buf[(l - 1) % 2]
             o.x3_layer(l, src, dst, model.wfrag[l], 0, model.bias[l], model.wscale[l], 0, ws.aff[l - 1],
                        0 if l == 1 else 2 * CH[l], ws.stats[l] if l == stats_layer else None, m, 1, l == 1,
-                       l == 1, thr[l - 1], thr[l], seed, pb, int(window_offset) + s, 0)
+                       thr[l - 1], thr[l], seed, pb, int(window_offset) + s, 0, ws.ascale[l - 1][:1],
+                       ws.rmax[l][: CH[l + 1]] if (l == stats_layer and l < 5) else None)
 
     def finish_layer(l: int, repeat: int) -> None:
         if sync is not None:
             _sync_stats(sync, ws.stats[l], 1, CH[l + 1])
+            if l < 5:
+                _sync_max(sync, ws.rmax[l][: CH[l + 1]])
         g, b, mm, mv = model.bn[l]
         o.x3_aff(ws.stats[l], g, b, mm, mv, ws.aff[l], CH[l + 1], 1, 0, bool(update_moving), repeat, inv_count, eps,
-                 mom, dsc[l])
+                 mom, dsc[l], ws.rmax[l][: CH[l + 1]] if l < 5 else None, ws.ascale[l][:1] if l < 5 else None)
 
     # block 1: no dropout before it, so its moments (and affine) are shared by every pass
     ws.stats[0].zero_()
+    ws.rmax[0].zero_()
     for s, e in bounds:
         run(s, e, 0, int(pass_base), 0)
     finish_layer(0, n_pass)
@@ -293,6 +326,8 @@ def _mcd_batch_windowed(model: X3Model, x: torch.Tensor, n_pass: int, seed: int,
         pb = int(pass_base) + t
         for l in range(1, 6):
             ws.stats[l].zero_()
+            if l < 5:
+                ws.rmax[l].zero_()
             for s, e in bounds:
                 run(s, e, l, pb, l)
             finish_layer(l, 1)
@@ -317,7 +352,7 @@ def forward_running(model: X3Model, x: torch.Tensor, n_pass: int = 1, dropout: b
     n = x.shape[0]
     groups = (n_pass if dropout else model.G) if n > 0 else 1
     if max_samples is None:
-        max_samples = _max_samples(model.device, BYTES_PER_SAMPLE)
+        max_samples = _max_samples(model.device, BYTES_PER_SAMPLE + R1_BYTES)
     wc = max(1, int(max_samples) // max(groups, 1))
     if n <= wc:
         return _forward_running(model, x, n_pass, dropout, seed, pass_offset, window_offset, logits)
@@ -341,21 +376,31 @@ def _forward_running(model: X3Model, x: torch.Tensor, n_pass: int, dropout: bool
     dsc = [_dsc(b.dropout) if dropout else 1.0 for b in spec.blocks]
     eps, mom = float(spec.bn_epsilon), float(spec.bn_momentum)
     seed = int(seed) & ((1 << 63) - 1)
-    # BN affine of the moving statistics, per member (shared by all passes with dropout)
-    for l in range(6):
+    # BN affine of the moving statistics, per member (shared by all passes with dropout), computed after
+    # the block's output exists: its channel maxima set the power-of-two prescale of the fp16 split
+    def aff(l: int) -> None:
         g, b, mm, mv = model.bn[l]
+        rm = ws.rmax[l][: G * CH[l + 1]] if l < 5 else None
         o.x3_aff(None, g, b, mm, mv, ws.aff[l], CH[l + 1], G, CH[l + 1] if G > 1 else 0, False, 1, 1.0, eps, mom,
-                 dsc[l])
-    o.x3_l1(x, model.w1, model.b1, ws.r1, None, n, G)
+                 dsc[l], rm, ws.ascale[l][:G] if rm is not None else None)
+
+    ws.rmax[0][: G * CH[1]].zero_()
+    o.x3_l1(x, model.w1, model.b1, ws.r1, None, n, G, ws.rmax[0][: G * CH[1]])
+    aff(0)
     per_member = G > 1
     for l in range(1, 6):
         src = ws.r1 if l == 1 else ws.buf[(l - 2) % 2]
         dst = ws.sums if l == 5 else ws.buf[(l - 1) % 2]
         wstride = model.wfrag[l].shape[1] // 8 if per_member else 0
+        # one maxima row per member (DE), or one row shared by the passes of one model (MC Dropout)
+        rm = ws.rmax[l][: G * CH[l + 1]] if l < 5 else None
+        if rm is not None:
+            rm.zero_()
         o.x3_layer(l, src, dst, model.wfrag[l], wstride, model.bias[l], model.wscale[l],
                    CH[l + 1] if per_member else 0, ws.aff[l - 1], 2 * CH[l] if per_member else 0, None, n, groups,
-                   dropout and l == 1, dropout and l == 1, thr[l - 1], thr[l], seed, int(pass_offset),
-                   int(window_offset), 0)
+                   dropout and l == 1, thr[l - 1], thr[l], seed, int(pass_offset),
+                   int(window_offset), 0, ws.ascale[l - 1], rm)
+        aff(l)
     o.x3_head(ws.sums, ws.aff[5], 2 * CH[6] if per_member else 0, model.dw, model.db, CH[6] if per_member else 0,
               ws.out, n, groups, bool(logits))
     return ws.out[: groups * n].view(G, n_pass, n).clone()

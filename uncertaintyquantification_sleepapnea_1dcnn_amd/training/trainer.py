@@ -164,11 +164,18 @@ def _fit_batched(models: List, x, y, per_cbs, **fit_kwargs) -> List[History]:
     streams: List = []
     while req:
         live = sorted(req)
-        for key in [k for k in steps if not set(k[0]) <= set(live)]:  # a member finished: free its graphs
-            del steps[key]
         by_n = {}
         for i in live:
             by_n.setdefault(int(req[i][0].shape[0]), []).append(i)
+        # keep only the graphs of the live set's groupings (any batch size: the tail batch's graphs are
+        # replayed every epoch): when a member stops early the live members are regrouped, and a step of
+        # the old grouping (a workspace per member + a graph pool) would never be replayed again
+        want = set()
+        for ids in [live] + list(by_n.values()):
+            ng = min(n_groups, len(ids))
+            want.update(tuple(ids[g::ng]) for g in range(ng))
+        for key in [k for k in steps if k[0] not in want]:
+            del steps[key]
         for n, ids in by_n.items():
             ng = min(n_groups, len(ids))
             subs = [ids[g::ng] for g in range(ng)]
