@@ -30,6 +30,10 @@ statistics, synthetic standardised windows.  Timing: W untimed warmup steps, the
 barrier + synchronize; the max over ranks is reported.  On the GPU a process group is formed even for
 one rank (RCCL, world size 1), so the N=1 point runs the same code path as N=8.
 
+``extra.train`` (``bench/train_extra.py``): BASELINE.json's training config (Adam, BCE, 1 x MI355X) on the
+HIP training kernels -- the graphed single-model step at batch 1024 and 8192, 8 member-batched ensemble
+members, and the loss deviation of 10 HIP steps from the same steps on fp32 autograd.
+
 ``--device cpu`` is a dry run of the same launcher / collectives / metrics on gloo with the fp32
 reference model (CPU tests); its numbers are not performance claims.
 """
@@ -73,6 +77,7 @@ def parse(argv=None):
                          "Dropout)")
     ap.add_argument("--no-secondary", action="store_true", help="skip the bf16 engine's timing (extra.bf16)")
     ap.add_argument("--no-deviation", action="store_true", help="skip the fp32 deviation block")
+    ap.add_argument("--no-train", action="store_true", help="skip the training block (extra.train)")
     ap.add_argument("--deviation-windows", type=int, default=1024)
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu = dry run of launcher + collectives on gloo with the fp32 reference model")
@@ -242,6 +247,13 @@ def run(a):
         if not a.no_deviation:
             secondary["fp32_deviation"] = eng2.deviation(x_glob[: a.deviation_windows], y_glob[: a.deviation_windows])
 
+    train = None
+    if not cpu and not a.no_train:  # BASELINE.json config #2: the training step (every rank trains its own models)
+        from bench import train_extra
+
+        torch.cuda.empty_cache()
+        train = train_extra.measure(dev, a.seed)
+
     macs = SPEC.forward_macs()
     devices = pdist.gather_device_ids()  # collective: every rank
     if rank == 0:
@@ -287,6 +299,7 @@ def run(a):
                 "de_mean_mutual_info": round(agg_de["mean_mutual_info"], 6),
                 "fp32_deviation": deviation,
                 ("bf16" if head_prec == "fp32" else "fp32"): secondary,
+                "train": train,
             },
         }
         _emit(json.dumps(out))

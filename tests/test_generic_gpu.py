@@ -74,12 +74,14 @@ def test_generic_matches_fused_on_reference_spec():
 
 
 def test_model_api_uses_generic_path():
-    """mc_dropout_predict / deep_ensembles_predict / predict of a pooled model run on the HIP kernels."""
+    """mc_dropout_predict / deep_ensembles_predict / predict of a pooled bf16 model run on the HIP kernels
+    (the fp32 default: tests/test_fp32_gpu.py)."""
     _ext.require()
     from uncertaintyquantification_sleepapnea_1dcnn_amd.models.cnn import AlarconCNN1D
     from uncertaintyquantification_sleepapnea_1dcnn_amd.uq import uq_techniques as U
 
-    models = [AlarconCNN1D(spec=POOLED, seed=s, device="cuda", params=_params(POOLED, s)) for s in (1, 2)]
+    models = [AlarconCNN1D(spec=POOLED, seed=s, device="cuda", params=_params(POOLED, s), precision="bf16")
+              for s in (1, 2)]
     assert all(m.uses_generic() and m.uses_hip() and not m.uses_fused() for m in models)
     x = np.random.default_rng(0).standard_normal((33, 60, 4)).astype(np.float32)
     mcd = U.mc_dropout_predict(models[0], x, n_pred=4, bn_mode="running", seed=3)

@@ -80,9 +80,10 @@ def test_generic_fit_reduces_loss(name):
 
 @pytest.mark.parametrize("name", ["pooled", "odd"])
 def test_generic_batch_bn_mc_dropout_matches_reference(name, deterministic):
+    """bf16 kernels (the fp32 default: tests/test_fp32_gpu.py)."""
     _ext.require()
     spec = SPECS[name]
-    m = AlarconCNN1D(spec=spec, seed=6, device="cuda")
+    m = AlarconCNN1D(spec=spec, seed=6, device="cuda", precision="bf16")
     x, _ = _batch(spec, 50, 0)
     snap = m.snapshot()
     got = generic_train.forward_batch_stats(m, x, 3, pass_base=0, seed=m.seed, update_moving=True)

@@ -49,12 +49,12 @@ hipError_t launch_gt_bn_finalize(const float* st, int nslots, int C, float inv_c
                                  float* bn, hipStream_t stream);
 hipError_t launch_gt_apply(const void* z, const float* bn, void* out, int n, int L, int C, int pool, int out_rs,
                            int out_off, int dropout, unsigned thr, float inv_keep, unsigned skey,
-                           unsigned window_offset, hipStream_t stream, const unsigned* skey_dev);
+                           unsigned window_offset, hipStream_t stream, const unsigned* skey_dev, int f32);
 hipError_t launch_gt_bwd(int dz_mode, const void* z, const float* bn, const void* dh, const float* dlog,
                          const float* w, float invL, int n, int L, int C, int pool, int dropout, unsigned thr,
                          float inv_keep, unsigned skey, unsigned window_offset, float* bst, const float* coef,
                          const float* gamma, void* dz, int dz_rs, int dz_off, float* gbias, hipStream_t stream,
-                         const unsigned* skey_dev, int det_slots);
+                         const unsigned* skey_dev, int det_slots, int f32);
 hipError_t launch_gt_bwd_finalize(const float* bst, int nslots, int C, float inv_count, float* coef, float* ggamma,
                                   float* gbeta, hipStream_t stream);
 hipError_t launch_metrics_update(const float* p, const float* y, long long n, const float* thr, int n_thr,
@@ -65,7 +65,12 @@ hipError_t launch_gt_wgrad(const void* x, long long x_rows, const void* dz, long
                            float* gw, hipStream_t st, float* part, long long part_floats);
 hipError_t launch_gt_head(const void* h, const float* w, const float* b, const float* y, float* prob, float* dlog,
                           float* loss, float* gw, float* gb, int n, int L, int C, float inv_gb, hipStream_t st,
-                          float* part, long long part_floats);
+                          float* part, long long part_floats, int f32);
+hipError_t launch_gf32_conv(const float* x, const float* w, const float* bias, float* y, float* stats, int n, int L,
+                            int cin, int cout, int ksize, int mode, int in_rs, int in_off, int flip, int det_slots,
+                            hipStream_t st);
+hipError_t launch_gf32_wgrad(const float* x, const float* dz, long long R, int cin, int cout, int k, float* gw,
+                             float* part, long long part_floats, hipStream_t st);
 int gt_pack_max_blocks();
 long long train_wgrad_part_floats(int B);
 int train_det_floats(int B);
@@ -508,8 +513,11 @@ at::Tensor generic_conv(const at::Tensor& x, const at::Tensor& wfrag, const at::
 }
 
 // ---- generic-spec training (csrc/generic_train.hip); every buffer is preallocated by ops/generic_train.py ----
+// activation buffers of the generic training path: bf16, or fp32 (precision="fp32"); one launch's
+// activation tensors must share the dtype (need_same)
 inline void need_rows(const at::Tensor& t, int64_t rows, int64_t c, const char* what) {
-  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.is_contiguous(), what, ": bf16 contiguous GPU tensor required");
+  TORCH_CHECK(t.is_cuda() && (t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kFloat) && t.is_contiguous(), what,
+              ": bf16 or fp32 contiguous GPU tensor required");
   TORCH_CHECK(t.numel() >= rows * c, what, ": buffer too small (", t.numel(), " < ", rows * c, ")");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, what, ": 16-B alignment required");
 }
@@ -519,6 +527,9 @@ inline void need_f32(const at::Tensor& t, int64_t n, const char* what) {
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, what, ": 16-B alignment required");
 }
 constexpr int64_t kGtSlots = 16;
+inline void need_same(const at::Tensor& a, const at::Tensor& b, const char* what) {
+  TORCH_CHECK(a.scalar_type() == b.scalar_type(), what, ": activation buffers must share one dtype");
+}
 
 // mode 1: y = relu(conv(x) + bias) (N, L, Cout) + BN moment slots; mode 2: y = conv(x) (dgrad).
 // x row (n, t) lives at n * in_rs + in_off + t (zero-padded layouts); the conv reads rows
@@ -548,6 +559,7 @@ void gt_conv(const at::Tensor& x, const at::Tensor& wfrag, const c10::optional<a
   // deterministic mode: one plain-store slot per (workgroup, wave row); the launcher checks the count
   const int det_slots = (mode == 1 && det) ? (int)(stats->numel() / (2 * cout)) : 0;
   TORCH_CHECK(n * L < (int64_t(1) << 31), "gt_conv: too many rows");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16, "gt_conv: bf16 (fp32: gf_conv)");
   const at::DeviceGuard guard(y.device());
   check(apneauq::launch_generic_conv(x.data_ptr(), wfrag.data_ptr(), bp, y.data_ptr(), (int)n, (int)L, (int)cin,
                                      (int)cout, (int)(wfrag.size(1) * 16), (int)ksize, 0, 0, 0u, 0, 1, 0u, 0u, 0ull,
@@ -587,10 +599,11 @@ void gt_apply(const at::Tensor& z, const at::Tensor& bn, at::Tensor& out, int64_
   need_f32(bn, 4 * C, "gt_apply bn");
   TORCH_CHECK(out_rs >= lout && out_off >= 0, "gt_apply: bad output row layout");
   if (n > 0) need_rows(out, (n - 1) * out_rs + out_off + lout, C, "gt_apply out");
+  need_same(z, out, "gt_apply");
   const at::DeviceGuard guard(out.device());
   check(apneauq::launch_gt_apply(z.data_ptr(), bn.data_ptr<float>(), out.data_ptr(), (int)n, (int)L, (int)C, pool ? 1 : 0,
                                  (int)out_rs, (int)out_off, dropout ? 1 : 0, (unsigned)thr, (float)inv_keep,
-                                 (unsigned)skey, (unsigned)window_offset, cur_stream(), kd),
+                                 (unsigned)skey, (unsigned)window_offset, cur_stream(), kd, z.scalar_type() == at::kFloat),
         "gt_apply");
 }
 
@@ -610,6 +623,7 @@ void gt_bwd(bool dz_mode, const at::Tensor& z, const at::Tensor& bn, const c10::
   const float *dlp = nullptr, *wp = nullptr;
   if (dh.has_value()) {
     need_rows(*dh, n * lout, C, "gt_bwd dh");
+    need_same(z, *dh, "gt_bwd");
     dhp = dh->data_ptr();
   } else {
     TORCH_CHECK(dlog.has_value() && w.has_value(), "gt_bwd: need dh or (dlog, w)");
@@ -632,6 +646,7 @@ void gt_bwd(bool dz_mode, const at::Tensor& z, const at::Tensor& bn, const c10::
     TORCH_CHECK(gamma->is_cuda() && gamma->numel() == C, "gt_bwd gamma");
     TORCH_CHECK(dz_rs >= L && dz_off >= 0, "gt_bwd: bad dz row layout");
     if (n > 0) need_rows(*dz, (n - 1) * dz_rs + dz_off + L, C, "gt_bwd dz");
+    need_same(z, *dz, "gt_bwd");
     need_f32(*gbias, kGtSlots * C, "gt_bwd gbias slots");
     cp = coef->data_ptr<float>();
     gp = gamma->data_ptr<float>();
@@ -644,7 +659,7 @@ void gt_bwd(bool dz_mode, const at::Tensor& z, const at::Tensor& bn, const c10::
   check(apneauq::launch_gt_bwd(dz_mode ? 1 : 0, z.data_ptr(), bn.data_ptr<float>(), dhp, dlp, wp, (float)invL, (int)n,
                                (int)L, (int)C, pool ? 1 : 0, dropout ? 1 : 0, (unsigned)thr, (float)inv_keep,
                                (unsigned)skey, (unsigned)window_offset, bp, cp, gp, dzp, (int)dz_rs, (int)dz_off, gbp,
-                               cur_stream(), skey_dev_ptr(skey_dev), det_slots),
+                               cur_stream(), skey_dev_ptr(skey_dev), det_slots, z.scalar_type() == at::kFloat),
         "gt_bwd");
 }
 
@@ -667,6 +682,7 @@ void gt_wgrad(const at::Tensor& x, const at::Tensor& dz, int64_t R, int64_t cin,
               const c10::optional<at::Tensor>& part) {
   need_rows(x, R + k - 1, cin, "gt_wgrad x");
   need_rows(dz, R, cout, "gt_wgrad dz");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && dz.scalar_type() == at::kBFloat16, "gt_wgrad: bf16 (fp32: gf_wgrad)");
   need_f32(gw, k * cin * cout, "gt_wgrad gw");
   TORCH_CHECK(k >= 1 && k <= 15 && cin >= 1 && cout >= 1, "gt_wgrad: 1 <= k <= 15");
   const at::DeviceGuard guard(x.device());
@@ -699,8 +715,59 @@ void gt_head(const at::Tensor& h, const at::Tensor& w, const at::Tensor& b, cons
   check(apneauq::launch_gt_head(h.data_ptr(), w.data_ptr<float>(), b.data_ptr<float>(), y.data_ptr<float>(),
                                 prob.data_ptr<float>(), dlog.data_ptr<float>(), loss.data_ptr<float>(),
                                 gw.data_ptr<float>(), gb.data_ptr<float>(), (int)n, (int)L, (int)C, (float)inv_gb,
-                                cur_stream(), pp, pp ? part->numel() : 0),
+                                cur_stream(), pp, pp ? part->numel() : 0, h.scalar_type() == at::kFloat),
         "gt_head");
+}
+
+// fp32 conv (csrc/gf32_conv.hip): mode 1 y = relu(conv(x) + bias) + BN moment slots (det: one slot per
+// (workgroup, wave row)); mode 2 y = conv(x) with the flipped kernel (flip, dgrad).  w is the Keras kernel
+// (k, Cin_k, Cout_k) read in place: forward cin = Cin_k, cout = Cout_k; dgrad cin = Cout_k, cout = Cin_k.
+void gf_conv(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias, at::Tensor& y,
+             const c10::optional<at::Tensor>& stats, int64_t n, int64_t L, int64_t cin, int64_t cout, int64_t ksize,
+             int64_t mode, int64_t in_rs, int64_t in_off, bool det) {
+  TORCH_CHECK(mode == 1 || mode == 2, "gf_conv: mode must be 1 (train) or 2 (dgrad)");
+  TORCH_CHECK(ksize % 2 == 1 && ksize <= 15 && cout % 4 == 0 && cin >= 1 && n >= 0 && L >= 1, "gf_conv: bad shape");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && y.scalar_type() == at::kFloat, "gf_conv: fp32 activations");
+  need_f32(w, ksize * cin * cout, "gf_conv w");
+  TORCH_CHECK(w.dim() == 3 && w.size(0) == ksize &&
+                  (mode == 1 ? (w.size(1) == cin && w.size(2) == cout) : (w.size(1) == cout && w.size(2) == cin)),
+              "gf_conv: kernel shape must be (k, cin, cout) forward / (k, cout, cin) dgrad");
+  TORCH_CHECK(in_rs >= L && in_off >= 0, "gf_conv: bad input row layout");
+  if (n > 0) need_rows(x, (n - 1) * in_rs + in_off + L, cin, "gf_conv x");
+  need_rows(y, n * L, cout, "gf_conv y");
+  TORCH_CHECK(n * L < (int64_t(1) << 31), "gf_conv: too many rows");
+  const float* bp = nullptr;
+  float* sp = nullptr;
+  int det_slots = 0;
+  if (mode == 1) {
+    TORCH_CHECK(bias.has_value() && stats.has_value(), "gf_conv: mode 1 needs bias and stats");
+    need_f32(*bias, cout, "gf_conv bias");
+    need_f32(*stats, kGtSlots * 2 * cout, "gf_conv stats");
+    bp = bias->data_ptr<float>();
+    sp = stats->data_ptr<float>();
+    if (det) det_slots = (int)(stats->numel() / (2 * cout));
+  }
+  const at::DeviceGuard guard(y.device());
+  check(apneauq::launch_gf32_conv(x.data_ptr<float>(), w.data_ptr<float>(), bp, y.data_ptr<float>(), sp, (int)n, (int)L,
+                                  (int)cin, (int)cout, (int)ksize, (int)mode, (int)in_rs, (int)in_off, mode == 2 ? 1 : 0,
+                                  det_slots, cur_stream()),
+        "gf_conv");
+}
+
+// fp32 wgrad (csrc/gf32_conv.hip): gw (k, cin, cout) = sum_R x[R + tap] dz[R], row-group partials in part
+// summed in a fixed order (deterministic).
+void gf_wgrad(const at::Tensor& x, const at::Tensor& dz, int64_t R, int64_t cin, int64_t cout, int64_t k, at::Tensor& gw,
+              at::Tensor& part) {
+  TORCH_CHECK(x.scalar_type() == at::kFloat && dz.scalar_type() == at::kFloat, "gf_wgrad: fp32 activations");
+  need_rows(x, R + k - 1, cin, "gf_wgrad x");
+  need_rows(dz, R, cout, "gf_wgrad dz");
+  need_f32(gw, k * cin * cout, "gf_wgrad gw");
+  need_f32(part, k * cin * cout, "gf_wgrad part");
+  TORCH_CHECK(k >= 1 && k <= 15 && cin >= 1 && cout >= 1, "gf_wgrad: 1 <= k <= 15");
+  const at::DeviceGuard guard(x.device());
+  check(apneauq::launch_gf32_wgrad(x.data_ptr<float>(), dz.data_ptr<float>(), R, (int)cin, (int)cout, (int)k,
+                                   gw.data_ptr<float>(), part.data_ptr<float>(), part.numel(), cur_stream()),
+        "gf_wgrad");
 }
 
 // All blocks' forward (+ dgrad) MFMA fragments in one launch (csrc/generic_wgrad.hip pack_kernel).
@@ -850,6 +917,9 @@ TORCH_LIBRARY(apneauq, m) {
   m.def("gt_head(Tensor h, Tensor w, Tensor b, Tensor y, Tensor(a!) prob, Tensor(b!) dlog, Tensor(c!) loss, "
         "Tensor(d!) gw, Tensor(e!) gb, int n, int L, int C, float inv_gb, Tensor(f!)? part=None) -> ()");
   m.def("gt_pack(Tensor[] w, Tensor(a!)[] fwd, Tensor(b!)[] dgr, int[] k, int[] cin, int[] cout) -> ()");
+  m.def("gf_conv(Tensor x, Tensor w, Tensor? bias, Tensor(a!) y, Tensor(b!)? stats, int n, int L, int cin, int cout, "
+        "int ksize, int mode, int in_rs, int in_off, bool det=False) -> ()");
+  m.def("gf_wgrad(Tensor x, Tensor dz, int R, int cin, int cout, int k, Tensor(a!) gw, Tensor(b!) part) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
@@ -876,6 +946,8 @@ TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
   m.impl("gt_wgrad", &gt_wgrad);
   m.impl("gt_head", &gt_head);
   m.impl("gt_pack", &gt_pack);
+  m.impl("gf_conv", &gf_conv);
+  m.impl("gf_wgrad", &gf_wgrad);
   m.impl("prep_standardize", &prep_standardize);
   m.impl("prep_knn", &prep_knn);
 }

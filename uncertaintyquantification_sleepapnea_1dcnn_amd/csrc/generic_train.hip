@@ -78,15 +78,23 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* st, int n
   }
 }
 
+// Activation storage: bf16 (the bf16 training path) or fp32 (precision="fp32", csrc/gf32_conv.hip);
+// the kernels below are templated on it (4 consecutive channels per thread either way).
 __device__ __forceinline__ f32x4 load4(const __bf16* p) {
   const bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
   return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
 }
+__device__ __forceinline__ f32x4 load4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ void store4(__bf16* p, const f32x4& v) {
+  *reinterpret_cast<bf16x4*>(p) = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+}
+__device__ __forceinline__ void store4(float* p, const f32x4& v) { *reinterpret_cast<f32x4*>(p) = v; }
 
+template <typename T>
 struct ApplyArgs {
-  const __bf16* z;  // (N, L, C) pre-BN activations
+  const T* z;       // (N, L, C) pre-BN activations
   const float* bn;  // (4, C): scale, shift, mean, rstd
-  __bf16* out;      // row (n, t) at n * out_rs + out_off + t
+  T* out;           // row (n, t) at n * out_rs + out_off + t
   int n, L, C, pool, lout, out_rs, out_off, dropout;
   unsigned thr;
   float inv_keep;
@@ -95,7 +103,8 @@ struct ApplyArgs {
   const unsigned* skey_dev;  // optional: the key read from device memory (HIP-graph replays)
 };
 
-__global__ __launch_bounds__(256) void apply_kernel(ApplyArgs A) {
+template <typename T>
+__global__ __launch_bounds__(256) void apply_kernel(ApplyArgs<T> A) {
   if (A.skey_dev != nullptr) A.skey = *A.skey_dev;
   const int G = A.C >> 2;
   const long long total = (long long)A.n * A.lout * G;
@@ -104,7 +113,7 @@ __global__ __launch_bounds__(256) void apply_kernel(ApplyArgs A) {
     const long long row = i / G;
     const int ns = (int)(row / A.lout), to = (int)(row - (long long)ns * A.lout);
     const int t0 = A.pool ? 2 * to : to;
-    const __bf16* zr = A.z + ((long long)ns * A.L + t0) * A.C + c;
+    const T* zr = A.z + ((long long)ns * A.L + t0) * A.C + c;
     const f32x4 sc = *reinterpret_cast<const f32x4*>(A.bn + c);
     const f32x4 sh = *reinterpret_cast<const f32x4*>(A.bn + A.C + c);
     f32x4 y = load4(zr);
@@ -124,15 +133,15 @@ __global__ __launch_bounds__(256) void apply_kernel(ApplyArgs A) {
       y[2] = (b23 & 0xFFFFu) >= A.thr ? y[2] * A.inv_keep : 0.f;
       y[3] = (b23 >> 16) >= A.thr ? y[3] * A.inv_keep : 0.f;
     }
-    __bf16* dst = A.out + ((long long)ns * A.out_rs + A.out_off + to) * A.C + c;
-    *reinterpret_cast<bf16x4*>(dst) = bf16x4{(__bf16)y[0], (__bf16)y[1], (__bf16)y[2], (__bf16)y[3]};
+    store4(A.out + ((long long)ns * A.out_rs + A.out_off + to) * A.C + c, y);
   }
 }
 
+template <typename T>
 struct BwdArgs {
-  const __bf16* z;     // (N, L, C)
+  const T* z;          // (N, L, C)
   const float* bn;     // (4, C)
-  const __bf16* dh;    // (N, lout, C) upstream gradient, or nullptr in head mode
+  const T* dh;         // (N, lout, C) upstream gradient, or nullptr in head mode
   const float* dlog;   // head mode: dh[n, t, c] = dlog[n] * w[c] * invL
   const float* w;
   float invL;
@@ -144,14 +153,15 @@ struct BwdArgs {
   float* bst;          // bwd_stats: (kSlots, 2, C) sums of dy, dy * xhat
   const float* coef;   // bwd_dz: (2, C) E[dy], E[dy xhat]
   const float* gamma;
-  __bf16* dz;          // bwd_dz: row (n, t) at n * dz_rs + dz_off + t
+  T* dz;               // bwd_dz: row (n, t) at n * dz_rs + dz_off + t
   int dz_rs, dz_off;
   float* gbias;        // bwd_dz: bias-gradient slots (kSlots, C), summed by the host
   int det;             // deterministic mode: block b writes slot b with plain stores (grid <= slots)
 };
 
 // Gradient w.r.t. the BN output y at pre-pool row (ns, t), channels c .. c+3.
-__device__ __forceinline__ f32x4 upstream_dy(const BwdArgs& A, int ns, int t, int c, const f32x4& sc,
+template <typename T>
+__device__ __forceinline__ f32x4 upstream_dy(const BwdArgs<T>& A, int ns, int t, int c, const f32x4& sc,
                                              const f32x4& sh) {
   f32x4 g = f32x4{0.f, 0.f, 0.f, 0.f};
   const int to = A.pool ? (t >> 1) : t;
@@ -173,7 +183,7 @@ __device__ __forceinline__ f32x4 upstream_dy(const BwdArgs& A, int ns, int t, in
     g[3] = (b23 >> 16) >= A.thr ? g[3] * A.inv_keep : 0.f;
   }
   if (A.pool) {  // max-pool backward: the gradient goes to the (first) maximum of the pair
-    const __bf16* zr = A.z + (long long)ns * A.L * A.C + c;
+    const T* zr = A.z + (long long)ns * A.L * A.C + c;
     const f32x4 za = load4(zr + (long long)t * A.C), zb = load4(zr + (long long)(t ^ 1) * A.C);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -201,8 +211,8 @@ __device__ __forceinline__ void block_reduce8(float* lds, float (&v)[8], int G, 
   }
 }
 
-template <bool DZ>
-__global__ __launch_bounds__(256) void bwd_kernel(BwdArgs A) {
+template <bool DZ, typename T>
+__global__ __launch_bounds__(256) void bwd_kernel(BwdArgs<T> A) {
   __shared__ float lds[8 * 256];
   if (A.skey_dev != nullptr) A.skey = *A.skey_dev;
   const int G = A.C >> 2;
@@ -242,8 +252,7 @@ __global__ __launch_bounds__(256) void bwd_kernel(BwdArgs A) {
           d[j] = z[j] > 0.f ? gr[j] * (dy[j] - k0[j] - xh * k1[j]) : 0.f;
           acc[j] += d[j];
         }
-        __bf16* dst = A.dz + ((long long)ns * A.dz_rs + A.dz_off + t) * A.C + c;
-        *reinterpret_cast<bf16x4*>(dst) = bf16x4{(__bf16)d[0], (__bf16)d[1], (__bf16)d[2], (__bf16)d[3]};
+        store4(A.dz + ((long long)ns * A.dz_rs + A.dz_off + t) * A.C + c, d);
       }
     }
   }
@@ -301,14 +310,15 @@ hipError_t launch_gt_bn_finalize(const float* st, int nslots, int C, float inv_c
   return hipGetLastError();
 }
 
-hipError_t launch_gt_apply(const void* z, const float* bn, void* out, int n, int L, int C, int pool, int out_rs,
-                           int out_off, int dropout, unsigned thr, float inv_keep, unsigned skey,
-                           unsigned window_offset, hipStream_t stream, const unsigned* skey_dev) {
-  gtrain::ApplyArgs A;
+template <typename T>
+static hipError_t gt_apply_t(const void* z, const float* bn, void* out, int n, int L, int C, int pool, int out_rs,
+                             int out_off, int dropout, unsigned thr, float inv_keep, unsigned skey,
+                             unsigned window_offset, hipStream_t stream, const unsigned* skey_dev) {
+  gtrain::ApplyArgs<T> A;
   A.skey_dev = skey_dev;
-  A.z = reinterpret_cast<const __bf16*>(z);
+  A.z = reinterpret_cast<const T*>(z);
   A.bn = bn;
-  A.out = reinterpret_cast<__bf16*>(out);
+  A.out = reinterpret_cast<T*>(out);
   A.n = n;
   A.L = L;
   A.C = C;
@@ -323,20 +333,30 @@ hipError_t launch_gt_apply(const void* z, const float* bn, void* out, int n, int
   A.window_offset = window_offset;
   const long long items = (long long)n * A.lout * (C / 4);
   if (items == 0) return hipSuccess;
-  hipLaunchKernelGGL(gtrain::apply_kernel, dim3(gtrain::elem_grid(items, 256)), dim3(256), 0, stream, A);
+  hipLaunchKernelGGL(gtrain::apply_kernel<T>, dim3(gtrain::elem_grid(items, 256)), dim3(256), 0, stream, A);
   return hipGetLastError();
 }
 
-hipError_t launch_gt_bwd(int dz_mode, const void* z, const float* bn, const void* dh, const float* dlog,
-                         const float* w, float invL, int n, int L, int C, int pool, int dropout, unsigned thr,
-                         float inv_keep, unsigned skey, unsigned window_offset, float* bst, const float* coef,
-                         const float* gamma, void* dz, int dz_rs, int dz_off, float* gbias, hipStream_t stream,
-                         const unsigned* skey_dev, int det_slots) {
-  gtrain::BwdArgs A;
+hipError_t launch_gt_apply(const void* z, const float* bn, void* out, int n, int L, int C, int pool, int out_rs,
+                           int out_off, int dropout, unsigned thr, float inv_keep, unsigned skey,
+                           unsigned window_offset, hipStream_t stream, const unsigned* skey_dev, int f32) {
+  return f32 ? gt_apply_t<float>(z, bn, out, n, L, C, pool, out_rs, out_off, dropout, thr, inv_keep, skey,
+                                 window_offset, stream, skey_dev)
+             : gt_apply_t<__bf16>(z, bn, out, n, L, C, pool, out_rs, out_off, dropout, thr, inv_keep, skey,
+                                  window_offset, stream, skey_dev);
+}
+
+template <typename T>
+static hipError_t gt_bwd_t(int dz_mode, const void* z, const float* bn, const void* dh, const float* dlog,
+                           const float* w, float invL, int n, int L, int C, int pool, int dropout, unsigned thr,
+                           float inv_keep, unsigned skey, unsigned window_offset, float* bst, const float* coef,
+                           const float* gamma, void* dz, int dz_rs, int dz_off, float* gbias, hipStream_t stream,
+                           const unsigned* skey_dev, int det_slots) {
+  gtrain::BwdArgs<T> A;
   A.skey_dev = skey_dev;
-  A.z = reinterpret_cast<const __bf16*>(z);
+  A.z = reinterpret_cast<const T*>(z);
   A.bn = bn;
-  A.dh = reinterpret_cast<const __bf16*>(dh);
+  A.dh = reinterpret_cast<const T*>(dh);
   A.dlog = dlog;
   A.w = w;
   A.invL = invL;
@@ -353,7 +373,7 @@ hipError_t launch_gt_bwd(int dz_mode, const void* z, const float* bn, const void
   A.bst = bst;
   A.coef = coef;
   A.gamma = gamma;
-  A.dz = reinterpret_cast<__bf16*>(dz);
+  A.dz = reinterpret_cast<T*>(dz);
   A.dz_rs = dz_rs;
   A.dz_off = dz_off;
   A.gbias = gbias;
@@ -365,10 +385,21 @@ hipError_t launch_gt_bwd(int dz_mode, const void* z, const float* bn, const void
   if (A.det && g > det_slots) g = det_slots;  // one slot per block (grid-stride rows)
   const dim3 grid(g);
   if (dz_mode)
-    hipLaunchKernelGGL(gtrain::bwd_kernel<true>, grid, dim3(256), 0, stream, A);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(gtrain::bwd_kernel<true, T>), grid, dim3(256), 0, stream, A);
   else
-    hipLaunchKernelGGL(gtrain::bwd_kernel<false>, grid, dim3(256), 0, stream, A);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(gtrain::bwd_kernel<false, T>), grid, dim3(256), 0, stream, A);
   return hipGetLastError();
+}
+
+hipError_t launch_gt_bwd(int dz_mode, const void* z, const float* bn, const void* dh, const float* dlog,
+                         const float* w, float invL, int n, int L, int C, int pool, int dropout, unsigned thr,
+                         float inv_keep, unsigned skey, unsigned window_offset, float* bst, const float* coef,
+                         const float* gamma, void* dz, int dz_rs, int dz_off, float* gbias, hipStream_t stream,
+                         const unsigned* skey_dev, int det_slots, int f32) {
+  return f32 ? gt_bwd_t<float>(dz_mode, z, bn, dh, dlog, w, invL, n, L, C, pool, dropout, thr, inv_keep, skey,
+                               window_offset, bst, coef, gamma, dz, dz_rs, dz_off, gbias, stream, skey_dev, det_slots)
+             : gt_bwd_t<__bf16>(dz_mode, z, bn, dh, dlog, w, invL, n, L, C, pool, dropout, thr, inv_keep, skey,
+                                window_offset, bst, coef, gamma, dz, dz_rs, dz_off, gbias, stream, skey_dev, det_slots);
 }
 
 hipError_t launch_gt_bwd_finalize(const float* bst, int nslots, int C, float inv_count, float* coef, float* ggamma,

@@ -243,8 +243,9 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(WgArgs A) {
 // gradients.  One wave per sample, lanes over channels; workgroup-level sums, then one atomic per
 // channel / scalar per workgroup.
 // ---------------------------------------------------------------------------------------------
+template <typename T>
 struct HeadArgs {
-  const __bf16* h;   // (n, L, C)
+  const T* h;        // (n, L, C) bf16, or fp32 (precision="fp32")
   const float* w;    // (C)
   const float* b;    // (1)
   const float* y;    // (n)
@@ -258,14 +259,15 @@ struct HeadArgs {
   float* part;       // deterministic mode: per-workgroup records [loss, dense bias, dense weights (C)]
 };
 
-__global__ __launch_bounds__(256) void head_kernel(HeadArgs A) {
+template <typename T>
+__global__ __launch_bounds__(256) void head_kernel(HeadArgs<T> A) {
   extern __shared__ __attribute__((aligned(16))) float hsm[];  // [4 waves][C] gap, then 2 sums
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int s = blockIdx.x * 4 + wave;
   float* gap = hsm + wave * A.C;
   float part = 0.f;
   if (s < A.n) {
-    const __bf16* base = A.h + (long long)s * A.L * A.C;
+    const T* base = A.h + (long long)s * A.L * A.C;
     for (int c = lane; c < A.C; c += 64) {
       float acc = 0.f;
       for (int t = 0; t < A.L; ++t) acc += (float)base[(long long)t * A.C + c];
@@ -422,10 +424,17 @@ static hipError_t wg_dispatch(const gwgrad::WgArgs& A, int grid, bool im2col, hi
 }
 
 // gw must be zeroed by the caller (the step zeroes the whole flat gradient).
-static hipError_t ordered_reduce(const float* part, int nrows, long long ncols, gwgrad::RedDst d, hipStream_t st) {
+hipError_t ordered_reduce(const float* part, int nrows, long long ncols, gwgrad::RedDst d, hipStream_t st) {
   hipLaunchKernelGGL(gwgrad::ordered_reduce_kernel, dim3((unsigned)((ncols + 15) / 16)), dim3(256), 0, st, part, nrows,
                      ncols, d);
   return hipGetLastError();
+}
+
+// out[c] = sum over the nrows rows of part[r][c], in the fixed order of ordered_reduce_kernel
+hipError_t launch_ordered_sum(const float* part, int nrows, long long ncols, float* out, hipStream_t st) {
+  gwgrad::RedDst d = {};
+  d.seg[0] = {out, ncols};
+  return ordered_reduce(part, nrows, ncols, d, st);
 }
 
 // part (deterministic mode, nullable): room for part_floats partials; the row groups are capped so that
@@ -495,13 +504,19 @@ hipError_t launch_gt_wgrad(const void* x, long long x_rows, const void* dz, long
 // part (deterministic mode, nullable): ceil(n / 4) * (C + 2) floats of per-workgroup records.
 hipError_t launch_gt_head(const void* h, const float* w, const float* b, const float* y, float* prob, float* dlog,
                           float* loss, float* gw, float* gb, int n, int L, int C, float inv_gb, hipStream_t st,
-                          float* part, long long part_floats) {
+                          float* part, long long part_floats, int f32) {
   if (n <= 0) return hipSuccess;
   const int nblk = (n + 3) / 4;
   if (part != nullptr && (long long)nblk * (C + 2) > part_floats) return hipErrorInvalidValue;
-  gwgrad::HeadArgs A{reinterpret_cast<const __bf16*>(h), w, b, y, prob, dlog, loss, gw, gb, n, L, C, inv_gb, part};
   const size_t lds = (4 * (size_t)C + 8) * sizeof(float);
-  hipLaunchKernelGGL(gwgrad::head_kernel, dim3(nblk), dim3(256), lds, st, A);
+  if (f32) {
+    gwgrad::HeadArgs<float> A{reinterpret_cast<const float*>(h), w, b, y, prob, dlog, loss, gw, gb, n, L, C, inv_gb, part};
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(gwgrad::head_kernel<float>), dim3(nblk), dim3(256), lds, st, A);
+  } else {
+    gwgrad::HeadArgs<__bf16> A{reinterpret_cast<const __bf16*>(h), w, b, y, prob, dlog, loss, gw, gb, n, L, C, inv_gb,
+                               part};
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(gwgrad::head_kernel<__bf16>), dim3(nblk), dim3(256), lds, st, A);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || part == nullptr) return e;
   gwgrad::RedDst d = {};

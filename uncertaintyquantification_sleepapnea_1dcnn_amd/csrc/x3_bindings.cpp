@@ -13,6 +13,7 @@
 namespace apneauq {
 int x3_lds_bytes(int layer);
 int x3_tile_samples(int layer);
+int x3_wg_per_cu(int layer);
 hipError_t x3_launch_layer(int layer, const x3::LayerArgs& A, int grid, hipStream_t stream);
 hipError_t x3_launch_l1(const x3::L1Args& A, hipStream_t stream);
 hipError_t x3_launch_aff(const x3::AffArgs& A, hipStream_t stream);
@@ -110,7 +111,7 @@ void x3_layer(int64_t layer, const at::Tensor& in, at::Tensor& out, const at::Te
   A.pass_base = (unsigned)pass_base;
   A.window_offset = (unsigned)window_offset;
   A.seed = (unsigned long long)seed;
-  int g = grid > 0 ? (int)grid : num_cus(in);
+  int g = grid > 0 ? (int)grid : num_cus(in) * apneauq::x3_wg_per_cu((int)layer);
   if (g > A.total_tiles) g = A.total_tiles;
   check(apneauq::x3_launch_layer((int)layer, A, g, cur_stream()), "x3_layer");
 }

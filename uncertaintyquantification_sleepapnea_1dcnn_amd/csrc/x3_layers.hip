@@ -101,12 +101,11 @@ __device__ __forceinline__ int xcd_wg() {
 // chunk c+2, BN affine + dropout + fp16 split of chunk c+1 into LDS.  vmcnt retires in order, so an MFMA
 // wave that issued HBM loads would stall its next weight-fragment wait on them; loader waves take that
 // latency instead, and wait at the chunk barrier without using issue slots.
-// Register budget: 2 waves per SIMD up to 8 waves per workgroup, ceil(NW / 4) beyond (one workgroup per
-// CU: the two chunk buffers leave no LDS for a second).
-template <int NW>
-constexpr int waves_per_eu() { return NW > 8 ? (NW + 3) / 4 : 2; }
-template <int CIN, int COUT, int KS, int S, int WM, int WN, bool LAST, int LW, int CK>
-__global__ __launch_bounds__((WM * WN + LW) * 64, waves_per_eu<WM * WN + LW>()) void layer_kernel(const LayerArgs A) {
+// Register budget: the waves of WPC workgroups per CU over the 4 SIMDs, at least 2 per SIMD.
+template <int NW, int WPC>
+constexpr int waves_per_eu() { return NW * WPC > 8 ? (NW * WPC + 3) / 4 : 2; }
+template <int CIN, int COUT, int KS, int S, int WM, int WN, bool LAST, int LW, int CK, int WPC>
+__global__ __launch_bounds__((WM * WN + LW) * 64, (waves_per_eu<WM * WN + LW, WPC>())) void layer_kernel(const LayerArgs A) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NWM = WM * WN, NW = NWM + LW, kThreads = NW * 64;
   constexpr int kCK = CK, kRowB = row_bytes(CK), NQ = CK / 32, kQ = CK / 4;  // 32-ch sub-chunks, quads / row
@@ -671,11 +670,11 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs A) {
 }
 
 // ------------------------------------------------------------------------------- launch helpers
-template <int CIN, int COUT, int KS, int S, int WM, int WN, bool LAST, int LW, int CK>
+template <int CIN, int COUT, int KS, int S, int WM, int WN, bool LAST, int LW, int CK, int WPC>
 hipError_t launch_layer(const LayerArgs& A, int grid, hipStream_t stream) {
   constexpr int lds = lds_bytes(S, COUT, CK);
-  static_assert(lds <= 160 * 1024, "LDS per workgroup");
-  auto k = layer_kernel<CIN, COUT, KS, S, WM, WN, LAST, LW, CK>;
+  static_assert(WPC * lds <= 160 * 1024, "LDS of the workgroups sharing a CU");
+  auto k = layer_kernel<CIN, COUT, KS, S, WM, WN, LAST, LW, CK, WPC>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -690,7 +689,7 @@ hipError_t launch_layer(const LayerArgs& A, int grid, hipStream_t stream) {
 
 // Layer table of the reference architecture (cnn_baseline_train.py:59-86), blocks 2..6:
 //   <Cin, Cout, k, samples per tile, wave rows WM, wave channel groups WN, block 6, loader waves LW,
-//    input channels per staged chunk CK>
+//    input channels per staged chunk CK, persistent workgroups per CU WPC>
 // Each MFMA wave owns (4 S / WM) 16-row tiles x (Cout / 16 / WN) 16-channel tiles; the 64-accumulator-tile
 // layers (Cout 224 / 256) run 2-sample tiles so that the next k-step's weight fragments and the B
 // double-buffer fit beside the accumulators without spilling.  Loader waves (ablation table in
@@ -698,15 +697,21 @@ hipError_t launch_layer(const LayerArgs& A, int grid, hipStream_t stream) {
 // budget of 8 waves (loaders at 2-sample tiles: slower; at 4: 99 VGPRs spilled).  64-channel chunks for
 // blocks 3 and 6 (block 2 would spill; Cin 224 / 96 are not multiples of 64).  Measurements:
 // profiles/x3_epilogue_ab_r3.md.
-#define APNEAUQ_X3_LAYERS(X)               \
-  X(1, 128, 192, 5, 4, 2, 4, false, 0, 32) \
-  X(2, 192, 224, 3, 2, 1, 7, false, 4, 64) \
-  X(3, 224, 96, 7, 4, 4, 2, false, 4, 32)  \
-  X(4, 96, 256, 9, 2, 1, 8, false, 4, 32)  \
-  X(5, 256, 96, 9, 4, 4, 2, true, 4, 64)
+// A/B builds may substitute another table (-DAPNEAUQ_X3_TABLE='"path.h"', tools/probes/x3_tables/):
+// every entry is a complete, correct configuration, only the speed differs.
+#ifdef APNEAUQ_X3_TABLE
+#include APNEAUQ_X3_TABLE
+#else
+#define APNEAUQ_X3_LAYERS(X)                  \
+  X(1, 128, 192, 5, 4, 2, 4, false, 0, 32, 1) \
+  X(2, 192, 224, 3, 2, 1, 7, false, 4, 64, 1) \
+  X(3, 224, 96, 7, 4, 4, 2, false, 4, 32, 1)  \
+  X(4, 96, 256, 9, 2, 1, 8, false, 4, 32, 1)  \
+  X(5, 256, 96, 9, 4, 4, 2, true, 4, 64, 1)
+#endif
 
 int x3_lds_bytes(int layer) {
-#define APNEAUQ_X3_LDS(L, CI, CO, K, S, WM, WN, LAST, LW, CK) \
+#define APNEAUQ_X3_LDS(L, CI, CO, K, S, WM, WN, LAST, LW, CK, WPC) \
   if (layer == L) return x3::lds_bytes(S, CO, CK);
   APNEAUQ_X3_LAYERS(APNEAUQ_X3_LDS)
 #undef APNEAUQ_X3_LDS
@@ -714,17 +719,25 @@ int x3_lds_bytes(int layer) {
 }
 
 int x3_tile_samples(int layer) {
-#define APNEAUQ_X3_TS(L, CI, CO, K, S, WM, WN, LAST, LW, CK) \
+#define APNEAUQ_X3_TS(L, CI, CO, K, S, WM, WN, LAST, LW, CK, WPC) \
   if (layer == L) return S;
   APNEAUQ_X3_LAYERS(APNEAUQ_X3_TS)
 #undef APNEAUQ_X3_TS
   return 0;
 }
 
+int x3_wg_per_cu(int layer) {
+#define APNEAUQ_X3_WPC(L, CI, CO, K, S, WM, WN, LAST, LW, CK, WPC) \
+  if (layer == L) return WPC;
+  APNEAUQ_X3_LAYERS(APNEAUQ_X3_WPC)
+#undef APNEAUQ_X3_WPC
+  return 1;
+}
+
 hipError_t x3_launch_layer(int layer, const x3::LayerArgs& A, int grid, hipStream_t stream) {
   using namespace x3;
-#define APNEAUQ_X3_LAUNCH(L, CI, CO, K, S, WM, WN, LAST, LW, CK) \
-  if (layer == L) return launch_layer<CI, CO, K, S, WM, WN, LAST, LW, CK>(A, grid, stream);
+#define APNEAUQ_X3_LAUNCH(L, CI, CO, K, S, WM, WN, LAST, LW, CK, WPC) \
+  if (layer == L) return launch_layer<CI, CO, K, S, WM, WN, LAST, LW, CK, WPC>(A, grid, stream);
   APNEAUQ_X3_LAYERS(APNEAUQ_X3_LAUNCH)
 #undef APNEAUQ_X3_LAUNCH
   return hipErrorInvalidValue;

@@ -13,8 +13,10 @@ Execution backends (MI355X-first):
   ``precision="bf16"`` the bf16 fused whole-network kernel (``ops/fused.py``); other architectures
   run the layer-wise bf16 kernels (``ops/generic.py``).  Packed weights are cached per weight version;
 * training steps run the layer-wise HIP kernels (``ops/train_ops.py``; replayed from a captured
-  HIP graph on a single device) with the Keras BatchNorm/Dropout/Adam semantics, or fp32 autograd
-  over the reference ops where no kernel exists (CPU, non-default architectures);
+  HIP graph on a single device) with the Keras BatchNorm/Dropout/Adam semantics -- bf16 MFMA operands
+  by default, or with ``train_precision="fp32"`` the reference's fp32 (fp32 activations and gradients,
+  fp32-input MFMA convs: ``ops/generic_train.py``, ``csrc/gf32_conv.hip``) -- or fp32 autograd over the
+  reference ops where no kernel exists (CPU);
 * ``model(x, training=True)`` reproduces Keras exactly: dropout on, BatchNorm on the statistics of
   the batch passed in, moving averages updated as a side effect (the reference's MC Dropout
   quirk).
@@ -41,7 +43,7 @@ def _default_device():
 class AlarconCNN1D:
     def __init__(self, input_shape: Sequence[int] = (60, 4), spec: Optional[ModelSpec] = None, seed: int = 2025,
                  device=None, name: str = "Alarcon_1D_CNN_Model", params=None, pool: bool = False,
-                 precision: Optional[str] = None):
+                 precision: Optional[str] = None, train_precision: Optional[str] = None):
         self.spec = spec if spec is not None else ModelSpec.with_input(input_shape, pool=pool)
         self.name = name
         self.seed = int(seed)
@@ -49,6 +51,11 @@ class AlarconCNN1D:
         self.precision = precision or os.environ.get("APNEAUQ_PRECISION", "fp32")
         if self.precision not in ("fp32", "bf16"):
             raise ValueError("precision must be 'fp32' or 'bf16'")
+        # training precision on the GPU: "bf16" (bf16 MFMA operands, fp32 accumulation / master weights) or
+        # "fp32" (the reference's: fp32 activations and gradients, fp32-input MFMA convs, csrc/gf32_conv.hip)
+        self.train_precision = train_precision or os.environ.get("APNEAUQ_TRAIN_PRECISION", "bf16")
+        if self.train_precision not in ("fp32", "bf16"):
+            raise ValueError("train_precision must be 'fp32' or 'bf16'")
         self.device = torch.device(device) if device is not None else _default_device()
         init = params if params is not None else R.init_params(self.spec, self.seed)
         self.store = ParamStore(self.spec, init, self.device)
@@ -120,7 +127,8 @@ class AlarconCNN1D:
         self._blob = None
         self._gpack = None
         self._x3m = None
-        for attr in ("_train_ws", "_mcd_ws", "_train_graphs", "_gtrain_ws", "_gfwd_ws"):  # device workspaces / captured graphs
+        for attr in ("_train_ws", "_mcd_ws", "_train_graphs", "_gtrain_ws", "_gfwd_ws", "_gtrain_ws32", "_gfwd_ws32",
+                     "_gtrain_graphs"):  # device workspaces / captured graphs
             if hasattr(self, attr):
                 delattr(self, attr)
         if self.optimizer.m is not None:
@@ -167,7 +175,8 @@ class AlarconCNN1D:
     def hip_infer(self, x: torch.Tensor, n_pass: int = 1, dropout: bool = False, seed: Optional[int] = None,
                   pass_offset: int = 0, window_offset: int = 0, logits: bool = False) -> torch.Tensor:
         """(n_pass, N) fp32 probabilities (or logits), BN on running statistics, on the engine chosen by
-        ``precision``: fp32-faithful (``x``'s fp32 values) or bf16 (``x`` rounded to bf16)."""
+        ``precision``: fp32 (the fp32-faithful x3 engine for the reference architecture, the fp32-input
+        MFMA layer-wise kernels for any other; ``x``'s fp32 values) or bf16 (``x`` rounded to bf16)."""
         if self.uses_x3():
             from ..ops import x3
 
@@ -175,6 +184,16 @@ class AlarconCNN1D:
             return x3.forward_running(self.x3_model(), x, n_pass=n_pass, dropout=dropout,
                                       seed=self.seed if seed is None else seed, pass_offset=pass_offset,
                                       window_offset=window_offset, logits=logits)[0]
+        if self.precision == "fp32" and self.uses_generic():
+            # any other architecture (MaxPool1D blocks, the 30 s single-channel window) at fp32: the
+            # fp32-input MFMA layer-wise path (ops/generic_train.py:forward_running_f32)
+            from ..ops import generic_train
+
+            _ext.require()
+            return generic_train.forward_running_f32(self, x, n_pass=n_pass, dropout=dropout,
+                                                     seed=self.seed if seed is None else seed,
+                                                     pass_offset=pass_offset, window_offset=window_offset,
+                                                     logits=logits)
         return self.hip_forward(x.to(torch.bfloat16).contiguous(), n_pass=n_pass, dropout=dropout, seed=seed,
                                 pass_offset=pass_offset, window_offset=window_offset, logits=logits)
 

@@ -52,6 +52,18 @@ def deterministic() -> bool:
     return bool(train_ops.DETERMINISTIC)
 
 
+def supports_fp32(spec: ModelSpec) -> bool:
+    """True if the fp32 kernels (``csrc/gf32_conv.hip`` + the fp32 instantiations of the elementwise
+    kernels) implement ``spec`` -- any architecture the generic path handles, the reference one included."""
+    if not generic.supports(spec) or any(b.kernel_size > 15 for b in spec.blocks):
+        return False
+    if _ext.available():
+        return True
+    if not _ext.fallback_allowed():
+        _ext.require()
+    return False
+
+
 def supports(spec: ModelSpec) -> bool:
     """True if the generic HIP training kernels implement ``spec`` (the same shapes as the generic
     inference kernels).  On a GPU box a missing extension raises unless APNEAUQ_ALLOW_FALLBACK=1."""
@@ -67,17 +79,20 @@ def supports(spec: ModelSpec) -> bool:
 class GenericTrainWorkspace:
     """Device buffers of one model for batches of up to ``batch`` windows."""
 
-    def __init__(self, model, batch: int, with_backward: bool = True, det: Optional[bool] = None):
+    def __init__(self, model, batch: int, with_backward: bool = True, det: Optional[bool] = None, f32: bool = False):
         spec: ModelSpec = model.spec
         dev = model.store.device
         self.model = model
         self.B = int(batch)
         self.with_backward = with_backward
+        # f32: precision="fp32" -- fp32 activations / gradients and fp32-input MFMA convs (csrc/gf32_conv.hip)
+        self.f32 = bool(f32)
         # deterministic mode (SURVEY §5): every cross-workgroup sum -- BN moments, backward sums, bias,
         # weight and head gradients -- goes through per-workgroup partial slots written with plain
-        # stores and added in a fixed order (csrc/generic_*.hip ``det``), instead of fp32 atomics
-        self.det = deterministic() if det is None else bool(det)
-        B, bf = self.B, torch.bfloat16
+        # stores and added in a fixed order (csrc/generic_*.hip ``det``), instead of fp32 atomics.
+        # The fp32 path is always deterministic.
+        self.det = True if self.f32 else (deterministic() if det is None else bool(det))
+        B, bf = self.B, (torch.float32 if self.f32 else torch.bfloat16)
         self.L = spec.lengths()
         self.ch = spec.channels()
         self.ks = [b.kernel_size for b in spec.blocks]
@@ -109,7 +124,12 @@ class GenericTrainWorkspace:
             # deterministic mode: wgrad row-group partials (shared by the sequential wgrad launches) and
             # the head's per-workgroup records
             wmax = max(self.ks[l] * self.ch[l] * self.ch[l + 1] for l in range(nl))
-            self.wpart = torch.empty(DET_WGRAD_GROUPS * wmax, device=dev) if self.det else None
+            if self.f32:  # gf_wgrad row groups: up to ~512 workgroups per layer (csrc/gf32_conv.hip)
+                want = [-(-512 // (-(-self.ch[l] // 16) * -(-self.ch[l + 1] // 64))) for l in range(nl)]
+                nf = max(w * self.ks[l] * self.ch[l] * self.ch[l + 1] for l, w in enumerate(want))
+                self.wpart = torch.empty(min(nf, 1 << 24), device=dev)
+            else:
+                self.wpart = torch.empty(DET_WGRAD_GROUPS * wmax, device=dev) if self.det else None
             self.hpart = torch.empty(-(-B // 4) * (self.ch[-1] + 2), device=dev) if self.det else None
             self.coef = [torch.zeros(2 * self.ch[l + 1], device=dev) for l in range(nl)]
             self.y = torch.zeros(B, device=dev)
@@ -132,9 +152,13 @@ class GenericTrainWorkspace:
 
     def pack(self, backward: bool):
         """bf16 MFMA fragments of every conv kernel (forward; + dgrad orientation when training), all
-        blocks in one HIP launch into buffers allocated once (the weights change every step)."""
+        blocks in one HIP launch into buffers allocated once (the weights change every step).  The fp32
+        kernels read the Keras kernels in place: nothing to pack."""
         v = self.model.store.views
         nl = len(self.ks)
+        if self.f32:
+            w = [v[f"conv1d_{l + 1}/kernel"] for l in range(nl)]
+            return w, w
         if getattr(self, "_wf", None) is None:
             dev = self.model.store.device
             self._wf, self._wd = [], []
@@ -158,11 +182,11 @@ def _frag(w: torch.Tensor) -> torch.Tensor:
     return fused.pack_conv_fragments(torch.nn.functional.pad(w, (0, cpad - cout)))
 
 
-def _get_ws(model, batch: int, with_backward: bool = True) -> GenericTrainWorkspace:
-    attr = "_gtrain_ws" if with_backward else "_gfwd_ws"
+def _get_ws(model, batch: int, with_backward: bool = True, f32: bool = False) -> GenericTrainWorkspace:
+    attr = ("_gtrain_ws" if with_backward else "_gfwd_ws") + ("32" if f32 else "")
     ws = getattr(model, attr, None)
-    if ws is None or ws.B < batch or ws.det != deterministic():
-        ws = GenericTrainWorkspace(model, batch, with_backward=with_backward)
+    if ws is None or ws.B < batch or (not f32 and ws.det != deterministic()):
+        ws = GenericTrainWorkspace(model, batch, with_backward=with_backward, f32=f32)
         setattr(model, attr, ws)
     return ws
 
@@ -179,8 +203,9 @@ def _forward(ws: GenericTrainWorkspace, n: int, global_n: int, seed: int, pass_i
     for l, b in enumerate(spec.blocks):
         i = l + 1
         cin, cout, L = ws.ch[l], ws.ch[l + 1], ws.L[l]
-        o.gt_conv(ws.xin[l], wf[l], v[f"conv1d_{i}/bias"], ws.z[l], ws.st[l], n, L, cin, cout, ws.ks[l], 1,
-                  ws.rs[l], 2 * ws.pads[l], ws.det)
+        conv = o.gf_conv if ws.f32 else o.gt_conv
+        conv(ws.xin[l], wf[l], v[f"conv1d_{i}/bias"], ws.z[l], ws.st[l], n, L, cin, cout, ws.ks[l], 1,
+             ws.rs[l], 2 * ws.pads[l], ws.det)
         if sync is not None:
             sync(ws.st[l])
         o.gt_bn_finalize(ws.st[l], cout, 1.0 / (global_n * L), v[f"batchnorm_{i}/gamma"], v[f"batchnorm_{i}/beta"],
@@ -243,17 +268,26 @@ def _grads(model, ws: GenericTrainWorkspace, y: torch.Tensor, n: int, gb: int, p
                  ws.dbs[l], kd, ws.det)
         torch.sum(ws.dbs[l], 0, out=g[f"conv1d_{i}/bias"])
         if l > 0:
-            o.gt_conv(ws.dzp[l], wd[l], None, ws.dh[l], None, n, L, cout, cin, k, 2, ws.rs[l], p)
+            (o.gf_conv if ws.f32 else o.gt_conv)(ws.dzp[l], wd[l], None, ws.dh[l], None, n, L, cout, cin, k, 2,
+                                                 ws.rs[l], p)
         # wgrad: dW[tap] = Xpad[tap : tap + R]^T dZpad (R = n * rs rows), split-K MFMA into the zeroed grad
-        o.gt_wgrad(ws.xin[l], ws.dzp[l], n * ws.rs[l], cin, cout, k, g[f"conv1d_{i}/kernel"], ws.wpart)
+        if ws.f32:
+            o.gf_wgrad(ws.xin[l], ws.dzp[l], n * ws.rs[l], cin, cout, k, g[f"conv1d_{i}/kernel"], ws.wpart)
+        else:
+            o.gt_wgrad(ws.xin[l], ws.dzp[l], n * ws.rs[l], cin, cout, k, g[f"conv1d_{i}/kernel"], ws.wpart)
+
+
+def _f32(model) -> bool:
+    return getattr(model, "train_precision", "bf16") == "fp32"
 
 
 def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, sync: Optional[Callable] = None,
                global_batch: Optional[int] = None, window_offset: int = 0, sync_world: int = 1):
-    """One Keras-semantics optimizer step on the generic HIP kernels; returns (loss_sum, probs)."""
+    """One Keras-semantics optimizer step on the generic HIP kernels (bf16, or fp32 when the model's
+    ``train_precision`` is "fp32"); returns (loss_sum, probs)."""
     n = int(x.shape[0])
     gb = int(global_batch or n)
-    ws = _get_ws(model, n)
+    ws = _get_ws(model, n, f32=_f32(model))
     ws.load_input(x)
     _grads(model, ws, y, n, gb, TRAIN_PASS_BASE + model._train_step_counter, window_offset, sync)
     g = ws.gviews
@@ -285,7 +319,8 @@ class GraphedGenericStep:
         self.batch = int(batch)
         dev = model.store.device
         spec = model.spec
-        self.ws = GenericTrainWorkspace(model, self.batch)
+        self.f32 = _f32(model)
+        self.ws = GenericTrainWorkspace(model, self.batch, f32=self.f32)
         self.det = self.ws.det
         self.x_in = torch.zeros(self.batch, spec.input_length, spec.input_channels, device=dev)
         self.y_in = torch.zeros(self.batch, device=dev)
@@ -342,7 +377,8 @@ def graph_train_step(model, x: torch.Tensor, y: torch.Tensor):
         g = model._gtrain_graphs = {}
     n = int(x.shape[0])
     cur = g.get(n)
-    if cur is None or not train_ops._same_bound(cur.bound, train_ops.bound_key(model)) or cur.det != deterministic():
+    if (cur is None or not train_ops._same_bound(cur.bound, train_ops.bound_key(model)) or cur.f32 != _f32(model)
+            or (not cur.f32 and cur.det != deterministic())):
         g[n] = cur = GraphedGenericStep(model, n)
     return cur(x, y)
 
@@ -350,13 +386,16 @@ def graph_train_step(model, x: torch.Tensor, y: torch.Tensor):
 @torch.no_grad()
 def forward_batch_stats(model, x: torch.Tensor, n_pass: int, pass_base: int, seed: int, update_moving: bool = True,
                         sync: Optional[Callable] = None, window_offset: int = 0,
-                        global_n: Optional[int] = None) -> torch.Tensor:
+                        global_n: Optional[int] = None, f32: Optional[bool] = None) -> torch.Tensor:
     """MC Dropout with BN on per-pass batch statistics of the whole set (the reference's
     ``model(x, training=True)``) for any spec: (T, N) probabilities, one layer-synchronous
-    sweep per pass."""
+    sweep per pass.  ``f32`` (default: the model's inference ``precision`` is "fp32"): fp32 activations
+    and fp32-input MFMA convs (exact fp32 products, the reference's precision); else bf16."""
     n = int(x.shape[0])
     gn = int(global_n or n)
-    ws = _get_ws(model, n, with_backward=False)
+    if f32 is None:
+        f32 = getattr(model, "precision", "fp32") == "fp32"
+    ws = _get_ws(model, n, with_backward=False, f32=bool(f32))
     ws.load_input(x)
     wf, _ = ws.pack(backward=False)
     v = model.store.views
@@ -366,4 +405,60 @@ def forward_batch_stats(model, x: torch.Tensor, n_pass: int, pass_base: int, see
         h = _forward(ws, n, gn, seed, pass_base + t, window_offset, True, update_moving, sync, wf)
         out[t] = torch.sigmoid(torch.addmv(v["output_layer/bias"], h.float().mean(dim=1), wdense))
     model.store.bump()
+    return out
+
+
+def running_affine(model, ws: GenericTrainWorkspace) -> None:
+    """BN on the moving statistics, as the (4, C) rows [scale, shift, mean, rstd] gt_apply reads."""
+    spec, v = model.spec, model.store.views
+    for l in range(len(spec.blocks)):
+        i = l + 1
+        mm, mv = v[f"batchnorm_{i}/moving_mean"], v[f"batchnorm_{i}/moving_variance"]
+        rstd = torch.rsqrt(mv + spec.bn_epsilon)
+        scale = v[f"batchnorm_{i}/gamma"] * rstd
+        ws.bn[l].copy_(torch.cat([scale, v[f"batchnorm_{i}/beta"] - mm * scale, mm, rstd]))
+
+
+@torch.no_grad()
+def forward_running_f32(model, x: torch.Tensor, n_pass: int = 1, dropout: bool = False, seed: int = 0,
+                        pass_offset: int = 0, window_offset: int = 0, logits: bool = False) -> torch.Tensor:
+    """Inference with BN on the moving statistics (Deep-Ensemble ``predict`` / standard MC Dropout,
+    ``uq_techniques.py:22-30``) at the reference's fp32 for ANY spec -- the MaxPool1D variant of the
+    thesis' ``ensemble_cnn`` members (``evaluate_de_global.py:18-38``), the 30 s single-channel window --
+    on the fp32-input MFMA conv (``csrc/gf32_conv.hip``) and the fp32 BN / pool / dropout kernels:
+    (n_pass, N) probabilities (or logits).  The passes run one after the other (each its own dropout
+    stream, keyed by the global window id)."""
+    n = int(x.shape[0])
+    out = torch.empty(n_pass, n, dtype=torch.float32, device=x.device)
+    if n == 0:
+        return out
+    spec, o = model.spec, _ext.ops()
+    ws = _get_ws(model, n, with_backward=False, f32=True)
+    running_affine(model, ws)
+    ws.load_input(x)
+    v = model.store.views
+    wdense = v["output_layer/kernel"].reshape(-1)
+    nl = len(spec.blocks)
+    conv0 = True
+    for t in range(n_pass if dropout else 1):
+        for l, b in enumerate(spec.blocks):
+            i = l + 1
+            cin, cout, L = ws.ch[l], ws.ch[l + 1], ws.L[l]
+            if l > 0 or conv0:  # block 1 does not depend on the pass (no dropout before it)
+                o.gf_conv(ws.xin[l], v[f"conv1d_{i}/kernel"], v[f"conv1d_{i}/bias"], ws.z[l], ws.st[l], n, L, cin,
+                          cout, ws.ks[l], 1, ws.rs[l], 2 * ws.pads[l], True)
+            if l + 1 < nl:
+                dst, drs, doff = ws.xin[l + 1], ws.rs[l + 1], 2 * ws.pads[l + 1]
+            else:
+                dst, drs, doff = ws.hlast, ws.L[-1], 0
+            drop = bool(dropout and b.dropout > 0)
+            o.gt_apply(ws.z[l], ws.bn[l], dst, n, L, cout, bool(b.pool), drs, doff, drop,
+                       rng.dropout_threshold(b.dropout), _inv_keep(b.dropout),
+                       rng.stream_key(seed, l, pass_offset + t), int(window_offset), None)
+        conv0 = False
+        h = ws.hlast[: n * ws.L[-1]].view(n, ws.L[-1], ws.ch[-1])
+        lg = torch.addmv(v["output_layer/bias"], h.mean(dim=1), wdense)
+        out[t] = lg if logits else torch.sigmoid(lg)
+    if not dropout:
+        out[1:] = out[0]
     return out

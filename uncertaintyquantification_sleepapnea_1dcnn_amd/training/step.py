@@ -3,7 +3,8 @@
 Backends:
 * ``"hip"``  — the reference architecture's layer-wise HIP kernels (``ops/train_ops.py``);
 * ``"hip_generic"`` — any other architecture (pool blocks, other window shapes) on the generic
-  HIP kernels (``ops/generic_train.py``);
+  HIP kernels (``ops/generic_train.py``), and every architecture with ``train_precision="fp32"``
+  (fp32 activations / gradients, fp32-input MFMA convs, ``csrc/gf32_conv.hip``);
 * ``"torch"``— autograd over the fp32 reference ops (CPU, and the fallback/oracle on GPU).
 
 Gradients land in ONE flat fp32 buffer (views of ``ParamStore.flat``), so the data-parallel
@@ -25,13 +26,14 @@ def _backend(model) -> str:
     if b != "auto":
         return b
     if model.device.type == "cuda":
-        from ..ops import train_ops
+        from ..ops import generic_train, train_ops
 
-        if train_ops.supports(model.spec):
+        if getattr(model, "train_precision", "bf16") == "fp32":  # any architecture, fp32 kernels
+            if generic_train.supports_fp32(model.spec):
+                return "hip_generic"
+        elif train_ops.supports(model.spec):
             return "hip"
-        from ..ops import generic_train
-
-        if generic_train.supports(model.spec):
+        elif generic_train.supports(model.spec):
             return "hip_generic"
         from ..ops import fused
 
