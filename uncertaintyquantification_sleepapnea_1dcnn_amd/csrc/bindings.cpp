@@ -103,7 +103,6 @@ hipError_t train_launch_finalize(const train::Args& A, int update_moving, int gr
 hipError_t train_launch_tab(const apneauq::train::Args& A, int mode, int l, hipStream_t st);
 hipError_t train_launch_mb(const train::Args& A0, const train::Args* Am, int M, int op, int layer, int flag,
                            hipStream_t st);
-hipError_t train_launch_pack(const float* w, int k, int cin, int cout, void* fwd, void* dgr, hipStream_t st);
 }  // namespace apneauq
 
 namespace {
@@ -471,18 +470,6 @@ void train_call_mb(const at::Tensor& args_dev, const at::Tensor& ctx0, int64_t M
 int64_t train_wgrad_part_size(int64_t B) { return apneauq::train_wgrad_part_floats((int)B); }
 int64_t train_det_size(int64_t B) { return apneauq::train_det_floats((int)B); }
 
-void train_pack(const at::Tensor& w, int64_t k, int64_t cin, int64_t cout, at::Tensor& fwd, at::Tensor& dgr) {
-  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == k * cin * cout,
-              "train_pack: w must be a contiguous fp32 (k, cin, cout) GPU tensor");
-  const int64_t nf = ((cin * k + 31) / 32) * 32 * cout, nd = ((cout * k + 31) / 32) * 32 * cin;
-  TORCH_CHECK(fwd.scalar_type() == at::kBFloat16 && fwd.numel() == nf && dgr.scalar_type() == at::kBFloat16 &&
-                  dgr.numel() == nd && fwd.is_contiguous() && dgr.is_contiguous(),
-              "train_pack: fragment buffers have the wrong size/dtype");
-  const at::DeviceGuard guard(w.device());
-  check(apneauq::train_launch_pack(w.data_ptr<float>(), (int)k, (int)cin, (int)cout, fwd.data_ptr(), dgr.data_ptr(),
-                                   cur_stream()),
-        "train_pack");
-}
 
 // Generic-spec conv block (csrc/generic_conv.hip): x (N, L, Cin) bf16 -> (N, L or L/2, Cout) bf16.
 at::Tensor generic_conv(const at::Tensor& x, const at::Tensor& wfrag, const at::Tensor& epi, int64_t cout,
@@ -886,7 +873,6 @@ TORCH_LIBRARY(apneauq, m) {
   m.def("train_call(Tensor ctx, int op, int layer, int flag, int pass_base, int device) -> ()", &train_call);
   m.def("train_args_dev(Tensor[] ctxs, int device) -> Tensor", &train_args_dev);
   m.def("train_call_mb(Tensor args_dev, Tensor ctx0, int M, int op, int layer, int flag) -> ()", &train_call_mb);
-  m.def("train_pack(Tensor w, int k, int cin, int cout, Tensor(a!) fwd, Tensor(b!) dgr) -> ()");
   m.def("train_wgrad_part_size(int B) -> int", &train_wgrad_part_size);
   m.def("train_det_size(int B) -> int", &train_det_size);
   m.def("prep_standardize(Tensor x, float eps) -> Tensor");
@@ -934,7 +920,6 @@ TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
   m.impl("bump_counters", &bump_counters);
   m.impl("stream_keys", &stream_keys);
   m.impl("zero_buffers", &zero_buffers);
-  m.impl("train_pack", &train_pack);
   m.impl("generic_conv", &generic_conv);
   m.impl("generic_head", &generic_head);
   m.impl("metrics_update", &metrics_update);

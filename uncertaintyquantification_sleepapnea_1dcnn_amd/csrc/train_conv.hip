@@ -1782,35 +1782,6 @@ __global__ void bn_finalize_kernel(Args A_, const Args* __restrict__ Am, int upd
   }
 }
 
-// ------------------------------------------------------------------------------------------------
-// Pack fp32 master kernels into bf16 MFMA A-operand fragments (forward and dgrad orientation).
-//   forward: frag[s][ct][lane][j] = W[tap][ci][co],  co = 16ct + (lane&15), kk = 32s + 8(lane>>4) + j,
-//            kk = tap*Cin + ci   (zero for kk >= k*Cin)
-//   dgrad:   W'[tap'][co][ci] = W[k-1-tap'][ci][co]: same formula with (Cin, Cout) swapped.
-// ------------------------------------------------------------------------------------------------
-__global__ void pack_kernel(const float* __restrict__ w, int k, int cin, int cout, __bf16* __restrict__ fwd,
-                            __bf16* __restrict__ dgr) {
-  const long long nf = (long long)((cin * k + 31) / 32) * 32 * cout;
-  const long long nd = (long long)((cout * k + 31) / 32) * 32 * cin;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < nf + nd; e += (long long)gridDim.x * blockDim.x) {
-    const bool is_f = e < nf;
-    const long long i = is_f ? e : e - nf;
-    const int ci_ = is_f ? cin : cout, co_ = is_f ? cout : cin;
-    const int j = (int)(i & 7), lane = (int)((i >> 3) & 63);
-    const long long fr = i >> 9;
-    const int nct = co_ / 16;
-    const int ct = (int)(fr % nct), s = (int)(fr / nct);
-    const int co = 16 * ct + (lane & 15);
-    const int kk = 32 * s + 8 * (lane >> 4) + j;
-    float v = 0.f;
-    if (kk < ci_ * k) {
-      const int tap = kk / ci_, ci = kk - tap * ci_;
-      v = is_f ? w[((long long)tap * cin + ci) * cout + co] : w[((long long)(k - 1 - tap) * cin + co) * cout + ci];
-    }
-    (is_f ? fwd : dgr)[i] = (__bf16)v;
-  }
-}
-
 }  // namespace train
 
 // ------------------------------------------------------------------------------------------------ host
@@ -1850,17 +1821,6 @@ hipError_t train_stream_keys(unsigned* keys, const int* c, int n, unsigned long 
                              hipStream_t st) {
   hipLaunchKernelGGL(stream_keys_kernel, dim3(1), dim3(64), 0, st, keys, c, n, seed, pass_base);
   return hipGetLastError();
-}
-
-static int cu_count() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        n <= 0)
-      n = 256;
-  }
-  return n;
 }
 
 static hipError_t det_reduce(const float* part, int n, int w, train::DetDst d, hipStream_t st) {
@@ -2093,15 +2053,6 @@ hipError_t train_launch_mb(const Args& A0, const Args* Am, int M, int op, int la
       return hipGetLastError();
     default: return hipErrorInvalidValue;
   }
-}
-
-hipError_t train_launch_pack(const float* w, int k, int cin, int cout, void* fwd, void* dgr, hipStream_t st) {
-  const long long n = (long long)((cin * k + 31) / 32) * 32 * cout + (long long)((cout * k + 31) / 32) * 32 * cin;
-  long long blocks = (n + 255) / 256;
-  if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(train::pack_kernel, dim3((unsigned)blocks), dim3(256), 0, st, w, k, cin, cout,
-                     reinterpret_cast<__bf16*>(fwd), reinterpret_cast<__bf16*>(dgr));
-  return hipGetLastError();
 }
 
 }  // namespace apneauq

@@ -13,12 +13,14 @@ struct LayerArgs {
   const float* bias;      // [G][COUT]
   const float* wscale;    // [G] 2^-sw (exact) undoing the host weight pre-scale
   int p_gstride;          // bias floats per weight group (0: shared; then wscale[0] too)
-  const float* aff_in;    // [G][2][CIN] BN affine of block l-1 (scale | shift) x 1/(1-p_{l-1}) x 2^sa
+  const float* aff_in;    // [G][2][CIN] BN affine of block l-1 (scale | shift) x 1/(1-p_{l-1})
   int aff_gstride;        // floats per group (0: shared)
-  const float* ascale;    // [G] 2^-sa undoing the activation prescale folded into aff_in (nullptr: 1);
-                          // indexed like aff_in (aff_gstride 0: one value)
-  unsigned* rmax;         // [G][COUT] running max of R_l (fp32 bits, R_l >= 0; nullptr: not tracked)
-  int rmax_gstride;       // COUT: one row per group; 0: one row shared by all groups (passes sharing an affine)
+  // range-safe fp16 split (see x3_layers.hip sample_prescale): per-sample power-of-two prescale of the
+  // staged activations from the sample's max of R_{l-1} and the affine's channel maxima
+  const unsigned* smax_in;  // max of R_{l-1} per input sample (fp32 bits), indexed like the input rows
+                            // (in_shared: window; else group * n_win + window); nullptr: no prescale
+  const float* amax_in;     // [G][2] max_c |scale|, max_c |shift| of aff_in (aff_gstride 0: one pair)
+  unsigned* smax_out;       // [G * n_win] max of R_l per sample (fp32 bits, atomicMax; nullptr: none)
   double* stats;          // [G][16 slots][2][COUT] moment sums of R_l (nullptr: none)
   int n_win;              // windows per group
   int groups;
@@ -39,7 +41,7 @@ struct L1Args {
   const float* b;      // [G][128]
   float* out;          // [G][n_win][60][128]
   double* stats;       // [G][16][2][128] or nullptr
-  unsigned* rmax;      // [G][128] max of R_1 (fp32 bits) or nullptr
+  unsigned* smax;      // [G][n_win] max of R_1 per sample (fp32 bits) or nullptr
   int n_win, groups, blocks_per_group;
 };
 
@@ -50,8 +52,7 @@ struct AffArgs {
   float* mmean;
   float* mvar;
   float* aff;            // [G][2][C]
-  const unsigned* rmax;  // [G][C] max of the block's ReLU output (nullptr: no activation prescale)
-  float* ascale;         // [G] out: 2^-sa, the inverse of the power-of-two prescale folded into aff
+  float* amax;           // [G][2] out: max_c |aff scale|, max_c |aff shift| (nullptr: not written)
   int C, groups, p_gstride, update;
   int repeat;            // moving updates per stats group (block 1 moments are shared by all passes)
   double inv_count;

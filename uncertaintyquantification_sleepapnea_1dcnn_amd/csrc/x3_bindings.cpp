@@ -46,8 +46,8 @@ void x3_layer(int64_t layer, const at::Tensor& in, at::Tensor& out, const at::Te
               const at::Tensor& bias, const at::Tensor& wscale, int64_t p_gstride, const at::Tensor& aff_in,
               int64_t aff_gstride, const c10::optional<at::Tensor>& stats, int64_t n_win, int64_t groups,
               bool in_shared, int64_t thr_in, int64_t thr_out, int64_t seed, int64_t pass_base,
-              int64_t window_offset, int64_t grid, const c10::optional<at::Tensor>& ascale,
-              const c10::optional<at::Tensor>& rmax) {
+              int64_t window_offset, int64_t grid, const c10::optional<at::Tensor>& smax_in,
+              const c10::optional<at::Tensor>& amax_in, const c10::optional<at::Tensor>& smax_out) {
   TORCH_CHECK(layer >= 1 && layer <= 5, "x3_layer: layer must be 1..5 (block 2..6)");
   TORCH_CHECK(n_win >= 1 && groups >= 1, "x3_layer: empty launch");
   const int cin = kCh[layer], cout = kCh[layer + 1], ks = kKs[layer];
@@ -72,18 +72,18 @@ void x3_layer(int64_t layer, const at::Tensor& in, at::Tensor& out, const at::Te
     st = stats->data_ptr<double>();
   }
   TORCH_CHECK(thr_in >= 0 && thr_in <= 65536 && thr_out >= 0 && thr_out <= 65536, "x3_layer: thresholds");
-  const float* asp = nullptr;
-  if (ascale.has_value() && ascale->defined()) {
-    need(*ascale, at::kFloat, aff_gstride ? groups : 1, "x3_layer: ascale");
-    asp = ascale->data_ptr<float>();
+  // range-safe split: per-sample maxima of the input (indexed like its rows) + the affine's channel maxima
+  const bool pre = smax_in.has_value() && smax_in->defined();
+  TORCH_CHECK(pre == (amax_in.has_value() && amax_in->defined()), "x3_layer: smax_in and amax_in go together");
+  if (pre) {
+    need(*smax_in, at::kInt, samples_in, "x3_layer: smax_in");
+    need(*amax_in, at::kFloat, (aff_gstride ? groups : 1) * 2, "x3_layer: amax_in");
   }
-  unsigned* rmp = nullptr;
-  if (rmax.has_value() && rmax->defined()) {
-    TORCH_CHECK(layer < 5, "x3_layer: block 6 has no split consumer (no rmax)");
-    need(*rmax, at::kInt, cout, "x3_layer: rmax");
-    // exactly one row per group, or one row shared by every group (passes sharing one affine)
-    TORCH_CHECK(rmax->numel() == groups * cout || rmax->numel() == cout, "x3_layer: rmax must hold groups x Cout or Cout");
-    rmp = reinterpret_cast<unsigned*>(rmax->data_ptr<int>());
+  unsigned* smo = nullptr;
+  if (smax_out.has_value() && smax_out->defined()) {
+    TORCH_CHECK(layer < 5, "x3_layer: block 6 feeds the fp32 head (no smax_out)");
+    need(*smax_out, at::kInt, samples, "x3_layer: smax_out");
+    smo = reinterpret_cast<unsigned*>(smax_out->data_ptr<int>());
   }
   const at::DeviceGuard guard(in.device());
   apneauq::x3::LayerArgs A;
@@ -97,9 +97,9 @@ void x3_layer(int64_t layer, const at::Tensor& in, at::Tensor& out, const at::Te
   A.aff_in = aff_in.data_ptr<float>();
   A.aff_gstride = (int)aff_gstride;
   A.stats = st;
-  A.ascale = asp;
-  A.rmax = rmp;
-  A.rmax_gstride = (rmp != nullptr && rmax->numel() == groups * cout) ? cout : 0;
+  A.smax_in = pre ? reinterpret_cast<const unsigned*>(smax_in->data_ptr<int>()) : nullptr;
+  A.amax_in = pre ? amax_in->data_ptr<float>() : nullptr;
+  A.smax_out = smo;
   A.n_win = (int)n_win;
   A.groups = (int)groups;
   A.tiles_per_group = (int)tpg;
@@ -117,7 +117,7 @@ void x3_layer(int64_t layer, const at::Tensor& in, at::Tensor& out, const at::Te
 }
 
 void x3_l1(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b, at::Tensor& out,
-           const c10::optional<at::Tensor>& stats, int64_t n_win, int64_t groups, const c10::optional<at::Tensor>& rmax) {
+           const c10::optional<at::Tensor>& stats, int64_t n_win, int64_t groups, const c10::optional<at::Tensor>& smax) {
   TORCH_CHECK(n_win >= 1 && groups >= 1, "x3_l1: empty launch");
   need(x, at::kFloat, n_win * 60 * 4, "x3_l1: x");
   need(w, at::kFloat, groups * 7 * 4 * 128, "x3_l1: w");
@@ -128,15 +128,15 @@ void x3_l1(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b, at::Te
     need(*stats, at::kDouble, groups * apneauq::x3::kStatSlots * 2 * 128, "x3_l1: stats");
     st = stats->data_ptr<double>();
   }
-  unsigned* rmp = nullptr;
-  if (rmax.has_value() && rmax->defined()) {
-    need(*rmax, at::kInt, groups * 128, "x3_l1: rmax");
-    rmp = reinterpret_cast<unsigned*>(rmax->data_ptr<int>());
+  unsigned* smp = nullptr;
+  if (smax.has_value() && smax->defined()) {
+    need(*smax, at::kInt, groups * n_win, "x3_l1: smax");
+    smp = reinterpret_cast<unsigned*>(smax->data_ptr<int>());
   }
   const int64_t bpg = (n_win + apneauq::x3::kL1Win - 1) / apneauq::x3::kL1Win;
   TORCH_CHECK(bpg * groups < (int64_t(1) << 31), "x3_l1: too many blocks");
   const at::DeviceGuard guard(x.device());
-  apneauq::x3::L1Args A{x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(), out.data_ptr<float>(), st, rmp,
+  apneauq::x3::L1Args A{x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(), out.data_ptr<float>(), st, smp,
                         (int)n_win, (int)groups, (int)bpg};
   check(apneauq::x3_launch_l1(A, cur_stream()), "x3_l1");
 }
@@ -144,7 +144,7 @@ void x3_l1(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b, at::Te
 void x3_aff(const c10::optional<at::Tensor>& stats, const at::Tensor& gamma, const at::Tensor& beta, at::Tensor& mmean,
             at::Tensor& mvar, at::Tensor& aff, int64_t C, int64_t groups, int64_t p_gstride, bool update,
             int64_t repeat, double inv_count, double eps, double momentum, double dsc,
-            const c10::optional<at::Tensor>& rmax, const c10::optional<at::Tensor>& ascale) {
+            const c10::optional<at::Tensor>& amax) {
   TORCH_CHECK(C >= 1 && C <= 4096 && groups >= 1, "x3_aff: bad sizes");
   TORCH_CHECK(p_gstride == 0 || p_gstride == C, "x3_aff: p_gstride must be 0 or C");
   const int64_t pg = p_gstride ? groups : 1;
@@ -159,18 +159,14 @@ void x3_aff(const c10::optional<at::Tensor>& stats, const at::Tensor& gamma, con
     st = stats->data_ptr<double>();
   }
   TORCH_CHECK(!update || st != nullptr, "x3_aff: the moving update needs batch moments");
-  const unsigned* rmp = nullptr;
-  float* asp = nullptr;
-  if (rmax.has_value() && rmax->defined()) {  // range-safe prescale: needs the output of 2^-sa too
-    TORCH_CHECK(ascale.has_value() && ascale->defined(), "x3_aff: rmax needs ascale");
-    need(*rmax, at::kInt, groups * C, "x3_aff: rmax");
-    need(*ascale, at::kFloat, groups, "x3_aff: ascale");
-    rmp = reinterpret_cast<const unsigned*>(rmax->data_ptr<int>());
-    asp = ascale->data_ptr<float>();
+  float* amp = nullptr;
+  if (amax.has_value() && amax->defined()) {
+    need(*amax, at::kFloat, groups * 2, "x3_aff: amax");
+    amp = amax->data_ptr<float>();
   }
   const at::DeviceGuard guard(gamma.device());
   apneauq::x3::AffArgs A{st, gamma.data_ptr<float>(), beta.data_ptr<float>(), mmean.data_ptr<float>(),
-                         mvar.data_ptr<float>(), aff.data_ptr<float>(), rmp, asp, (int)C, (int)groups, (int)p_gstride,
+                         mvar.data_ptr<float>(), aff.data_ptr<float>(), amp, (int)C, (int)groups, (int)p_gstride,
                          update ? 1 : 0, (int)repeat, inv_count, (float)eps, (float)momentum, (float)dsc};
   check(apneauq::x3_launch_aff(A, cur_stream()), "x3_aff");
 }
@@ -201,13 +197,13 @@ int64_t x3_lds(int64_t layer) { return apneauq::x3_lds_bytes((int)layer); }
 TORCH_LIBRARY_FRAGMENT(apneauq, m) {
   m.def("x3_layer(int layer, Tensor input, Tensor(a!) out, Tensor wfrag, int w_gstride, Tensor bias, Tensor wscale, "
         "int p_gstride, Tensor aff_in, int aff_gstride, Tensor(b!)? stats, int n_win, int groups, bool in_shared, "
-        "int thr_in, int thr_out, int seed, int pass_base, int window_offset, int grid, Tensor? ascale=None, "
-        "Tensor(c!)? rmax=None) -> ()");
+        "int thr_in, int thr_out, int seed, int pass_base, int window_offset, int grid, Tensor? smax_in=None, "
+        "Tensor? amax_in=None, Tensor(c!)? smax_out=None) -> ()");
   m.def("x3_l1(Tensor x, Tensor w, Tensor b, Tensor(a!) out, Tensor(b!)? stats, int n_win, int groups, "
-        "Tensor(c!)? rmax=None) -> ()");
+        "Tensor(c!)? smax=None) -> ()");
   m.def("x3_aff(Tensor? stats, Tensor gamma, Tensor beta, Tensor(a!) mmean, Tensor(b!) mvar, Tensor(c!) aff, int C, "
         "int groups, int p_gstride, bool update, int repeat, float inv_count, float eps, float momentum, float dsc, "
-        "Tensor? rmax=None, Tensor(d!)? ascale=None) -> ()");
+        "Tensor(d!)? amax=None) -> ()");
   m.def("x3_head(Tensor sums, Tensor aff, int aff_gstride, Tensor dw, Tensor db, int p_gstride, Tensor(a!) out, "
         "int n_win, int groups, bool logits) -> ()");
   m.def("x3_lds(int layer) -> int", &x3_lds);

@@ -59,11 +59,25 @@ constexpr int kL = 60, kSR = 64, kHalo = 4;
 // (row stride 2 mod 4 16-B slots for either CK).  Layers with few taps take 64-channel chunks: twice the
 // k-steps per chunk barrier.
 __host__ __device__ constexpr int row_bytes(int ck) { return 4 * ck + 32; }
+// Range-safe fp16 split.  The staging splits a = s_c R + t_c (BN affine x dropout rescale, R >= 0) into
+// fp16 hi + lo, which needs |a| < 65504 (hi finite) and |a| well above 2^-14 (lo normal).  Per SAMPLE
+// (the rows of one window in one pass / member), |a| <= max_c |s_c| * max R + max_c |t_c| =: b, so the
+// sample's activations are multiplied by the exact power of two 2^sa that puts b in [2^13, 2^14), and
+// the accumulator rows of that sample by 2^-sa (a conv row sums over its own sample's rows only).  The
+// prescale depends on the sample's own data and the (global) affine only: results are independent of
+// sharding, chunking and grouping.
+__device__ __forceinline__ int sample_prescale(unsigned rmax_bits, const float* amax) {
+  const float b = __builtin_fmaf(amax[0], __uint_as_float(rmax_bits), amax[1]);
+  int e = 0;
+  if (b > 0.f && b < INFINITY) frexpf(b, &e);  // b = m 2^e, m in [0.5, 1)
+  return min(100, max(-100, 14 - e));
+}
+
 // per tile of S samples (S x 64 GEMM rows): LDS rows, chunk-buffer bytes, staged rows, 16-B staging units
 __host__ __device__ constexpr int lds_rows(int S) { return kHalo + S * kSR + kHalo; }
 __host__ __device__ constexpr int buf_bytes(int S, int ck) { return lds_rows(S) * row_bytes(ck); }
-// + per-workgroup fp64 moment sums [2][COUT] and the R_l channel maxima [COUT] (u32)
-__host__ __device__ constexpr int lds_bytes(int S, int cout, int ck) { return 2 * buf_bytes(S, ck) + 2 * cout * 8 + cout * 4; }
+// + per-workgroup fp64 moment sums [2][COUT]
+__host__ __device__ constexpr int lds_bytes(int S, int cout, int ck) { return 2 * buf_bytes(S, ck) + 2 * cout * 8; }
 
 // global-address-space load (keeps global_load_*, never flat_*)
 template <typename T>
@@ -131,7 +145,6 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, (waves_per_eu<WM * WN + LW, WP
   static_assert(NCTA % WN == 0 && (4 * S) % WM == 0, "wave tiling");
   static_assert(NRT % 4 == 0, "whole 64-row sample slots per wave row (epilogue keys, block 6 sums)");
   double* st = reinterpret_cast<double*>(smem + 2 * kBufB);  // [2][COUT] per-workgroup moment sums
-  unsigned* lmax = reinterpret_cast<unsigned*>(st + 2 * COUT);  // [COUT] channel maxima of R_l (fp32 bits)
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -142,7 +155,6 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, (waves_per_eu<WM * WN + LW, WP
 
   for (int i = tid; i < 2 * kBufB / 16; i += kThreads) reinterpret_cast<f32x4*>(smem)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int i = tid; i < 2 * COUT; i += kThreads) st[i] = 0.0;
-  for (int i = tid; i < COUT; i += kThreads) lmax[i] = 0u;
   __syncthreads();
 
   const int wg = xcd_wg();
@@ -168,8 +180,10 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, (waves_per_eu<WM * WN + LW, WP
   // hash of block l-1 here, at the consumer: the producer's epilogue then runs no hash at all, and the
   // loader waves' hashing overlaps the MFMA waves); recomputed when the staged tile changes
   const bool hash_in = A.thr_in != 0u;
+  const bool prescale = A.smax_in != nullptr;
   int key_tile = -1;
   unsigned skeys[kS];
+  float sup[kS];  // 2^sa of the staging tile's samples (range-safe split)
   auto load_chunk = [&](int tile, int c, Stage& R) {
     const int tid = opaque_tid() - kSBase, q = tid % kQ;
     const int g = tile / tpg;
@@ -194,10 +208,18 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, (waves_per_eu<WM * WN + LW, WP
     const int tid = opaque_tid() - kSBase, q = tid % kQ;
     const int g = tile / tpg;
     const int w0 = (tile - g * tpg) * kS;
-    if (hash_in && tile != key_tile) {  // workgroup-uniform
+    if ((hash_in || prescale) && tile != key_tile) {  // workgroup-uniform
       const unsigned skey = stream_key(A.seed, A.layer - 1, A.pass_base + g);
+      const float* am = A.amax_in + (A.aff_gstride ? 2 * g : 0);
 #pragma unroll
-      for (int s = 0; s < kS; ++s) skeys[s] = sample_key(skey, A.window_offset + w0 + s);
+      for (int s = 0; s < kS; ++s) {
+        skeys[s] = sample_key(skey, A.window_offset + w0 + s);
+        sup[s] = 1.f;
+        if (prescale && w0 + s < A.n_win) {
+          const long long si = A.in_shared ? w0 + s : (long long)g * A.n_win + w0 + s;
+          sup[s] = ldexpf(1.f, sample_prescale(A.smax_in[si], am));
+        }
+      }
       key_tile = tile;
     }
 #pragma unroll
@@ -222,10 +244,16 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, (waves_per_eu<WM * WN + LW, WP
         for (int i = 0; i < 4; ++i) keep[i] = true;
       }
       const bool valid = w < A.n_win;
+      float up = 1.f;
+      if (prescale) {
+        up = sup[0];
+#pragma unroll
+        for (int j = 1; j < kS; ++j) up = s == j ? sup[j] : up;
+      }
       f16x4 hi, lo;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float a = (valid && keep[i]) ? __builtin_fmaf(v[i], R.a[i], R.b[i]) : 0.f;
+        const float a = (valid && keep[i]) ? __builtin_fmaf(v[i], R.a[i], R.b[i]) * up : 0.f;
         hi[i] = (_Float16)a;
         lo[i] = (_Float16)(a - (float)hi[i]);
       }
@@ -327,9 +355,22 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, (waves_per_eu<WM * WN + LW, WP
     const int lane = opaque_tid() & 63, m = lane & 15, h = lane >> 4;
     const int g = tile / tpg;
     const int w0 = (tile - g * tpg) * kS;
-    // weight prescale 2^-sw and activation prescale 2^-sa (range-safe fp16 split of the input), both exact
-    const float ws = A.wscale[A.p_gstride ? g : 0] * (A.ascale != nullptr ? A.ascale[A.aff_gstride ? g : 0] : 1.f);
-    const bool track = !LAST && A.rmax != nullptr;
+    // undo the weight prescale 2^sw and each sample's activation prescale 2^sa (exact powers of two)
+    const float ws0 = A.wscale[A.p_gstride ? g : 0];
+    float wsq[NRT / 4];
+#pragma unroll
+    for (int q = 0; q < NRT / 4; ++q) {
+      wsq[q] = ws0;
+      const int w = w0 + (rt0 >> 2) + q;
+      if (A.smax_in != nullptr && w < A.n_win) {
+        const long long si = A.in_shared ? w : (long long)g * A.n_win + w;
+        wsq[q] = ws0 * ldexpf(1.f, -sample_prescale(A.smax_in[si], A.amax_in + (A.aff_gstride ? 2 * g : 0)));
+      }
+    }
+    const bool track = !LAST && A.smax_out != nullptr;
+    float mxs[NRT / 4];  // max of R_l per sample slot of the wave (range-safe split of the next block)
+#pragma unroll
+    for (int q = 0; q < NRT / 4; ++q) mxs[q] = 0.f;
     const float* bias = A.bias + (long long)g * A.p_gstride;
     // only block 6 draws its output mask here (the masked per-sample sums); blocks 2..5 store the plain
     // ReLU output and their consumer draws the mask while staging it
@@ -348,14 +389,14 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, (waves_per_eu<WM * WN + LW, WP
     for (int ct = 0; ct < NCT; ++ct) {
       const int co0 = (ct0 + ct) * 16 + 4 * h;
       const f32x4 b4 = gld<f32x4>(bias + co0);
-      f32x4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1, k1 = s1, k0 = s1, mx = s1;
+      f32x4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1, k1 = s1, k0 = s1;
 #pragma unroll
       for (int rt = 0; rt < NRT; ++rt) {
         const int s = (rt0 + rt) >> 2, t = (((rt0 + rt) & 3) << 4) + m, w = w0 + s;
         const bool valid = t < kL && w < A.n_win;
         f32x4 r;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) r[e] = fmaxf(__builtin_fmaf(acc[ct][rt][e], ws, b4[e]), 0.f);
+        for (int e = 0; e < 4; ++e) r[e] = fmaxf(__builtin_fmaf(acc[ct][rt][e], wsq[rt >> 2], b4[e]), 0.f);
         acc[ct][rt] = f32x4{0.f, 0.f, 0.f, 0.f};
         bool keep[4] = {true, true, true, true};
         if (drop) {
@@ -371,7 +412,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, (waves_per_eu<WM * WN + LW, WP
           for (int e = 0; e < 4; ++e) {
             s1[e] += r[e];
             s2[e] = __builtin_fmaf(r[e], r[e], s2[e]);
-            if (!LAST) mx[e] = fmaxf(mx[e], r[e]);
+            if (!LAST) mxs[rt >> 2] = fmaxf(mxs[rt >> 2], r[e]);
             if constexpr (LAST) {
               k1[e] += keep[e] ? r[e] : 0.f;
               k0[e] += keep[e] ? 1.f : 0.f;
@@ -401,13 +442,6 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, (waves_per_eu<WM * WN + LW, WP
         }
       }
       // reduce over the 16 rows of each lane group (lanes sharing h hold the same 4 channels)
-      if (track) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float a = group16_max(mx[e]);
-          if (m == 0) atomicMax(&lmax[co0 + e], __float_as_uint(a));  // R_l >= 0: bit order = value order
-        }
-      }
       if (A.stats != nullptr) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -419,6 +453,14 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, (waves_per_eu<WM * WN + LW, WP
         }
       }
     }
+    if (track) {  // per-sample maxima of R_l (R_l >= 0: fp32 bit order = value order; max is order-free)
+#pragma unroll
+      for (int q = 0; q < NRT / 4; ++q) {
+        const float mq = wave_max(mxs[q]);
+        const int w = w0 + (rt0 >> 2) + q;
+        if (lane == 0 && w < A.n_win) atomicMax(A.smax_out + (long long)g * A.n_win + w, __float_as_uint(mq));
+      }
+    }
   };
 
   auto flush_stats = [&](int g) {
@@ -428,12 +470,6 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, (waves_per_eu<WM * WN + LW, WP
       for (int i = tid; i < 2 * COUT; i += kThreads) {
         atomicAdd(dst + i, st[i]);
         st[i] = 0.0;
-      }
-    }
-    if (!LAST && A.rmax != nullptr) {
-      for (int i = tid; i < COUT; i += kThreads) {
-        if (lmax[i] != 0u) atomicMax(A.rmax + (long long)g * A.rmax_gstride + i, lmax[i]);
-        lmax[i] = 0u;
       }
     }
     __syncthreads();
@@ -533,7 +569,8 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, (waves_per_eu<WM * WN + LW, WP
 // per 256-thread block (thread = one output channel x one half of the time steps), + batch moments.
 __global__ __launch_bounds__(256) void l1_kernel(const L1Args A) {
   __shared__ float xs[kL1Win][kL + 6][4];
-  __shared__ float red[2][3][128];
+  __shared__ float red[2][2][128];
+  __shared__ unsigned wmax[kL1Win];  // per-window max of R_1 (fp32 bits)
   const int g = blockIdx.x / A.blocks_per_group;
   const int w0 = (blockIdx.x - g * A.blocks_per_group) * kL1Win;
   const int tid = threadIdx.x, c = tid & 127, half = tid >> 7;
@@ -548,12 +585,14 @@ __global__ __launch_bounds__(256) void l1_kernel(const L1Args A) {
 #pragma unroll
     for (int ci = 0; ci < 4; ++ci) wr[j][ci] = A.w[(((long long)g * 7 + j) * 4 + ci) * 128 + c];
   const float bc = A.b[g * 128 + c];
+  if (tid < kL1Win) wmax[tid] = 0u;
   __syncthreads();
-  float s1 = 0.f, s2 = 0.f, mx = 0.f;
+  float s1 = 0.f, s2 = 0.f;
   for (int s = 0; s < kL1Win; ++s) {
     const int w = w0 + s;
     if (w >= A.n_win) break;
     float* o = A.out + (((long long)g * A.n_win + w) * kL) * 128 + c;
+    float mx = 0.f;
     for (int t = half * 30; t < half * 30 + 30; ++t) {
       float v = bc;
 #pragma unroll
@@ -566,20 +605,22 @@ __global__ __launch_bounds__(256) void l1_kernel(const L1Args A) {
       s2 = __builtin_fmaf(v, v, s2);
       mx = fmaxf(mx, v);
     }
+    if (A.smax != nullptr) {
+      mx = wave_max(mx);
+      if ((tid & 63) == 0) atomicMax(&wmax[s], __float_as_uint(mx));
+    }
   }
-  if (A.stats != nullptr || A.rmax != nullptr) {  // block-uniform
+  if (A.stats != nullptr || A.smax != nullptr) {  // block-uniform
     red[half][0][c] = s1;
     red[half][1][c] = s2;
-    red[half][2][c] = mx;
     __syncthreads();
-    if (tid < 128) {
-      if (A.stats != nullptr) {
-        double* dst = A.stats + ((long long)g * kStatSlots + (blockIdx.x % kStatSlots)) * 2 * 128;
-        atomicAdd(dst + c, (double)red[0][0][c] + (double)red[1][0][c]);
-        atomicAdd(dst + 128 + c, (double)red[0][1][c] + (double)red[1][1][c]);
-      }
-      if (A.rmax != nullptr) atomicMax(A.rmax + (long long)g * 128 + c, __float_as_uint(fmaxf(red[0][2][c], red[1][2][c])));
+    if (A.stats != nullptr && tid < 128) {
+      double* dst = A.stats + ((long long)g * kStatSlots + (blockIdx.x % kStatSlots)) * 2 * 128;
+      atomicAdd(dst + c, (double)red[0][0][c] + (double)red[1][0][c]);
+      atomicAdd(dst + 128 + c, (double)red[0][1][c] + (double)red[1][1][c]);
     }
+    // every window belongs to this block alone: a plain store of its max
+    if (A.smax != nullptr && tid < kL1Win && w0 + tid < A.n_win) A.smax[(long long)g * A.n_win + w0 + tid] = wmax[tid];
   }
 }
 
@@ -587,19 +628,13 @@ __global__ __launch_bounds__(256) void l1_kernel(const L1Args A) {
 // aff[g][0][c] = gamma * rstd * dsc, aff[g][1][c] = (beta - mean * gamma * rstd) * dsc, where (mean, var)
 // are the biased batch moments of group g (stats != nullptr) or the moving statistics.  With
 // update != 0 the Keras moving averages are updated once per group in group order (one MC-Dropout
-// pass after the other, the side effect of model(x, training=True)).
-//
-// Range-safe fp16 split (rmax != nullptr): the consumer splits a = aff(R) into fp16 hi + lo, which
-// needs |a| < 65504 (hi finite) and |a| >> 2^-14 (lo normal).  R >= 0 is bounded by the tracked
-// channel maxima, so max |a| over the group is max_c max(|rmax_c s_c + t_c|, |t_c|) (an affine map
-// takes its extremes at the ends of [0, rmax]); the affine is pre-scaled by the exact power of two
-// 2^sa that puts that maximum in [2^13, 2^14), and ascale[g] = 2^-sa lets the consumer's epilogue undo
-// it.  One workgroup; the groups run in order (the moving updates of consecutive passes chain).
+// pass after the other, the side effect of model(x, training=True)).  amax[g] = (max_c |aff scale|,
+// max_c |aff shift|): the consumer's range-safe split (sample_prescale).  One workgroup, groups in order.
 __global__ __launch_bounds__(256) void aff_kernel(const AffArgs A) {
-  __shared__ float red[4];
+  __shared__ float red[2][4];
   const int tid = threadIdx.x;
   for (int g = 0; g < A.groups; ++g) {
-    float amax = 0.f;
+    float ms = 0.f, mt = 0.f;
     for (int c = tid; c < A.C; c += 256) {
       const long long po = (long long)g * A.p_gstride + c;
       float mean, var;
@@ -627,26 +662,22 @@ __global__ __launch_bounds__(256) void aff_kernel(const AffArgs A) {
       const float s_ = sc * A.dsc, t_ = (A.beta[po] - mean * sc) * A.dsc;
       A.aff[((long long)g * 2) * A.C + c] = s_;
       A.aff[((long long)g * 2 + 1) * A.C + c] = t_;
-      if (A.rmax != nullptr) {
-        const float rm = __uint_as_float(A.rmax[(long long)g * A.C + c]);
-        amax = fmaxf(amax, fmaxf(fabsf(__builtin_fmaf(rm, s_, t_)), fabsf(t_)));
-      }
+      ms = fmaxf(ms, fabsf(s_));
+      mt = fmaxf(mt, fabsf(t_));
     }
-    if (A.rmax == nullptr) continue;  // kernel-uniform
-    amax = wave_max(amax);
-    if ((tid & 63) == 0) red[tid >> 6] = amax;
+    if (A.amax == nullptr) continue;  // kernel-uniform
+    ms = wave_max(ms);
+    mt = wave_max(mt);
+    if ((tid & 63) == 0) {
+      red[0][tid >> 6] = ms;
+      red[1][tid >> 6] = mt;
+    }
     __syncthreads();
-    amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    __syncthreads();  // red is rewritten by the next group
-    int e = 0;
-    if (amax > 0.f && amax < INFINITY) frexpf(amax, &e);  // amax = m 2^e, m in [0.5, 1)
-    const int sa = min(100, max(-100, 14 - e));  // amax 2^sa in [2^13, 2^14)
-    const float up = ldexpf(1.f, sa);
-    for (int c = tid; c < A.C; c += 256) {  // the values this thread wrote above
-      A.aff[((long long)g * 2) * A.C + c] *= up;
-      A.aff[((long long)g * 2 + 1) * A.C + c] *= up;
+    if (tid == 0) {
+      A.amax[2 * g] = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+      A.amax[2 * g + 1] = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
     }
-    if (tid == 0) A.ascale[g] = ldexpf(1.f, -sa);
+    __syncthreads();  // red is rewritten by the next group
   }
 }
 

@@ -145,10 +145,10 @@ class _Workspace:
         self.stats = [torch.zeros(max(groups, 1) * STAT_SLOTS * 2 * CH[l + 1], dtype=torch.float64, device=dev)
                       for l in range(6)]
         self.aff = [torch.empty(max(groups, 1) * 2 * CH[l + 1], **f32) for l in range(6)]
-        # range-safe fp16 split of block l+2's input: channel maxima of R_l (fp32 bits) and the inverse
-        # power-of-two prescale folded into aff[l] (blocks 1..5; block 6 feeds the fp32 head)
-        self.rmax = [torch.zeros(max(groups, 1) * CH[l + 1], dtype=torch.int32, device=dev) for l in range(5)]
-        self.ascale = [torch.ones(max(groups, 1), **f32) for l in range(5)]
+        # range-safe fp16 split of block l+2's input (csrc/x3_layers.hip sample_prescale): the max of R_l per
+        # sample (fp32 bits; block 1: per window and member) and the channel maxima of each affine
+        self.smax = [torch.zeros(n_r1 if l == 0 else samples, dtype=torch.int32, device=dev) for l in range(5)]
+        self.amax = [torch.zeros(max(groups, 1) * 2, **f32) for l in range(6)]
 
 
 def _ops():
@@ -157,15 +157,6 @@ def _ops():
 
 def _dsc(rate: float) -> float:
     return 1.0 / (1.0 - rate) if rate < 1.0 else 0.0
-
-
-def _sync_max(sync: Callable, t: torch.Tensor) -> None:
-    """All ranks must prescale a block's activations alike (identical fp16 splits on every shard): MAX
-    all-reduce of the channel maxima (non-negative fp32 bit patterns order like the int32 values)."""
-    import torch.distributed as dist
-
-    if dist.is_available() and dist.is_initialized():
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
 
 
 def _sync_stats(sync: Callable, st: torch.Tensor, groups: int, c: int) -> None:
@@ -235,14 +226,12 @@ def mcd_batch(model: X3Model, x: torch.Tensor, n_pass: int, seed: int, pass_base
     out = torch.empty(n_pass, n, dtype=torch.float32, device=model.device)
     # block 1 once: no dropout precedes it, so every pass sees the same R_1 and the same moments
     ws.stats[0].zero_()
-    ws.rmax[0][: CH[1]].zero_()
-    o.x3_l1(x, model.w1, model.b1, ws.r1, ws.stats[0], n, 1, ws.rmax[0][: CH[1]])
+    o.x3_l1(x, model.w1, model.b1, ws.r1, ws.stats[0], n, 1, ws.smax[0])
     if sync is not None:
         _sync_stats(sync, ws.stats[0], 1, CH[1])
-        _sync_max(sync, ws.rmax[0][: CH[1]])
     g, b, mm, mv = model.bn[0]
     o.x3_aff(ws.stats[0], g, b, mm, mv, ws.aff[0], CH[1], 1, 0, bool(update_moving), n_pass, inv_count, eps, mom, dsc[0],
-             ws.rmax[0][: CH[1]], ws.ascale[0][:1])
+             ws.amax[0])
     for t0 in range(0, n_pass, chunk):
         tc = min(chunk, n_pass - t0)
         pb = int(pass_base) + t0
@@ -250,21 +239,19 @@ def mcd_batch(model: X3Model, x: torch.Tensor, n_pass: int, seed: int, pass_base
             c = CH[l + 1]
             st = ws.stats[l]
             st[: tc * STAT_SLOTS * 2 * c].zero_()
-            rm = ws.rmax[l][: tc * c] if l < 5 else None
-            if rm is not None:
-                rm.zero_()
+            sm = ws.smax[l][: tc * n] if l < 5 else None
+            if sm is not None:
+                sm.zero_()
             src = ws.r1 if l == 1 else ws.buf[(l - 2) % 2]
             dst = ws.sums if l == 5 else ws.buf[(l - 1) % 2]
             o.x3_layer(l, src, dst, model.wfrag[l], 0, model.bias[l], model.wscale[l], 0, ws.aff[l - 1],
                        0 if l == 1 else 2 * CH[l], st, n, tc, l == 1, thr[l - 1], thr[l], seed, pb,
-                       int(window_offset), int(grid), ws.ascale[l - 1], rm)
+                       int(window_offset), int(grid), ws.smax[l - 1], ws.amax[l - 1], sm)
             if sync is not None:
                 _sync_stats(sync, st, tc, c)
-                if rm is not None:
-                    _sync_max(sync, rm)
             g, b, mm, mv = model.bn[l]
             o.x3_aff(st, g, b, mm, mv, ws.aff[l], c, tc, 0, bool(update_moving), 1, inv_count, eps, mom, dsc[l],
-                     rm, ws.ascale[l][:tc] if rm is not None else None)
+                     ws.amax[l])
         o.x3_head(ws.sums, ws.aff[5], 2 * CH[6], model.dw, model.db, 0, ws.out, n, tc, False)
         out[t0: t0 + tc].copy_(ws.out[: tc * n].view(tc, n))
     return out
@@ -297,28 +284,27 @@ def _mcd_batch_windowed(model: X3Model, x: torch.Tensor, n_pass: int, seed: int,
     def run(s: int, e: int, upto: int, pb: int, stats_layer: int) -> None:
         """Blocks 1..upto+1 over windows [s, e) of pass pb; moments of block stats_layer+1 into its slots."""
         m = e - s
-        o.x3_l1(x[s:e], model.w1, model.b1, ws.r1, ws.stats[0] if stats_layer == 0 else None, m, 1,
-                ws.rmax[0][: CH[1]] if stats_layer == 0 else None)
+        # the per-sample maxima of every block's output are recomputed with it (chunk-local data)
+        o.x3_l1(x[s:e], model.w1, model.b1, ws.r1, ws.stats[0] if stats_layer == 0 else None, m, 1, ws.smax[0])
         for l in range(1, upto + 1):
             src = ws.r1 if l == 1 else ws.buf[(l - 2) % 2]
             dst = ws.sums if l == 5 else ws.buf[(l - 1) % 2]
+            sm = ws.smax[l][:m] if l < 5 else None
+            if sm is not None:
+                sm.zero_()
             o.x3_layer(l, src, dst, model.wfrag[l], 0, model.bias[l], model.wscale[l], 0, ws.aff[l - 1],
                        0 if l == 1 else 2 * CH[l], ws.stats[l] if l == stats_layer else None, m, 1, l == 1,
-                       thr[l - 1], thr[l], seed, pb, int(window_offset) + s, 0, ws.ascale[l - 1][:1],
-                       ws.rmax[l][: CH[l + 1]] if (l == stats_layer and l < 5) else None)
+                       thr[l - 1], thr[l], seed, pb, int(window_offset) + s, 0, ws.smax[l - 1], ws.amax[l - 1], sm)
 
     def finish_layer(l: int, repeat: int) -> None:
         if sync is not None:
             _sync_stats(sync, ws.stats[l], 1, CH[l + 1])
-            if l < 5:
-                _sync_max(sync, ws.rmax[l][: CH[l + 1]])
         g, b, mm, mv = model.bn[l]
         o.x3_aff(ws.stats[l], g, b, mm, mv, ws.aff[l], CH[l + 1], 1, 0, bool(update_moving), repeat, inv_count, eps,
-                 mom, dsc[l], ws.rmax[l][: CH[l + 1]] if l < 5 else None, ws.ascale[l][:1] if l < 5 else None)
+                 mom, dsc[l], ws.amax[l])
 
     # block 1: no dropout before it, so its moments (and affine) are shared by every pass
     ws.stats[0].zero_()
-    ws.rmax[0].zero_()
     for s, e in bounds:
         run(s, e, 0, int(pass_base), 0)
     finish_layer(0, n_pass)
@@ -326,8 +312,6 @@ def _mcd_batch_windowed(model: X3Model, x: torch.Tensor, n_pass: int, seed: int,
         pb = int(pass_base) + t
         for l in range(1, 6):
             ws.stats[l].zero_()
-            if l < 5:
-                ws.rmax[l].zero_()
             for s, e in bounds:
                 run(s, e, l, pb, l)
             finish_layer(l, 1)
@@ -376,31 +360,24 @@ def _forward_running(model: X3Model, x: torch.Tensor, n_pass: int, dropout: bool
     dsc = [_dsc(b.dropout) if dropout else 1.0 for b in spec.blocks]
     eps, mom = float(spec.bn_epsilon), float(spec.bn_momentum)
     seed = int(seed) & ((1 << 63) - 1)
-    # BN affine of the moving statistics, per member (shared by all passes with dropout), computed after
-    # the block's output exists: its channel maxima set the power-of-two prescale of the fp16 split
-    def aff(l: int) -> None:
+    # BN affine of the moving statistics, per member (shared by all passes with dropout)
+    for l in range(6):
         g, b, mm, mv = model.bn[l]
-        rm = ws.rmax[l][: G * CH[l + 1]] if l < 5 else None
         o.x3_aff(None, g, b, mm, mv, ws.aff[l], CH[l + 1], G, CH[l + 1] if G > 1 else 0, False, 1, 1.0, eps, mom,
-                 dsc[l], rm, ws.ascale[l][:G] if rm is not None else None)
-
-    ws.rmax[0][: G * CH[1]].zero_()
-    o.x3_l1(x, model.w1, model.b1, ws.r1, None, n, G, ws.rmax[0][: G * CH[1]])
-    aff(0)
+                 dsc[l], ws.amax[l])
+    o.x3_l1(x, model.w1, model.b1, ws.r1, None, n, G, ws.smax[0])
     per_member = G > 1
     for l in range(1, 6):
         src = ws.r1 if l == 1 else ws.buf[(l - 2) % 2]
         dst = ws.sums if l == 5 else ws.buf[(l - 1) % 2]
         wstride = model.wfrag[l].shape[1] // 8 if per_member else 0
-        # one maxima row per member (DE), or one row shared by the passes of one model (MC Dropout)
-        rm = ws.rmax[l][: G * CH[l + 1]] if l < 5 else None
-        if rm is not None:
-            rm.zero_()
+        sm = ws.smax[l][: groups * n] if l < 5 else None
+        if sm is not None:
+            sm.zero_()
         o.x3_layer(l, src, dst, model.wfrag[l], wstride, model.bias[l], model.wscale[l],
                    CH[l + 1] if per_member else 0, ws.aff[l - 1], 2 * CH[l] if per_member else 0, None, n, groups,
                    dropout and l == 1, thr[l - 1], thr[l], seed, int(pass_offset),
-                   int(window_offset), 0, ws.ascale[l - 1], rm)
-        aff(l)
+                   int(window_offset), 0, ws.smax[l - 1], ws.amax[l - 1], sm)
     o.x3_head(ws.sums, ws.aff[5], 2 * CH[6] if per_member else 0, model.dw, model.db, CH[6] if per_member else 0,
               ws.out, n, groups, bool(logits))
     return ws.out[: groups * n].view(G, n_pass, n).clone()
