@@ -118,14 +118,17 @@ __device__ __forceinline__ int xcd_wg() {
 // Register budget: the waves of WPC workgroups per CU over the 4 SIMDs, at least 2 per SIMD.
 template <int NW, int WPC>
 constexpr int waves_per_eu() { return NW * WPC > 8 ? (NW * WPC + 3) / 4 : 2; }
+// LW > 0: LW loader waves; LW <= 0: no loaders, MFMA waves 0 .. -LW-1 stage (LW = 0: kStagers of them)
+constexpr int loaders(int lw) { return lw > 0 ? lw : 0; }
 template <int CIN, int COUT, int KS, int S, int WM, int WN, bool LAST, int LW, int CK, int WPC>
-__global__ __launch_bounds__((WM * WN + LW) * 64, (waves_per_eu<WM * WN + LW, WPC>())) void layer_kernel(const LayerArgs A) {
+__global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN + loaders(LW), WPC>())) void layer_kernel(
+    const LayerArgs A) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int NWM = WM * WN, NW = NWM + LW, kThreads = NW * 64;
+  constexpr int NWM = WM * WN, NW = NWM + loaders(LW), kThreads = NW * 64;
   constexpr int kCK = CK, kRowB = row_bytes(CK), NQ = CK / 32, kQ = CK / 4;  // 32-ch sub-chunks, quads / row
   constexpr int kS = S, kBufB = buf_bytes(S, CK), kValidRows = S * kL, kUnits = kValidRows * kQ;
   // staging waves: the LW loader waves, else MFMA waves 0..SW-1 (one per SIMD by default)
-  constexpr int SW = LW > 0 ? LW : (kStagers < NW ? kStagers : NW);
+  constexpr int SW = LW > 0 ? LW : LW < 0 ? (-LW < NW ? -LW : NW) : (kStagers < NW ? kStagers : NW);
   constexpr int kSBase = LW > 0 ? NWM * 64 : 0;              // first staging thread
   constexpr int kST = SW * 64;                                // staging threads
   constexpr int kNU = (kUnits + kST - 1) / kST;              // 16-B staging units per staging thread
@@ -183,7 +186,9 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, (waves_per_eu<WM * WN + LW, WP
   const bool prescale = A.smax_in != nullptr;
   int key_tile = -1;
   unsigned skeys[kS];
-  float sup[kS];  // 2^sa of the staging tile's samples (range-safe split)
+  // prescale exponents sa of the staging tile's samples, one signed byte each (kS <= 4; one register)
+  static_assert(kS <= 4, "packed per-sample exponents");
+  unsigned sa_pack = 0u;
   auto load_chunk = [&](int tile, int c, Stage& R) {
     const int tid = opaque_tid() - kSBase, q = tid % kQ;
     const int g = tile / tpg;
@@ -211,13 +216,13 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, (waves_per_eu<WM * WN + LW, WP
     if ((hash_in || prescale) && tile != key_tile) {  // workgroup-uniform
       const unsigned skey = stream_key(A.seed, A.layer - 1, A.pass_base + g);
       const float* am = A.amax_in + (A.aff_gstride ? 2 * g : 0);
+      sa_pack = 0u;
 #pragma unroll
       for (int s = 0; s < kS; ++s) {
         skeys[s] = sample_key(skey, A.window_offset + w0 + s);
-        sup[s] = 1.f;
         if (prescale && w0 + s < A.n_win) {
           const long long si = A.in_shared ? w0 + s : (long long)g * A.n_win + w0 + s;
-          sup[s] = ldexpf(1.f, sample_prescale(A.smax_in[si], am));
+          sa_pack |= ((unsigned)sample_prescale(A.smax_in[si], am) & 0xFFu) << (8 * s);
         }
       }
       key_tile = tile;
@@ -244,16 +249,12 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, (waves_per_eu<WM * WN + LW, WP
         for (int i = 0; i < 4; ++i) keep[i] = true;
       }
       const bool valid = w < A.n_win;
-      float up = 1.f;
-      if (prescale) {
-        up = sup[0];
-#pragma unroll
-        for (int j = 1; j < kS; ++j) up = s == j ? sup[j] : up;
-      }
+      // the sample's exponent: a signed byte of sa_pack (v_bfe_i32), applied exactly by v_ldexp_f32
+      const int sa = prescale ? __builtin_amdgcn_sbfe((int)sa_pack, 8 * s, 8) : 0;
       f16x4 hi, lo;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float a = (valid && keep[i]) ? __builtin_fmaf(v[i], R.a[i], R.b[i]) * up : 0.f;
+        const float a = (valid && keep[i]) ? ldexpf(__builtin_fmaf(v[i], R.a[i], R.b[i]), sa) : 0.f;
         hi[i] = (_Float16)a;
         lo[i] = (_Float16)(a - (float)hi[i]);
       }
@@ -712,14 +713,15 @@ hipError_t launch_layer(const LayerArgs& A, int grid, hipStream_t stream) {
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL(k, dim3(grid), dim3((WM * WN + LW) * 64), lds, stream, A);
+  hipLaunchKernelGGL(k, dim3(grid), dim3((WM * WN + loaders(LW)) * 64), lds, stream, A);
   return hipGetLastError();
 }
 
 }  // namespace x3
 
 // Layer table of the reference architecture (cnn_baseline_train.py:59-86), blocks 2..6:
-//   <Cin, Cout, k, samples per tile, wave rows WM, wave channel groups WN, block 6, loader waves LW,
+//   <Cin, Cout, k, samples per tile, wave rows WM, wave channel groups WN, block 6, loader waves LW
+//    (<= 0: no loaders, -LW MFMA waves stage),
 //    input channels per staged chunk CK, persistent workgroups per CU WPC>
 // Each MFMA wave owns (4 S / WM) 16-row tiles x (Cout / 16 / WN) 16-channel tiles; the 64-accumulator-tile
 // layers (Cout 224 / 256) run 2-sample tiles so that the next k-step's weight fragments and the B
@@ -734,7 +736,7 @@ hipError_t launch_layer(const LayerArgs& A, int grid, hipStream_t stream) {
 #include APNEAUQ_X3_TABLE
 #else
 #define APNEAUQ_X3_LAYERS(X)                  \
-  X(1, 128, 192, 5, 4, 2, 4, false, 0, 32, 1) \
+  X(1, 128, 192, 5, 4, 2, 4, false, -8, 32, 1) \
   X(2, 192, 224, 3, 2, 1, 7, false, 4, 64, 1) \
   X(3, 224, 96, 7, 4, 4, 2, false, 4, 32, 1)  \
   X(4, 96, 256, 9, 2, 1, 8, false, 4, 32, 1)  \
