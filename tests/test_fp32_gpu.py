@@ -21,7 +21,7 @@ from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import _ext, generic_tra
 from uncertaintyquantification_sleepapnea_1dcnn_amd.training import step as tstep
 
 from .test_generic_gpu import SPECS
-from .test_train_gpu import _torch_grads
+from .test_train_gpu import TRAIN_PASS_BASE
 
 pytestmark = pytest.mark.gpu
 
@@ -35,6 +35,31 @@ def _batch(spec, n, seed):
     return x.cuda(), y.cuda()
 
 
+def _grads64(model, x, y):
+    """float64 CPU autograd over the reference ops: the exact oracle (GPU fp32 autograd is itself only
+    fp32-accurate -- its MIOpen convolutions may use reduced-precision paths -- so it cannot pin 1e-4)."""
+    store = model.store
+    flat = store.flat.detach().cpu().double().requires_grad_(True)
+    stats = store.stats.detach().cpu().double()
+    p = {}
+    for n in store.trainable:
+        off = store.offsets[n]
+        p[n] = flat[off: off + store.views[n].numel()].view(store.shapes[n])
+    off = 0
+    for n in store.nontrainable:
+        k = store.views[n].numel()
+        p[n] = stats[off: off + k].view(store.shapes[n])
+        off += k
+    xc, yc = x.detach().cpu().double(), y.detach().cpu().double()
+    logits = R.forward(model.spec, p, xc, dropout=True, bn_batch_stats=True, update_moving=True, seed=model.seed,
+                       pass_id=TRAIN_PASS_BASE + model._train_step_counter, sample_ids=torch.arange(xc.shape[0]),
+                       return_logits=True, dtype=torch.float64)
+    lv = torch.nn.functional.binary_cross_entropy_with_logits(logits.reshape(-1), yc, reduction="none")
+    lv.mean().backward()
+    dev = store.flat.device
+    return lv.sum().item(), flat.grad.detach().float().to(dev), stats.float().to(dev)
+
+
 @pytest.mark.parametrize("name", list(ALL))
 def test_fp32_train_step_matches_autograd(name):
     _ext.require()
@@ -43,7 +68,7 @@ def test_fp32_train_step_matches_autograd(name):
     assert tstep._backend(m) == "hip_generic"
     x, y = _batch(spec, 64, 3)
     m.optimizer.learning_rate = 0.0
-    ref_loss, ref_grad, ref_stats, _ = _torch_grads(m, x, y)
+    ref_loss, ref_grad, ref_stats = _grads64(m, x, y)
     loss, _ = generic_train.train_step(m, x, y)
     ws = m._gtrain_ws32
     assert ws.f32 and ws.z[0].dtype == torch.float32
@@ -81,8 +106,12 @@ def test_fp32_graph_step_is_the_eager_step(monkeypatch):
 
 def test_fp32_training_loss_history_matches_torch_backend(monkeypatch):
     """10 epochs of Keras fit (batch 1024, validation_split 0.1) on the HIP fp32 kernels and on fp32
-    autograd from the same init, data and dropout masks: per-epoch losses within 1e-3 (relative)."""
+    autograd from the same init, data and dropout masks: per-epoch losses within 1e-3 (relative; the
+    late-epoch losses are ~1e-3, so an absolute 1e-6 floor)."""
     _ext.require()
+    # the torch side in true fp32 (no TF32-style reduced-precision convolutions / matmuls)
+    monkeypatch.setattr(torch.backends.cudnn, "allow_tf32", False)
+    monkeypatch.setattr(torch.backends.cuda.matmul, "allow_tf32", False)
     from uncertaintyquantification_sleepapnea_1dcnn_amd.data.synthetic import synthetic_windows
 
     x, y, _ = synthetic_windows(4608, seed=17)
@@ -92,7 +121,7 @@ def test_fp32_training_loss_history_matches_torch_backend(monkeypatch):
         m = AlarconCNN1D(seed=2025, device="cuda", train_precision="fp32")
         hist[backend] = m.fit(x, y.astype(np.float32), batch_size=1024, epochs=10, validation_split=0.1,
                               verbose=0).history["loss"]
-    np.testing.assert_allclose(hist["auto"], hist["torch"], rtol=1e-3)
+    np.testing.assert_allclose(hist["auto"], hist["torch"], rtol=1e-3, atol=1e-6)
 
 
 @pytest.mark.parametrize("name", ["pooled", "single30"])

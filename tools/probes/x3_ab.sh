@@ -11,6 +11,8 @@ for r in $(seq 1 $rounds); do
     echo -n "$so round $r: "
     if [ "$so" = "default" ]; then
       timeout -k 10 200 python3 bench/x3_micro.py "$@"
+    elif [ "$so" = "noprescale" ]; then
+      APNEAUQ_X3_PRESCALE=0 timeout -k 10 200 python3 bench/x3_micro.py "$@"
     else
       APNEAUQ_SO_PATH=$so timeout -k 10 200 python3 bench/x3_micro.py "$@"
     fi

@@ -7,11 +7,14 @@ R=/root/repo; export PYTHONPATH=$R TMPDIR=/tmp
 OUT=$R/gpurun_out/abl_$tag; rm -rf $OUT; mkdir -p $OUT
 for so in "$@"; do
   name=$(basename $so .so)
-  if [ "$so" = "default" ]; then unset APNEAUQ_SO_PATH; else export APNEAUQ_SO_PATH=$R/$so; fi
+  unset APNEAUQ_X3_PRESCALE
+  if [ "$so" = "default" ]; then unset APNEAUQ_SO_PATH
+  elif [ "$so" = "noprescale" ]; then unset APNEAUQ_SO_PATH; export APNEAUQ_X3_PRESCALE=0
+  else export APNEAUQ_SO_PATH=$R/$so; fi
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$name -o run -- \
     python3 $R/bench/x3_micro.py --reps 1 --only mcd --passes 20 > $OUT/$name.log 2>&1
 done
-unset APNEAUQ_SO_PATH
+unset APNEAUQ_SO_PATH APNEAUQ_X3_PRESCALE
 python3 - "$OUT" <<'PY'
 import csv, glob, os, sys
 root = sys.argv[1]

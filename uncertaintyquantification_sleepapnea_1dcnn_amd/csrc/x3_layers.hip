@@ -182,7 +182,14 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
   // dropout keys of the current staging tile's S samples (the input's mask is drawn from the counter
   // hash of block l-1 here, at the consumer: the producer's epilogue then runs no hash at all, and the
   // loader waves' hashing overlaps the MFMA waves); recomputed when the staged tile changes
-  const bool hash_in = A.thr_in != 0u;
+#ifndef APNEAUQ_X3_PRODUCER_MASK
+#define APNEAUQ_X3_PRODUCER_MASK 0
+#endif
+  // A/B: APNEAUQ_X3_PRODUCER_MASK=1 draws blocks 2..5's masks in the producer's epilogue and carries
+  // them in the stored value's sign bit (the block-1 output is shared across passes: always hashed here)
+  constexpr bool kProdMask = APNEAUQ_X3_PRODUCER_MASK != 0;
+  const bool hash_in = A.thr_in != 0u && (!kProdMask || A.in_shared);
+  const bool sign_in = kProdMask && A.thr_in != 0u && !A.in_shared;
   const bool prescale = A.smax_in != nullptr;
   int key_tile = -1;
   unsigned skeys[kS];
@@ -244,6 +251,9 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
         keep[1] = (b01 >> 16) >= A.thr_in;
         keep[2] = (b23 & 0xFFFFu) >= A.thr_in;
         keep[3] = (b23 >> 16) >= A.thr_in;
+      } else if (sign_in) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) keep[i] = !__builtin_signbit(v[i]);
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) keep[i] = true;
@@ -375,7 +385,7 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
     const float* bias = A.bias + (long long)g * A.p_gstride;
     // only block 6 draws its output mask here (the masked per-sample sums); blocks 2..5 store the plain
     // ReLU output and their consumer draws the mask while staging it
-    const bool drop = LAST && A.thr_out != 0u;
+    const bool drop = (LAST || kProdMask) && A.thr_out != 0u;
     // a wave's row tiles cover whole 64-row sample slots (NRT % 4 == 0): the sample of row tile rt is
     // wave-uniform, so its dropout key is computed once per sample (scalar ALU), not per (ct, rt, lane)
     unsigned skeys[NRT / 4];
@@ -421,7 +431,12 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
           }
           if constexpr (!LAST) {
             const long long sample = (long long)g * A.n_win + w;
-            *reinterpret_cast<f32x4*>(A.out + (sample * kL + t) * COUT + co0) = r;
+            f32x4 o = r;
+            if (kProdMask && drop) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) o[e] = keep[e] ? r[e] : __builtin_copysignf(r[e], -1.f);
+            }
+            *reinterpret_cast<f32x4*>(A.out + (sample * kL + t) * COUT + co0) = o;
           }
         }
         if constexpr (LAST) {

@@ -104,7 +104,7 @@ class GenericTrainWorkspace:
         self.z = [torch.empty(B * self.L[l], self.ch[l + 1], dtype=bf, device=dev) for l in range(nl)]
         self.hlast = torch.empty(B * self.L[-1], self.ch[-1], dtype=bf, device=dev)
         # forward moment slots: (slots, 2, C); deterministic: one per (conv workgroup of 128 rows, wave row)
-        fslots = [2 * -(-B * self.L[l] // 128) if self.det else SLOTS for l in range(nl)]
+        fslots = [max(SLOTS, 2 * -(-B * self.L[l] // 128)) if self.det else SLOTS for l in range(nl)]
         sizes = [fslots[l] * 2 * self.ch[l + 1] for l in range(nl)]
         self.st_all = torch.zeros(sum(sizes), device=dev)
         self.st = list(torch.split(self.st_all, sizes))

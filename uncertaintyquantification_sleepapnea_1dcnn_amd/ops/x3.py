@@ -20,6 +20,7 @@ block that stages it, block l + 1).
 from __future__ import annotations
 
 import math
+import os
 from typing import Callable, Dict, List, Optional, Sequence
 
 import torch
@@ -147,8 +148,18 @@ class _Workspace:
         self.aff = [torch.empty(max(groups, 1) * 2 * CH[l + 1], **f32) for l in range(6)]
         # range-safe fp16 split of block l+2's input (csrc/x3_layers.hip sample_prescale): the max of R_l per
         # sample (fp32 bits; block 1: per window and member) and the channel maxima of each affine
-        self.smax = [torch.zeros(n_r1 if l == 0 else samples, dtype=torch.int32, device=dev) for l in range(5)]
-        self.amax = [torch.zeros(max(groups, 1) * 2, **f32) for l in range(6)]
+        # (APNEAUQ_X3_PRESCALE=0 turns the prescale off -- an A/B switch for its cost, valid only when
+        # every activation is within fp16's range)
+        on = os.environ.get("APNEAUQ_X3_PRESCALE", "1") != "0"
+        self.smax = [torch.zeros(n_r1 if l == 0 else samples, dtype=torch.int32, device=dev) if on else None
+                     for l in range(5)]
+        self.amax = [torch.zeros(max(groups, 1) * 2, **f32) if on else None for l in range(6)]
+
+    def smax_out(self, l: int, k: int) -> Optional[torch.Tensor]:
+        """Block l+1's per-sample maxima (first k samples, zeroed: atomicMax targets); None for block 6."""
+        if l >= 5 or self.smax[l] is None:
+            return None
+        return self.smax[l][:k].zero_()
 
 
 def _ops():
@@ -239,9 +250,7 @@ def mcd_batch(model: X3Model, x: torch.Tensor, n_pass: int, seed: int, pass_base
             c = CH[l + 1]
             st = ws.stats[l]
             st[: tc * STAT_SLOTS * 2 * c].zero_()
-            sm = ws.smax[l][: tc * n] if l < 5 else None
-            if sm is not None:
-                sm.zero_()
+            sm = ws.smax_out(l, tc * n)
             src = ws.r1 if l == 1 else ws.buf[(l - 2) % 2]
             dst = ws.sums if l == 5 else ws.buf[(l - 1) % 2]
             o.x3_layer(l, src, dst, model.wfrag[l], 0, model.bias[l], model.wscale[l], 0, ws.aff[l - 1],
@@ -289,9 +298,7 @@ def _mcd_batch_windowed(model: X3Model, x: torch.Tensor, n_pass: int, seed: int,
         for l in range(1, upto + 1):
             src = ws.r1 if l == 1 else ws.buf[(l - 2) % 2]
             dst = ws.sums if l == 5 else ws.buf[(l - 1) % 2]
-            sm = ws.smax[l][:m] if l < 5 else None
-            if sm is not None:
-                sm.zero_()
+            sm = ws.smax_out(l, m)
             o.x3_layer(l, src, dst, model.wfrag[l], 0, model.bias[l], model.wscale[l], 0, ws.aff[l - 1],
                        0 if l == 1 else 2 * CH[l], ws.stats[l] if l == stats_layer else None, m, 1, l == 1,
                        thr[l - 1], thr[l], seed, pb, int(window_offset) + s, 0, ws.smax[l - 1], ws.amax[l - 1], sm)
@@ -371,9 +378,7 @@ def _forward_running(model: X3Model, x: torch.Tensor, n_pass: int, dropout: bool
         src = ws.r1 if l == 1 else ws.buf[(l - 2) % 2]
         dst = ws.sums if l == 5 else ws.buf[(l - 1) % 2]
         wstride = model.wfrag[l].shape[1] // 8 if per_member else 0
-        sm = ws.smax[l][: groups * n] if l < 5 else None
-        if sm is not None:
-            sm.zero_()
+        sm = ws.smax_out(l, groups * n)
         o.x3_layer(l, src, dst, model.wfrag[l], wstride, model.bias[l], model.wscale[l],
                    CH[l + 1] if per_member else 0, ws.aff[l - 1], 2 * CH[l] if per_member else 0, None, n, groups,
                    dropout and l == 1, thr[l - 1], thr[l], seed, int(pass_offset),
