@@ -8,11 +8,13 @@ OUT=$R/gpurun_out/abl_$tag; rm -rf $OUT; mkdir -p $OUT
 for so in "$@"; do
   name=$(basename $so .so)
   unset APNEAUQ_X3_PRESCALE
+  T=$R  # "tree:<dir>" = another whole checkout (e.g. probes_src/r3), its own package and bench
   if [ "$so" = "default" ]; then unset APNEAUQ_SO_PATH
   elif [ "$so" = "noprescale" ]; then unset APNEAUQ_SO_PATH; export APNEAUQ_X3_PRESCALE=0
+  elif [ "${so#tree:}" != "$so" ]; then unset APNEAUQ_SO_PATH; T=$R/${so#tree:}
   else export APNEAUQ_SO_PATH=$R/$so; fi
-  timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$name -o run -- \
-    python3 $R/bench/x3_micro.py --reps 1 --only mcd --passes 20 > $OUT/$name.log 2>&1
+  PYTHONPATH=$T timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$name -o run -- \
+    python3 $T/bench/x3_micro.py --reps 1 --only mcd --passes 20 > $OUT/$name.log 2>&1
 done
 unset APNEAUQ_SO_PATH APNEAUQ_X3_PRESCALE
 python3 - "$OUT" <<'PY'

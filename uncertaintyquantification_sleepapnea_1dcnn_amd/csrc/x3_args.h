@@ -21,6 +21,8 @@ struct LayerArgs {
                             // (in_shared: window; else group * n_win + window); nullptr: no prescale
   const float* amax_in;     // [G][2] max_c |scale|, max_c |shift| of aff_in (aff_gstride 0: one pair)
   unsigned* smax_out;       // [G * n_win] max of R_l per sample (fp32 bits, atomicMax; nullptr: none)
+  const float* gscale_in;   // [G] 2^-sa of aff_in's folded per-group prescale (aff_gstride 0: one), or
+                            // nullptr
   double* stats;          // [G][16 slots][2][COUT] moment sums of R_l (nullptr: none)
   int n_win;              // windows per group
   int groups;
@@ -53,6 +55,8 @@ struct AffArgs {
   float* mvar;
   float* aff;            // [G][2][C]
   float* amax;           // [G][2] out: max_c |aff scale|, max_c |aff shift| (nullptr: not written)
+  float* gscale;         // [G] out (batch moments only): 2^-sa of the per-group prescale folded into aff
+                         // (nullptr: none)
   int C, groups, p_gstride, update;
   int repeat;            // moving updates per stats group (block 1 moments are shared by all passes)
   double inv_count;

@@ -47,7 +47,8 @@ void x3_layer(int64_t layer, const at::Tensor& in, at::Tensor& out, const at::Te
               int64_t aff_gstride, const c10::optional<at::Tensor>& stats, int64_t n_win, int64_t groups,
               bool in_shared, int64_t thr_in, int64_t thr_out, int64_t seed, int64_t pass_base,
               int64_t window_offset, int64_t grid, const c10::optional<at::Tensor>& smax_in,
-              const c10::optional<at::Tensor>& amax_in, const c10::optional<at::Tensor>& smax_out) {
+              const c10::optional<at::Tensor>& amax_in, const c10::optional<at::Tensor>& smax_out,
+              const c10::optional<at::Tensor>& gscale_in) {
   TORCH_CHECK(layer >= 1 && layer <= 5, "x3_layer: layer must be 1..5 (block 2..6)");
   TORCH_CHECK(n_win >= 1 && groups >= 1, "x3_layer: empty launch");
   const int cin = kCh[layer], cout = kCh[layer + 1], ks = kKs[layer];
@@ -79,6 +80,10 @@ void x3_layer(int64_t layer, const at::Tensor& in, at::Tensor& out, const at::Te
     need(*smax_in, at::kInt, samples_in, "x3_layer: smax_in");
     need(*amax_in, at::kFloat, (aff_gstride ? groups : 1) * 2, "x3_layer: amax_in");
   }
+  // or: a per-group prescale folded into aff_in (batch moments; x3_aff gscale)
+  const bool gpre = gscale_in.has_value() && gscale_in->defined();
+  TORCH_CHECK(!(pre && gpre), "x3_layer: per-sample and per-group prescale are exclusive");
+  if (gpre) need(*gscale_in, at::kFloat, aff_gstride ? groups : 1, "x3_layer: gscale_in");
   unsigned* smo = nullptr;
   if (smax_out.has_value() && smax_out->defined()) {
     TORCH_CHECK(layer < 5, "x3_layer: block 6 feeds the fp32 head (no smax_out)");
@@ -100,6 +105,7 @@ void x3_layer(int64_t layer, const at::Tensor& in, at::Tensor& out, const at::Te
   A.smax_in = pre ? reinterpret_cast<const unsigned*>(smax_in->data_ptr<int>()) : nullptr;
   A.amax_in = pre ? amax_in->data_ptr<float>() : nullptr;
   A.smax_out = smo;
+  A.gscale_in = gpre ? gscale_in->data_ptr<float>() : nullptr;
   A.n_win = (int)n_win;
   A.groups = (int)groups;
   A.tiles_per_group = (int)tpg;
@@ -144,7 +150,7 @@ void x3_l1(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b, at::Te
 void x3_aff(const c10::optional<at::Tensor>& stats, const at::Tensor& gamma, const at::Tensor& beta, at::Tensor& mmean,
             at::Tensor& mvar, at::Tensor& aff, int64_t C, int64_t groups, int64_t p_gstride, bool update,
             int64_t repeat, double inv_count, double eps, double momentum, double dsc,
-            const c10::optional<at::Tensor>& amax) {
+            const c10::optional<at::Tensor>& amax, const c10::optional<at::Tensor>& gscale) {
   TORCH_CHECK(C >= 1 && C <= 4096 && groups >= 1, "x3_aff: bad sizes");
   TORCH_CHECK(p_gstride == 0 || p_gstride == C, "x3_aff: p_gstride must be 0 or C");
   const int64_t pg = p_gstride ? groups : 1;
@@ -164,9 +170,15 @@ void x3_aff(const c10::optional<at::Tensor>& stats, const at::Tensor& gamma, con
     need(*amax, at::kFloat, groups * 2, "x3_aff: amax");
     amp = amax->data_ptr<float>();
   }
+  float* gsp = nullptr;
+  if (gscale.has_value() && gscale->defined()) {
+    TORCH_CHECK(st != nullptr && amp == nullptr, "x3_aff: gscale needs batch moments and excludes amax");
+    need(*gscale, at::kFloat, groups, "x3_aff: gscale");
+    gsp = gscale->data_ptr<float>();
+  }
   const at::DeviceGuard guard(gamma.device());
   apneauq::x3::AffArgs A{st, gamma.data_ptr<float>(), beta.data_ptr<float>(), mmean.data_ptr<float>(),
-                         mvar.data_ptr<float>(), aff.data_ptr<float>(), amp, (int)C, (int)groups, (int)p_gstride,
+                         mvar.data_ptr<float>(), aff.data_ptr<float>(), amp, gsp, (int)C, (int)groups, (int)p_gstride,
                          update ? 1 : 0, (int)repeat, inv_count, (float)eps, (float)momentum, (float)dsc};
   check(apneauq::x3_launch_aff(A, cur_stream()), "x3_aff");
 }
@@ -198,12 +210,12 @@ TORCH_LIBRARY_FRAGMENT(apneauq, m) {
   m.def("x3_layer(int layer, Tensor input, Tensor(a!) out, Tensor wfrag, int w_gstride, Tensor bias, Tensor wscale, "
         "int p_gstride, Tensor aff_in, int aff_gstride, Tensor(b!)? stats, int n_win, int groups, bool in_shared, "
         "int thr_in, int thr_out, int seed, int pass_base, int window_offset, int grid, Tensor? smax_in=None, "
-        "Tensor? amax_in=None, Tensor(c!)? smax_out=None) -> ()");
+        "Tensor? amax_in=None, Tensor(c!)? smax_out=None, Tensor? gscale_in=None) -> ()");
   m.def("x3_l1(Tensor x, Tensor w, Tensor b, Tensor(a!) out, Tensor(b!)? stats, int n_win, int groups, "
         "Tensor(c!)? smax=None) -> ()");
   m.def("x3_aff(Tensor? stats, Tensor gamma, Tensor beta, Tensor(a!) mmean, Tensor(b!) mvar, Tensor(c!) aff, int C, "
         "int groups, int p_gstride, bool update, int repeat, float inv_count, float eps, float momentum, float dsc, "
-        "Tensor(d!)? amax=None) -> ()");
+        "Tensor(d!)? amax=None, Tensor(e!)? gscale=None) -> ()");
   m.def("x3_head(Tensor sums, Tensor aff, int aff_gstride, Tensor dw, Tensor db, int p_gstride, Tensor(a!) out, "
         "int n_win, int groups, bool logits) -> ()");
   m.def("x3_lds(int layer) -> int", &x3_lds);

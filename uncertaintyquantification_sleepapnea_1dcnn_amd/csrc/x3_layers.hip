@@ -65,7 +65,9 @@ __host__ __device__ constexpr int row_bytes(int ck) { return 4 * ck + 32; }
 // sample's activations are multiplied by the exact power of two 2^sa that puts b in [2^13, 2^14), and
 // the accumulator rows of that sample by 2^-sa (a conv row sums over its own sample's rows only).  The
 // prescale depends on the sample's own data and the (global) affine only: results are independent of
-// sharding, chunking and grouping.
+// sharding, chunking and grouping.  Under batch moments the bound comes free with the moments instead
+// (max R_c <= sqrt(sum R_c^2), aff_kernel): one power of two per group, folded into the affine, and no
+// per-sample tracking in the producer's epilogue (the moments are global, so this is invariant too).
 __device__ __forceinline__ int sample_prescale(unsigned rmax_bits, const float* amax) {
   const float b = __builtin_fmaf(amax[0], __uint_as_float(rmax_bits), amax[1]);
   int e = 0;
@@ -77,7 +79,11 @@ __device__ __forceinline__ int sample_prescale(unsigned rmax_bits, const float* 
 __host__ __device__ constexpr int lds_rows(int S) { return kHalo + S * kSR + kHalo; }
 __host__ __device__ constexpr int buf_bytes(int S, int ck) { return lds_rows(S) * row_bytes(ck); }
 // + per-workgroup fp64 moment sums [2][COUT]
-__host__ __device__ constexpr int lds_bytes(int S, int cout, int ck) { return 2 * buf_bytes(S, ck) + 2 * cout * 8; }
+// two LDS chunk buffers, the workgroup's fp64 moment sums, and the epilogue down-scale factors of the
+// two most recently staged tiles ([2][S] floats, written by the staging waves)
+__host__ __device__ constexpr int lds_bytes(int S, int cout, int ck) {
+  return 2 * buf_bytes(S, ck) + 2 * cout * 8 + 2 * S * 4;
+}
 
 // global-address-space load (keeps global_load_*, never flat_*)
 template <typename T>
@@ -148,6 +154,8 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
   static_assert(NCTA % WN == 0 && (4 * S) % WM == 0, "wave tiling");
   static_assert(NRT % 4 == 0, "whole 64-row sample slots per wave row (epilogue keys, block 6 sums)");
   double* st = reinterpret_cast<double*>(smem + 2 * kBufB);  // [2][COUT] per-workgroup moment sums
+  // [tile & 1][sample of the tile]: wscale x 2^-sa, the epilogue's undo of both prescales
+  float* wsc = reinterpret_cast<float*>(smem + 2 * kBufB + 2 * COUT * 8);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -182,14 +190,9 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
   // dropout keys of the current staging tile's S samples (the input's mask is drawn from the counter
   // hash of block l-1 here, at the consumer: the producer's epilogue then runs no hash at all, and the
   // loader waves' hashing overlaps the MFMA waves); recomputed when the staged tile changes
-#ifndef APNEAUQ_X3_PRODUCER_MASK
-#define APNEAUQ_X3_PRODUCER_MASK 0
-#endif
-  // A/B: APNEAUQ_X3_PRODUCER_MASK=1 draws blocks 2..5's masks in the producer's epilogue and carries
-  // them in the stored value's sign bit (the block-1 output is shared across passes: always hashed here)
-  constexpr bool kProdMask = APNEAUQ_X3_PRODUCER_MASK != 0;
-  const bool hash_in = A.thr_in != 0u && (!kProdMask || A.in_shared);
-  const bool sign_in = kProdMask && A.thr_in != 0u && !A.in_shared;
+  // (drawing blocks 2..5's masks in the producer's epilogue instead, carried in the stored value's sign
+  // bit, measured no faster: profiles/x3_prescale_ab_r4.md)
+  const bool hash_in = A.thr_in != 0u;
   const bool prescale = A.smax_in != nullptr;
   int key_tile = -1;
   unsigned skeys[kS];
@@ -220,17 +223,24 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
     const int tid = opaque_tid() - kSBase, q = tid % kQ;
     const int g = tile / tpg;
     const int w0 = (tile - g * tpg) * kS;
-    if ((hash_in || prescale) && tile != key_tile) {  // workgroup-uniform
+    if (tile != key_tile) {  // workgroup-uniform
       const unsigned skey = stream_key(A.seed, A.layer - 1, A.pass_base + g);
       const float* am = A.amax_in + (A.aff_gstride ? 2 * g : 0);
+      float ws0 = A.wscale[A.p_gstride ? g : 0];
+      if (A.gscale_in != nullptr) ws0 *= A.gscale_in[A.aff_gstride ? g : 0];
       sa_pack = 0u;
 #pragma unroll
       for (int s = 0; s < kS; ++s) {
         skeys[s] = sample_key(skey, A.window_offset + w0 + s);
+        int sa = 0;
         if (prescale && w0 + s < A.n_win) {
           const long long si = A.in_shared ? w0 + s : (long long)g * A.n_win + w0 + s;
-          sa_pack |= ((unsigned)sample_prescale(A.smax_in[si], am) & 0xFFu) << (8 * s);
+          sa = sample_prescale(A.smax_in[si], am);
+          sa_pack |= ((unsigned)sa & 0xFFu) << (8 * s);
         }
+        // read by this tile's epilogue (after >= 1 barrier); the slot's previous tile (tile - 2) had its
+        // epilogue before the barrier that precedes this store
+        if (tid == s) wsc[(tile & 1) * kS + s] = ldexpf(ws0, -sa);
       }
       key_tile = tile;
     }
@@ -251,9 +261,6 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
         keep[1] = (b01 >> 16) >= A.thr_in;
         keep[2] = (b23 & 0xFFFFu) >= A.thr_in;
         keep[3] = (b23 >> 16) >= A.thr_in;
-      } else if (sign_in) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) keep[i] = !__builtin_signbit(v[i]);
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) keep[i] = true;
@@ -366,18 +373,11 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
     const int lane = opaque_tid() & 63, m = lane & 15, h = lane >> 4;
     const int g = tile / tpg;
     const int w0 = (tile - g * tpg) * kS;
-    // undo the weight prescale 2^sw and each sample's activation prescale 2^sa (exact powers of two)
-    const float ws0 = A.wscale[A.p_gstride ? g : 0];
+    // undo the weight prescale 2^sw and each sample's activation prescale 2^sa (exact powers of two;
+    // the factors were put in LDS by the staging waves)
     float wsq[NRT / 4];
 #pragma unroll
-    for (int q = 0; q < NRT / 4; ++q) {
-      wsq[q] = ws0;
-      const int w = w0 + (rt0 >> 2) + q;
-      if (A.smax_in != nullptr && w < A.n_win) {
-        const long long si = A.in_shared ? w : (long long)g * A.n_win + w;
-        wsq[q] = ws0 * ldexpf(1.f, -sample_prescale(A.smax_in[si], A.amax_in + (A.aff_gstride ? 2 * g : 0)));
-      }
-    }
+    for (int q = 0; q < NRT / 4; ++q) wsq[q] = wsc[(tile & 1) * kS + (rt0 >> 2) + q];
     const bool track = !LAST && A.smax_out != nullptr;
     float mxs[NRT / 4];  // max of R_l per sample slot of the wave (range-safe split of the next block)
 #pragma unroll
@@ -385,7 +385,7 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
     const float* bias = A.bias + (long long)g * A.p_gstride;
     // only block 6 draws its output mask here (the masked per-sample sums); blocks 2..5 store the plain
     // ReLU output and their consumer draws the mask while staging it
-    const bool drop = (LAST || kProdMask) && A.thr_out != 0u;
+    const bool drop = LAST && A.thr_out != 0u;
     // a wave's row tiles cover whole 64-row sample slots (NRT % 4 == 0): the sample of row tile rt is
     // wave-uniform, so its dropout key is computed once per sample (scalar ALU), not per (ct, rt, lane)
     unsigned skeys[NRT / 4];
@@ -431,12 +431,7 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
           }
           if constexpr (!LAST) {
             const long long sample = (long long)g * A.n_win + w;
-            f32x4 o = r;
-            if (kProdMask && drop) {
-#pragma unroll
-              for (int e = 0; e < 4; ++e) o[e] = keep[e] ? r[e] : __builtin_copysignf(r[e], -1.f);
-            }
-            *reinterpret_cast<f32x4*>(A.out + (sample * kL + t) * COUT + co0) = o;
+            *reinterpret_cast<f32x4*>(A.out + (sample * kL + t) * COUT + co0) = r;
           }
         }
         if constexpr (LAST) {
@@ -678,8 +673,36 @@ __global__ __launch_bounds__(256) void aff_kernel(const AffArgs A) {
       const float s_ = sc * A.dsc, t_ = (A.beta[po] - mean * sc) * A.dsc;
       A.aff[((long long)g * 2) * A.C + c] = s_;
       A.aff[((long long)g * 2 + 1) * A.C + c] = t_;
-      ms = fmaxf(ms, fabsf(s_));
-      mt = fmaxf(mt, fabsf(t_));
+      if (A.gscale != nullptr) {
+        // batch moments: R >= 0 gives max R_c <= sqrt(sum R_c^2) over the group's rows (of all ranks), so
+        // b = max_c |s_c| sqrt(sum R_c^2) + |t_c| bounds every staged |a| of the group
+        const double* p = A.stats + (long long)g * kStatSlots * 2 * A.C + A.C + c;
+        double q = 0.0;
+        for (int s = 0; s < kStatSlots; ++s) q += p[s * 2 * A.C];
+        ms = fmaxf(ms, __builtin_fmaf(fabsf(s_), (float)sqrt(fmax(q, 0.0)) * 1.0001f, fabsf(t_)));
+      } else {
+        ms = fmaxf(ms, fabsf(s_));
+        mt = fmaxf(mt, fabsf(t_));
+      }
+    }
+    if (A.gscale != nullptr) {
+      // per-group power of two 2^sa putting the bound in [2^13, 2^14), folded into the affine; the layer
+      // kernel multiplies its accumulators by gscale = 2^-sa
+      ms = wave_max(ms);
+      if ((tid & 63) == 0) red[0][tid >> 6] = ms;
+      __syncthreads();
+      const float bnd = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+      int e = 0;
+      if (bnd > 0.f && bnd < INFINITY) frexpf(bnd, &e);
+      const int sa = min(100, max(-100, 14 - e));
+      for (int c = tid; c < A.C; c += 256) {
+        float* af = A.aff + (long long)g * 2 * A.C + c;
+        af[0] = ldexpf(af[0], sa);
+        af[A.C] = ldexpf(af[A.C], sa);
+      }
+      if (tid == 0) A.gscale[g] = ldexpf(1.f, -sa);
+      __syncthreads();  // red is rewritten by the next group
+      continue;
     }
     if (A.amax == nullptr) continue;  // kernel-uniform
     ms = wave_max(ms);

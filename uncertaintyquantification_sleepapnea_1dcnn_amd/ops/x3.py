@@ -146,14 +146,16 @@ class _Workspace:
         self.stats = [torch.zeros(max(groups, 1) * STAT_SLOTS * 2 * CH[l + 1], dtype=torch.float64, device=dev)
                       for l in range(6)]
         self.aff = [torch.empty(max(groups, 1) * 2 * CH[l + 1], **f32) for l in range(6)]
-        # range-safe fp16 split of block l+2's input (csrc/x3_layers.hip sample_prescale): the max of R_l per
-        # sample (fp32 bits; block 1: per window and member) and the channel maxima of each affine
-        # (APNEAUQ_X3_PRESCALE=0 turns the prescale off -- an A/B switch for its cost, valid only when
-        # every activation is within fp16's range)
+        # range-safe fp16 split of block l+2's input (csrc/x3_layers.hip sample_prescale).  Moving statistics:
+        # the max of R_l per sample (fp32 bits; block 1: per window and member) and the channel maxima of
+        # each affine.  Batch moments: one power of two per group, from the moments themselves, folded into
+        # the affine (x3_aff gscale).  APNEAUQ_X3_PRESCALE=0 turns both off -- an A/B switch for their
+        # cost, valid only when every activation is within fp16's range.
         on = os.environ.get("APNEAUQ_X3_PRESCALE", "1") != "0"
         self.smax = [torch.zeros(n_r1 if l == 0 else samples, dtype=torch.int32, device=dev) if on else None
                      for l in range(5)]
         self.amax = [torch.zeros(max(groups, 1) * 2, **f32) if on else None for l in range(6)]
+        self.gscale = [torch.ones(max(groups, 1), **f32) if on else None for l in range(5)] + [None]
 
     def smax_out(self, l: int, k: int) -> Optional[torch.Tensor]:
         """Block l+1's per-sample maxima (first k samples, zeroed: atomicMax targets); None for block 6."""
@@ -237,12 +239,12 @@ def mcd_batch(model: X3Model, x: torch.Tensor, n_pass: int, seed: int, pass_base
     out = torch.empty(n_pass, n, dtype=torch.float32, device=model.device)
     # block 1 once: no dropout precedes it, so every pass sees the same R_1 and the same moments
     ws.stats[0].zero_()
-    o.x3_l1(x, model.w1, model.b1, ws.r1, ws.stats[0], n, 1, ws.smax[0])
+    o.x3_l1(x, model.w1, model.b1, ws.r1, ws.stats[0], n, 1, None)
     if sync is not None:
         _sync_stats(sync, ws.stats[0], 1, CH[1])
     g, b, mm, mv = model.bn[0]
     o.x3_aff(ws.stats[0], g, b, mm, mv, ws.aff[0], CH[1], 1, 0, bool(update_moving), n_pass, inv_count, eps, mom, dsc[0],
-             ws.amax[0])
+             None, ws.gscale[0])
     for t0 in range(0, n_pass, chunk):
         tc = min(chunk, n_pass - t0)
         pb = int(pass_base) + t0
@@ -250,17 +252,16 @@ def mcd_batch(model: X3Model, x: torch.Tensor, n_pass: int, seed: int, pass_base
             c = CH[l + 1]
             st = ws.stats[l]
             st[: tc * STAT_SLOTS * 2 * c].zero_()
-            sm = ws.smax_out(l, tc * n)
             src = ws.r1 if l == 1 else ws.buf[(l - 2) % 2]
             dst = ws.sums if l == 5 else ws.buf[(l - 1) % 2]
             o.x3_layer(l, src, dst, model.wfrag[l], 0, model.bias[l], model.wscale[l], 0, ws.aff[l - 1],
                        0 if l == 1 else 2 * CH[l], st, n, tc, l == 1, thr[l - 1], thr[l], seed, pb,
-                       int(window_offset), int(grid), ws.smax[l - 1], ws.amax[l - 1], sm)
+                       int(window_offset), int(grid), None, None, None, ws.gscale[l - 1])
             if sync is not None:
                 _sync_stats(sync, st, tc, c)
             g, b, mm, mv = model.bn[l]
             o.x3_aff(st, g, b, mm, mv, ws.aff[l], c, tc, 0, bool(update_moving), 1, inv_count, eps, mom, dsc[l],
-                     ws.amax[l])
+                     None, ws.gscale[l])
         o.x3_head(ws.sums, ws.aff[5], 2 * CH[6], model.dw, model.db, 0, ws.out, n, tc, False)
         out[t0: t0 + tc].copy_(ws.out[: tc * n].view(tc, n))
     return out
@@ -293,22 +294,20 @@ def _mcd_batch_windowed(model: X3Model, x: torch.Tensor, n_pass: int, seed: int,
     def run(s: int, e: int, upto: int, pb: int, stats_layer: int) -> None:
         """Blocks 1..upto+1 over windows [s, e) of pass pb; moments of block stats_layer+1 into its slots."""
         m = e - s
-        # the per-sample maxima of every block's output are recomputed with it (chunk-local data)
-        o.x3_l1(x[s:e], model.w1, model.b1, ws.r1, ws.stats[0] if stats_layer == 0 else None, m, 1, ws.smax[0])
+        o.x3_l1(x[s:e], model.w1, model.b1, ws.r1, ws.stats[0] if stats_layer == 0 else None, m, 1, None)
         for l in range(1, upto + 1):
             src = ws.r1 if l == 1 else ws.buf[(l - 2) % 2]
             dst = ws.sums if l == 5 else ws.buf[(l - 1) % 2]
-            sm = ws.smax_out(l, m)
             o.x3_layer(l, src, dst, model.wfrag[l], 0, model.bias[l], model.wscale[l], 0, ws.aff[l - 1],
                        0 if l == 1 else 2 * CH[l], ws.stats[l] if l == stats_layer else None, m, 1, l == 1,
-                       thr[l - 1], thr[l], seed, pb, int(window_offset) + s, 0, ws.smax[l - 1], ws.amax[l - 1], sm)
+                       thr[l - 1], thr[l], seed, pb, int(window_offset) + s, 0, None, None, None, ws.gscale[l - 1])
 
     def finish_layer(l: int, repeat: int) -> None:
         if sync is not None:
             _sync_stats(sync, ws.stats[l], 1, CH[l + 1])
         g, b, mm, mv = model.bn[l]
         o.x3_aff(ws.stats[l], g, b, mm, mv, ws.aff[l], CH[l + 1], 1, 0, bool(update_moving), repeat, inv_count, eps,
-                 mom, dsc[l], ws.amax[l])
+                 mom, dsc[l], None, ws.gscale[l])
 
     # block 1: no dropout before it, so its moments (and affine) are shared by every pass
     ws.stats[0].zero_()
