@@ -8,11 +8,15 @@ while [ "$1" != "--" ]; do sos+=("$1"); shift; done
 shift
 for r in $(seq 1 $rounds); do
   for so in "${sos[@]}"; do
-    echo -n "$so round $r: "
+    echo "== $so round $r"
     if [ "$so" = "default" ]; then
       timeout -k 10 200 python3 bench/x3_micro.py "$@"
     elif [ "$so" = "noprescale" ]; then
       APNEAUQ_X3_PRESCALE=0 timeout -k 10 200 python3 bench/x3_micro.py "$@"
+    elif [ "${so#env:}" != "$so" ]; then
+      env "${so#env:}" timeout -k 10 200 python3 bench/x3_micro.py "$@"
+    elif [ "${so#tree:}" != "$so" ]; then
+      (cd ${so#tree:} && PYTHONPATH=. timeout -k 10 200 python3 bench/x3_micro.py "$@")
     else
       APNEAUQ_SO_PATH=$so timeout -k 10 200 python3 bench/x3_micro.py "$@"
     fi

@@ -6,17 +6,18 @@ tag=$1; shift
 R=/root/repo; export PYTHONPATH=$R TMPDIR=/tmp
 OUT=$R/gpurun_out/abl_$tag; rm -rf $OUT; mkdir -p $OUT
 for so in "$@"; do
-  name=$(basename $so .so)
-  unset APNEAUQ_X3_PRESCALE
+  name=$(basename $so .so | tr '=,:/' '____')
   T=$R  # "tree:<dir>" = another whole checkout (e.g. probes_src/r3), its own package and bench
+  E=()  # "env:VAR=VALUE" = the library build under that environment variable
   if [ "$so" = "default" ]; then unset APNEAUQ_SO_PATH
-  elif [ "$so" = "noprescale" ]; then unset APNEAUQ_SO_PATH; export APNEAUQ_X3_PRESCALE=0
+  elif [ "$so" = "noprescale" ]; then unset APNEAUQ_SO_PATH; E=(APNEAUQ_X3_PRESCALE=0)
+  elif [ "${so#env:}" != "$so" ]; then unset APNEAUQ_SO_PATH; E=("${so#env:}")
   elif [ "${so#tree:}" != "$so" ]; then unset APNEAUQ_SO_PATH; T=$R/${so#tree:}
   else export APNEAUQ_SO_PATH=$R/$so; fi
-  PYTHONPATH=$T timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$name -o run -- \
+  env "${E[@]}" PYTHONPATH=$T timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$name -o run -- \
     python3 $T/bench/x3_micro.py --reps 1 --only mcd --passes 20 > $OUT/$name.log 2>&1
 done
-unset APNEAUQ_SO_PATH APNEAUQ_X3_PRESCALE
+unset APNEAUQ_SO_PATH
 python3 - "$OUT" <<'PY'
 import csv, glob, os, sys
 root = sys.argv[1]

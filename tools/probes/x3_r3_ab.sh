@@ -4,7 +4,7 @@
 set -e
 R=$PWD
 for r in $(seq 1 $1); do
-  echo -n "current round $r: "; timeout -k 10 200 python3 bench/x3_micro.py --reps 3
-  echo -n "noprescale round $r: "; APNEAUQ_X3_PRESCALE=0 timeout -k 10 200 python3 bench/x3_micro.py --reps 3
-  echo -n "r3 round $r: "; (cd $R/probes_src/r3 && PYTHONPATH=. timeout -k 10 200 python3 bench/x3_micro.py --reps 3)
+  echo "== current round $r"; timeout -k 10 200 python3 bench/x3_micro.py --reps 3
+  echo "== noprescale round $r"; APNEAUQ_X3_PRESCALE=0 timeout -k 10 200 python3 bench/x3_micro.py --reps 3
+  echo "== r3 round $r"; (cd $R/probes_src/r3 && PYTHONPATH=. timeout -k 10 200 python3 bench/x3_micro.py --reps 3)
 done

@@ -29,6 +29,8 @@ struct LayerArgs {
   int tiles_per_group;    // informational (the kernel derives its tiling from n_win, groups and its tile size)
   int total_tiles;
   int in_shared;          // input indexed by window only (block-1 output shared by all passes)
+  int sign_in;            // the input carries block l-1's dropout mask in its sign bits (else: hashed here)
+  int sign_out;           // draw block l's mask in the epilogue, stored as the sign bit (blocks 2..5)
   unsigned thr_in;        // 16-bit drop threshold of block l-1, whose mask the staging draws (0: no dropout)
   unsigned thr_out;       // 16-bit drop threshold of block l (block 6 only: its masked sums; 0: no dropout)
   int layer;              // 0-based index of this block (dropout streams: layer - 1 in, layer out)

@@ -48,7 +48,7 @@ void x3_layer(int64_t layer, const at::Tensor& in, at::Tensor& out, const at::Te
               bool in_shared, int64_t thr_in, int64_t thr_out, int64_t seed, int64_t pass_base,
               int64_t window_offset, int64_t grid, const c10::optional<at::Tensor>& smax_in,
               const c10::optional<at::Tensor>& amax_in, const c10::optional<at::Tensor>& smax_out,
-              const c10::optional<at::Tensor>& gscale_in) {
+              const c10::optional<at::Tensor>& gscale_in, bool sign_in, bool sign_out) {
   TORCH_CHECK(layer >= 1 && layer <= 5, "x3_layer: layer must be 1..5 (block 2..6)");
   TORCH_CHECK(n_win >= 1 && groups >= 1, "x3_layer: empty launch");
   const int cin = kCh[layer], cout = kCh[layer + 1], ks = kKs[layer];
@@ -111,6 +111,10 @@ void x3_layer(int64_t layer, const at::Tensor& in, at::Tensor& out, const at::Te
   A.tiles_per_group = (int)tpg;
   A.total_tiles = (int)(tpg * groups);
   A.in_shared = in_shared ? 1 : 0;
+  TORCH_CHECK(!(sign_in && in_shared), "x3_layer: the shared block-1 output carries no masks");
+  TORCH_CHECK(!(sign_out && layer == 5), "x3_layer: block 6 reduces its masked output in place");
+  A.sign_in = sign_in ? 1 : 0;
+  A.sign_out = sign_out ? 1 : 0;
   A.thr_in = (unsigned)thr_in;
   A.thr_out = (unsigned)thr_out;
   A.layer = (int)layer;
@@ -210,7 +214,7 @@ TORCH_LIBRARY_FRAGMENT(apneauq, m) {
   m.def("x3_layer(int layer, Tensor input, Tensor(a!) out, Tensor wfrag, int w_gstride, Tensor bias, Tensor wscale, "
         "int p_gstride, Tensor aff_in, int aff_gstride, Tensor(b!)? stats, int n_win, int groups, bool in_shared, "
         "int thr_in, int thr_out, int seed, int pass_base, int window_offset, int grid, Tensor? smax_in=None, "
-        "Tensor? amax_in=None, Tensor(c!)? smax_out=None, Tensor? gscale_in=None) -> ()");
+        "Tensor? amax_in=None, Tensor(c!)? smax_out=None, Tensor? gscale_in=None, bool sign_in=False, bool sign_out=False) -> ()");
   m.def("x3_l1(Tensor x, Tensor w, Tensor b, Tensor(a!) out, Tensor(b!)? stats, int n_win, int groups, "
         "Tensor(c!)? smax=None) -> ()");
   m.def("x3_aff(Tensor? stats, Tensor gamma, Tensor beta, Tensor(a!) mmean, Tensor(b!) mvar, Tensor(c!) aff, int C, "

@@ -126,7 +126,9 @@ template <int NW, int WPC>
 constexpr int waves_per_eu() { return NW * WPC > 8 ? (NW * WPC + 3) / 4 : 2; }
 // LW > 0: LW loader waves; LW <= 0: no loaders, MFMA waves 0 .. -LW-1 stage (LW = 0: kStagers of them)
 constexpr int loaders(int lw) { return lw > 0 ? lw : 0; }
-template <int CIN, int COUT, int KS, int S, int WM, int WN, bool LAST, int LW, int CK, int WPC>
+// PS: the per-sample prescale (moving statistics) is compiled in; without it (batch moments: per-group
+// prescale folded into the affine) the kernel has the registers of its tracking for other uses.
+template <int CIN, int COUT, int KS, int S, int WM, int WN, bool LAST, int LW, int CK, int WPC, bool PS>
 __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN + loaders(LW), WPC>())) void layer_kernel(
     const LayerArgs A) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -190,10 +192,11 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
   // dropout keys of the current staging tile's S samples (the input's mask is drawn from the counter
   // hash of block l-1 here, at the consumer: the producer's epilogue then runs no hash at all, and the
   // loader waves' hashing overlaps the MFMA waves); recomputed when the staged tile changes
-  // (drawing blocks 2..5's masks in the producer's epilogue instead, carried in the stored value's sign
-  // bit, measured no faster: profiles/x3_prescale_ab_r4.md)
-  const bool hash_in = A.thr_in != 0u;
-  const bool prescale = A.smax_in != nullptr;
+  // or the producer drew it and the input carries it in the sign bit (A.sign_in: per layer, whichever
+  // side has the slack, profiles/x3_mask_side_r4.md)
+  const bool hash_in = A.thr_in != 0u && !A.sign_in;
+  const bool sign_in = A.thr_in != 0u && A.sign_in;
+  const bool prescale = PS && A.smax_in != nullptr;
   int key_tile = -1;
   unsigned skeys[kS];
   // prescale exponents sa of the staging tile's samples, one signed byte each (kS <= 4; one register)
@@ -261,6 +264,9 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
         keep[1] = (b01 >> 16) >= A.thr_in;
         keep[2] = (b23 & 0xFFFFu) >= A.thr_in;
         keep[3] = (b23 >> 16) >= A.thr_in;
+      } else if (sign_in) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) keep[i] = !__builtin_signbit(v[i]);
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) keep[i] = true;
@@ -378,14 +384,14 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
     float wsq[NRT / 4];
 #pragma unroll
     for (int q = 0; q < NRT / 4; ++q) wsq[q] = wsc[(tile & 1) * kS + (rt0 >> 2) + q];
-    const bool track = !LAST && A.smax_out != nullptr;
+    const bool track = PS && !LAST && A.smax_out != nullptr;
     float mxs[NRT / 4];  // max of R_l per sample slot of the wave (range-safe split of the next block)
 #pragma unroll
     for (int q = 0; q < NRT / 4; ++q) mxs[q] = 0.f;
     const float* bias = A.bias + (long long)g * A.p_gstride;
-    // only block 6 draws its output mask here (the masked per-sample sums); blocks 2..5 store the plain
-    // ReLU output and their consumer draws the mask while staging it
-    const bool drop = LAST && A.thr_out != 0u;
+    // block 6 draws its output mask here (the masked per-sample sums); blocks 2..5 either store the plain
+    // ReLU output (their consumer draws the mask while staging it) or, with A.sign_out, draw it here too
+    const bool drop = (LAST || A.sign_out) && A.thr_out != 0u;
     // a wave's row tiles cover whole 64-row sample slots (NRT % 4 == 0): the sample of row tile rt is
     // wave-uniform, so its dropout key is computed once per sample (scalar ALU), not per (ct, rt, lane)
     unsigned skeys[NRT / 4];
@@ -431,7 +437,12 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
           }
           if constexpr (!LAST) {
             const long long sample = (long long)g * A.n_win + w;
-            *reinterpret_cast<f32x4*>(A.out + (sample * kL + t) * COUT + co0) = r;
+            f32x4 o = r;
+            if (drop) {  // the mask travels in the sign bit (-0 for a dropped zero)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) o[e] = keep[e] ? r[e] : __builtin_copysignf(r[e], -1.f);
+            }
+            *reinterpret_cast<f32x4*>(A.out + (sample * kL + t) * COUT + co0) = o;
           }
         }
         if constexpr (LAST) {
@@ -740,11 +751,11 @@ __global__ __launch_bounds__(256) void head_kernel(const HeadArgs A) {
 }
 
 // ------------------------------------------------------------------------------- launch helpers
-template <int CIN, int COUT, int KS, int S, int WM, int WN, bool LAST, int LW, int CK, int WPC>
+template <int CIN, int COUT, int KS, int S, int WM, int WN, bool LAST, int LW, int CK, int WPC, bool PS>
 hipError_t launch_layer(const LayerArgs& A, int grid, hipStream_t stream) {
   constexpr int lds = lds_bytes(S, COUT, CK);
   static_assert(WPC * lds <= 160 * 1024, "LDS of the workgroups sharing a CU");
-  auto k = layer_kernel<CIN, COUT, KS, S, WM, WN, LAST, LW, CK, WPC>;
+  auto k = layer_kernel<CIN, COUT, KS, S, WM, WN, LAST, LW, CK, WPC, PS>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -759,13 +770,14 @@ hipError_t launch_layer(const LayerArgs& A, int grid, hipStream_t stream) {
 
 // Layer table of the reference architecture (cnn_baseline_train.py:59-86), blocks 2..6:
 //   <Cin, Cout, k, samples per tile, wave rows WM, wave channel groups WN, block 6, loader waves LW
-//    (<= 0: no loaders, -LW MFMA waves stage),
+//    (<= 0: no loaders, -LW MFMA waves stage) with / LWB without the per-sample prescale,
 //    input channels per staged chunk CK, persistent workgroups per CU WPC>
 // Each MFMA wave owns (4 S / WM) 16-row tiles x (Cout / 16 / WN) 16-channel tiles; the 64-accumulator-tile
 // layers (Cout 224 / 256) run 2-sample tiles so that the next k-step's weight fragments and the B
 // double-buffer fit beside the accumulators without spilling.  Loader waves (ablation table in
 // profiles/x3_loader_waves.md) on every layer but block 2, whose 96-accumulator tile needs the 256-VGPR
-// budget of 8 waves (loaders at 2-sample tiles: slower; at 4: 99 VGPRs spilled).  64-channel chunks for
+// budget of 8 waves (loaders at 2-sample tiles: slower; at 4: 99 VGPRs spilled); its staging runs on
+// MFMA waves 0..3, or on all 8 where the per-sample prescale's registers would otherwise spill.  64-channel chunks for
 // blocks 3 and 6 (block 2 would spill; Cin 224 / 96 are not multiples of 64).  Measurements:
 // profiles/x3_epilogue_ab_r3.md.
 // A/B builds may substitute another table (-DAPNEAUQ_X3_TABLE='"path.h"', tools/probes/x3_tables/):
@@ -773,16 +785,16 @@ hipError_t launch_layer(const LayerArgs& A, int grid, hipStream_t stream) {
 #ifdef APNEAUQ_X3_TABLE
 #include APNEAUQ_X3_TABLE
 #else
-#define APNEAUQ_X3_LAYERS(X)                  \
-  X(1, 128, 192, 5, 4, 2, 4, false, -8, 32, 1) \
-  X(2, 192, 224, 3, 2, 1, 7, false, 4, 64, 1) \
-  X(3, 224, 96, 7, 4, 4, 2, false, 4, 32, 1)  \
-  X(4, 96, 256, 9, 2, 1, 8, false, 4, 32, 1)  \
-  X(5, 256, 96, 9, 4, 4, 2, true, 4, 64, 1)
+#define APNEAUQ_X3_LAYERS(X)                     \
+  X(1, 128, 192, 5, 4, 2, 4, false, -8, 0, 32, 1) \
+  X(2, 192, 224, 3, 2, 1, 7, false, 4, 4, 64, 1) \
+  X(3, 224, 96, 7, 4, 4, 2, false, 4, 4, 32, 1)  \
+  X(4, 96, 256, 9, 2, 1, 8, false, 4, 4, 32, 1)  \
+  X(5, 256, 96, 9, 4, 4, 2, true, 4, 4, 64, 1)
 #endif
 
 int x3_lds_bytes(int layer) {
-#define APNEAUQ_X3_LDS(L, CI, CO, K, S, WM, WN, LAST, LW, CK, WPC) \
+#define APNEAUQ_X3_LDS(L, CI, CO, K, S, WM, WN, LAST, LW, LWB, CK, WPC) \
   if (layer == L) return x3::lds_bytes(S, CO, CK);
   APNEAUQ_X3_LAYERS(APNEAUQ_X3_LDS)
 #undef APNEAUQ_X3_LDS
@@ -790,7 +802,7 @@ int x3_lds_bytes(int layer) {
 }
 
 int x3_tile_samples(int layer) {
-#define APNEAUQ_X3_TS(L, CI, CO, K, S, WM, WN, LAST, LW, CK, WPC) \
+#define APNEAUQ_X3_TS(L, CI, CO, K, S, WM, WN, LAST, LW, LWB, CK, WPC) \
   if (layer == L) return S;
   APNEAUQ_X3_LAYERS(APNEAUQ_X3_TS)
 #undef APNEAUQ_X3_TS
@@ -798,7 +810,7 @@ int x3_tile_samples(int layer) {
 }
 
 int x3_wg_per_cu(int layer) {
-#define APNEAUQ_X3_WPC(L, CI, CO, K, S, WM, WN, LAST, LW, CK, WPC) \
+#define APNEAUQ_X3_WPC(L, CI, CO, K, S, WM, WN, LAST, LW, LWB, CK, WPC) \
   if (layer == L) return WPC;
   APNEAUQ_X3_LAYERS(APNEAUQ_X3_WPC)
 #undef APNEAUQ_X3_WPC
@@ -807,8 +819,13 @@ int x3_wg_per_cu(int layer) {
 
 hipError_t x3_launch_layer(int layer, const x3::LayerArgs& A, int grid, hipStream_t stream) {
   using namespace x3;
-#define APNEAUQ_X3_LAUNCH(L, CI, CO, K, S, WM, WN, LAST, LW, CK, WPC) \
-  if (layer == L) return launch_layer<CI, CO, K, S, WM, WN, LAST, LW, CK, WPC>(A, grid, stream);
+  // the per-sample prescale variant only where it is used (moving statistics)
+  const bool ps = A.smax_in != nullptr || A.smax_out != nullptr;
+#define APNEAUQ_X3_LAUNCH(L, CI, CO, K, S, WM, WN, LAST, LW, LWB, CK, WPC)                                  \
+  if (layer == L) {                                                                                       \
+    return ps ? launch_layer<CI, CO, K, S, WM, WN, LAST, LW, CK, WPC, true>(A, grid, stream)               \
+              : launch_layer<CI, CO, K, S, WM, WN, LAST, LWB, CK, WPC, false>(A, grid, stream);            \
+  }
   APNEAUQ_X3_LAYERS(APNEAUQ_X3_LAUNCH)
 #undef APNEAUQ_X3_LAUNCH
   return hipErrorInvalidValue;

@@ -168,6 +168,23 @@ def _ops():
     return _ext.ops()
 
 
+# layers (x3_layer index 1..4 = blocks 2..5) whose epilogue draws its block's dropout mask and stores it in
+# the output's sign bit; the others store plain ReLU output and their consumer draws the mask while it
+# stages the input (which side has the slack differs per layer: profiles/x3_mask_side_r4.md).
+# APNEAUQ_X3_SIGN_MASK="2,3" overrides (A/B probes).
+_SIGN_DEFAULT = "2,4"
+
+
+def _sign_layers() -> frozenset:
+    v = os.environ.get("APNEAUQ_X3_SIGN_MASK", _SIGN_DEFAULT)
+    return frozenset(int(t) for t in v.replace(" ", "").split(",") if t)
+
+
+def _sign(l: int, sl: frozenset):
+    """(sign_in, sign_out) of x3_layer l."""
+    return (l - 1) in sl and l >= 2, l in sl and l <= 4
+
+
 def _dsc(rate: float) -> float:
     return 1.0 / (1.0 - rate) if rate < 1.0 else 0.0
 
@@ -236,6 +253,7 @@ def mcd_batch(model: X3Model, x: torch.Tensor, n_pass: int, seed: int, pass_base
     dsc = [_dsc(b.dropout) for b in spec.blocks]
     eps, mom = float(spec.bn_epsilon), float(spec.bn_momentum)
     seed = int(seed) & ((1 << 63) - 1)
+    sl = _sign_layers()
     out = torch.empty(n_pass, n, dtype=torch.float32, device=model.device)
     # block 1 once: no dropout precedes it, so every pass sees the same R_1 and the same moments
     ws.stats[0].zero_()
@@ -256,7 +274,7 @@ def mcd_batch(model: X3Model, x: torch.Tensor, n_pass: int, seed: int, pass_base
             dst = ws.sums if l == 5 else ws.buf[(l - 1) % 2]
             o.x3_layer(l, src, dst, model.wfrag[l], 0, model.bias[l], model.wscale[l], 0, ws.aff[l - 1],
                        0 if l == 1 else 2 * CH[l], st, n, tc, l == 1, thr[l - 1], thr[l], seed, pb,
-                       int(window_offset), int(grid), None, None, None, ws.gscale[l - 1])
+                       int(window_offset), int(grid), None, None, None, ws.gscale[l - 1], *_sign(l, sl))
             if sync is not None:
                 _sync_stats(sync, st, tc, c)
             g, b, mm, mv = model.bn[l]
@@ -289,6 +307,7 @@ def _mcd_batch_windowed(model: X3Model, x: torch.Tensor, n_pass: int, seed: int,
     dsc = [_dsc(b.dropout) for b in spec.blocks]
     eps, mom = float(spec.bn_epsilon), float(spec.bn_momentum)
     seed = int(seed) & ((1 << 63) - 1)
+    sl = _sign_layers()
     out = torch.empty(n_pass, n, dtype=torch.float32, device=model.device)
 
     def run(s: int, e: int, upto: int, pb: int, stats_layer: int) -> None:
@@ -300,7 +319,8 @@ def _mcd_batch_windowed(model: X3Model, x: torch.Tensor, n_pass: int, seed: int,
             dst = ws.sums if l == 5 else ws.buf[(l - 1) % 2]
             o.x3_layer(l, src, dst, model.wfrag[l], 0, model.bias[l], model.wscale[l], 0, ws.aff[l - 1],
                        0 if l == 1 else 2 * CH[l], ws.stats[l] if l == stats_layer else None, m, 1, l == 1,
-                       thr[l - 1], thr[l], seed, pb, int(window_offset) + s, 0, None, None, None, ws.gscale[l - 1])
+                       thr[l - 1], thr[l], seed, pb, int(window_offset) + s, 0, None, None, None, ws.gscale[l - 1],
+                       *_sign(l, sl))
 
     def finish_layer(l: int, repeat: int) -> None:
         if sync is not None:
@@ -366,6 +386,7 @@ def _forward_running(model: X3Model, x: torch.Tensor, n_pass: int, dropout: bool
     dsc = [_dsc(b.dropout) if dropout else 1.0 for b in spec.blocks]
     eps, mom = float(spec.bn_epsilon), float(spec.bn_momentum)
     seed = int(seed) & ((1 << 63) - 1)
+    sl = _sign_layers()
     # BN affine of the moving statistics, per member (shared by all passes with dropout)
     for l in range(6):
         g, b, mm, mv = model.bn[l]
@@ -381,7 +402,7 @@ def _forward_running(model: X3Model, x: torch.Tensor, n_pass: int, dropout: bool
         o.x3_layer(l, src, dst, model.wfrag[l], wstride, model.bias[l], model.wscale[l],
                    CH[l + 1] if per_member else 0, ws.aff[l - 1], 2 * CH[l] if per_member else 0, None, n, groups,
                    dropout and l == 1, thr[l - 1], thr[l], seed, int(pass_offset),
-                   int(window_offset), 0, ws.smax[l - 1], ws.amax[l - 1], sm)
+                   int(window_offset), 0, ws.smax[l - 1], ws.amax[l - 1], sm, None, *_sign(l, sl))
     o.x3_head(ws.sums, ws.aff[5], 2 * CH[6] if per_member else 0, model.dw, model.db, CH[6] if per_member else 0,
               ws.out, n, groups, bool(logits))
     return ws.out[: groups * n].view(G, n_pass, n).clone()
