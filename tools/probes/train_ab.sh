@@ -1,0 +1,14 @@
+#!/bin/bash
+# Interleaved bench.train_micro rounds (batch 8192 and 1024) of the library build and probe builds:
+#   tools/probes/train_ab.sh <rounds> so1 so2 ...
+set -o pipefail
+n=$1; shift
+export PYTHONPATH=$PWD
+for rep in $(seq 1 $n); do
+  for so in main "$@"; do
+    if [ $so = main ]; then unset APNEAUQ_SO_PATH; else export APNEAUQ_SO_PATH=$PWD/$so; fi
+    a=$(timeout -k 10 200 python3 -m bench.train_micro --batch 8192 --steps 30 2>/dev/null | tail -1) || exit 1
+    b=$(timeout -k 10 200 python3 -m bench.train_micro --batch 1024 --steps 100 2>/dev/null | tail -1) || exit 1
+    echo "$rep $(basename $so .so) b8192 $(echo $a | cut -d, -f3) | b1024 $(echo $b | cut -d, -f3)"
+  done
+done

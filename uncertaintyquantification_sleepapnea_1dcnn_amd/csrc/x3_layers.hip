@@ -199,6 +199,7 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
   const bool prescale = PS && A.smax_in != nullptr;
   int key_tile = -1;
   unsigned skeys[kS];
+  unsigned skey_tile = 0u;  // the tile's stream key (APNEAUQ_X3_UNIT_KEY: sample keys per staged unit)
   // prescale exponents sa of the staging tile's samples, one signed byte each (kS <= 4; one register)
   static_assert(kS <= 4, "packed per-sample exponents");
   unsigned sa_pack = 0u;
@@ -228,6 +229,7 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
     const int w0 = (tile - g * tpg) * kS;
     if (tile != key_tile) {  // workgroup-uniform
       const unsigned skey = stream_key(A.seed, A.layer - 1, A.pass_base + g);
+      skey_tile = skey;
       const float* am = A.amax_in + (A.aff_gstride ? 2 * g : 0);
       float ws0 = A.wscale[A.p_gstride ? g : 0];
       if (A.gscale_in != nullptr) ws0 *= A.gscale_in[A.aff_gstride ? g : 0];
@@ -255,9 +257,17 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
       const f32x4 v = R.v[u];
       bool keep[4];
       if (hash_in) {
-        unsigned k = skeys[0];
+#ifndef APNEAUQ_X3_UNIT_KEY
+#define APNEAUQ_X3_UNIT_KEY 0
+#endif
+        unsigned k;
+        if constexpr (APNEAUQ_X3_UNIT_KEY && !PS) {
+          k = sample_key(skey_tile, A.window_offset + w);
+        } else {
+          k = skeys[0];
 #pragma unroll
-        for (int j = 1; j < kS; ++j) k = s == j ? skeys[j] : k;
+          for (int j = 1; j < kS; ++j) k = s == j ? skeys[j] : k;
+        }
         const unsigned b01 = dropout_bits2(k, t, c * kCK + 4 * q);
         const unsigned b23 = dropout_bits2(k, t, c * kCK + 4 * q + 2);
         keep[0] = (b01 & 0xFFFFu) >= A.thr_in;
