@@ -199,7 +199,7 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
   const bool prescale = PS && A.smax_in != nullptr;
   int key_tile = -1;
   unsigned skeys[kS];
-  unsigned skey_tile = 0u;  // the tile's stream key (APNEAUQ_X3_UNIT_KEY: sample keys per staged unit)
+  unsigned skey_tile = 0u;  // the tile's stream key
   // prescale exponents sa of the staging tile's samples, one signed byte each (kS <= 4; one register)
   static_assert(kS <= 4, "packed per-sample exponents");
   unsigned sa_pack = 0u;
@@ -257,11 +257,10 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
       const f32x4 v = R.v[u];
       bool keep[4];
       if (hash_in) {
-#ifndef APNEAUQ_X3_UNIT_KEY
-#define APNEAUQ_X3_UNIT_KEY 0
-#endif
+        // the sample's key: recomputed per staged unit (batch moments: block 2 -4 % over a select from
+        // the tile's cached keys), or selected from the cache where the prescale needs its registers
         unsigned k;
-        if constexpr (APNEAUQ_X3_UNIT_KEY && !PS) {
+        if constexpr (!PS) {
           k = sample_key(skey_tile, A.window_offset + w);
         } else {
           k = skeys[0];
