@@ -1,0 +1,183 @@
+// Reductions of the layer-wise training step (train_conv.hip): the wgrad partial sums, the
+// deterministic-mode column sums and the BN finalize (moving averages, dgamma / dbeta).
+#include "train_args.h"
+
+namespace apneauq {
+namespace train {
+
+// dW, db = sum over the row groups of the wgrad partials in a fixed order: deterministic, and cheaper
+// than the ~K*Cin*Cout fp32 atomics per row group it replaces (25-35 us of a 70-80 us wgrad at batch
+// 1024, profiles/train_step_r2.md).  A workgroup covers 256/J float4 columns with J threads per column:
+// thread j sums row groups j, j + J, ... (8 loads in flight), then the J partials are added in j order
+// through LDS.  J > 1 when the row groups outnumber the columns' parallelism (block 1: 512 row groups
+// of 928 float4 columns took 26 us with one thread per column).
+__device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ part, int rgs, int kcc, int cout,
+                                                  float* __restrict__ gw, float* __restrict__ gb, int J,
+                                                  const TabBwd& tb, int bx, int nbx, bool side_block) {
+  __shared__ f32x4 red[256];
+  if (side_block) {  // the table's backward rows of the block the NEXT dgrad / wgrad read
+    const int c = threadIdx.x;
+    if (c < tb.cc) {
+      tb.mdy[c] = (float)(slot_sumd(tb.bst + c, 2 * tb.cc) * (double)tb.inv_count);
+      tb.mdyx[c] = (float)(slot_sumd(tb.bst + tb.cc + c, 2 * tb.cc) * (double)tb.inv_count);
+    }
+    return;
+  }
+  const int S = kcc + cout;  // a multiple of 4 (Cout is)
+  const int S4 = S >> 2;
+  const int ncol = 256 / J;
+  const int cl = threadIdx.x % ncol, j = threadIdx.x / ncol;
+  const f32x4* p4 = reinterpret_cast<const f32x4*>(part);
+  for (int base = bx * ncol; base < S4; base += nbx * ncol) {  // workgroup-uniform
+    const int e4 = base + cl;
+    f32x4 acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (e4 < S4) {
+      int r = j;
+      for (; r + 7 * J < rgs; r += 8 * J) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] += p4[(long long)(r + q * J) * S4 + e4];
+      }
+      for (int q = 0; r < rgs; r += J, ++q) acc[q] += p4[(long long)r * S4 + e4];
+    }
+    red[threadIdx.x] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    __syncthreads();
+    if (j == 0 && e4 < S4) {
+      f32x4 s = red[cl];
+      for (int q = 1; q < J; ++q) s += red[q * ncol + cl];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = 4 * e4 + i;
+        if (e < kcc)
+          gw[e] = s[i];
+        else
+          gb[e - kcc] = s[i];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int rgs, int kcc, int cout,
+                                                           float* __restrict__ gw, float* __restrict__ gb, int J,
+                                                           TabBwd tb) {
+  if (blockIdx.y == 1 && blockIdx.x != 0) return;
+  wgrad_reduce_body(part, rgs, kcc, cout, gw, gb, J, tb, blockIdx.x, gridDim.x, blockIdx.y == 1);
+}
+
+// member-batched: the member's partial slots (written by its wgrad on its XCDs), gradients and table
+// rows from its Args; with the table the last x-block of each member does the side job
+__global__ __launch_bounds__(256) void wgrad_reduce_mb_kernel(const Args* __restrict__ Am, int l, int rgs, int kcc,
+                                                              int cout, int J, int side) {
+  const MbPos pos = mb_pos<true>();
+  const Args& A = Am[pos.member];
+  TabBwd tb = {};
+  if (side) {
+    tb.bst = A.L[l - 1].bst;
+    tb.cc = C[l];
+    tb.mdy = A.tab + ((l - 1) * kTabRows + kTabMdy) * 256;
+    tb.mdyx = A.tab + ((l - 1) * kTabRows + kTabMdyx) * 256;
+    tb.inv_count = A.inv_count;
+  }
+  const int nbx = gridDim.x - (side ? 1 : 0);
+  wgrad_reduce_body(A.wpart, rgs, kcc, cout, A.L[l].gw, A.L[l].gb, J, tb, pos.bx, nbx, side && pos.bx == nbx);
+}
+
+// ------------------------------------------------------------------------------------------------
+// BN finalize: moving averages (Keras momentum update on batch moments) and dgamma / dbeta.
+// ------------------------------------------------------------------------------------------------
+// Deterministic mode: column sums of an (n, w) row-major fp32 partial table in a fixed order (fp64
+// accumulation), scattered to up to four destination segments (consecutive column ranges; fp64 or
+// fp32 stores).  One thread per column; the rows are read coalesced across threads.
+
+__device__ __forceinline__ void det_reduce_col(const float* __restrict__ part, int n, int w, const DetDst& d, int c) {
+  double acc = 0.0;
+  int i = 0;
+  for (; i + 4 <= n; i += 4) {  // fixed association: ((r0 + r1) + (r2 + r3)) per group of four rows
+    const double a = (double)part[(long long)i * w + c] + (double)part[(long long)(i + 1) * w + c];
+    const double b = (double)part[(long long)(i + 2) * w + c] + (double)part[(long long)(i + 3) * w + c];
+    acc += a + b;
+  }
+  for (; i < n; ++i) acc += (double)part[(long long)i * w + c];
+  int k = c;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (k < d.seg[q].cols) {
+      if (d.seg[q].f64)
+        reinterpret_cast<double*>(d.seg[q].ptr)[k] = acc;
+      else
+        reinterpret_cast<float*>(d.seg[q].ptr)[k] = (float)acc;
+      return;
+    }
+    k -= d.seg[q].cols;
+  }
+}
+
+__global__ __launch_bounds__(256) void det_reduce_kernel(const float* __restrict__ part, int n, int w, DetDst d) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < w) det_reduce_col(part, n, w, d, c);
+}
+
+// member-batched: member blockIdx.z's partial table and destinations (from its Args) of the reduce that
+// follows op 0 (forward of layer l: the moments of block l), 1 (head: loss, dense grads, block-6
+// backward sums) or 2 (dgrad of layer l: backward sums of block l - 1); same association as the
+// single-model det_reduce_kernel, so member-batched deterministic steps equal single-model ones bitwise
+__global__ __launch_bounds__(256) void det_reduce_mb_kernel(const Args* __restrict__ Am, int op, int l, int n, int w) {
+  const Args& A = Am[blockIdx.z];
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= w) return;
+  DetDst d = {};
+  if (op == 0) {
+    d.seg[0] = {A.L[l].st, w, 1};
+  } else if (op == 1) {
+    d.seg[0] = {A.loss_sum, 1, 0};
+    d.seg[1] = {A.g_dense_b, 1, 0};
+    d.seg[2] = {A.g_dense_w, C[6], 0};
+    d.seg[3] = {A.L[5].bst, 2 * C[6], 1};
+  } else {
+    d.seg[0] = {A.L[l - 1].bst, w, 1};
+  }
+  det_reduce_col(A.det, n, w, d, c);
+}
+
+template <bool MB>
+__global__ void bn_finalize_kernel(Args A_, const Args* __restrict__ Am, int update_moving, int grads) {
+  const MbPos pos = mb_pos<MB>();
+  const Args& A = member_args<MB>(A_, Am, pos);
+  const int l = pos.bx;
+  const Layer& Ly = A.L[l];
+  const int Cc = (l == 0) ? C[1] : (l == 1) ? C[2] : (l == 2) ? C[3] : (l == 3) ? C[4] : (l == 4) ? C[5] : C[6];
+  for (int c = threadIdx.x; c < Cc; c += blockDim.x) {
+    if (update_moving) {
+      for (int g = 0; g < A.groups; ++g) {  // one Keras call (= one moving update) per group
+        float mu, var;
+        bn_moments(A, l, g, c, mu, var);
+        Ly.mmean[c] = Ly.mmean[c] * A.momentum + mu * (1.f - A.momentum);
+        Ly.mvar[c] = Ly.mvar[c] * A.momentum + var * (1.f - A.momentum);
+      }
+    }
+    if (grads) {
+      Ly.gbeta[c] = (float)slot_sumd(Ly.bst + c, 2 * Cc);
+      Ly.ggamma[c] = (float)slot_sumd(Ly.bst + Cc + c, 2 * Cc);
+    }
+  }
+  if (grads && l == 5 && A.hpart != nullptr) {  // the head's slotted sums, in slot order
+    for (int c = threadIdx.x; c < Cc + 2; c += blockDim.x) {
+      float v = 0.f;
+      for (int sl = 0; sl < kStatSlots; ++sl) v += A.hpart[sl * (Cc + 2) + c];
+      if (c < Cc)
+        A.g_dense_w[c] = v;
+      else if (c == Cc)
+        *A.loss_sum = v;
+      else
+        *A.g_dense_b = v;
+    }
+  }
+}
+
+template __global__ void bn_finalize_kernel<false>(Args, const Args* __restrict__, int, int);
+template __global__ void bn_finalize_kernel<true>(Args, const Args* __restrict__, int, int);
+
+}  // namespace train
+}  // namespace apneauq
