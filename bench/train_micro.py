@@ -15,10 +15,11 @@ def main():
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--backend", default="hip")
+    ap.add_argument("--precision", default="bf16", help="train_precision (fp32: the fp32 kernels, backend auto)")
     a = ap.parse_args()
     import os
-    os.environ["APNEAUQ_TRAIN_BACKEND"] = a.backend
-    m = AlarconCNN1D(seed=1, device="cuda")
+    os.environ["APNEAUQ_TRAIN_BACKEND"] = "auto" if a.precision == "fp32" else a.backend
+    m = AlarconCNN1D(seed=1, device="cuda", train_precision=a.precision)
     g = torch.Generator().manual_seed(0)
     x = torch.randn(a.batch, 60, 4, generator=g).cuda()
     y = (torch.rand(a.batch, generator=g) > 0.5).float().cuda()
@@ -30,7 +31,7 @@ def main():
         m.train_step(x, y, return_probs=True)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t) / a.steps
-    print(json.dumps({"backend": a.backend, "batch": a.batch, "ms_per_step": dt * 1e3, "windows_per_s": a.batch / dt,
+    print(json.dumps({"backend": a.backend, "precision": a.precision, "batch": a.batch, "ms_per_step": dt * 1e3, "windows_per_s": a.batch / dt,
                       "tflops_eff": 3 * 2 * 50.9e6 * a.batch / dt / 1e12}))
 
 

@@ -11,7 +11,7 @@
 //                      A = the Keras kernel read in place (forward: W[tap][ci][co]; dgrad: the flipped,
 //                      transposed W[K-1-tap][co][ci]), B = input rows (zero-padded row layout); a
 //                      workgroup is 2 x 2 waves over 128 rows x 128 channels, each wave 4 x 4 tiles of
-//                      16 x 16; operands of k-step s + 1 are loaded while step s's 16 MFMAs run.
+//                      16 x 16; B staged through LDS per (tap, 32-channel) chunk, A one k-step ahead.
 //                      Epilogue: kTrain = relu(acc + bias) + BN moment slots (deterministic mode: one
 //                      slot per (workgroup, wave row), plain stores), kLinear = acc (dgrad).
 //   wgrad_kernel       dW[tap][ci][co] = sum_r Xpad[r + tap][ci] dZpad[r][co] over a row group; every
@@ -42,8 +42,18 @@ struct ConvArgs {
   int n, L, cin, cout, ksize, in_rs, in_off, flip, det;
 };
 
+// The B operand streams through LDS in chunks of one tap x kCK input channels for the tile's 128 rows
+// (each lane of the staging loads reads kCK / 4 consecutive channels of one input row: whole 128-B
+// lines instead of the 64 rows-apart single floats of a direct fragment load), double-buffered with
+// one barrier per chunk; row stride kBS floats: the fragment read (16 rows x 4 k) hits 16 distinct
+// 4-bank groups.  The A operand (the Keras kernel's [kCK][128 co] block of the chunk) is staged beside
+// it (row stride kAS = 16 mod 64 floats: conflict-free fragment reads); a direct fragment load from
+// L2 one k-step ahead left the MFMAs waiting on its latency (26 % of the f32 peak).
+constexpr int kCK = 32, kBS = 36, kAS = 144;
 template <int MODE>
-__global__ __launch_bounds__(256) void conv_kernel(ConvArgs A) {
+__global__ __launch_bounds__(256, 2) void conv_kernel(ConvArgs A) {
+  __shared__ float bs[2][128 * kBS];
+  __shared__ float as[2][kCK * kAS];  // A chunk [k][co] of the workgroup's 128 output channels
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int m = lane & 15, h = lane >> 4;
   const int wr = wave >> 1, wc = wave & 1;
@@ -51,9 +61,8 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs A) {
   const long long row_base = (long long)blockIdx.x * 128 + wr * 64;
   const int ct0 = (blockIdx.y * 2 + wc) * kCT;  // first 16-channel tile of this wave
   const int nct = (A.cout + 15) / 16;
-  if (ct0 >= nct) return;  // wave-uniform; no barriers in this kernel
+  const bool active = ct0 < nct;  // wave-uniform (inactive waves still stage and pass the barriers)
   const int pad = (A.ksize - 1) / 2;
-  const int K = A.ksize * A.cin;
 
   int rn[kRT], rt[kRT];
   bool rok[kRT];
@@ -64,36 +73,46 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs A) {
     rn[r] = rok[r] ? (int)(row / A.L) : 0;
     rt[r] = rok[r] ? (int)(row - (long long)rn[r] * A.L) : 0;
   }
-  // A operand rows (output channels) of this lane per channel tile
-  int co[kCT];
+  // staging: thread i owns tile row i / 2 and channels (i % 2) * 16 .. +15 of every chunk
+  const int srow = threadIdx.x >> 1, sc0 = (threadIdx.x & 1) * 16;
+  const long long sgrow = (long long)blockIdx.x * 128 + srow;
+  const bool s_ok = sgrow < rows;
+  const int s_n = s_ok ? (int)(sgrow / A.L) : 0;
+  const int s_t = s_ok ? (int)(sgrow - (long long)s_n * A.L) : 0;
+  const int ncc = (A.cin + kCK - 1) / kCK;
+  const int nchunk = A.ksize * ncc;
+  float sv[16], sw[16];
+  const int cob = blockIdx.y * 128;  // the workgroup's first output channel
+  auto load_chunk = [&](int ch) {
+    const int tp = ch / ncc, ccb = (ch - tp * ncc) * kCK, cc0 = ccb + sc0;
+    const int ts = s_t + tp - pad;
+    const bool ok = s_ok && ts >= 0 && ts < A.L;
+    const float* src = A.x + ((long long)s_n * A.in_rs + A.in_off + ts) * A.cin;
 #pragma unroll
-  for (int c = 0; c < kCT; ++c) co[c] = (ct0 + c) * 16 + m;
-
-  // this lane's k = 4 s + h as (tap, ci), advanced incrementally
-  int tap = h / A.cin, ci = h - (h / A.cin) * A.cin;
-  auto load = [&](int kk, int tp, int cc, float (&a)[kCT], float (&b)[kRT]) {
-    const bool kok = kk < K;
+    for (int j = 0; j < 16; ++j) sv[j] = (ok && cc0 + j < A.cin) ? src[cc0 + j] : 0.f;
+    // A chunk: element i = (kk, c) of [kCK][128]; forward kernel W[tap][ci][co] is co-contiguous
+    // (c fastest), the dgrad kernel W[K-1-tap][co][ci] ci-contiguous (kk fastest)
 #pragma unroll
-    for (int c = 0; c < kCT; ++c) {
+    for (int j = 0; j < 16; ++j) {
+      const int i = threadIdx.x + 256 * j;
+      const int kk = A.flip ? (i & (kCK - 1)) : (i >> 7), c = A.flip ? (i >> 5) : (i & 127);
+      const int cc = ccb + kk, o = cob + c;
       float v = 0.f;
-      if (kok && co[c] < A.cout)
-        v = A.flip ? A.w[((long long)(A.ksize - 1 - tp) * A.cout + co[c]) * A.cin + cc]
-                   : A.w[((long long)tp * A.cin + cc) * A.cout + co[c]];
-      a[c] = v;
-    }
-#pragma unroll
-    for (int r = 0; r < kRT; ++r) {
-      const int ts = rt[r] + tp - pad;
-      b[r] = (kok && rok[r] && ts >= 0 && ts < A.L)
-                 ? A.x[((long long)rn[r] * A.in_rs + A.in_off + ts) * A.cin + cc]
-                 : 0.f;
+      if (cc < A.cin && o < A.cout)
+        v = A.flip ? A.w[((long long)(A.ksize - 1 - tp) * A.cout + o) * A.cin + cc]
+                   : A.w[((long long)tp * A.cin + cc) * A.cout + o];
+      sw[j] = v;
     }
   };
-  auto advance = [&](int& tp, int& cc) {
-    cc += 4;
-    while (cc >= A.cin) {
-      cc -= A.cin;
-      ++tp;
+  auto store_chunk = [&](int buf) {
+    float* d = &bs[buf][srow * kBS + sc0];
+#pragma unroll
+    for (int j = 0; j < 16; j += 4) *reinterpret_cast<f32x4*>(d + j) = f32x4{sv[j], sv[j + 1], sv[j + 2], sv[j + 3]};
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int i = threadIdx.x + 256 * j;
+      const int kk = A.flip ? (i & (kCK - 1)) : (i >> 7), c = A.flip ? (i >> 5) : (i & 127);
+      as[buf][kk * kAS + c] = sw[j];
     }
   };
 
@@ -102,22 +121,40 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs A) {
   for (int c = 0; c < kCT; ++c)
 #pragma unroll
     for (int r = 0; r < kRT; ++r) acc[c][r] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nstep = (K + 3) / 4;
-  float a0[kCT], b0[kRT], a1[kCT], b1[kRT];
-  load(h, tap, ci, a0, b0);
-  advance(tap, ci);
-  for (int s = 0; s < nstep; ++s) {
-    load(4 * (s + 1) + h, tap, ci, a1, b1);  // next k-step in flight under this step's MFMAs
-    advance(tap, ci);
+  load_chunk(0);
+  store_chunk(0);
+  if (nchunk > 1) load_chunk(1);
+  __syncthreads();
+  const int brow = wr * 64 + m;  // this lane's B rows: brow + 16 r
+  const int acol = wc * 64 + m;  // this lane's A columns (output channels): acol + 16 c
+  for (int ch = 0; ch < nchunk; ++ch) {
+    const float* b = bs[ch & 1];
+    const float* a = as[ch & 1];
+    // k-steps of this chunk: its channels (cin < kCK: the first layers) in groups of 4
+    const int ccb = (ch % ncc) * kCK;
+    const int nq = (min(kCK, A.cin - ccb) + 3) / 4;
+    if (active) {
 #pragma unroll
-    for (int c = 0; c < kCT; ++c)
+      for (int q = 0; q < kCK / 4; ++q) {
+        if (q >= nq) break;  // uniform
+        float aq[kCT], bq[kRT];
 #pragma unroll
-      for (int r = 0; r < kRT; ++r) acc[c][r] = mfma4(a0[c], b0[r], acc[c][r]);
+        for (int c = 0; c < kCT; ++c) aq[c] = a[(4 * q + h) * kAS + acol + 16 * c];
 #pragma unroll
-    for (int c = 0; c < kCT; ++c) a0[c] = a1[c];
+        for (int r = 0; r < kRT; ++r) bq[r] = b[(brow + 16 * r) * kBS + 4 * q + h];
 #pragma unroll
-    for (int r = 0; r < kRT; ++r) b0[r] = b1[r];
+        for (int c = 0; c < kCT; ++c)
+#pragma unroll
+          for (int r = 0; r < kRT; ++r) acc[c][r] = mfma4(aq[c], bq[r], acc[c][r]);
+      }
+    }
+    // chunk ch + 1 (loaded one chunk ago) into the other buffer, whose readers (chunk ch - 1) passed
+    // the previous barrier; then chunk ch + 2's loads go out under the next chunk's MFMAs
+    if (ch + 1 < nchunk) store_chunk((ch + 1) & 1);
+    __syncthreads();
+    if (ch + 2 < nchunk) load_chunk(ch + 2);
   }
+  if (!active) return;
 
   // epilogue: lane holds channels co0 .. co0+3 (= 16 ct + 4 h + e) of row (rn[r], rt[r])
   float* st = nullptr;
@@ -176,43 +213,68 @@ struct WgArgs {
   int cin, cout, k, rows_per_group;
 };
 
-// workgroup = one 16-ci tile x 4 waves of 16-co tiles x one row group; a wave holds every tap's tile
+// workgroup = 32 ci (2 tiles) x 64 co (4 waves, one 16-co tile each) x one row group; a wave holds every
+// tap's 2 tiles in registers.  The row group streams through LDS in chunks of kWgRC rows (X with its
+// k - 1 halo rows, dZ), so each operand float is read from global memory once per workgroup and from
+// LDS by the MFMAs (one ds_read_b32 per v_mfma_f32_16x16x4_f32); row strides 48 / 80 floats put the
+// 4 row groups of a fragment read on disjoint bank quarters.
+// K (taps) is a template parameter: the accumulators of every tap stay in registers (a runtime tap
+// count indexed them through scratch memory).
+constexpr int kWgRC = 64, kWgKMax = 15, kWgXS = 48, kWgDS = 80;
+template <int K>
 __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs A) {
+  __shared__ float xs[(kWgRC + kWgKMax - 1) * kWgXS];
+  __shared__ float ds[kWgRC * kWgDS];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int m = lane & 15, h = lane >> 4;
-  const int ci0 = blockIdx.x * 16, co0 = (blockIdx.y * 4 + wave) * 16;
+  const int ci0 = blockIdx.x * 32, cog = blockIdx.y * 64;
   const int rg = blockIdx.z;
-  if (co0 >= A.cout) return;  // wave-uniform
   const long long r_begin = (long long)rg * A.rows_per_group;
   const long long r_end = r_begin + A.rows_per_group < A.R ? r_begin + A.rows_per_group : A.R;
-  constexpr int KMAX = 15;
-  f32x4 acc[KMAX];
+  const long long x_rows = A.R + A.k - 1;
+  f32x4 acc[K][2];
 #pragma unroll
-  for (int t = 0; t < KMAX; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bool aok = ci0 + m < A.cin, bok = co0 + m < A.cout;
-  // D[i = ci][j = co]: A[i][k] = X[r + k + tap][ci0 + i], B[k][j] = dZ[r + k][co0 + j], k = h
-  for (long long r = r_begin; r < r_end; r += 4) {
-    const long long rr = r + h;
-    const bool rok = rr < r_end;
-    const float b = (rok && bok) ? A.dz[rr * A.cout + co0 + m] : 0.f;
+  for (int t = 0; t < K; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int xr = kWgRC + K - 1;
+  for (long long r0 = r_begin; r0 < r_end; r0 += kWgRC) {  // workgroup-uniform
+    __syncthreads();
+    for (int i = threadIdx.x; i < xr * 32; i += 256) {
+      const int rr = i >> 5, c = i & 31;
+      const long long row = r0 + rr;
+      xs[rr * kWgXS + c] = (row < x_rows && row < r_end + K - 1 && ci0 + c < A.cin) ? A.x[row * A.cin + ci0 + c] : 0.f;
+    }
+    for (int i = threadIdx.x; i < kWgRC * 64; i += 256) {
+      const int rr = i >> 6, c = i & 63;
+      const long long row = r0 + rr;
+      ds[rr * kWgDS + c] = (row < r_end && cog + c < A.cout) ? A.dz[row * A.cout + cog + c] : 0.f;
+    }
+    __syncthreads();
+    if (cog + wave * 16 >= A.cout) continue;  // wave-uniform (the barriers above are shared)
+#pragma unroll 4
+    for (int kk = 0; kk < kWgRC / 4; ++kk) {
+      const int rb = 4 * kk + h;
+      const float b = ds[rb * kWgDS + wave * 16 + m];
 #pragma unroll
-    for (int t = 0; t < KMAX; ++t) {
-      if (t < A.k) {  // uniform
-        const float a = (rok && aok) ? A.x[(rr + t) * A.cin + ci0 + m] : 0.f;
-        acc[t] = mfma4(a, b, acc[t]);
+      for (int t = 0; t < K; ++t) {
+        const float a0 = xs[(rb + t) * kWgXS + m], a1 = xs[(rb + t) * kWgXS + 16 + m];
+        acc[t][0] = mfma4(a0, b, acc[t][0]);
+        acc[t][1] = mfma4(a1, b, acc[t][1]);
       }
     }
   }
   // D layout: lane holds rows i = 4 h + e (ci), column j = m (co)
-  float* p = A.part + (long long)rg * A.k * A.cin * A.cout;
+  const int co = cog + wave * 16 + m;
+  if (co >= A.cout) return;
+  float* p = A.part + (long long)rg * K * A.cin * A.cout;
 #pragma unroll
-  for (int t = 0; t < KMAX; ++t) {
-    if (t >= A.k) break;
+  for (int t = 0; t < K; ++t) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int ci = ci0 + 4 * h + e, co = co0 + m;
-      if (ci < A.cin && co < A.cout) p[((long long)t * A.cin + ci) * A.cout + co] = acc[t][e];
-    }
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int ci = ci0 + ct * 16 + 4 * h + e;
+        if (ci < A.cin) p[((long long)t * A.cin + ci) * A.cout + co] = acc[t][ct][e];
+      }
   }
 }
 
@@ -240,18 +302,27 @@ hipError_t launch_gf32_wgrad(const float* x, const float* dz, long long R, int c
   if (k < 1 || k > 15) return hipErrorInvalidValue;
   const long long wfl = (long long)k * cin * cout;
   long long groups = part_floats / wfl;
-  const long long ci_t = (cin + 15) / 16, co_g = (cout + 63) / 64;
-  // ~2 workgroups per CU in total, at least 256 rows per group
-  long long want = (512 + ci_t * co_g - 1) / (ci_t * co_g);
+  const long long ci_t = (cin + 31) / 32, co_g = (cout + 63) / 64;
+  // ~3 workgroups per CU in total, at least 256 rows per group
+  long long want = (768 + ci_t * co_g - 1) / (ci_t * co_g);
   if (want > (R + 255) / 256) want = (R + 255) / 256;
   if (groups > want) groups = want;
   if (groups > 65535) groups = 65535;
   if (groups < 1) return hipErrorInvalidValue;
   long long rpg = (R + groups - 1) / groups;
-  rpg = (rpg + 3) / 4 * 4;
+  rpg = (rpg + gf32::kWgRC - 1) / gf32::kWgRC * gf32::kWgRC;  // whole LDS row chunks
   groups = (R + rpg - 1) / rpg;
   gf32::WgArgs A{x, dz, part, R, cin, cout, k, (int)rpg};
-  hipLaunchKernelGGL(gf32::wgrad_kernel, dim3((unsigned)ci_t, (unsigned)co_g, (unsigned)groups), dim3(256), 0, st, A);
+  const dim3 grid((unsigned)ci_t, (unsigned)co_g, (unsigned)groups);
+  switch (k) {
+#define APNEAUQ_GF32_WG(KK) \
+  case KK: hipLaunchKernelGGL(gf32::wgrad_kernel<KK>, grid, dim3(256), 0, st, A); break;
+    APNEAUQ_GF32_WG(1) APNEAUQ_GF32_WG(2) APNEAUQ_GF32_WG(3) APNEAUQ_GF32_WG(4) APNEAUQ_GF32_WG(5)
+    APNEAUQ_GF32_WG(6) APNEAUQ_GF32_WG(7) APNEAUQ_GF32_WG(8) APNEAUQ_GF32_WG(9) APNEAUQ_GF32_WG(10)
+    APNEAUQ_GF32_WG(11) APNEAUQ_GF32_WG(12) APNEAUQ_GF32_WG(13) APNEAUQ_GF32_WG(14) APNEAUQ_GF32_WG(15)
+#undef APNEAUQ_GF32_WG
+    default: return hipErrorInvalidValue;
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return launch_ordered_sum(part, (int)groups, wfl, gw, st);
