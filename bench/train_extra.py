@@ -67,13 +67,15 @@ def measure(dev, seed: int = 2025, steps: int = 50, warmup: int = 5, members: in
     xs = [x[(i % 8) * batch:(i % 8 + 1) * batch] for i in range(members)]
     ys = [y[(i % 8) * batch:(i % 8 + 1) * batch] for i in range(members)]
 
+    for s_ in streams:  # the inputs were written on the default stream
+        s_.wait_stream(cur)
+
     def ens_step():
+        # each group's steps are ordered on its own stream; the groups are independent models, so (as in
+        # training/trainer.py:_fit_batched) nothing joins them between steps (_timeit synchronizes the device)
         for p, st, s_ in zip(parts, ens, streams):
-            s_.wait_stream(cur)
             with torch.cuda.stream(s_):
                 st([xs[i] for i in p], [ys[i] for i in p])
-        for s_ in streams:
-            cur.wait_stream(s_)
 
     t = _timeit(torch, ens_step, steps, warmup)
     out["members8_b1024"] = {"members": members, "groups": ng, "batch_per_member": batch,

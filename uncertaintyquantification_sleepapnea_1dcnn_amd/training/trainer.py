@@ -145,7 +145,7 @@ def _fit_batched(models: List, x, y, per_cbs, **fit_kwargs) -> List[History]:
     (``external_step``); each round the live members of one batch size are split into up to
     ``APNEAUQ_ENSEMBLE_GROUPS`` (default 4) groups, each run as one GraphedEnsembleStep replayed on its
     own HIP stream (the groups' latency-bound phases overlap: 8 members 1.67 M -> 1.80 M windows/s with
-    4 groups of 2)."""
+    4 groups of 2).  A group's steps, gathers and metric updates all run on its stream: no joins."""
     import os
 
     from ..ops import train_ops
@@ -162,6 +162,11 @@ def _fit_batched(models: List, x, y, per_cbs, **fit_kwargs) -> List[History]:
             hist[i] = stop.value
     steps = {}
     streams: List = []
+    # every member's step, its next batch's gather and its metric updates run on its group's stream, so
+    # the groups are never joined between steps; a member whose group (stream) changes -- regrouping
+    # after an early stop, the tail batch -- first waits for the stream that ran its previous step
+    home = torch.cuda.current_stream(dev)
+    last = {i: home for i in range(len(models))}
     while req:
         live = sorted(req)
         by_n = {}
@@ -181,26 +186,29 @@ def _fit_batched(models: List, x, y, per_cbs, **fit_kwargs) -> List[History]:
             subs = [ids[g::ng] for g in range(ng)]
             while len(streams) < ng:
                 streams.append(torch.cuda.Stream(device=dev))
-            cur = torch.cuda.current_stream(dev)
-            outs = {}
             for sub, s_ in zip(subs, streams):
                 ms = [models[i] for i in sub]
                 key = (tuple(sub), n)
                 st = steps.get(key)
                 if st is None or not st.valid_for(ms):
                     st = steps[key] = train_ops.GraphedEnsembleStep(ms, n)
-                s_.wait_stream(cur)  # the batches were gathered on the current stream
+                for prev in {id(last[i]): last[i] for i in sub if last[i] is not s_}.values():
+                    s_.wait_stream(prev)
+                for i in sub:
+                    if last[i] is not s_:  # a batch allocated on another stream, read on this one
+                        req[i][0].record_stream(s_)
+                        req[i][1].record_stream(s_)
                 with torch.cuda.stream(s_):
-                    for i, res in zip(sub, st([req[i][0] for i in sub], [req[i][1] for i in sub])):
-                        outs[i] = res
-            for s_ in streams[:ng]:
-                cur.wait_stream(s_)  # the generators' metric updates read the step outputs
-            for i in ids:
-                try:
-                    req[i] = gens[i].send(outs[i])
-                except StopIteration as stop:
-                    hist[i] = stop.value
-                    del req[i]
+                    outs = st([req[i][0] for i in sub], [req[i][1] for i in sub])
+                    for i, res in zip(sub, outs):
+                        last[i] = s_
+                        try:
+                            req[i] = gens[i].send(res)
+                        except StopIteration as stop:
+                            hist[i] = stop.value
+                            del req[i]
+    for s_ in streams:
+        home.wait_stream(s_)
     return hist
 
 
