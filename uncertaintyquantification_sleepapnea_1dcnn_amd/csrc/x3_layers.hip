@@ -787,8 +787,10 @@ hipError_t launch_layer(const LayerArgs& A, int grid, hipStream_t stream) {
 // profiles/x3_loader_waves.md) on every layer but block 2, whose 96-accumulator tile needs the 256-VGPR
 // budget of 8 waves (loaders at 2-sample tiles: slower; at 4: 99 VGPRs spilled); its staging runs on
 // MFMA waves 0..3, or on all 8 where the per-sample prescale's registers would otherwise spill.  64-channel chunks for
-// blocks 3 and 6 (block 2 would spill; Cin 224 / 96 are not multiples of 64).  Measurements:
-// profiles/x3_epilogue_ab_r3.md.
+// blocks 3 and 6 (block 2 would spill; Cin 224 / 96 are not multiples of 64).  The Cout-96 blocks 4 and
+// 6 run 4 MFMA waves of 24 accumulator tiles (WM 2 x WN 2) rather than 8 of 12: each weight fragment
+// is re-read by 2 wave rows instead of 4 (their texture path was the busy one), -1.2 % MCD.
+// Measurements: profiles/x3_epilogue_ab_r3.md, profiles/x3_mask_side_r4.md.
 // A/B builds may substitute another table (-DAPNEAUQ_X3_TABLE='"path.h"', tools/probes/x3_tables/):
 // every entry is a complete, correct configuration, only the speed differs.
 #ifdef APNEAUQ_X3_TABLE
@@ -797,9 +799,9 @@ hipError_t launch_layer(const LayerArgs& A, int grid, hipStream_t stream) {
 #define APNEAUQ_X3_LAYERS(X)                     \
   X(1, 128, 192, 5, 4, 2, 4, false, -8, 0, 32, 1) \
   X(2, 192, 224, 3, 2, 1, 7, false, 4, 4, 64, 1) \
-  X(3, 224, 96, 7, 4, 4, 2, false, 4, 4, 32, 1)  \
+  X(3, 224, 96, 7, 4, 2, 2, false, 4, 4, 32, 1)  \
   X(4, 96, 256, 9, 2, 1, 8, false, 4, 4, 32, 1)  \
-  X(5, 256, 96, 9, 4, 4, 2, true, 4, 4, 64, 1)
+  X(5, 256, 96, 9, 4, 2, 2, true, 4, 4, 64, 1)
 #endif
 
 int x3_lds_bytes(int layer) {
