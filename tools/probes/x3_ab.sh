@@ -11,8 +11,6 @@ for r in $(seq 1 $rounds); do
     echo "== $so round $r"
     if [ "$so" = "default" ]; then
       timeout -k 10 200 python3 bench/x3_micro.py "$@"
-    elif [ "$so" = "noprescale" ]; then
-      APNEAUQ_X3_PRESCALE=0 timeout -k 10 200 python3 bench/x3_micro.py "$@"
     elif [ "${so#env:}" != "$so" ]; then
       env "${so#env:}" timeout -k 10 200 python3 bench/x3_micro.py "$@"
     elif [ "${so#tree:}" != "$so" ]; then

@@ -10,7 +10,6 @@ for so in "$@"; do
   T=$R  # "tree:<dir>" = another whole checkout (e.g. probes_src/r3), its own package and bench
   E=()  # "env:VAR=VALUE" = the library build under that environment variable
   if [ "$so" = "default" ]; then unset APNEAUQ_SO_PATH
-  elif [ "$so" = "noprescale" ]; then unset APNEAUQ_SO_PATH; E=(APNEAUQ_X3_PRESCALE=0)
   elif [ "${so#env:}" != "$so" ]; then unset APNEAUQ_SO_PATH; E=("${so#env:}")
   elif [ "${so#tree:}" != "$so" ]; then unset APNEAUQ_SO_PATH; T=$R/${so#tree:}
   else export APNEAUQ_SO_PATH=$R/$so; fi

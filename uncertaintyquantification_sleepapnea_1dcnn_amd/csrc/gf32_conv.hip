@@ -25,7 +25,7 @@ hipError_t launch_ordered_sum(const float* part, int nrows, long long ncols, flo
 
 namespace gf32 {
 
-constexpr int kRT = 4, kCT = 4;  // per wave: 4 row tiles x 4 channel tiles
+constexpr int kRT = 4;  // per wave: 4 row tiles x CT channel tiles (conv_kernel template)
 constexpr int kStatSlots = 16;   // atomic-mode moment slots (== generic::kStatSlots)
 enum { kTrain = 1, kLinear = 2 };
 
@@ -49,11 +49,16 @@ struct ConvArgs {
 // 4-bank groups.  The A operand (the Keras kernel's [kCK][128 co] block of the chunk) is staged beside
 // it (row stride kAS = 16 mod 64 floats: conflict-free fragment reads); a direct fragment load from
 // L2 one k-step ahead left the MFMAs waiting on its latency (26 % of the f32 peak).
-constexpr int kCK = 32, kBS = 36, kAS = 144;
-template <int MODE>
+// CT = 16-channel tiles per wave (a workgroup covers 32 CT output channels): 3 where Cout is a multiple
+// of 96 (the Cout-96 / 192 blocks padded to 128 / 256 channels computed 25 % zeros), else 4.
+constexpr int kCK = 32, kBS = 36;
+template <int MODE, int CT>
 __global__ __launch_bounds__(256, 2) void conv_kernel(ConvArgs A) {
+  constexpr int kCT = CT, AW = 32 * CT;       // the workgroup's output channels
+  constexpr int kAS = (AW + 47) / 64 * 64 + 16;  // >= AW, 16 mod 64
+  constexpr int kAU = kCK * AW / 256;           // A-chunk elements staged per thread
   __shared__ float bs[2][128 * kBS];
-  __shared__ float as[2][kCK * kAS];  // A chunk [k][co] of the workgroup's 128 output channels
+  __shared__ float as[2][kCK * kAS];  // A chunk [k][co] of the workgroup's AW output channels
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int m = lane & 15, h = lane >> 4;
   const int wr = wave >> 1, wc = wave & 1;
@@ -81,8 +86,8 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(ConvArgs A) {
   const int s_t = s_ok ? (int)(sgrow - (long long)s_n * A.L) : 0;
   const int ncc = (A.cin + kCK - 1) / kCK;
   const int nchunk = A.ksize * ncc;
-  float sv[16], sw[16];
-  const int cob = blockIdx.y * 128;  // the workgroup's first output channel
+  float sv[16], sw[kAU];
+  const int cob = blockIdx.y * AW;  // the workgroup's first output channel
   auto load_chunk = [&](int ch) {
     const int tp = ch / ncc, ccb = (ch - tp * ncc) * kCK, cc0 = ccb + sc0;
     const int ts = s_t + tp - pad;
@@ -90,12 +95,12 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(ConvArgs A) {
     const float* src = A.x + ((long long)s_n * A.in_rs + A.in_off + ts) * A.cin;
 #pragma unroll
     for (int j = 0; j < 16; ++j) sv[j] = (ok && cc0 + j < A.cin) ? src[cc0 + j] : 0.f;
-    // A chunk: element i = (kk, c) of [kCK][128]; forward kernel W[tap][ci][co] is co-contiguous
+    // A chunk: element i = (kk, c) of [kCK][AW]; forward kernel W[tap][ci][co] is co-contiguous
     // (c fastest), the dgrad kernel W[K-1-tap][co][ci] ci-contiguous (kk fastest)
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    for (int j = 0; j < kAU; ++j) {
       const int i = threadIdx.x + 256 * j;
-      const int kk = A.flip ? (i & (kCK - 1)) : (i >> 7), c = A.flip ? (i >> 5) : (i & 127);
+      const int kk = A.flip ? (i & (kCK - 1)) : (i / AW), c = A.flip ? (i >> 5) : (i % AW);
       const int cc = ccb + kk, o = cob + c;
       float v = 0.f;
       if (cc < A.cin && o < A.cout)
@@ -109,9 +114,9 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(ConvArgs A) {
 #pragma unroll
     for (int j = 0; j < 16; j += 4) *reinterpret_cast<f32x4*>(d + j) = f32x4{sv[j], sv[j + 1], sv[j + 2], sv[j + 3]};
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    for (int j = 0; j < kAU; ++j) {
       const int i = threadIdx.x + 256 * j;
-      const int kk = A.flip ? (i & (kCK - 1)) : (i >> 7), c = A.flip ? (i >> 5) : (i & 127);
+      const int kk = A.flip ? (i & (kCK - 1)) : (i / AW), c = A.flip ? (i >> 5) : (i % AW);
       as[buf][kk * kAS + c] = sw[j];
     }
   };
@@ -126,7 +131,7 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(ConvArgs A) {
   if (nchunk > 1) load_chunk(1);
   __syncthreads();
   const int brow = wr * 64 + m;  // this lane's B rows: brow + 16 r
-  const int acol = wc * 64 + m;  // this lane's A columns (output channels): acol + 16 c
+  const int acol = wc * 16 * CT + m;  // this lane's A columns (output channels): acol + 16 c
   for (int ch = 0; ch < nchunk; ++ch) {
     const float* b = bs[ch & 1];
     const float* a = as[ch & 1];
@@ -213,69 +218,102 @@ struct WgArgs {
   int cin, cout, k, rows_per_group;
 };
 
-// workgroup = 32 ci (2 tiles) x 64 co (4 waves, one 16-co tile each) x one row group; a wave holds every
-// tap's 2 tiles in registers.  The row group streams through LDS in chunks of kWgRC rows (X with its
-// k - 1 halo rows, dZ), so each operand float is read from global memory once per workgroup and from
-// LDS by the MFMAs (one ds_read_b32 per v_mfma_f32_16x16x4_f32); row strides 48 / 80 floats put the
-// 4 row groups of a fragment read on disjoint bank quarters.
+// workgroup = 32 ci x 64 co x one row group (4 waves, each 16 ci x 32 co x every tap in registers).
+// The row group streams through LDS in chunks of kWgRC rows (X with its k - 1 halo rows, dZ),
+// double-buffered and prefetched one chunk ahead through registers, so each operand float is read from
+// global memory once per workgroup; row strides 48 / 80 floats put the 4 row groups of a fragment read
+// on disjoint bank quarters.
 // K (taps) is a template parameter: the accumulators of every tap stay in registers (a runtime tap
 // count indexed them through scratch memory).
 constexpr int kWgRC = 64, kWgKMax = 15, kWgXS = 48, kWgDS = 80;
 template <int K>
-__global__ __launch_bounds__(256) void wgrad_kernel(WgArgs A) {
-  __shared__ float xs[(kWgRC + kWgKMax - 1) * kWgXS];
-  __shared__ float ds[kWgRC * kWgDS];
+__global__ __launch_bounds__(256, 2) void wgrad_kernel(WgArgs A) {
+  constexpr int XR = kWgRC + K - 1;                 // X rows of a chunk (with the tap halo)
+  constexpr int XU = (XR * 32 + 255) / 256, DU = kWgRC * 64 / 256;  // staged floats per thread
+  __shared__ float xs[2][(kWgRC + kWgKMax - 1) * kWgXS];
+  __shared__ float ds[2][kWgRC * kWgDS];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int m = lane & 15, h = lane >> 4;
+  // wave = one 16-ci tile x two 16-co tiles x every tap: per 4 rows, 2 dZ + K X fragment reads feed
+  // 2 K MFMAs
+  const int wci = wave & 1, wco = (wave >> 1) * 2;
   const int ci0 = blockIdx.x * 32, cog = blockIdx.y * 64;
   const int rg = blockIdx.z;
   const long long r_begin = (long long)rg * A.rows_per_group;
   const long long r_end = r_begin + A.rows_per_group < A.R ? r_begin + A.rows_per_group : A.R;
-  const long long x_rows = A.R + A.k - 1;
+  const long long x_rows = A.R + K - 1;
   f32x4 acc[K][2];
 #pragma unroll
   for (int t = 0; t < K; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int xr = kWgRC + K - 1;
-  for (long long r0 = r_begin; r0 < r_end; r0 += kWgRC) {  // workgroup-uniform
-    __syncthreads();
-    for (int i = threadIdx.x; i < xr * 32; i += 256) {
-      const int rr = i >> 5, c = i & 31;
-      const long long row = r0 + rr;
-      xs[rr * kWgXS + c] = (row < x_rows && row < r_end + K - 1 && ci0 + c < A.cin) ? A.x[row * A.cin + ci0 + c] : 0.f;
-    }
-    for (int i = threadIdx.x; i < kWgRC * 64; i += 256) {
-      const int rr = i >> 6, c = i & 63;
-      const long long row = r0 + rr;
-      ds[rr * kWgDS + c] = (row < r_end && cog + c < A.cout) ? A.dz[row * A.cout + cog + c] : 0.f;
-    }
-    __syncthreads();
-    if (cog + wave * 16 >= A.cout) continue;  // wave-uniform (the barriers above are shared)
-#pragma unroll 4
-    for (int kk = 0; kk < kWgRC / 4; ++kk) {
-      const int rb = 4 * kk + h;
-      const float b = ds[rb * kWgDS + wave * 16 + m];
+  // chunk staging through registers: the loads of chunk c + 1 are in flight during chunk c's MFMAs
+  float px[XU], pd[DU];
+  auto load = [&](long long r0) {
 #pragma unroll
-      for (int t = 0; t < K; ++t) {
-        const float a0 = xs[(rb + t) * kWgXS + m], a1 = xs[(rb + t) * kWgXS + 16 + m];
-        acc[t][0] = mfma4(a0, b, acc[t][0]);
-        acc[t][1] = mfma4(a1, b, acc[t][1]);
+    for (int j = 0; j < XU; ++j) {
+      const int i = threadIdx.x + 256 * j, rr = i >> 5, c = i & 31;
+      const long long row = r0 + rr;
+      px[j] = (i < XR * 32 && row < x_rows && row < r_end + K - 1 && ci0 + c < A.cin) ? A.x[row * A.cin + ci0 + c]
+                                                                                    : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < DU; ++j) {
+      const int i = threadIdx.x + 256 * j, rr = i >> 6, c = i & 63;
+      const long long row = r0 + rr;
+      pd[j] = (row < r_end && cog + c < A.cout) ? A.dz[row * A.cout + cog + c] : 0.f;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < XU; ++j) {
+      const int i = threadIdx.x + 256 * j;
+      if (i < XR * 32) xs[buf][(i >> 5) * kWgXS + (i & 31)] = px[j];
+    }
+#pragma unroll
+    for (int j = 0; j < DU; ++j) {
+      const int i = threadIdx.x + 256 * j;
+      ds[buf][(i >> 6) * kWgDS + (i & 63)] = pd[j];
+    }
+  };
+  const bool active = cog + wco * 16 < A.cout;  // wave-uniform
+  load(r_begin);
+  store(0);
+  if (r_begin + kWgRC < r_end) load(r_begin + kWgRC);
+  __syncthreads();
+  int buf = 0;
+  for (long long r0 = r_begin; r0 < r_end; r0 += kWgRC, buf ^= 1) {  // workgroup-uniform
+    if (active) {
+      const float* xb = xs[buf] + wci * 16 + m;
+      const float* db = ds[buf] + wco * 16 + m;
+#pragma unroll 4
+      for (int kk = 0; kk < kWgRC / 4; ++kk) {
+        const int rb = 4 * kk + h;
+        const float b0 = db[rb * kWgDS], b1 = db[rb * kWgDS + 16];
+#pragma unroll
+        for (int t = 0; t < K; ++t) {
+          const float a = xb[(rb + t) * kWgXS];
+          acc[t][0] = mfma4(a, b0, acc[t][0]);
+          acc[t][1] = mfma4(a, b1, acc[t][1]);
+        }
       }
     }
+    if (r0 + kWgRC < r_end) store(buf ^ 1);  // its readers (chunk c - 1) passed the last barrier
+    __syncthreads();
+    if (r0 + 2 * kWgRC < r_end) load(r0 + 2 * kWgRC);
   }
   // D layout: lane holds rows i = 4 h + e (ci), column j = m (co)
-  const int co = cog + wave * 16 + m;
-  if (co >= A.cout) return;
+  if (!active) return;
+  const int ci = ci0 + wci * 16 + 4 * h;
   float* p = A.part + (long long)rg * K * A.cin * A.cout;
 #pragma unroll
-  for (int t = 0; t < K; ++t) {
+  for (int t = 0; t < K; ++t)
 #pragma unroll
-    for (int ct = 0; ct < 2; ++ct)
+    for (int u = 0; u < 2; ++u) {
+      const int co = cog + (wco + u) * 16 + m;
+      if (co >= A.cout) continue;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int ci = ci0 + ct * 16 + 4 * h + e;
-        if (ci < A.cin) p[((long long)t * A.cin + ci) * A.cout + co] = acc[t][ct][e];
-      }
-  }
+      for (int e = 0; e < 4; ++e)
+        if (ci + e < A.cin) p[((long long)t * A.cin + ci + e) * A.cout + co] = acc[t][u][e];
+    }
 }
 
 }  // namespace gf32
@@ -286,12 +324,17 @@ hipError_t launch_gf32_conv(const float* x, const float* w, const float* bias, f
   gf32::ConvArgs A{x, w, bias, y, stats, n, L, cin, cout, ksize, in_rs, in_off, flip, det_slots > 0 ? 1 : 0};
   const long long rows = (long long)n * L;
   if (rows == 0) return hipSuccess;
-  const dim3 grid((unsigned)((rows + 127) / 128), (unsigned)(((cout + 15) / 16 + 7) / 8));
+  const int nct = (cout + 15) / 16, ct = nct % 6 == 0 ? 3 : 4;
+  const dim3 grid((unsigned)((rows + 127) / 128), (unsigned)((nct + 2 * ct - 1) / (2 * ct)));
   if (mode == gf32::kTrain && A.det && (long long)grid.x * 2 > det_slots) return hipErrorInvalidValue;
-  if (mode == gf32::kTrain)
-    hipLaunchKernelGGL(gf32::conv_kernel<gf32::kTrain>, grid, dim3(256), 0, st, A);
+  if (mode == gf32::kTrain && ct == 3)
+    hipLaunchKernelGGL((gf32::conv_kernel<gf32::kTrain, 3>), grid, dim3(256), 0, st, A);
+  else if (mode == gf32::kTrain)
+    hipLaunchKernelGGL((gf32::conv_kernel<gf32::kTrain, 4>), grid, dim3(256), 0, st, A);
+  else if (ct == 3)
+    hipLaunchKernelGGL((gf32::conv_kernel<gf32::kLinear, 3>), grid, dim3(256), 0, st, A);
   else
-    hipLaunchKernelGGL(gf32::conv_kernel<gf32::kLinear>, grid, dim3(256), 0, st, A);
+    hipLaunchKernelGGL((gf32::conv_kernel<gf32::kLinear, 4>), grid, dim3(256), 0, st, A);
   return hipGetLastError();
 }
 
@@ -303,8 +346,8 @@ hipError_t launch_gf32_wgrad(const float* x, const float* dz, long long R, int c
   const long long wfl = (long long)k * cin * cout;
   long long groups = part_floats / wfl;
   const long long ci_t = (cin + 31) / 32, co_g = (cout + 63) / 64;
-  // ~3 workgroups per CU in total, at least 256 rows per group
-  long long want = (768 + ci_t * co_g - 1) / (ci_t * co_g);
+  // ~2 workgroups per CU in total (71 KB of LDS each), at least 256 rows per group
+  long long want = (512 + ci_t * co_g - 1) / (ci_t * co_g);
   if (want > (R + 255) / 256) want = (R + 255) / 256;
   if (groups > want) groups = want;
   if (groups > 65535) groups = 65535;

@@ -149,17 +149,14 @@ class _Workspace:
         # range-safe fp16 split of block l+2's input (csrc/x3_layers.hip sample_prescale).  Moving statistics:
         # the max of R_l per sample (fp32 bits; block 1: per window and member) and the channel maxima of
         # each affine.  Batch moments: one power of two per group, from the moments themselves, folded into
-        # the affine (x3_aff gscale).  APNEAUQ_X3_PRESCALE=0 turns both off -- an A/B switch for their
-        # cost, valid only when every activation is within fp16's range.
-        on = os.environ.get("APNEAUQ_X3_PRESCALE", "1") != "0"
-        self.smax = [torch.zeros(n_r1 if l == 0 else samples, dtype=torch.int32, device=dev) if on else None
-                     for l in range(5)]
-        self.amax = [torch.zeros(max(groups, 1) * 2, **f32) if on else None for l in range(6)]
-        self.gscale = [torch.ones(max(groups, 1), **f32) if on else None for l in range(5)] + [None]
+        # the affine (x3_aff gscale).  Cost: profiles/x3_mask_side_r4.md.
+        self.smax = [torch.zeros(n_r1 if l == 0 else samples, dtype=torch.int32, device=dev) for l in range(5)]
+        self.amax = [torch.zeros(max(groups, 1) * 2, **f32) for l in range(6)]
+        self.gscale = [torch.ones(max(groups, 1), **f32) for l in range(5)] + [None]
 
     def smax_out(self, l: int, k: int) -> Optional[torch.Tensor]:
         """Block l+1's per-sample maxima (first k samples, zeroed: atomicMax targets); None for block 6."""
-        if l >= 5 or self.smax[l] is None:
+        if l >= 5:
             return None
         return self.smax[l][:k].zero_()
 
