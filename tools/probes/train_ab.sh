@@ -9,6 +9,6 @@ for rep in $(seq 1 $n); do
     if [ $so = main ]; then unset APNEAUQ_SO_PATH; else export APNEAUQ_SO_PATH=$PWD/$so; fi
     a=$(timeout -k 10 200 python3 -m bench.train_micro --batch 8192 --steps 30 2>/dev/null | tail -1) || exit 1
     b=$(timeout -k 10 200 python3 -m bench.train_micro --batch 1024 --steps 100 2>/dev/null | tail -1) || exit 1
-    echo "$rep $(basename $so .so) b8192 $(echo $a | cut -d, -f3) | b1024 $(echo $b | cut -d, -f3)"
+    echo "$rep $(basename $so .so) b8192 $(echo $a | python3 -c 'import json,sys; print(round(json.load(sys.stdin)["ms_per_step"], 4))') ms | b1024 $(echo $b | python3 -c 'import json,sys; print(round(json.load(sys.stdin)["ms_per_step"], 4))') ms"
   done
 done
