@@ -55,10 +55,15 @@ constexpr int kCK = 32, kBS = 36;
 template <int MODE, int CT>
 __global__ __launch_bounds__(256, 2) void conv_kernel(ConvArgs A) {
   constexpr int kCT = CT, AW = 32 * CT;       // the workgroup's output channels
+  // A chunk layout: forward [k][co] (row stride kAS = 16 mod 64: the fragment read's h rows x 16 co
+  // fill the banks), dgrad (MODE kLinear, the flipped kernel, ci-contiguous in global memory) [co][k]
+  // (row stride kBS like B): both staged from coalesced loads with contiguous LDS stores
+  constexpr bool kFlip = MODE == kLinear;
   constexpr int kAS = (AW + 47) / 64 * 64 + 16;  // >= AW, 16 mod 64
   constexpr int kAU = kCK * AW / 256;           // A-chunk elements staged per thread
+  constexpr int kASZ = kFlip ? AW * kBS : kCK * kAS;
   __shared__ float bs[2][128 * kBS];
-  __shared__ float as[2][kCK * kAS];  // A chunk [k][co] of the workgroup's AW output channels
+  __shared__ float as[2][kASZ];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int m = lane & 15, h = lane >> 4;
   const int wr = wave >> 1, wc = wave & 1;
@@ -95,17 +100,17 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(ConvArgs A) {
     const float* src = A.x + ((long long)s_n * A.in_rs + A.in_off + ts) * A.cin;
 #pragma unroll
     for (int j = 0; j < 16; ++j) sv[j] = (ok && cc0 + j < A.cin) ? src[cc0 + j] : 0.f;
-    // A chunk: element i = (kk, c) of [kCK][AW]; forward kernel W[tap][ci][co] is co-contiguous
-    // (c fastest), the dgrad kernel W[K-1-tap][co][ci] ci-contiguous (kk fastest)
+    // A chunk element i = (kk, c): the forward kernel W[tap][ci][co] is co-contiguous (c fastest), the
+    // dgrad kernel W[K-1-tap][co][ci] ci-contiguous (kk fastest)
 #pragma unroll
     for (int j = 0; j < kAU; ++j) {
       const int i = threadIdx.x + 256 * j;
-      const int kk = A.flip ? (i & (kCK - 1)) : (i / AW), c = A.flip ? (i >> 5) : (i % AW);
+      const int kk = kFlip ? (i & (kCK - 1)) : (i / AW), c = kFlip ? (i >> 5) : (i % AW);
       const int cc = ccb + kk, o = cob + c;
       float v = 0.f;
       if (cc < A.cin && o < A.cout)
-        v = A.flip ? A.w[((long long)(A.ksize - 1 - tp) * A.cout + o) * A.cin + cc]
-                   : A.w[((long long)tp * A.cin + cc) * A.cout + o];
+        v = kFlip ? A.w[((long long)(A.ksize - 1 - tp) * A.cout + o) * A.cin + cc]
+                  : A.w[((long long)tp * A.cin + cc) * A.cout + o];
       sw[j] = v;
     }
   };
@@ -116,8 +121,10 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(ConvArgs A) {
 #pragma unroll
     for (int j = 0; j < kAU; ++j) {
       const int i = threadIdx.x + 256 * j;
-      const int kk = A.flip ? (i & (kCK - 1)) : (i / AW), c = A.flip ? (i >> 5) : (i % AW);
-      as[buf][kk * kAS + c] = sw[j];
+      if constexpr (kFlip)
+        as[buf][(i >> 5) * kBS + (i & (kCK - 1))] = sw[j];
+      else
+        as[buf][(i / AW) * kAS + i % AW] = sw[j];
     }
   };
 
@@ -144,7 +151,8 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(ConvArgs A) {
         if (q >= nq) break;  // uniform
         float aq[kCT], bq[kRT];
 #pragma unroll
-        for (int c = 0; c < kCT; ++c) aq[c] = a[(4 * q + h) * kAS + acol + 16 * c];
+        for (int c = 0; c < kCT; ++c)
+          aq[c] = kFlip ? a[(acol + 16 * c) * kBS + 4 * q + h] : a[(4 * q + h) * kAS + acol + 16 * c];
 #pragma unroll
         for (int r = 0; r < kRT; ++r) bq[r] = b[(brow + 16 * r) * kBS + 4 * q + h];
 #pragma unroll
