@@ -21,6 +21,7 @@ namespace apneauq {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // Explicit global-address-space views (keep loads as global_load_*, never flat_*).
 typedef __attribute__((address_space(1))) const bf16x8 gbf16x8;

@@ -45,13 +45,13 @@ struct ConvArgs {
 // The B operand streams through LDS in chunks of one tap x kCK input channels for the tile's 128 rows
 // (each lane of the staging loads reads kCK / 4 consecutive channels of one input row: whole 128-B
 // lines instead of the 64 rows-apart single floats of a direct fragment load), double-buffered with
-// one barrier per chunk; row stride kBS floats: the fragment read (16 rows x 4 k) hits 16 distinct
-// 4-bank groups.  The A operand (the Keras kernel's [kCK][128 co] block of the chunk) is staged beside
+// one barrier per chunk; row stride kBS = 34 floats: each 32-lane half of a ds_read_b32 fragment read
+// (16 rows x 2 k) hits 32 distinct banks (36 was 2-way), rows 8-B aligned for ds_write_b64 staging.  The A operand (the Keras kernel's [kCK][128 co] block of the chunk) is staged beside
 // it (row stride kAS = 16 mod 64 floats: conflict-free fragment reads); a direct fragment load from
 // L2 one k-step ahead left the MFMAs waiting on its latency (26 % of the f32 peak).
 // CT = 16-channel tiles per wave (a workgroup covers 32 CT output channels): 3 where Cout is a multiple
 // of 96 (the Cout-96 / 192 blocks padded to 128 / 256 channels computed 25 % zeros), else 4.
-constexpr int kCK = 32, kBS = 36;
+constexpr int kCK = 32, kBS = 34;
 template <int MODE, int CT>
 __global__ __launch_bounds__(256, 2) void conv_kernel(ConvArgs A) {
   constexpr int kCT = CT, AW = 32 * CT;       // the workgroup's output channels
@@ -93,6 +93,19 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(ConvArgs A) {
   const int nchunk = A.ksize * ncc;
   float sv[16], sw[kAU];
   const int cob = blockIdx.y * AW;  // the workgroup's first output channel
+  // A chunk element j of this thread: i = tid + 256 j = (kk, c); the forward kernel W[tap][ci][co] is
+  // co-contiguous (c fastest), the dgrad kernel W[K-1-tap][co][ci] ci-contiguous (kk fastest).  The
+  // element's offset from the chunk's (uniform) base and its kk do not depend on the chunk: computed
+  // once (the per-chunk 64-bit index math and the divisions by AW were most of the staging VALU)
+  int aoff[kAU], akk[kAU];
+#pragma unroll
+  for (int j = 0; j < kAU; ++j) {
+    const int i = threadIdx.x + 256 * j;
+    const int kk = kFlip ? (i & (kCK - 1)) : (i / AW), c = kFlip ? (i >> 5) : (i % AW);
+    const bool cok = cob + c < A.cout;
+    akk[j] = cok ? kk : (1 << 30);  // never valid
+    aoff[j] = kFlip ? c * A.cin + kk : kk * A.cout + c;
+  }
   auto load_chunk = [&](int ch) {
     const int tp = ch / ncc, ccb = (ch - tp * ncc) * kCK, cc0 = ccb + sc0;
     const int ts = s_t + tp - pad;
@@ -100,24 +113,16 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(ConvArgs A) {
     const float* src = A.x + ((long long)s_n * A.in_rs + A.in_off + ts) * A.cin;
 #pragma unroll
     for (int j = 0; j < 16; ++j) sv[j] = (ok && cc0 + j < A.cin) ? src[cc0 + j] : 0.f;
-    // A chunk element i = (kk, c): the forward kernel W[tap][ci][co] is co-contiguous (c fastest), the
-    // dgrad kernel W[K-1-tap][co][ci] ci-contiguous (kk fastest)
+    const float* wb = kFlip ? A.w + ((long long)(A.ksize - 1 - tp) * A.cout + cob) * A.cin + ccb
+                            : A.w + ((long long)tp * A.cin + ccb) * A.cout + cob;
+    const int kmax = A.cin - ccb;
 #pragma unroll
-    for (int j = 0; j < kAU; ++j) {
-      const int i = threadIdx.x + 256 * j;
-      const int kk = kFlip ? (i & (kCK - 1)) : (i / AW), c = kFlip ? (i >> 5) : (i % AW);
-      const int cc = ccb + kk, o = cob + c;
-      float v = 0.f;
-      if (cc < A.cin && o < A.cout)
-        v = kFlip ? A.w[((long long)(A.ksize - 1 - tp) * A.cout + o) * A.cin + cc]
-                  : A.w[((long long)tp * A.cin + cc) * A.cout + o];
-      sw[j] = v;
-    }
+    for (int j = 0; j < kAU; ++j) sw[j] = akk[j] < kmax ? wb[aoff[j]] : 0.f;
   };
   auto store_chunk = [&](int buf) {
     float* d = &bs[buf][srow * kBS + sc0];
 #pragma unroll
-    for (int j = 0; j < 16; j += 4) *reinterpret_cast<f32x4*>(d + j) = f32x4{sv[j], sv[j + 1], sv[j + 2], sv[j + 3]};
+    for (int j = 0; j < 16; j += 2) *reinterpret_cast<f32x2*>(d + j) = f32x2{sv[j], sv[j + 1]};
 #pragma unroll
     for (int j = 0; j < kAU; ++j) {
       const int i = threadIdx.x + 256 * j;
