@@ -529,15 +529,10 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* lds, int ldsrs, int row_ba
   const char* a1 = lds + lds_off(ra + 16, (col0 + 4 * p) * 2, ldsrs);
   const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)a0);
   const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)a1);
-  bf16x8 r;
-  const __bf16* pl = reinterpret_cast<const __bf16*>(&lo);
-  const __bf16* ph = reinterpret_cast<const __bf16*>(&hi);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    r[j] = pl[j];
-    r[4 + j] = ph[j];
-  }
-  return r;
+  // one 8 x 16-bit register quad: no per-element moves
+  typedef short v8i16 __attribute__((ext_vector_type(8)));
+  const v8i16 r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, r);
 }
 
 // Weight-fragment prefetch depth of the forward conv (k-steps in flight): depth 1 everywhere 29.8 ms
