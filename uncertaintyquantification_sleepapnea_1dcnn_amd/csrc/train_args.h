@@ -274,8 +274,13 @@ struct DetDst {  // up to four destination segments (consecutive column ranges; 
 __global__ void wgrad_reduce_kernel(const float* __restrict__ part, int rgs, int kcc, int cout, float* __restrict__ gw,
                                     float* __restrict__ gb, int J, TabBwd tb);
 __global__ void wgrad_reduce_mb_kernel(const Args* __restrict__ Am, int l, int rgs, int kcc, int cout, int J, int side);
-__global__ void det_reduce_kernel(const float* __restrict__ part, int n, int w, DetDst d);
-__global__ void det_reduce_mb_kernel(const Args* __restrict__ Am, int op, int l, int n, int w);
+// deterministic column sums: kDetSeg row segments (pass 1, fp64 scratch [kDetSeg][w] behind the partial
+// table), then the segments in order (pass 2); w <= kDetMaxW
+constexpr int kDetSeg = 32, kDetMaxW = 512;
+__global__ void det_pass1_kernel(const float* __restrict__ part, int n, int w, double* __restrict__ scr);
+__global__ void det_pass2_kernel(const double* __restrict__ scr, int w, DetDst d);
+__global__ void det_pass1_mb_kernel(const Args* __restrict__ Am, int n, int w, long long sbase);
+__global__ void det_pass2_mb_kernel(const Args* __restrict__ Am, int op, int l, int w, long long sbase);
 template <bool MB>
 __global__ void bn_finalize_kernel(Args A_, const Args* __restrict__ Am, int update_moving, int grads);
 

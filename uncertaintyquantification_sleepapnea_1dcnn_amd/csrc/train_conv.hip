@@ -1410,8 +1410,13 @@ hipError_t train_stream_keys(unsigned* keys, const int* c, int n, unsigned long 
   return hipGetLastError();
 }
 
-static hipError_t det_reduce(const float* part, int n, int w, train::DetDst d, hipStream_t st) {
-  hipLaunchKernelGGL(train::det_reduce_kernel, dim3((w + 255) / 256), dim3(256), 0, st, part, n, w, d);
+static long long det_scratch_base(int B);
+// A.det's partial table (n rows of w) -> d, through the fp64 segment scratch behind the table
+static hipError_t det_reduce(const Args& A, int n, int w, train::DetDst d, hipStream_t st) {
+  if (w > train::kDetMaxW) return hipErrorInvalidValue;
+  double* scr = reinterpret_cast<double*>(A.det + det_scratch_base(A.B));
+  hipLaunchKernelGGL(train::det_pass1_kernel, dim3((w + 63) / 64, train::kDetSeg), dim3(256), 0, st, A.det, n, w, scr);
+  hipLaunchKernelGGL(train::det_pass2_kernel, dim3((w + 255) / 256), dim3(256), 0, st, scr, w, d);
   return hipGetLastError();
 }
 
@@ -1425,7 +1430,6 @@ static train::DetDst det_dst(void* p0, int c0, int f0, void* p1 = nullptr, int c
   return d;
 }
 
-// floats of the deterministic-mode partial table for a batch of B samples (fwd / head / dgrad reuse it)
 // Persistent forward: workgroups per CU (2 are resident at a time), each over a contiguous tile range.
 // Batch-BN MC Dropout (409,600 tiles per layer launch) measured 8 / 16 / 32 / 64 per CU: MCD phase
 // 91.9 / 91.1-91.4 / 91.0-91.4 / 90.5-90.9 ms (tools/probes/so_bench1.sh, one box), and 64 / 128 / 256
@@ -1433,10 +1437,14 @@ static train::DetDst det_dst(void* p0, int c0, int f0, void* p1 = nullptr, int c
 // balance the launch tail.  Batches of <= 16384 tiles (training) get one tile per workgroup anyway.
 constexpr int kFwdWgPerCu = 64;
 static int fwd_grid(int B) { return std::min((B + 1) / 2, 256 * kFwdWgPerCu); }
-int train_det_floats(int B) {
+// floats of the partial table (fwd / head / dgrad reuse it), then the fp64 scratch of the two-pass reduce
+static long long det_scratch_base(int B) {
   const int tiles = (B + 1) / 2;
-  return std::max({fwd_grid(B) * 2 * 256, B * train::kHeadRec, tiles * 2 * 2 * 256});
+  const long long t = std::max({(long long)fwd_grid(B) * 2 * 256, (long long)B * train::kHeadRec,
+                                (long long)tiles * 2 * 2 * 256});
+  return (t + 3) / 4 * 4;  // 16-B aligned scratch
 }
+int train_det_floats(int B) { return (int)(det_scratch_base(B) + 2LL * train::kDetSeg * train::kDetMaxW); }
 
 // Kernel launches shared by the single-model path (MB = false: by-value Args, Am = nullptr, M = 1)
 // and the member-batched path (MB = true: gridDim.z = M members, Args from the device array Am).
@@ -1476,7 +1484,7 @@ hipError_t train_launch_fwd(const Args& A, int l, hipStream_t st) {
     const hipError_t e = fwd_launch<false>(A, nullptr, 1, l, grid, st);
     if (e != hipSuccess) return e;
     const int cc = train::C[l + 1];
-    return det_reduce(A.det, grid, 2 * cc, det_dst(A.L[l].st, 2 * cc, 1), st);
+    return det_reduce(A, grid, 2 * cc, det_dst(A.L[l].st, 2 * cc, 1), st);
   }
   // persistent forward: each workgroup over a contiguous tile range
   return fwd_launch<false>(A, nullptr, 1, l, grid, st);
@@ -1495,7 +1503,7 @@ hipError_t train_launch_head(const Args& A, int backward, hipStream_t st) {
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess || !backward || A.det == nullptr) return e;
   constexpr int cc = train::C[6];  // per-sample records: loss, dlogit, dW, sum dY, sum dY xhat
-  return det_reduce(A.det, A.B, train::kHeadRec,
+  return det_reduce(A, A.B, train::kHeadRec,
                     det_dst(A.loss_sum, 1, 0, A.g_dense_b, 1, A.g_dense_w, cc, A.L[5].bst, 2 * cc, 1), st);
 }
 
@@ -1507,7 +1515,7 @@ hipError_t train_launch_dgrad(const Args& A, int l, hipStream_t st) {
                                 train::Tiling<train::C[3]>::WM, train::Tiling<train::C[4]>::WM,
                                 train::Tiling<train::C[5]>::WM};
   const int cc = train::C[l];  // block l's backward sums (of BN l-1's output) per (tile, wave row block)
-  return det_reduce(A.det, tiles * wm[l], 2 * cc, det_dst(A.L[l - 1].bst, 2 * cc, 1), st);
+  return det_reduce(A, tiles * wm[l], 2 * cc, det_dst(A.L[l - 1].bst, 2 * cc, 1), st);
 }
 
 template <int l>
@@ -1602,9 +1610,12 @@ hipError_t train_launch_finalize(const Args& A, int update_moving, int grads, hi
 // all M members' Args.  op: 0 fwd(layer) | 1 head(flag = backward) | 2 dgrad(layer) | 3 wgrad(layer)
 // | 4 finalize(layer = update_moving, flag = grads) | 5 forward rows of the parameter table.
 // Single-device training only (no shared block 1).  Deterministic mode (every member with partial
-// tables, A0.det set): each reduction is followed by det_reduce_mb_kernel over all members.
-static hipError_t det_reduce_mb(const Args* Am, int M, int op, int l, int n, int w, hipStream_t st) {
-  hipLaunchKernelGGL(train::det_reduce_mb_kernel, dim3((w + 255) / 256, 1, M), dim3(256), 0, st, Am, op, l, n, w);
+// tables, A0.det set): each reduction is followed by the two det passes over all members.
+static hipError_t det_reduce_mb(const Args& A0, const Args* Am, int M, int op, int l, int n, int w, hipStream_t st) {
+  if (w > train::kDetMaxW) return hipErrorInvalidValue;
+  const long long sb = det_scratch_base(A0.B);
+  hipLaunchKernelGGL(train::det_pass1_mb_kernel, dim3((w + 63) / 64, train::kDetSeg, M), dim3(256), 0, st, Am, n, w, sb);
+  hipLaunchKernelGGL(train::det_pass2_mb_kernel, dim3((w + 255) / 256, 1, M), dim3(256), 0, st, Am, op, l, w, sb);
   return hipGetLastError();
 }
 
@@ -1616,14 +1627,14 @@ hipError_t train_launch_mb(const Args& A0, const Args* Am, int M, int op, int la
     case 0: {
       const hipError_t e = fwd_launch<true>(A0, Am, M, layer, fwd_grid(A0.B), st);
       if (e != hipSuccess || !det) return e;
-      return det_reduce_mb(Am, M, 0, layer, fwd_grid(A0.B), 2 * train::C[layer + 1], st);
+      return det_reduce_mb(A0, Am, M, 0, layer, fwd_grid(A0.B), 2 * train::C[layer + 1], st);
     }
     case 1: {
       hipLaunchKernelGGL(train::head_kernel<true>, dim3((A0.B + 3) / 4, 1, M), dim3(256), (8 * train::C[6] + 2) * 4, st, A0,
                          Am, flag);
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess || !det || !flag) return e;
-      return det_reduce_mb(Am, M, 1, 0, A0.B, train::kHeadRec, st);
+      return det_reduce_mb(A0, Am, M, 1, 0, A0.B, train::kHeadRec, st);
     }
     case 2: {
       const hipError_t e = dgrad_launch<true>(A0, Am, M, layer, st);
@@ -1631,7 +1642,7 @@ hipError_t train_launch_mb(const Args& A0, const Args* Am, int M, int op, int la
       static constexpr int wm[6] = {0, train::Tiling<train::C[1]>::WM, train::Tiling<train::C[2]>::WM,
                                     train::Tiling<train::C[3]>::WM, train::Tiling<train::C[4]>::WM,
                                     train::Tiling<train::C[5]>::WM};
-      return det_reduce_mb(Am, M, 2, layer, ((A0.B + 1) / 2) * wm[layer], 2 * train::C[layer], st);
+      return det_reduce_mb(A0, Am, M, 2, layer, ((A0.B + 1) / 2) * wm[layer], 2 * train::C[layer], st);
     }
     case 3: return wgrad_launch<true>(A0, Am, M, layer, st);
     case 4:
