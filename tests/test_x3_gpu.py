@@ -107,6 +107,29 @@ def test_mcd_batch_bn_matches_fp32_reference(n, T):
             torch.testing.assert_close(p[k].cpu(), pc[k], atol=2e-6, rtol=2e-6)
 
 
+@pytest.mark.parametrize("sign", ["", "1,2,3,4"])
+@pytest.mark.parametrize("bn", ["batch", "running"])
+def test_mask_side_matches_reference(monkeypatch, sign, bn):
+    """Every block's dropout mask drawn by the consumer's staging (hash) or by the producer's epilogue (R's
+    sign bit; ops/x3.py _SIGN_DEFAULT picks per layer): both are the reference's masks."""
+    _ext.require()
+    monkeypatch.setenv("APNEAUQ_X3_SIGN_MASK", sign)
+    dev = torch.device("cuda")
+    x = _x(45, 4)
+    p = _params(17, dev)
+    pc = {k: v.detach().cpu().clone() for k, v in p.items()}
+    model = x3.X3Model(SPEC, [p])
+    ids = torch.arange(45)
+    if bn == "batch":
+        ph = x3.mcd_batch(model, x.to(dev), 2, seed=8, pass_base=3, update_moving=False)
+    else:
+        ph = x3.forward_running(model, x.to(dev), n_pass=2, dropout=True, seed=8, pass_offset=3)[0]
+    for t in range(2):
+        r = R.forward(SPEC, pc, x, dropout=True, bn_batch_stats=bn == "batch", seed=8, pass_id=3 + t,
+                      sample_ids=ids).reshape(-1)
+        assert (ph[t].cpu() - r).abs().max().item() <= BOUND
+
+
 def test_mcd_batch_chunked_equals_unchunked():
     _ext.require()
     dev = torch.device("cuda")
