@@ -47,3 +47,19 @@ def test_emulated_x3_conv_is_fp32_accurate():
     ref = R.conv1d_same(h.float().double(), w.double(), torch.zeros(256, dtype=torch.float64))
     err = ((y - ref).abs().max() / ref.abs().max()).item()
     assert err < 3e-7, err
+
+
+def test_mask_side_selection(monkeypatch):
+    """ops/x3.py: layer l draws block l+1's mask in its epilogue (sign_out) iff l is listed, and layer l+1
+    then decodes it (sign_in); the pass-shared block-1 output (layer 1's input) is always hashed."""
+    monkeypatch.setenv("APNEAUQ_X3_SIGN_MASK", "1, 3,4")
+    sl = x3._sign_layers()
+    assert sl == frozenset({1, 3, 4})
+    assert [x3._sign(l, sl) for l in range(1, 6)] == [(False, True), (True, False), (False, True), (True, True),
+                                                      (True, False)]
+    monkeypatch.setenv("APNEAUQ_X3_SIGN_MASK", "")
+    assert x3._sign_layers() == frozenset()
+    monkeypatch.delenv("APNEAUQ_X3_SIGN_MASK")
+    assert x3._sign_layers() == frozenset(int(t) for t in x3._SIGN_DEFAULT.split(","))
+    # layer 5 (block 6) never stores its mask: it reduces its masked output in place
+    assert x3._sign(5, frozenset({5}))[1] is False
