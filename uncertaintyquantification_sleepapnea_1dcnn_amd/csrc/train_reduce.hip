@@ -1,5 +1,7 @@
 // Reductions of the layer-wise training step (train_conv.hip): the wgrad partial sums, the
-// deterministic-mode column sums and the BN finalize (moving averages, dgamma / dbeta).
+// deterministic-mode column sums and the BN finalize (moving averages, dgamma / dbeta) -- the
+// gradient / BatchNorm bookkeeping of Keras model.fit (/root/reference/models/cnn_baseline_train.py:
+// 100-102 compile with Adam + BCE, :210-217 fit; Keras BatchNormalization momentum 0.99, eps 1e-3).
 #include "train_args.h"
 
 namespace apneauq {
