@@ -660,31 +660,48 @@ __global__ __launch_bounds__(256) void l1_kernel(const L1Args A) {
 // are the biased batch moments of group g (stats != nullptr) or the moving statistics.  With
 // update != 0 the Keras moving averages are updated once per group in group order (one MC-Dropout
 // pass after the other, the side effect of model(x, training=True)).  amax[g] = (max_c |aff scale|,
-// max_c |aff shift|): the consumer's range-safe split (sample_prescale).  One workgroup, groups in order.
+// max_c |aff shift|): the consumer's range-safe split (sample_prescale).
+// Blocks 0..groups-1: group g's affine (independent); block `groups` (batch moments with the moving
+// update only): the moving averages, groups in order (the recurrence is sequential; the affines use
+// the batch moments, so the two never touch the same data).  One block looping over every group's
+// affine and its two block reductions took ~25 us per call.
+__device__ __forceinline__ void aff_moments(const AffArgs& A, int g, int c, float& mean, float& var) {
+  const double* p = A.stats + (long long)g * kStatSlots * 2 * A.C + c;
+  double a = 0.0, b = 0.0;
+#pragma unroll
+  for (int s = 0; s < kStatSlots; ++s) {
+    a += p[s * 2 * A.C];
+    b += p[s * 2 * A.C + A.C];
+  }
+  const double mu = a * A.inv_count;
+  mean = (float)mu;
+  var = (float)fmax(b * A.inv_count - mu * mu, 0.0);
+}
+
 __global__ __launch_bounds__(256) void aff_kernel(const AffArgs A) {
   __shared__ float red[2][4];
   const int tid = threadIdx.x;
-  for (int g = 0; g < A.groups; ++g) {
+  if ((int)blockIdx.x == A.groups) {  // the moving-average side effect (launched with stats + update)
+    for (int c = tid; c < A.C; c += 256)
+      for (int g = 0; g < A.groups; ++g) {
+        const long long po = (long long)g * A.p_gstride + c;
+        float mean, var;
+        aff_moments(A, g, c, mean, var);
+        for (int r = 0; r < A.repeat; ++r) {
+          A.mmean[po] = A.mmean[po] * A.momentum + mean * (1.f - A.momentum);
+          A.mvar[po] = A.mvar[po] * A.momentum + var * (1.f - A.momentum);
+        }
+      }
+    return;
+  }
+  {
+    const int g = blockIdx.x;
     float ms = 0.f, mt = 0.f;
     for (int c = tid; c < A.C; c += 256) {
       const long long po = (long long)g * A.p_gstride + c;
       float mean, var;
       if (A.stats != nullptr) {
-        const double* p = A.stats + (long long)g * kStatSlots * 2 * A.C + c;
-        double a = 0.0, b = 0.0;
-        for (int s = 0; s < kStatSlots; ++s) {
-          a += p[s * 2 * A.C];
-          b += p[s * 2 * A.C + A.C];
-        }
-        const double mu = a * A.inv_count;
-        mean = (float)mu;
-        var = (float)fmax(b * A.inv_count - mu * mu, 0.0);
-        if (A.update) {
-          for (int r = 0; r < A.repeat; ++r) {
-            A.mmean[po] = A.mmean[po] * A.momentum + mean * (1.f - A.momentum);
-            A.mvar[po] = A.mvar[po] * A.momentum + var * (1.f - A.momentum);
-          }
-        }
+        aff_moments(A, g, c, mean, var);
       } else {
         mean = A.mmean[po];
         var = A.mvar[po];
@@ -721,10 +738,9 @@ __global__ __launch_bounds__(256) void aff_kernel(const AffArgs A) {
         af[A.C] = ldexpf(af[A.C], sa);
       }
       if (tid == 0) A.gscale[g] = ldexpf(1.f, -sa);
-      __syncthreads();  // red is rewritten by the next group
-      continue;
+      return;
     }
-    if (A.amax == nullptr) continue;  // kernel-uniform
+    if (A.amax == nullptr) return;  // kernel-uniform
     ms = wave_max(ms);
     mt = wave_max(mt);
     if ((tid & 63) == 0) {
@@ -736,7 +752,6 @@ __global__ __launch_bounds__(256) void aff_kernel(const AffArgs A) {
       A.amax[2 * g] = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
       A.amax[2 * g + 1] = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
     }
-    __syncthreads();  // red is rewritten by the next group
   }
 }
 
@@ -850,7 +865,8 @@ hipError_t x3_launch_l1(const x3::L1Args& A, hipStream_t stream) {
 }
 
 hipError_t x3_launch_aff(const x3::AffArgs& A, hipStream_t stream) {
-  hipLaunchKernelGGL(x3::aff_kernel, dim3(1), dim3(256), 0, stream, A);
+  const int blocks = A.groups + (A.stats != nullptr && A.update ? 1 : 0);
+  hipLaunchKernelGGL(x3::aff_kernel, dim3(blocks), dim3(256), 0, stream, A);
   return hipGetLastError();
 }
 
