@@ -155,6 +155,31 @@ def test_graphed_training_step_matches_eager(monkeypatch, deterministic):
     assert abs(lb[0] - la[0]) < 1e-4 * abs(la[0])
 
 
+def test_graphed_step_overlap_matches_single_stream(monkeypatch):
+    """The graphed step with the wgrad chain on its own captured stream (train_ops.OVERLAP) computes
+    the gradients of the one-stream graph: same loss and, up to the atomics' summation order, the
+    same flat gradient (the backward BN rows are summed from the same fp64 slots either way)."""
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.data.synthetic import synthetic_windows
+
+    x, y, _ = synthetic_windows(512, seed=9)
+    x = torch.as_tensor(x, dtype=torch.float32).cuda()
+    y = torch.as_tensor(y, dtype=torch.float32).cuda()
+    monkeypatch.setenv("APNEAUQ_TRAIN_GRAPH", "1")
+    train_ops.set_deterministic(False)
+    out = {}
+    for ov in (False, True):
+        monkeypatch.setattr(train_ops, "OVERLAP", ov)
+        m = AlarconCNN1D(seed=4, device="cuda")
+        loss = float(m.train_step(x, y))
+        step = m._train_graphs[512]
+        assert step.overlap == ov
+        out[ov] = (loss, step.ws.grad.clone())
+    assert abs(out[True][0] - out[False][0]) <= 1e-5 * abs(out[False][0])
+    g0, g1 = out[False][1], out[True][1]
+    assert torch.isfinite(g1).all()
+    assert torch.allclose(g1, g0, rtol=2e-3, atol=1e-6), (g1 - g0).abs().max().item()
+
+
 def test_fit_concurrent_on_streams_matches_sequential(deterministic):
     """Three members trained concurrently (training/trainer.py:fit_concurrent), on HIP streams and as
     member-batched launches, ARE back-to-back fits in deterministic mode (bitwise-identical loss

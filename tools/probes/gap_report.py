@@ -30,6 +30,8 @@ def main(path):
         per[n][0] += e - s
         per[n][1] += 1
     span = t1 - t0
+    ksum = sum(e - s for s, e, _ in ev)
+    print(f"kernel-time sum {ksum / 1e6:.3f} ms vs union {busy / 1e6:.3f} ms (concurrent {100 * (ksum - busy) / max(busy, 1):.1f} %)")
     print(f"span {span / 1e6:.3f} ms, busy {busy / 1e6:.3f} ms ({100 * busy / span:.1f} %), {len(ev)} dispatches, "
           f"{len(gaps)} gaps, mean gap {sum(gaps) / max(len(gaps), 1) / 1e3:.2f} us")
     for n, (t, c) in sorted(per.items(), key=lambda kv: -kv[1][0])[:30]:

@@ -88,6 +88,7 @@ struct Args {
   float* logits; float* dlogit; float* loss_sum;
   int B; int n_win; int groups; unsigned pass_base; unsigned window_offset; unsigned long long seed; int dropout;
   float inv_count; float inv_batch; float eps; float momentum; const unsigned* pass_dev; int st_groups; float* wpart; float* det; int shared0; float* tab; float* hpart;
+  int bwd_self;
 };
 }  // namespace train
 int train_args_size();
@@ -397,6 +398,7 @@ apneauq::train::Args args_from_ctx(const at::Tensor& ctx, int64_t pass_base) {
   A.det = reinterpret_cast<float*>(g[24]);
   A.tab = reinterpret_cast<float*>(g[25]);
   A.hpart = reinterpret_cast<float*>(g[26]);
+  A.bwd_self = 0;
   TORCH_CHECK(A.hpart == nullptr || A.det == nullptr, "train ctx: head slots are for the atomic mode");
   TORCH_CHECK(A.tab == nullptr || (A.det == nullptr && A.groups == 1 && A.wpart != nullptr),
               "train ctx: the parameter table needs one stats group, no deterministic partials and wgrad partials "
@@ -407,6 +409,7 @@ apneauq::train::Args args_from_ctx(const at::Tensor& ctx, int64_t pass_base) {
 
 // op: 0 fwd(layer; flag=1: the pass-shared block 1 of batch-BN MC Dropout, over the n_win windows)
 //     | 1 head(flag=backward) | 2 dgrad(layer) | 3 wgrad(layer) | 4 finalize(layer=update_moving, flag=grads)
+//     (2 / 3: flag 1 = Args::bwd_self, the backward BN rows from the slots instead of the table)
 //     | 5 parameter table (flag 0: forward rows of every block, 1: backward rows of block ``layer``)
 void train_call(const at::Tensor& ctx, int64_t op, int64_t layer, int64_t flag, int64_t pass_base, int64_t device) {
   const at::DeviceGuard guard(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(device)));
@@ -423,8 +426,16 @@ void train_call(const at::Tensor& ctx, int64_t op, int64_t layer, int64_t flag, 
       check(apneauq::train_launch_fwd(A, (int)layer, s), "train fwd");
       break;
     case 1: check(apneauq::train_launch_head(A, (int)flag, s), "train head"); break;
-    case 2: TORCH_CHECK(layer >= 1 && layer < 6); check(apneauq::train_launch_dgrad(A, (int)layer, s), "train dgrad"); break;
-    case 3: TORCH_CHECK(layer >= 0 && layer < 6); check(apneauq::train_launch_wgrad(A, (int)layer, s), "train wgrad"); break;
+    case 2:
+      TORCH_CHECK(layer >= 1 && layer < 6);
+      A.bwd_self = (int)(flag & 1);
+      check(apneauq::train_launch_dgrad(A, (int)layer, s), "train dgrad");
+      break;
+    case 3:
+      TORCH_CHECK(layer >= 0 && layer < 6);
+      A.bwd_self = (int)(flag & 1);
+      check(apneauq::train_launch_wgrad(A, (int)layer, s), "train wgrad");
+      break;
     case 4: check(apneauq::train_launch_finalize(A, (int)layer, (int)flag, s), "train finalize"); break;
     case 5: check(apneauq::train_launch_tab(A, (int)flag, (int)layer, s), "train param table"); break;
     default: TORCH_CHECK(false, "train_call: unknown op ", op);

@@ -81,6 +81,10 @@ struct Args {
                        // [kStatSlots][96 + 2] fp32 slots (workgroup % kStatSlots) that bn_finalize adds
                        // in slot order, instead of 256 workgroups' atomics on the same 98 addresses
                        // (nullptr: direct atomics)
+  int bwd_self;        // dgrad / wgrad launch flag (not in the ctx): sum the backward BN rows of block l
+                       // from bst[l] themselves instead of reading the table rows that wgrad_reduce's
+                       // side job writes -- so a wgrad chain on a second stream (GraphedTrainStep
+                       // overlap) carries no dependency back into the dgrad chain
 };
 
 template <typename T>

@@ -1010,7 +1010,7 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A_, const Args*
       gr[c] = tab_row(A, l, kTabS)[c];
       mean[c] = tab_row(A, l, kTabMean)[c];
       rstd[c] = tab_row(A, l, kTabRstd)[c];
-      if constexpr (l == 5) {  // block 6's backward sums come from the head, no table job in between
+      if (l == 5 || A.bwd_self) {  // block 6's backward sums come from the head, no table job in between
         mdy[c] = (float)(slot_sumd(A.L[l].bst + c, 2 * CIN) * (double)A.inv_count);
         mdyx[c] = (float)(slot_sumd(A.L[l].bst + CIN + c, 2 * CIN) * (double)A.inv_count);
       } else {
@@ -1221,7 +1221,7 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A_
       gr[c] = tab_row(A, l, kTabS)[c];
       mean[c] = tab_row(A, l, kTabMean)[c];
       rstd[c] = tab_row(A, l, kTabRstd)[c];
-      if constexpr (l == 5) {
+      if (l == 5 || A.bwd_self) {
         mdy[c] = (float)(slot_sumd(A.L[l].bst + c, 2 * COUT) * (double)A.inv_count);
         mdyx[c] = (float)(slot_sumd(A.L[l].bst + COUT + c, 2 * COUT) * (double)A.inv_count);
       } else {
@@ -1558,7 +1558,7 @@ static void wg_launch(const Args& A, const Args* Am, int M, hipStream_t st) {
     const int blocks = std::min(2048, (s4 * J + 255) / 256);
     // side job: block l-1's backward rows of the parameter table (bst[l-1] is complete after dgrad<l>,
     // which ran before this wgrad) for dgrad<l-1> / wgrad<l-1>
-    const bool side = A.tab != nullptr && l >= 1;
+    const bool side = A.tab != nullptr && l >= 1 && !A.bwd_self;
     if constexpr (MB) {
       hipLaunchKernelGGL(train::wgrad_reduce_mb_kernel, dim3(blocks + (side ? 1 : 0), 1, M), dim3(256), 0, st, Am, l,
                          rgs, kcc, train::C[l + 1], J, side ? 1 : 0);

@@ -203,6 +203,11 @@ def _call(ctx, op, layer=0, flag=0, pass_base=-1, device=0):
 # two runs give bitwise-identical weights.  APNEAUQ_DETERMINISTIC=1 or set_deterministic(True);
 # costs a few small reduce launches per step.
 DETERMINISTIC = os.environ.get("APNEAUQ_DETERMINISTIC", "0") not in ("", "0")
+# GraphedTrainStep: dgrad and wgrad chains on two captured streams (APNEAUQ_TRAIN_OVERLAP=1).  Off by
+# default: the chains do run concurrently (34 % of kernel time overlapped at batch 1024) but each
+# kernel already holds every CU, so both slow ~2x and the step got slower (0.76 -> 0.82 ms at batch
+# 1024, 4.37 -> 4.51 ms at 8192; profiles/train_step_r4.md)
+OVERLAP = os.environ.get("APNEAUQ_TRAIN_OVERLAP", "0") not in ("", "0")
 
 
 def set_deterministic(flag: bool = True) -> None:
@@ -340,6 +345,9 @@ class GraphedTrainStep:
         # tensor objects (a restored optimizer state or a moved model triggers a re-capture)
         self.bound = bound_key(model)
         self._sync_counters()
+        # wgrad chain on a second captured stream (see _body); needs the parameter table
+        self.overlap = OVERLAP and self.ws.tab is not None and not self.deterministic
+        self.aux = torch.cuda.Stream(dev) if self.overlap else None
         outs = []
         self.graph = capture_graph(lambda: outs.extend(self._body()), dev)
         self.loss_out, self.probs_out = outs
@@ -361,10 +369,33 @@ class GraphedTrainStep:
             _call(self.ctx, 0, l, 0, TRAIN_PASS_BASE, dev)
         _call(self.ctx, 5, 0, 0, TRAIN_PASS_BASE, dev)  # BN parameter table (forward rows)
         _call(self.ctx, 1, 0, 1, TRAIN_PASS_BASE, dev)
-        for l in range(5, 0, -1):
-            _call(self.ctx, 2, l, 0, TRAIN_PASS_BASE, dev)
-            _call(self.ctx, 3, l, 0, TRAIN_PASS_BASE, dev)
-        _call(self.ctx, 3, 0, 0, TRAIN_PASS_BASE, dev)
+        if self.overlap:
+            # wgrad_l needs only dgrad_l's dZ_l (and forward state), and no dgrad reads a wgrad
+            # output: the wgrad + reduce chain runs on its own stream, forked after each dgrad and
+            # joined before the finalize / Adam (measured slower, see OVERLAP).  Both sum the backward
+            # BN rows from the slots (flag 1) -- the table rows come from the reduces' side job, which
+            # would tie dgrad_{l-1} to wgrad_l again.
+            main, aux = torch.cuda.current_stream(), self.aux
+            self._evs = []  # alive for the capture
+            for l in range(5, 0, -1):
+                _call(self.ctx, 2, l, 1, TRAIN_PASS_BASE, dev)
+                ev = torch.cuda.Event()
+                self._evs.append(ev)
+                ev.record(main)
+                aux.wait_event(ev)
+                with torch.cuda.stream(aux):
+                    _call(self.ctx, 3, l, 1, TRAIN_PASS_BASE, dev)
+            with torch.cuda.stream(aux):
+                _call(self.ctx, 3, 0, 1, TRAIN_PASS_BASE, dev)
+            ev = torch.cuda.Event()
+            self._evs.append(ev)
+            ev.record(aux)
+            main.wait_event(ev)
+        else:
+            for l in range(5, 0, -1):
+                _call(self.ctx, 2, l, 0, TRAIN_PASS_BASE, dev)
+                _call(self.ctx, 3, l, 0, TRAIN_PASS_BASE, dev)
+            _call(self.ctx, 3, 0, 0, TRAIN_PASS_BASE, dev)
         _call(self.ctx, 4, 1, 1, TRAIN_PASS_BASE, dev)
         opt = self.model.optimizer
         o.adam_step(self.model.store.flat, ws.grad, opt.m, opt.v, opt.beta_1, opt.beta_2, opt.learning_rate,
