@@ -1191,6 +1191,9 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A_
   constexpr int DZRS = wg_rs(W::COB * 2);       // LDS row strides (bytes): odd multiples of 32 B
   constexpr int ARS = wg_rs(FIRST ? 64 : W::CIB * 2);
   static_assert(W::WCO * W::WCI == 4, "4 waves");
+  static_assert((FIRST || CIN % W::CIB == 0) && COUT % W::COB == 0 && W::CIB % (16 * W::WCI) == 0 &&
+                    W::COB % (16 * W::WCO) == 0,
+                "wgrad blocks must tile Cin x Cout exactly (e.g. CIB 64 on Cin 224 dropped channels)");
   char* dz_lds = smem;                                   // 128 rows x COB
   char* a_lds = smem + kR * DZRS;                        // 136 rows x CIB (or 128 x 32 im2col)
   float* prm = reinterpret_cast<float*>(a_lds + kRows * ARS);
