@@ -1142,6 +1142,13 @@ template <int l> struct WgCfg;
 // workgroups per CU save 17 % on block 4 and spill on block 6)
 // wgrad LDS tiles: the row stride is an odd multiple of 32 B (conflict-free tr_frag reads)
 __host__ __device__ constexpr int wg_rs(int width_bytes) { return (width_bytes / 32) % 2 ? width_bytes : width_bytes + 32; }
+// wgrad of block 4 prefetches the next row tile into registers during the MFMAs
+// (-DAPNEAUQ_WG_NOPF: stage each tile between the barriers, the round-3 loop)
+#ifdef APNEAUQ_WG_NOPF
+constexpr bool kWgPrefetch = false;
+#else
+constexpr bool kWgPrefetch = true;
+#endif
 // A/B builds may replace an entry (-DAPNEAUQ_WGCFG4='CIB = 32, COB = 128, ...'): every entry is a
 // complete, correct configuration, only the speed differs.
 // MINWG values: batch-1024 step measured with tools/probes/train_variants.sh (block 5 512 -> 768 took
@@ -1164,7 +1171,7 @@ template <> struct WgCfg<2> { static constexpr int CIB = 32, COB = 224, WCO = 2,
 #ifdef APNEAUQ_WGCFG3
 template <> struct WgCfg<3> { static constexpr int APNEAUQ_WGCFG3; };
 #else
-template <> struct WgCfg<3> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = 512, U = 8, MINB = 3; };
+template <> struct WgCfg<3> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = 512, U = 8, MINB = kWgPrefetch ? 2 : 3; };
 #endif
 #ifdef APNEAUQ_WGCFG4
 template <> struct WgCfg<4> { static constexpr int APNEAUQ_WGCFG4; };
@@ -1289,16 +1296,79 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A_
   // sizes the grid for >= ~512 workgroups)
   const int rgs = gridDim.x / (nci_blk * nco_blk);
   const int rt = (ntiles + rgs - 1) / rgs;
-  for (int it = 0; it < rt; ++it) {
-    const int tile = rg * rt + it;
-    if (tile >= ntiles) break;
+  const int tile0 = rg * rt, nt = min(rt, ntiles - tile0);
+  // Block 4 (kWgPrefetch, PF below): the next tile's dZ_l and R_{l-1} rows are loaded into registers
+  // before this tile's MFMAs and written to LDS (A decoded) after them, so the global-load latency
+  // of a tile hides under the previous tile's matrix work instead of being paid between barriers.
+  // One stats group (training): A_{l-1} = dropout(BN(R_{l-1})) with the table's single affine.
+  // block 4 only: blocks 2, 3 and 6 have no registers left for the prefetch (spills), and block 5
+  // loses more from 2 instead of 3 workgroups per CU than the prefetch gains (wgrad<4> 276 -> 333 us
+  // at batch 8192; wgrad<3>: 278 -> 243 us; profiles/train_step_r4.md)
+  constexpr bool PF = kWgPrefetch && l == 3;
+  constexpr int NCWD = W::COB / 8, ITD = PF ? kR * NCWD / kThreads : 1;
+  constexpr int NCWA = W::CIB / 8, RPA = kThreads / NCWA, ITA = PF ? (kRows + RPA - 1) / RPA : 1;
+  static_assert(!PF || (kR * NCWD) % kThreads == 0, "dZ rows split evenly over the threads");
+  bf16x8 pd[ITD];
+  u32x4 pa[ITA];
+  // the thread index is made opaque per call (see staged_loop): otherwise LICM keeps every item's
+  // offset live across the tile loop (~100 VGPRs of spills)
+  auto opaque_tid = [] {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+  };
+  auto pf_load = [&](int tile) {
+    const int ptid = opaque_tid(), cwa = ptid % NCWA, rina = ptid / NCWA;
+    const int row0 = kR * tile;
+    const __bf16* dz = A.L[l].dZ + (long long)(row0 + kHalo) * COUT + co0;
+#pragma unroll
+    for (int i = 0; i < ITD; ++i) {
+      const int idx = ptid + i * kThreads, rc = idx / NCWD, cw = idx - rc * NCWD;
+      pd[i] = gld<bf16x8>(dz + (long long)rc * COUT + cw * 8);
+    }
+    if constexpr (PF) {
+      const __bf16* R = A.L[l - 1].R + (long long)row0 * CIN + ci0 + cwa * 8;
+#pragma unroll
+      for (int j = 0; j < ITA; ++j) {
+        const int rc = rina + j * RPA;
+        if (rc < kRows) pa[j] = gld<u32x4>(R + (long long)rc * CIN);
+      }
+    }
+  };
+  auto pf_store = [&]() {
+    const int ptid = opaque_tid(), cwa = ptid % NCWA, rina = ptid / NCWA;
+#pragma unroll
+    for (int i = 0; i < ITD; ++i) {
+      const int idx = ptid + i * kThreads, rc = idx / NCWD, cw = idx - rc * NCWD;
+      *reinterpret_cast<bf16x8*>(dz_lds + lds_off(rc, cw * 16, DZRS)) = pd[i];
+    }
+    if constexpr (PF) {
+      const float dsc = A.dropout != 0 ? A.L[l - 1].dsc : 1.f;
+      float s0[8], t0[8];
+      lds_row8(sp, ci0 + cwa * 8, dsc, s0);
+      lds_row8(tp, ci0 + cwa * 8, dsc, t0);
+#pragma unroll
+      for (int j = 0; j < ITA; ++j) {
+        const int rc = rina + j * RPA;
+        if (rc >= kRows) continue;
+        u32x4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = decode_pair(pa[j][q], s0[2 * q], t0[2 * q], s0[2 * q + 1], t0[2 * q + 1]);
+        *reinterpret_cast<u32x4*>(a_lds + lds_off(rc, cwa * 16, ARS)) = o;
+      }
+    }
+  };
+  if constexpr (PF) {
+    if (nt > 0) pf_load(tile0);
+  }
+  for (int it = 0; it < nt; ++it) {
+    const int tile = tile0 + it;
     const int row0 = kR * tile;
     __syncthreads();
-    if constexpr (FIRST)  // no dgrad for block 1: dZ_1 is recomputed here (a single ci block)
+    if constexpr (PF) {
+      pf_store();
+    } else if constexpr (FIRST) {  // no dgrad for block 1: dZ_1 is recomputed here (a single ci block)
       stage_dz<l, kR, W::COB / 8>(A, dz_lds, DZRS, row0 + kHalo, co0, gr, mean, rstd, mdy, mdyx);
-    else
-      stage_dz_copy<l, kR, W::COB / 8, W::U>(A, dz_lds, DZRS, row0 + kHalo, co0);
-    if constexpr (FIRST) {
       // im2col of the raw input: col kk = tap*4 + ci (kk < 28), rows = tile rows
       for (int i = threadIdx.x; i < kR * 32; i += kThreads) {
         const int r = i >> 5, kk = i & 31;
@@ -1308,9 +1378,13 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A_
         *reinterpret_cast<__bf16*>(a_lds + lds_off(r, kk * 2, ARS)) = v;
       }
     } else {
+      stage_dz_copy<l, kR, W::COB / 8, W::U>(A, dz_lds, DZRS, row0 + kHalo, co0);
       stage_act<l - 1, kRows, W::CIB / 8, 4>(A, a_lds, ARS, row0, ci0, sp, tp, 0);
     }
     __syncthreads();
+    if constexpr (PF) {
+      if (it + 1 < nt) pf_load(tile + 1);
+    }
 #pragma unroll
     for (int ks = 0; ks < kR / 32; ++ks) {
       bf16x8 fb[NCO];
@@ -1601,7 +1675,10 @@ static hipError_t wgrad_launch(const Args& A, const Args* Am, int M, int l, hipS
   return hipGetLastError();
 }
 
-hipError_t train_launch_wgrad(const Args& A, int l, hipStream_t st) { return wgrad_launch<false>(A, nullptr, 1, l, st); }
+hipError_t train_launch_wgrad(const Args& A, int l, hipStream_t st) {
+  if (A.groups != 1) return hipErrorInvalidValue;  // training: one stats group (the staging's single affine)
+  return wgrad_launch<false>(A, nullptr, 1, l, st);
+}
 
 hipError_t train_launch_finalize(const Args& A, int update_moving, int grads, hipStream_t st) {
   hipLaunchKernelGGL(train::bn_finalize_kernel<false>, dim3(6), dim3(256), 0, st, A, nullptr, update_moving, grads);
