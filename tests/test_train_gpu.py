@@ -158,7 +158,10 @@ def test_graphed_training_step_matches_eager(monkeypatch, deterministic):
 def test_graphed_step_overlap_matches_single_stream(monkeypatch):
     """The graphed step with the wgrad chain on its own captured stream (train_ops.OVERLAP) computes
     the gradients of the one-stream graph: same loss and, up to the atomics' summation order, the
-    same flat gradient (the backward BN rows are summed from the same fp64 slots either way)."""
+    same gradient of every parameter (the backward BN rows are summed from the same fp64 slots either
+    way).  The atomic mode's order noise moves single near-zero elements through bf16 rounding (seen:
+    3.7e-5 absolute), so each tensor is compared by its relative L2 error; a missing fork / join
+    edge would leave a whole tensor stale or half-summed (O(1) error)."""
     from uncertaintyquantification_sleepapnea_1dcnn_amd.data.synthetic import synthetic_windows
 
     x, y, _ = synthetic_windows(512, seed=9)
@@ -173,11 +176,13 @@ def test_graphed_step_overlap_matches_single_stream(monkeypatch):
         loss = float(m.train_step(x, y))
         step = m._train_graphs[512]
         assert step.overlap == ov
-        out[ov] = (loss, step.ws.grad.clone())
+        out[ov] = (loss, {k: v.clone() for k, v in step.ws.gviews.items()})
     assert abs(out[True][0] - out[False][0]) <= 1e-5 * abs(out[False][0])
-    g0, g1 = out[False][1], out[True][1]
-    assert torch.isfinite(g1).all()
-    assert torch.allclose(g1, g0, rtol=2e-3, atol=1e-6), (g1 - g0).abs().max().item()
+    for name, g0 in out[False][1].items():
+        g1 = out[True][1][name]
+        assert torch.isfinite(g1).all(), name
+        rel = ((g1 - g0).norm() / g0.norm().clamp_min(1e-30)).item()
+        assert rel < 5e-3, (name, rel)
 
 
 def test_fit_concurrent_on_streams_matches_sequential(deterministic):

@@ -1142,7 +1142,7 @@ template <int l> struct WgCfg;
 // workgroups per CU save 17 % on block 4 and spill on block 6)
 // wgrad LDS tiles: the row stride is an odd multiple of 32 B (conflict-free tr_frag reads)
 __host__ __device__ constexpr int wg_rs(int width_bytes) { return (width_bytes / 32) % 2 ? width_bytes : width_bytes + 32; }
-// wgrad of block 4 prefetches the next row tile into registers during the MFMAs
+// wgrad of blocks 4 and 6 prefetch the next row tile into registers during the MFMAs
 // (-DAPNEAUQ_WG_NOPF: stage each tile between the barriers, the round-3 loop)
 #ifdef APNEAUQ_WG_NOPF
 constexpr bool kWgPrefetch = false;
@@ -1297,16 +1297,17 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A_
   const int rgs = gridDim.x / (nci_blk * nco_blk);
   const int rt = (ntiles + rgs - 1) / rgs;
   const int tile0 = rg * rt, nt = min(rt, ntiles - tile0);
-  // Block 4 (kWgPrefetch, PF below): the next tile's dZ_l and R_{l-1} rows are loaded into registers
+  // Blocks 4 and 6 (kWgPrefetch, PF below): the next tile's dZ_l and R_{l-1} rows are loaded into registers
   // before this tile's MFMAs and written to LDS (A decoded) after them, so the global-load latency
   // of a tile hides under the previous tile's matrix work instead of being paid between barriers.
   // One stats group (training): A_{l-1} = dropout(BN(R_{l-1})) with the table's single affine.
-  // block 4 only: blocks 2, 3 and 6 have no registers left for the prefetch (spills), and block 5
+  // blocks 4 and 6 (dZ only): blocks 2 and 3 have no registers left for it (spills), and block 5
   // loses more from 2 instead of 3 workgroups per CU than the prefetch gains (wgrad<4> 276 -> 333 us
   // at batch 8192; wgrad<3>: 278 -> 243 us; profiles/train_step_r4.md)
-  constexpr bool PF = kWgPrefetch && l == 3;
+  constexpr bool PF = kWgPrefetch && (l == 3 || l == 5);
+  constexpr bool PFA = PF && l == 3;  // block 6: dZ only (the A rows would spill)
   constexpr int NCWD = W::COB / 8, ITD = PF ? kR * NCWD / kThreads : 1;
-  constexpr int NCWA = W::CIB / 8, RPA = kThreads / NCWA, ITA = PF ? (kRows + RPA - 1) / RPA : 1;
+  constexpr int NCWA = W::CIB / 8, RPA = kThreads / NCWA, ITA = PFA ? (kRows + RPA - 1) / RPA : 1;
   static_assert(!PF || (kR * NCWD) % kThreads == 0, "dZ rows split evenly over the threads");
   bf16x8 pd[ITD];
   u32x4 pa[ITA];
@@ -1326,7 +1327,7 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A_
       const int idx = ptid + i * kThreads, rc = idx / NCWD, cw = idx - rc * NCWD;
       pd[i] = gld<bf16x8>(dz + (long long)rc * COUT + cw * 8);
     }
-    if constexpr (PF) {
+    if constexpr (PFA) {
       const __bf16* R = A.L[l - 1].R + (long long)row0 * CIN + ci0 + cwa * 8;
 #pragma unroll
       for (int j = 0; j < ITA; ++j) {
@@ -1342,7 +1343,7 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A_
       const int idx = ptid + i * kThreads, rc = idx / NCWD, cw = idx - rc * NCWD;
       *reinterpret_cast<bf16x8*>(dz_lds + lds_off(rc, cw * 16, DZRS)) = pd[i];
     }
-    if constexpr (PF) {
+    if constexpr (PFA) {
       const float dsc = A.dropout != 0 ? A.L[l - 1].dsc : 1.f;
       float s0[8], t0[8];
       lds_row8(sp, ci0 + cwa * 8, dsc, s0);
@@ -1367,6 +1368,7 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A_
     __syncthreads();
     if constexpr (PF) {
       pf_store();
+      if constexpr (!PFA) stage_act<l - 1, kRows, W::CIB / 8, 4>(A, a_lds, ARS, row0, ci0, sp, tp, 0);
     } else if constexpr (FIRST) {  // no dgrad for block 1: dZ_1 is recomputed here (a single ci block)
       stage_dz<l, kR, W::COB / 8>(A, dz_lds, DZRS, row0 + kHalo, co0, gr, mean, rstd, mdy, mdyx);
       // im2col of the raw input: col kk = tap*4 + ci (kk < 28), rows = tile rows
