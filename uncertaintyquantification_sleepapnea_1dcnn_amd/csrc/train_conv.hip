@@ -1371,13 +1371,13 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A_
       if constexpr (!PFA) stage_act<l - 1, kRows, W::CIB / 8, 4>(A, a_lds, ARS, row0, ci0, sp, tp, 0);
     } else if constexpr (FIRST) {  // no dgrad for block 1: dZ_1 is recomputed here (a single ci block)
       stage_dz<l, kR, W::COB / 8>(A, dz_lds, DZRS, row0 + kHalo, co0, gr, mean, rstd, mdy, mdyx);
-      // im2col of the raw input: col kk = tap*4 + ci (kk < 28), rows = tile rows
-      for (int i = threadIdx.x; i < kR * 32; i += kThreads) {
-        const int r = i >> 5, kk = i & 31;
-        const int tap = kk >> 2, ci = kk & 3;
-        __bf16 v = (__bf16)0.f;
-        if (tap < K) v = A.x[(long long)(row0 + kHalo + r + tap - PAD) * 4 + ci];
-        *reinterpret_cast<__bf16*>(a_lds + lds_off(r, kk * 2, ARS)) = v;
+      // im2col of the raw input: col kk = tap*4 + ci (kk < 28), rows = tile rows; one 8-B load per
+      // (row, tap) -- the 4 channels of an input row are contiguous
+      for (int i = threadIdx.x; i < kR * 8; i += kThreads) {
+        const int r = i >> 3, tap = i & 7;
+        bf16x4 v = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
+        if (tap < K) v = gld<bf16x4>(A.x + (long long)(row0 + kHalo + r + tap - PAD) * 4);
+        *reinterpret_cast<bf16x4*>(a_lds + lds_off(r, tap * 8, ARS)) = v;
       }
     } else {
       stage_dz_copy<l, kR, W::COB / 8, W::U>(A, dz_lds, DZRS, row0 + kHalo, co0);
