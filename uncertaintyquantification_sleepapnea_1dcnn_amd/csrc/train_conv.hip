@@ -801,10 +801,11 @@ __global__ __launch_bounds__(256) void tab_kernel(Args A_, const Args* __restric
 // each lane owning channels (lane, lane + 64).
 // ------------------------------------------------------------------------------------------------
 template <bool MB>
-__global__ __launch_bounds__(kThreads) void head_kernel(Args A_, const Args* __restrict__ Am, int backward) {
+__global__ __launch_bounds__(kThreads) void head_kernel(Args A_, const Args* __restrict__ Am, int backward, int spw) {
   const MbPos pos = mb_pos<MB>();
   const Args& A = member_args<MB>(A_, Am, pos);
-  // One sample per wave.  Lane (cw, ph) = (lane % 12, lane / 12), lanes 0..59: channels
+  // One sample at a time per wave, spw samples per wave (4 * spw per workgroup: fewer workgroups'
+  // sums to merge at large batches).  Lane (cw, ph) = (lane % 12, lane / 12), lanes 0..59: channels
   // [8cw, 8cw+8) of rows ph, ph+5, ..., ph+55 — twelve 16-B loads per lane, all in flight at once
   // (the previous per-channel/per-row scalar loop was load-latency bound: ~50 us at any batch size).
   constexpr int Cc = C[6], NCW = Cc / 8, NPH = 5, NJ = kL / NPH;
@@ -816,10 +817,10 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A_, const Args* __r
   float* bsum1 = bsum0 + Cc;
   float* red = bsum1 + Cc;      // per-workgroup loss / dense-bias sums: one global atomic per workgroup
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int n = pos.bx * 4 + wave;
+  const int nwg0 = pos.bx * 4 * spw;  // the workgroup's first sample
   const Layer& Ly = A.L[5];
-  const int g_first = min(pos.bx * 4, A.B - 1) / A.n_win;
-  const int g_last = min(pos.bx * 4 + 3, A.B - 1) / A.n_win;
+  const int g_first = min(nwg0, A.B - 1) / A.n_win;
+  const int g_last = min(nwg0 + 4 * spw - 1, A.B - 1) / A.n_win;
   for (int c = threadIdx.x; c < 3 * Cc + 2; c += kThreads) dw[c] = 0.f;
   auto params = [&](int g) {
     if (A.tab != nullptr) {  // single-device training (one group): the forward rows of T[5]
@@ -845,57 +846,58 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A_, const Args* __r
   };
   params(g_first);
   __syncthreads();
-  // (a workgroup whose 4 samples span two stats groups — an MC-Dropout pass boundary with n_win
-  //  not a multiple of 4 — recomputes its per-lane parameters from the global sums directly)
+  // (a workgroup whose samples span two stats groups — an MC-Dropout pass boundary — recomputes
+  //  its per-lane parameters of the other group from the global sums directly)
   const bool mixed = g_first != g_last;
   const int cw = lane % NCW, ph = lane / NCW;
-  const bool active = n < A.B && lane < NCW * NPH;
   const int c0 = cw * 8;
-  float mu[8], rs[8], sc[8], sh[8], w[8];
-  if (active) {
-    const int g = n / A.n_win;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = c0 + j;
-      if (mixed && g != g_first) {
-        float m1, var;
-        bn_moments(A, 5, g, c, m1, var);
-        rs[j] = rsqrtf(var + A.eps);
-        mu[j] = m1;
-        sc[j] = Ly.gamma[c] * rs[j];
-        sh[j] = Ly.beta[c] - m1 * sc[j];
-      } else {
-        mu[j] = pmu[c];
-        rs[j] = prs[c];
-        sc[j] = psc[c];
-        sh[j] = psh[c];
-      }
-      w[j] = pw[c];
-    }
-  }
-  bf16x8 v[NJ];
-  float gap[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const float dsc6 = A.dropout ? Ly.dsc : 1.f;
-  if (active) {
-    const __bf16* base = Ly.R + (long long)(kHalo + n * kSR) * Cc + c0;
+  for (int s = 0; s < spw; ++s) {  // wave-uniform
+    const int n = nwg0 + s * 4 + wave;
+    const bool active = n < A.B && lane < NCW * NPH;
+    float mu[8], rs[8], sc[8], sh[8], w[8];
+    if (active) {
+      const int g = n / A.n_win;
 #pragma unroll
-    for (int k = 0; k < NJ; ++k) v[k] = gld<bf16x8>(base + (long long)(ph + NPH * k) * Cc);
-#pragma unroll
-    for (int k = 0; k < NJ; ++k) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {  // block 6's dropout mask is R_6's sign bit
-        const float a = bf_abs(v[k][j]) * sc[j] + sh[j];
-        gap[j] += bf_dropped(v[k][j]) ? 0.f : a * dsc6;
+      for (int j = 0; j < 8; ++j) {
+        const int c = c0 + j;
+        if (mixed && g != g_first) {
+          float m1, var;
+          bn_moments(A, 5, g, c, m1, var);
+          rs[j] = rsqrtf(var + A.eps);
+          mu[j] = m1;
+          sc[j] = Ly.gamma[c] * rs[j];
+          sh[j] = Ly.beta[c] - m1 * sc[j];
+        } else {
+          mu[j] = pmu[c];
+          rs[j] = prs[c];
+          sc[j] = psc[c];
+          sh[j] = psh[c];
+        }
+        w[j] = pw[c];
       }
     }
-  }
-  float part = 0.f;
+    bf16x8 v[NJ];
+    float gap[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (active) {
+      const __bf16* base = Ly.R + (long long)(kHalo + n * kSR) * Cc + c0;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) part += gap[j] * w[j];
-  const float z = wave_sum(active ? part : 0.f) * (1.0f / kL) + A.dense_b[0];
-  if (n < A.B && lane == 0) A.logits[n] = z;
-  if (backward) {
-    if (n < A.B) {
+      for (int k = 0; k < NJ; ++k) v[k] = gld<bf16x8>(base + (long long)(ph + NPH * k) * Cc);
+#pragma unroll
+      for (int k = 0; k < NJ; ++k) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {  // block 6's dropout mask is R_6's sign bit
+          const float a = bf_abs(v[k][j]) * sc[j] + sh[j];
+          gap[j] += bf_dropped(v[k][j]) ? 0.f : a * dsc6;
+        }
+      }
+    }
+    float part = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) part += gap[j] * w[j];
+    const float z = wave_sum(active ? part : 0.f) * (1.0f / kL) + A.dense_b[0];
+    if (n < A.B && lane == 0) A.logits[n] = z;
+    if (backward && n < A.B) {
       const float pz = 1.0f / (1.0f + __expf(-z));
       const float yv = A.y[n];
       const float dl = (pz - yv) * A.inv_batch;
@@ -923,34 +925,34 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A_, const Args* __r
             b1[j] += dy * xh;
           }
         }
-        if (rec != nullptr) {
-          // the sample's sums over its 5 row-phase lanes (lanes cw + 12 ph), in a fixed order
+        // the sample's sums over its 5 row-phase lanes (lanes cw + 12 ph), in a fixed order; then
+        // one LDS atomic per channel from the ph = 0 lanes (not 5)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            float sdw = 0.f, sb0 = 0.f, sb1 = 0.f;
-            const float pdw = dl * gap[j] * (1.0f / kL);
+        for (int j = 0; j < 8; ++j) {
+          float sdw = 0.f, sb0 = 0.f, sb1 = 0.f;
+          const float pdw = dl * gap[j] * (1.0f / kL);
 #pragma unroll
-            for (int q = 0; q < NPH; ++q) {
-              sdw += __shfl(pdw, cw + NCW * q, kWave);
-              sb0 += __shfl(b0[j], cw + NCW * q, kWave);
-              sb1 += __shfl(b1[j], cw + NCW * q, kWave);
-            }
-            if (ph == 0) {
+          for (int q = 0; q < NPH; ++q) {
+            sdw += __shfl(pdw, cw + NCW * q, kWave);
+            sb0 += __shfl(b0[j], cw + NCW * q, kWave);
+            sb1 += __shfl(b1[j], cw + NCW * q, kWave);
+          }
+          if (ph == 0) {
+            if (rec != nullptr) {
               rec[2 + c0 + j] = sdw;
               rec[2 + Cc + c0 + j] = sb0;
               rec[2 + 2 * Cc + c0 + j] = sb1;
+            } else {
+              atomicAdd(&dw[c0 + j], sdw);
+              atomicAdd(&bsum0[c0 + j], sb0);
+              atomicAdd(&bsum1[c0 + j], sb1);
             }
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            atomicAdd(&dw[c0 + j], dl * gap[j] * (1.0f / kL));
-            atomicAdd(&bsum0[c0 + j], b0[j]);
-            atomicAdd(&bsum1[c0 + j], b1[j]);
           }
         }
       }
     }
+  }
+  if (backward) {
     if (A.det != nullptr) return;  // det_reduce_kernel sums the per-sample records
     __syncthreads();
     float* hp = A.hpart != nullptr ? A.hpart + (pos.bx % kStatSlots) * (Cc + 2) : nullptr;
@@ -1576,9 +1578,19 @@ hipError_t train_launch_tab(const Args& A, int mode, int l, hipStream_t st) {
   return hipGetLastError();
 }
 
+// training head samples per wave: 1 while that leaves <= 512 workgroups, else up to 4 (batch 8192:
+// 512 workgroups instead of 2048, a quarter of the per-workgroup global sums onto the same 16 slots);
+// the forward-only head (MC Dropout, no sums) keeps one sample per wave
+static int head_spw(int B, int M, int backward) {
+  int spw = 1;
+  while (backward && spw < 4 && (long long)B * M > 512LL * 4 * spw) spw *= 2;
+  return spw;
+}
+
 hipError_t train_launch_head(const Args& A, int backward, hipStream_t st) {
-  hipLaunchKernelGGL(train::head_kernel<false>, dim3((A.B + 3) / 4), dim3(256), (8 * train::C[6] + 2) * 4, st, A, nullptr,
-                     backward);
+  const int spw = head_spw(A.B, 1, backward);
+  hipLaunchKernelGGL(train::head_kernel<false>, dim3((A.B + 4 * spw - 1) / (4 * spw)), dim3(256), (8 * train::C[6] + 2) * 4, st,
+                     A, nullptr, backward, spw);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess || !backward || A.det == nullptr) return e;
   constexpr int cc = train::C[6];  // per-sample records: loss, dlogit, dW, sum dY, sum dY xhat
@@ -1712,8 +1724,9 @@ hipError_t train_launch_mb(const Args& A0, const Args* Am, int M, int op, int la
       return det_reduce_mb(A0, Am, M, 0, layer, fwd_grid(A0.B), 2 * train::C[layer + 1], st);
     }
     case 1: {
-      hipLaunchKernelGGL(train::head_kernel<true>, dim3((A0.B + 3) / 4, 1, M), dim3(256), (8 * train::C[6] + 2) * 4, st, A0,
-                         Am, flag);
+      const int spw = head_spw(A0.B, M, flag);
+      hipLaunchKernelGGL(train::head_kernel<true>, dim3((A0.B + 4 * spw - 1) / (4 * spw), 1, M), dim3(256),
+                         (8 * train::C[6] + 2) * 4, st, A0, Am, flag, spw);
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess || !det || !flag) return e;
       return det_reduce_mb(A0, Am, M, 1, 0, A0.B, train::kHeadRec, st);
