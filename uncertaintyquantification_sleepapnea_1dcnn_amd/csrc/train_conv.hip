@@ -1154,7 +1154,9 @@ constexpr bool kWgPrefetch = true;
 // A/B builds may replace an entry (-DAPNEAUQ_WGCFG4='CIB = 32, COB = 128, ...'): every entry is a
 // complete, correct configuration, only the speed differs.
 // MINWG values: batch-1024 step measured with tools/probes/train_variants.sh (block 5 512 -> 768 took
-// the step 0.795 -> 0.786 ms, block 2 256 -> 512 0.766-0.775 -> 0.758-0.768 ms, three interleaved rounds)
+// the step 0.795 -> 0.786 ms, block 2 256 -> 512 0.766-0.775 -> 0.758-0.768 ms, three interleaved rounds;
+// round 4, with the straggler-free grouping: block 3 256 -> 512 batch 8192 4.20-4.22 -> 4.13-4.16 ms,
+// batch 1024 / 8 members unchanged; block 4 512 -> 1024 slower)
 #ifdef APNEAUQ_WGCFG0
 template <> struct WgCfg<0> { static constexpr int APNEAUQ_WGCFG0; };
 #else
@@ -1168,7 +1170,7 @@ template <> struct WgCfg<1> { static constexpr int CIB = 32, COB = 192, WCO = 2,
 #ifdef APNEAUQ_WGCFG2
 template <> struct WgCfg<2> { static constexpr int APNEAUQ_WGCFG2; };
 #else
-template <> struct WgCfg<2> { static constexpr int CIB = 32, COB = 224, WCO = 2, WCI = 2, RTILES = 8, MINWG = 256, U = 8, MINB = 2; };
+template <> struct WgCfg<2> { static constexpr int CIB = 32, COB = 224, WCO = 2, WCI = 2, RTILES = 8, MINWG = 512, U = 8, MINB = 2; };
 #endif
 #ifdef APNEAUQ_WGCFG3
 template <> struct WgCfg<3> { static constexpr int APNEAUQ_WGCFG3; };
