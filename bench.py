@@ -79,6 +79,8 @@ def parse(argv=None):
     ap.add_argument("--no-deviation", action="store_true", help="skip the fp32 deviation block")
     ap.add_argument("--no-train", action="store_true", help="skip the training block (extra.train)")
     ap.add_argument("--deviation-windows", type=int, default=1024)
+    ap.add_argument("--comm-steps", type=int, default=2,
+                    help="steps after the timed region with every collective metered (extra.comm; 0: off)")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu = dry run of launcher + collectives on gloo with the fp32 reference model")
     return ap.parse_args(argv)
@@ -124,6 +126,7 @@ def run(a):
     from uncertaintyquantification_sleepapnea_1dcnn_amd.models import reference as R
     from uncertaintyquantification_sleepapnea_1dcnn_amd.models.spec import DEFAULT_SPEC as SPEC
     from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import uq as uq_ops
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel import comm
     from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel import dist as pdist
     from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel import inference as pinf
     from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel import launch
@@ -157,7 +160,9 @@ def run(a):
                if member_parallel else list(range(a.members)))
     params_de = [{k: v.to(dev) for k, v in R.synthetic_params(SPEC, a.seed + 100 + m).items()} for m in mem_ids]
     use_pg = torch.distributed.is_available() and torch.distributed.is_initialized()
-    sync = (lambda t: torch.distributed.all_reduce(t)) if (use_pg and not cpu) or world > 1 else None
+    # SyncBN all-reduce of the fp64 BN moment sums (one per BN layer and pass chunk)
+    sync = ((lambda t: comm.run("syncbn_all_reduce", t, lambda: torch.distributed.all_reduce(t)))
+            if (use_pg and not cpu) or world > 1 else None)
 
     def make(precision):
         if cpu:
@@ -165,25 +170,32 @@ def run(a):
         cls = _X3Engine if precision == "fp32" else _Bf16Engine
         return cls(R, SPEC, params_mcd, params_de, world, start, n_glob, a.seed, a.passes, sync)
 
-    def timed(engine, mode: str, steps: int, warmup: int, step_base: int):
+    def timed(engine, mode: str, steps: int, warmup: int, step_base: int, comm_steps: int = 0):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if not cpu else None
         phase = [0.0, 0.0]
 
-        def step(i):
+        def step(i, meter=None):
             if ev:
                 ev[0].record()
             t0 = time.perf_counter()
+            if meter is not None:
+                meter.step()
+                meter.phase("mcd")
             pm = engine.mcd(mode, x_loc, step_base + i)
             s_mcd = pinf.aggregate_sums(uq_ops.metrics(pm), y_loc)
             if ev:
                 ev[1].record()
             t1 = time.perf_counter()
+            if meter is not None:
+                meter.phase("de")
             if member_parallel:
                 pd = pinf.all_to_all_members(engine.de(x_glob), world)
             else:
                 pd = engine.de(x_loc)
             s_de = pinf.aggregate_sums(uq_ops.metrics(pd), y_loc)
             sums = torch.stack([s_mcd, s_de])
+            if meter is not None:
+                meter.phase("aggregate")
             pdist.all_reduce_sum_(sums)
             if ev:
                 ev[2].record()
@@ -213,11 +225,22 @@ def run(a):
         if not cpu:
             torch.cuda.synchronize()
         elapsed = pdist.all_reduce_max(time.perf_counter() - t0)
-        return elapsed, sums, phase
+        # collective accounting (extra.comm): a few MORE steps after the timed region, metered (events
+        # around every collective), so the timed steps carry no instrumentation
+        comm_rec = None
+        if comm_steps > 0:
+            meter = comm.CommMeter()
+            with comm.metering(meter):
+                for i in range(comm_steps):
+                    step(warmup + steps + i, meter)
+            comm_rec = meter.summary()
+            comm_rec["note"] = "per step; metered on steps after the timed region; ms = HIP-event time on the compute stream"
+            pdist.barrier()
+        return elapsed, sums, phase, comm_rec
 
     head_prec = "fp32" if cpu else a.precision
     engine = make(head_prec)
-    elapsed, sums, phase = timed(engine, a.bn_mode, a.steps, a.warmup, 0)
+    elapsed, sums, phase, comm_rec = timed(engine, a.bn_mode, a.steps, a.warmup, 0, comm_steps=a.comm_steps)
     agg_mcd = pinf.finalize_aggregates(sums[0])
     agg_de = pinf.finalize_aggregates(sums[1])
     ms = elapsed * 1e3 / a.steps
@@ -234,7 +257,7 @@ def run(a):
         torch.cuda.empty_cache()
         eng2 = make(other)
         k2 = max(1, min(a.steps, 10))
-        e2, s2, ph2 = timed(eng2, a.bn_mode, k2, 1, 10_000)
+        e2, s2, ph2, _ = timed(eng2, a.bn_mode, k2, 1, 10_000)
         secondary = {
             "precision": other,
             "value": round(n_glob * k2 / e2, 1),
@@ -297,6 +320,7 @@ def run(a):
                 "effective_tflops_per_gpu": round(n_loc * (a.passes + a.members) * 2 * macs / (ms / 1e3) / 1e12, 1),
                 "mcd_mean_entropy": round(agg_mcd["mean_total_pred_entropy"], 6),
                 "de_mean_mutual_info": round(agg_de["mean_mutual_info"], 6),
+                "comm": comm_rec,
                 "fp32_deviation": deviation,
                 ("bf16" if head_prec == "fp32" else "fp32"): secondary,
                 "train": train,
@@ -482,8 +506,10 @@ class _CpuEngine:
         s = torch.stack([h.sum(dim=(0, 1)), (h * h).sum(dim=(0, 1))]).double()
         cnt = torch.tensor([float(h.shape[0] * h.shape[1])], dtype=torch.float64)
         if dist.is_initialized() and self.world > 1:
-            dist.all_reduce(s)
-            dist.all_reduce(cnt)
+            from uncertaintyquantification_sleepapnea_1dcnn_amd.parallel import comm
+
+            comm.run("syncbn_all_reduce", s, lambda: dist.all_reduce(s))
+            comm.run("syncbn_all_reduce", cnt, lambda: dist.all_reduce(cnt))
         mean = s[0] / cnt
         var = (s[1] / cnt - mean * mean).clamp_min(0)
         return mean.float(), var.float()

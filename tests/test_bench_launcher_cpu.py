@@ -56,3 +56,25 @@ def test_launch_spawn_exit_codes(n, tmp_path):
                       "sys.exit(7 if r == %d - 1 and %d > 1 else 0)\n" % (n, n, n))
     rc = launch.spawn(n, [sys.executable, str(script)])
     assert rc == (7 if n > 1 else 0)
+
+
+def test_bench_comm_block_counts_collectives():
+    """extra.comm: the metered steps after the timed region report, per step and phase,
+    how many collectives ran and their bytes.  2 ranks, T=3 passes, M=2 members (member-parallel):
+    MC Dropout = one SyncBN all-reduce of (sum, sum of squares) per BN layer and pass, plus one of the
+    row count (6 layers x 2 x T); Deep Ensemble = one all_to_all of the member probabilities; then one
+    all-reduce of the 2 x 9 fp64 aggregate sums."""
+    out = _bench("--gpus", "2", "--windows", "24", "--passes", "3", "--members", "2", "--steps", "1", "--warmup", "1",
+                 "--no-secondary", "--comm-steps", "2")
+    c = out["extra"]["comm"]
+    assert c["steps"] == 2
+    ph = c["phases"]
+    chans = 128 + 192 + 224 + 96 + 256 + 96
+    assert ph["mcd"]["syncbn_all_reduce"]["count"] == 6 * 2 * 3
+    assert ph["mcd"]["syncbn_all_reduce"]["bytes"] == 3 * (chans * 2 * 8 + 6 * 8)
+    assert ph["de"]["all_to_all"]["count"] == 1
+    assert ph["de"]["all_to_all"]["bytes"] == 2 * 1 * 24 * 4  # (ranks, members per rank, windows per rank) fp32
+    assert ph["aggregate"]["all_reduce"]["count"] == 1 and ph["aggregate"]["all_reduce"]["bytes"] == 2 * 9 * 8
+    for p in ph.values():
+        for v in p.values():
+            assert v["ms"] >= 0.0

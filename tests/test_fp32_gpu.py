@@ -106,24 +106,28 @@ def test_fp32_graph_step_is_the_eager_step(monkeypatch):
 
 def test_fp32_training_loss_history_matches_torch_backend(monkeypatch):
     """10 epochs of Keras fit (batch 1024, validation_split 0.1) on the HIP fp32 kernels and on fp32
-    autograd from the same init, data and dropout masks: per-epoch losses within 1e-3 relative or 2e-5
-    absolute.  (The synthetic set is nearly separable: from epoch 3 on the mean loss is 1e-3..6e-3 and
-    rests on a handful of windows, so two fp32 trajectories -- any two summation orders -- drift apart
-    by ~1e-5 absolute there; measured: epoch 1 2.8e-5 relative, at most 9.6e-6 absolute.)"""
+    autograd from the same init, data and dropout masks: every epoch's loss within 1e-3 relative, no
+    absolute floor.  The windows are the synthetic apnea set with extra noise, re-standardised per
+    window (as tests/test_train_gpu.py's bf16 parity test), so the task does not saturate: every
+    epoch's loss stays >= 0.05 and is decided by the whole set, not by a handful of windows."""
     _ext.require()
     # the torch side in true fp32 (no TF32-style reduced-precision convolutions / matmuls)
     monkeypatch.setattr(torch.backends.cudnn, "allow_tf32", False)
     monkeypatch.setattr(torch.backends.cuda.matmul, "allow_tf32", False)
     from uncertaintyquantification_sleepapnea_1dcnn_amd.data.synthetic import synthetic_windows
 
-    x, y, _ = synthetic_windows(4608, seed=17)
+    x, y, _ = synthetic_windows(8192, seed=17)
+    rs = np.random.RandomState(17)
+    x = (x + rs.randn(*x.shape).astype(np.float32) * 1.6).astype(np.float32)
+    x = ((x - x.mean(1, keepdims=True)) / (x.std(1, keepdims=True) + 1e-8)).astype(np.float32)
     hist = {}
     for backend in ("auto", "torch"):
         monkeypatch.setenv("APNEAUQ_TRAIN_BACKEND", backend)
         m = AlarconCNN1D(seed=2025, device="cuda", train_precision="fp32")
         hist[backend] = m.fit(x, y.astype(np.float32), batch_size=1024, epochs=10, validation_split=0.1,
                               verbose=0).history["loss"]
-    np.testing.assert_allclose(hist["auto"], hist["torch"], rtol=1e-3, atol=2e-5)
+    assert len(hist["auto"]) == 10 and min(hist["auto"]) >= 0.05, hist["auto"]
+    np.testing.assert_allclose(hist["auto"], hist["torch"], rtol=1e-3, atol=0)
 
 
 @pytest.mark.parametrize("name", ["pooled", "single30"])

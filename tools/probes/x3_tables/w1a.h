@@ -1,0 +1,8 @@
+// A/B table (round 5): one MFMA wave per SIMD (4 waves, 512 registers), no loader waves, 2x rows per
+// weight fragment where the LDS allows
+#define APNEAUQ_X3_LAYERS(X)                     \
+  X(1, 128, 192, 5, 4, 1, 4, false, 0, 0, 32, 1) \
+  X(2, 192, 224, 3, 4, 2, 2, false, 0, 0, 64, 1) \
+  X(3, 224, 96, 7, 6, 2, 2, false, 0, 0, 32, 1)  \
+  X(4, 96, 256, 9, 4, 1, 4, false, 0, 0, 32, 1)  \
+  X(5, 256, 96, 9, 6, 2, 2, true, 0, 0, 32, 1)

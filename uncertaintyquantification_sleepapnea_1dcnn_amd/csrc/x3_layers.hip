@@ -122,8 +122,10 @@ __device__ __forceinline__ int xcd_wg() {
 // wave that issued HBM loads would stall its next weight-fragment wait on them; loader waves take that
 // latency instead, and wait at the chunk barrier without using issue slots.
 // Register budget: the waves of WPC workgroups per CU over the 4 SIMDs, at least 2 per SIMD.
+// A single workgroup of <= 4 waves per CU runs one wave per SIMD with the whole 512-register file
+// (VGPR + AGPR): accumulators of twice the rows per weight fragment.
 template <int NW, int WPC>
-constexpr int waves_per_eu() { return NW * WPC > 8 ? (NW * WPC + 3) / 4 : 2; }
+constexpr int waves_per_eu() { return NW * WPC > 8 ? (NW * WPC + 3) / 4 : NW * WPC <= 4 ? 1 : 2; }
 // LW > 0: LW loader waves; LW <= 0: no loaders, MFMA waves 0 .. -LW-1 stage (LW = 0: kStagers of them)
 constexpr int loaders(int lw) { return lw > 0 ? lw : 0; }
 // PS: the per-sample prescale (moving statistics) is compiled in; without it (batch moments: per-group
@@ -200,9 +202,10 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
   int key_tile = -1;
   unsigned skeys[kS];
   unsigned skey_tile = 0u;  // the tile's stream key
-  // prescale exponents sa of the staging tile's samples, one signed byte each (kS <= 4; one register)
-  static_assert(kS <= 4, "packed per-sample exponents");
-  unsigned sa_pack = 0u;
+  // prescale exponents sa of the staging tile's samples, one signed byte each (4 per register)
+  static_assert(kS <= 8, "packed per-sample exponents");
+  constexpr int kSP = (kS + 3) / 4;
+  unsigned sa_pack[kSP];
   auto load_chunk = [&](int tile, int c, Stage& R) {
     const int tid = opaque_tid() - kSBase, q = tid % kQ;
     const int g = tile / tpg;
@@ -233,7 +236,8 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
       const float* am = A.amax_in + (A.aff_gstride ? 2 * g : 0);
       float ws0 = A.wscale[A.p_gstride ? g : 0];
       if (A.gscale_in != nullptr) ws0 *= A.gscale_in[A.aff_gstride ? g : 0];
-      sa_pack = 0u;
+#pragma unroll
+      for (int i = 0; i < kSP; ++i) sa_pack[i] = 0u;
 #pragma unroll
       for (int s = 0; s < kS; ++s) {
         skeys[s] = sample_key(skey, A.window_offset + w0 + s);
@@ -241,7 +245,7 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
         if (prescale && w0 + s < A.n_win) {
           const long long si = A.in_shared ? w0 + s : (long long)g * A.n_win + w0 + s;
           sa = sample_prescale(A.smax_in[si], am);
-          sa_pack |= ((unsigned)sa & 0xFFu) << (8 * s);
+          sa_pack[s >> 2] |= ((unsigned)sa & 0xFFu) << (8 * (s & 3));
         }
         // read by this tile's epilogue (after >= 1 barrier); the slot's previous tile (tile - 2) had its
         // epilogue before the barrier that precedes this store
@@ -282,7 +286,13 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
       }
       const bool valid = w < A.n_win;
       // the sample's exponent: a signed byte of sa_pack (v_bfe_i32), applied exactly by v_ldexp_f32
-      const int sa = prescale ? __builtin_amdgcn_sbfe((int)sa_pack, 8 * s, 8) : 0;
+      int sa = 0;
+      if (prescale) {
+        unsigned sp = sa_pack[0];
+#pragma unroll
+        for (int i = 1; i < kSP; ++i) sp = (s >> 2) == i ? sa_pack[i] : sp;
+        sa = __builtin_amdgcn_sbfe((int)sp, 8 * (s & 3), 8);
+      }
       f16x4 hi, lo;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {

@@ -230,7 +230,9 @@ def mcd_batch(model: X3Model, x: torch.Tensor, n_pass: int, seed: int, pass_base
             t = torch.tensor([float(max_samples)], dtype=torch.float64, device=model.device)
             import torch.distributed as dist
 
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            from ..parallel import comm
+
+            comm.run("chunking_all_reduce_min", t, lambda: dist.all_reduce(t, op=dist.ReduceOp.MIN))
             max_samples = int(t.item())
     ref_n = n
     if sync is not None and global_n:

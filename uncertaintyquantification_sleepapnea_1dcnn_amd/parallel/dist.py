@@ -114,7 +114,9 @@ def all_reduce_max(x: float) -> float:
 
 def all_reduce_sum_(t: torch.Tensor) -> torch.Tensor:
     if dist.is_available() and dist.is_initialized():
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        from . import comm
+
+        comm.run("all_reduce", t, lambda: dist.all_reduce(t, op=dist.ReduceOp.SUM))
     return t
 
 

@@ -40,12 +40,15 @@ def all_to_all_members(p_local: torch.Tensor, world: int, group=None) -> torch.T
     n = ng // world
     send = p_local.reshape(mloc, world, n).transpose(0, 1).contiguous()  # (G dest, M/G, n)
     recv = torch.empty_like(send)  # (G src, M/G, n)
+    from . import comm
+
     if send.is_cuda and dist.get_backend(group) == "gloo":  # single-card rehearsal: gloo has no GPU all_to_all
         rc = recv.cpu()
-        dist.all_to_all_single(rc, send.cpu(), group=group)
+        sc = send.cpu()
+        comm.run("all_to_all", sc, lambda: dist.all_to_all_single(rc, sc, group=group))
         recv.copy_(rc)
     else:
-        dist.all_to_all_single(recv, send, group=group)
+        comm.run("all_to_all", send, lambda: dist.all_to_all_single(recv, send, group=group))
     return recv.reshape(world * mloc, n)
 
 
