@@ -160,3 +160,22 @@ def test_fp32_inference_matches_reference(name):
         assert np.abs(bat[t, :, 0] - ref.numpy()).max() <= 1e-5, t
     for k, v in pc.items():  # the moving-average side effect of model(x, training=True), per pass
         torch.testing.assert_close(mb.store.as_dict()[k].cpu(), v, atol=1e-6, rtol=1e-5)
+
+
+def test_fp32_inference_window_chunks_match_one_chunk(monkeypatch):
+    """fp32 inference of a non-reference architecture runs in bounded window chunks (the
+    cached workspace stays bounded); the dropout keys stay global, so 7-window chunks give the same
+    standard-MC-Dropout probabilities as one chunk."""
+    _ext.require()
+    spec = SPECS["pooled"]
+    m = AlarconCNN1D(spec=spec, seed=3, device="cuda", params=R.synthetic_params(spec, 3))
+    x = torch.randn(40, spec.input_length, spec.input_channels, generator=torch.Generator().manual_seed(4)).cuda()
+    one = generic_train.forward_running_f32(m, x, n_pass=3, dropout=True, seed=11, window_offset=5)
+    per = sum((L + b.kernel_size) * c + L * c2 for L, b, c, c2 in
+              zip(spec.lengths(), spec.blocks, spec.channels(), spec.channels()[1:])) * 4
+    monkeypatch.setattr(generic_train, "F32_INFER_WS_BYTES", 7 * per)
+    assert generic_train._f32_chunk_windows(m) == 7
+    m._gfwd_ws32 = None
+    chunked = generic_train.forward_running_f32(m, x, n_pass=3, dropout=True, seed=11, window_offset=5)
+    torch.testing.assert_close(chunked, one, atol=0, rtol=0)
+    assert m._gfwd_ws32.B < 40

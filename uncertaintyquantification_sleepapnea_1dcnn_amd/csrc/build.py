@@ -38,7 +38,10 @@ ARCH = os.environ.get("APNEAUQ_OFFLOAD_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 DEBUG = os.environ.get("APNEAUQ_DEBUG", "0") not in ("", "0")
 HOST_SAN = os.environ.get("APNEAUQ_HOST_SANITIZE", "")
-EXTRA = os.environ.get("APNEAUQ_HIPCC_FLAGS", "").split()  # probe builds (e.g. -DAPNEAUQ_ABL=...)
+# A/B builds of the x3 layer kernels swap the complete layer table (csrc/x3_layers.hip): every table is
+# a correct configuration, only the speed differs (tools/probes/x3_tables/)
+X3_TABLE = os.environ.get("APNEAUQ_X3_TABLE", "")
+EXTRA = [f'-DAPNEAUQ_X3_TABLE="{os.path.abspath(X3_TABLE)}"'] if X3_TABLE else []
 
 
 def _torch_paths():

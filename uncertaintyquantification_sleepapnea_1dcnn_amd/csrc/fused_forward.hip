@@ -64,56 +64,11 @@ struct Args {
   float dscale[6];         // 1/(1-rate) per block
 };
 
-// Ablation hooks for tools/probes/fused_ablation.hip (always 0 in the library build):
-//   1 = epilogue without bias/ReLU/BN/dropout math   2 = no epilogue LDS stores
-//   4 = K loop without B (LDS) reads                  8 = K loop without A (global) loads
-//  16 = no block-level barriers                      32 = multiply-free stand-in for the dropout hash
-//  (timing only; results are garbage for every nonzero value)
-#ifndef APNEAUQ_ABL
-#define APNEAUQ_ABL 0
-#endif
-#define APNEAUQ_SYNC() \
-  do {                 \
-    if constexpr (!(APNEAUQ_ABL & 16)) __syncthreads(); \
-  } while (0)
-
-// In-kernel phase stamps for tools/probes (never enabled in the library build): s_memtime at
-// every phase boundary of the first kStampWG workgroups, lane 0 of each wave.
-#ifdef APNEAUQ_STAMPS
-constexpr int kStampWG = 2048, kStampN = 32;
-__device__ unsigned long long g_stamps[kStampWG][4][kStampN];
-__device__ unsigned g_stamp_cu[kStampWG];
-#define APNEAUQ_STAMP(i)                                                              \
-  do {                                                                                \
-    if (blockIdx.x < kStampWG && (threadIdx.x & 63) == 0)                             \
-      g_stamps[blockIdx.x][threadIdx.x >> 6][(i)] = __builtin_amdgcn_s_memtime();     \
-  } while (0)
-#else
-#define APNEAUQ_STAMP(i) ((void)0)
-#endif
-
-// Weight-prefetch depth per block (steps in flight ahead of the MFMAs; see the K loop).  Measured
-// on MI355X (tools/probes/fused_ablation.hip, same box, 3 interleaved reps): depth 1 everywhere
-// 64.1-64.3 ms for MCD T=50 x 16384 windows; depths (1,2,2,3,3,3) 65.4-66.5 ms.  The weight
-// stream is bound by vector-memory issue (~2.6 MB of fragments per 2-sample tile), not latency.
-#ifndef APNEAUQ_PD0
-#define APNEAUQ_PD0 1
-#endif
-#ifndef APNEAUQ_PD1
-#define APNEAUQ_PD1 1
-#endif
-#ifndef APNEAUQ_PD2
-#define APNEAUQ_PD2 1
-#endif
-#ifndef APNEAUQ_PD3
-#define APNEAUQ_PD3 1
-#endif
-#ifndef APNEAUQ_PD4
-#define APNEAUQ_PD4 1
-#endif
-#ifndef APNEAUQ_PD5
-#define APNEAUQ_PD5 1
-#endif
+// Weight-prefetch depth: 1 k-step on every block.  Measured on MI355X (same box, 3 interleaved
+// reps): depth 1 everywhere 64.1-64.3 ms for MCD T=50 x 16384 windows; depths (1,2,2,3,3,3)
+// 65.4-66.5 ms.  The weight stream is bound by vector-memory issue (~2.6 MB of fragments per
+// 2-sample tile), not latency.
+constexpr int kPD = 1;
 
 // One Conv1D(relu) -> BN -> Dropout block as an LDS-resident implicit GEMM.
 //
@@ -127,9 +82,6 @@ __device__ unsigned g_stamp_cu[kStampWG];
 //     load the same weight fragments.  Used for Cout = 96 (6 tiles), where the pair split above
 //     doubles the B-operand (LDS) reads per MFMA and measured 10-19 % slower per layer
 //     (profiles/fused_ablation_r1.md, v8).
-#ifndef APNEAUQ_BLOCK_INLINE
-#define APNEAUQ_BLOCK_INLINE __forceinline__
-#endif
 
 // Per-block context passed by value to the block functions.
 struct BlockCtx {
@@ -142,7 +94,7 @@ struct BlockCtx {
 };
 
 template <int LAYER, int WM, int NF, bool HALF, int PD, bool HEAD, bool DROP>
-__device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
+__device__ __forceinline__ void block(const BlockCtx X) {
   char* act = smem;
   const char* x0 = smem + kActBytes;
   float* head = reinterpret_cast<float*>(smem + kActBytes + kX0Bytes);
@@ -198,10 +150,7 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
   const char* xb_hi = x0 + (kHalo + rt_hi * 16 + m - PAD) * kX0RS + 16 * h;
   // B fragment (activations, LDS) of local row tile r at k-step s
   auto load_b = [&](int s, int r) -> bf16x8 {
-    if constexpr ((APNEAUQ_ABL & 4) != 0) {
-      const __bf16 v = (__bf16)(float)(lane + s + r);
-      return bf16x8{v, v, v, v, v, v, v, v};
-    } else if constexpr (FIRST) {
+    if constexpr (FIRST) {
       // k = tap*4 + ci: 8 consecutive k = two consecutive rows x 4 channels (16 B, 8-B aligned)
       const char* base = (r < HRT ? xb_lo : xb_hi) + (r % HRT) * 16 * kX0RS + 64 * s;
       const bf16x4 lo = *reinterpret_cast<const bf16x4*>(base);
@@ -219,12 +168,7 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
   auto load_a = [&](int s, bf16x8 (&a)[NA]) {
 #pragma unroll
     for (int c = 0; c < NA; ++c) {
-      if constexpr ((APNEAUQ_ABL & 8) != 0) {
-        const __bf16 v = (__bf16)(float)(lane + s + c);
-        a[c] = bf16x8{v, v, v, v, v, v, v, v};
-      } else {
-        a[c] = (c < NF ? wpf + c * 64 : wph)[s * NCT * 64];
-      }
+      a[c] = (c < NF ? wpf + c * 64 : wph)[s * NCT * 64];
     }
   };
   // (B fragments are read just in time: a register ring over the (k-step, row-tile) sequence
@@ -244,10 +188,6 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
   // ---- K loop.  A ring of PD+1 weight-fragment stages: the fragments of step s+PD are in flight
   // under step s's MFMAs.  Every load is unconditional (indices are clamped)
   // so hipcc's vmcnt bookkeeping stays exact; sched_barrier keeps each prefetch ahead of the MFMAs.
-  APNEAUQ_STAMP(2 + 4 * LAYER);  // K loop start
-#ifdef APNEAUQ_PRIO_K
-  __builtin_amdgcn_s_setprio(APNEAUQ_PRIO_K);  // probe: wave priority during the MFMA phase
-#endif
   constexpr int NS = PD + 1;
   bf16x8 a[NS][NA];
 #pragma unroll
@@ -266,7 +206,6 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
   }
 #pragma unroll
   for (int j = 0; j < NSTEP - NFULL; ++j) step(NFULL + j, a[j]);
-  APNEAUQ_STAMP(3 + 4 * LAYER);  // K loop issued (MFMAs may still drain)
 
   // ---- epilogue: bias + ReLU + BN(running) + dropout, then bf16 in place (or GAP head).
   // relu(acc + b) * s + t == clamp(fma(acc, s, b*s + t), lo, hi) (host-folded constants, one v_fma +
@@ -279,11 +218,7 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
   char* ob_lo = act + (kHalo + rt_lo * 16 + m) * kRS;
   char* ob_hi = act + (kHalo + rt_hi * 16 + m) * kRS;
 
-  if constexpr (!HEAD) APNEAUQ_SYNC();  // every wave has finished reading this block's input
-  APNEAUQ_STAMP(4 + 4 * LAYER);  // epilogue start (after the barrier)
-#ifdef APNEAUQ_PRIO_E
-  __builtin_amdgcn_s_setprio(APNEAUQ_PRIO_E);  // probe: wave priority during the VALU epilogue
-#endif
+  if constexpr (!HEAD) __syncthreads();  // every wave has finished reading this block's input
 
   // HEAD: this lane's share of sum_t sum_co w[co] * y[t][co], per (channel tile, slot).  Every
   // (tile, slot) sum is formed by exactly one wave and combined in tile order, so a sample's logit
@@ -307,27 +242,19 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
       const bool tail_tile = (r % 4) == 3;  // the row tile holding t = 48..63 of its sample
       const int t = (r % 4) * 16 + m;
       f32x4 v = acc[c][r];
-      if constexpr ((APNEAUQ_ABL & 1) == 0) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = __builtin_amdgcn_fmed3f(__builtin_fmaf(v[i], sc[i], sh[i]), lo[i], hi[i]);
-        if constexpr (DROP) {
-          const unsigned k = r < HRT ? key_lo : key_hi;
-#if (APNEAUQ_ABL & 32)
-          auto cheap = [](unsigned x) { x ^= x >> 13; x ^= x << 7; x ^= x >> 17; return x; };
-          const unsigned b01 = cheap(k ^ ((t << 9) | (co0 >> 1)));
-          const unsigned b23 = cheap(k ^ ((t << 9) | ((co0 + 2) >> 1)));
-#else
-          const unsigned b01 = dropout_bits2(k, t, co0);
-          const unsigned b23 = dropout_bits2(k, t, co0 + 2);
-#endif
-          v[0] = (b01 & 0xFFFFu) >= X.thr ? v[0] : 0.f;
-          v[1] = (b01 >> 16) >= X.thr ? v[1] : 0.f;
-          v[2] = (b23 & 0xFFFFu) >= X.thr ? v[2] : 0.f;
-          v[3] = (b23 >> 16) >= X.thr ? v[3] : 0.f;
-          // keep the selects in fp32: otherwise LLVM folds cvt(select(x, 0)) into select(cvt(x), 0),
-          // converting every element separately and re-packing the pairs with v_perm
-          asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
-        }
+      for (int i = 0; i < 4; ++i) v[i] = __builtin_amdgcn_fmed3f(__builtin_fmaf(v[i], sc[i], sh[i]), lo[i], hi[i]);
+      if constexpr (DROP) {
+        const unsigned k = r < HRT ? key_lo : key_hi;
+        const unsigned b01 = dropout_bits2(k, t, co0);
+        const unsigned b23 = dropout_bits2(k, t, co0 + 2);
+        v[0] = (b01 & 0xFFFFu) >= X.thr ? v[0] : 0.f;
+        v[1] = (b01 >> 16) >= X.thr ? v[1] : 0.f;
+        v[2] = (b23 & 0xFFFFu) >= X.thr ? v[2] : 0.f;
+        v[3] = (b23 >> 16) >= X.thr ? v[3] : 0.f;
+        // keep the selects in fp32: otherwise LLVM folds cvt(select(x, 0)) into select(cvt(x), 0),
+        // converting every element separately and re-packing the pairs with v_perm
+        asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
       }
       if constexpr (HEAD) {
         const float g = v[0] * dw[0] + v[1] * dw[1] + v[2] * dw[2] + v[3] * dw[3];
@@ -335,11 +262,7 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
       } else {
         bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
         bf16x4* dst = reinterpret_cast<bf16x4*>((r < HRT ? ob_lo : ob_hi) + (r % HRT) * 16 * kRS + co0 * 2);
-        if constexpr ((APNEAUQ_ABL & 2) != 0) {
-          if (v[0] == 123.f) *dst = o;
-        } else if (!(tail_tile && tail_lane)) {
-          *dst = o;
-        }
+        if (!(tail_tile && tail_lane)) *dst = o;
       }
     }
   }
@@ -364,8 +287,7 @@ __device__ APNEAUQ_BLOCK_INLINE void block(const BlockCtx X) {
       head[kHeadOut + sl] = X.out_logits ? logit : 1.0f / (1.0f + __expf(-logit));
     }
   } else {
-    APNEAUQ_STAMP(5 + 4 * LAYER);  // epilogue done, before the barrier
-    APNEAUQ_SYNC();  // block output visible before the next block reads it
+    __syncthreads();  // block output visible before the next block reads it
   }
 }
 
@@ -388,13 +310,6 @@ __global__ __launch_bounds__(kThreads, 2) void fused_forward_kernel(Args A) {
     reinterpret_cast<f32x4*>(x0 + (kHalo + kR) * kX0RS)[threadIdx.x] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
-#ifdef APNEAUQ_STAGGER_US
-  // probe: delay the second co-resident workgroup of every CU by ~half a tile
-  if (blockIdx.x >= 256 && blockIdx.x < 512) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__builtin_amdgcn_s_memrealtime() - t0 < 100ull * APNEAUQ_STAGGER_US) __builtin_amdgcn_s_sleep(8);
-  }
-#endif
   // XCD-aware item assignment (T1): blocks sharing an XCD get a contiguous item range, so a
   // Deep-Ensemble member's weights stay in one XCD's L2.  Bijective for any grid size.
   const int nwg = gridDim.x, bid = blockIdx.x;
@@ -404,10 +319,6 @@ __global__ __launch_bounds__(kThreads, 2) void fused_forward_kernel(Args A) {
   // One tile per workgroup.  (A persistent tile loop lets LICM hoist every block's address math
   // out of the loop, which blows the 256-VGPR budget; one tile per launch slot keeps it at ~206.)
   {
-    APNEAUQ_STAMP(0);
-#ifdef APNEAUQ_STAMPS
-    if (blockIdx.x < kStampWG && threadIdx.x == 0) g_stamp_cu[blockIdx.x] = __smid();
-#endif
     const int item = wg;
     APNEAUQ_DASSERT(item < A.total_items && (int)gridDim.x == A.total_items && blockDim.x == kThreads);
     const int member = item / A.tiles_per_member;
@@ -438,25 +349,24 @@ __global__ __launch_bounds__(kThreads, 2) void fused_forward_kernel(Args A) {
     X.blob = blob;
     X.out_logits = A.out_logits;
     X.skey0 = X.skey1 = 0u;
-#define APNEAUQ_CTX(L)                                                                                   \
+#define FUSED_CTX(L)                                                                                   \
   X.thr = A.thr[L];                                                                                      \
   X.dsc = A.dscale[L];                                                                                   \
   if (DROP) {                                                                                            \
     X.skey0 = sample_key(stream_key(A.seed, L, A.pass_offset + pass[0]), A.window_offset + win[0]);      \
     X.skey1 = sample_key(stream_key(A.seed, L, A.pass_offset + pass[1]), A.window_offset + win[1]);      \
   }
-    APNEAUQ_CTX(0) block<0, 1, 2, false, APNEAUQ_PD0, false, DROP>(X);
-    APNEAUQ_CTX(1) block<1, 1, 3, false, APNEAUQ_PD1, false, DROP>(X);
-    APNEAUQ_CTX(2) block<2, 1, 3, true, APNEAUQ_PD2, false, DROP>(X);
-    APNEAUQ_CTX(3) block<3, 2, 3, false, APNEAUQ_PD3, false, DROP>(X);
-    APNEAUQ_CTX(4) block<4, 1, 4, false, APNEAUQ_PD4, false, DROP>(X);
-    APNEAUQ_CTX(5) block<5, 2, 3, false, APNEAUQ_PD5, true, DROP>(X);
-#undef APNEAUQ_CTX
+    FUSED_CTX(0) block<0, 1, 2, false, kPD, false, DROP>(X);
+    FUSED_CTX(1) block<1, 1, 3, false, kPD, false, DROP>(X);
+    FUSED_CTX(2) block<2, 1, 3, true, kPD, false, DROP>(X);
+    FUSED_CTX(3) block<3, 2, 3, false, kPD, false, DROP>(X);
+    FUSED_CTX(4) block<4, 1, 4, false, kPD, false, DROP>(X);
+    FUSED_CTX(5) block<5, 2, 3, false, kPD, true, DROP>(X);
+#undef FUSED_CTX
     if (threadIdx.x < kSlots && valid[threadIdx.x]) {
       const int sl = threadIdx.x;
       A.out[((long long)member * A.n_pass + pass[sl]) * A.n_win + win[sl]] = head[kHeadOut + sl];
     }
-    APNEAUQ_STAMP(1);
   }
 }
 

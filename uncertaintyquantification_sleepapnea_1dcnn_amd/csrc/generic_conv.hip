@@ -24,6 +24,8 @@
 
 #include "common.h"
 
+#include <type_traits>
+
 namespace apneauq {
 namespace generic {
 
@@ -423,11 +425,7 @@ hipError_t launch_generic_conv(const void* x, const void* wfrag, const float* ep
   A.x_rows = x_rows;
   A.lds_rows = (int)span;
   A.lds_stride = stride;
-  static const bool lds_enabled = [] {  // APNEAUQ_GCONV_LDS=0 forces the direct-gather kernel (A/B runs)
-    const char* e = getenv("APNEAUQ_GCONV_LDS");
-    return !(e && e[0] == '0');
-  }();
-  const bool use_lds = lds_enabled && cin % 8 == 0 && span * stride <= 80 * 1024 && x_rows > 0;
+  const bool use_lds = cin % 8 == 0 && span * stride <= 80 * 1024 && x_rows > 0;
   if (use_lds) {
     const size_t lds = (size_t)span * stride;
     if (mode == generic::kTrain)
@@ -438,19 +436,20 @@ hipError_t launch_generic_conv(const void* x, const void* wfrag, const float* ep
       hipLaunchKernelGGL(generic::conv_lds_kernel<generic::kInfer>, grid, dim3(256), lds, stream, A);
     return hipGetLastError();
   }
-#define APNEAUQ_GCONV(M)                                                                   \
-  if (cin % 8 == 0)                                                                        \
-    hipLaunchKernelGGL((generic::conv_block_kernel<true, M>), grid, dim3(256), 0, stream, A); \
-  else                                                                                     \
-    hipLaunchKernelGGL((generic::conv_block_kernel<false, M>), grid, dim3(256), 0, stream, A);
-  if (mode == generic::kTrain) {
-    APNEAUQ_GCONV(generic::kTrain)
-  } else if (mode == generic::kLinear) {
-    APNEAUQ_GCONV(generic::kLinear)
-  } else {
-    APNEAUQ_GCONV(generic::kInfer)
-  }
-#undef APNEAUQ_GCONV
+  // direct-gather kernel: channel counts that are not a multiple of 8, or rows beyond the LDS span
+  auto gather = [&](auto mode_c) {
+    constexpr int M = decltype(mode_c)::value;
+    if (cin % 8 == 0)
+      hipLaunchKernelGGL((generic::conv_block_kernel<true, M>), grid, dim3(256), 0, stream, A);
+    else
+      hipLaunchKernelGGL((generic::conv_block_kernel<false, M>), grid, dim3(256), 0, stream, A);
+  };
+  if (mode == generic::kTrain)
+    gather(std::integral_constant<int, generic::kTrain>{});
+  else if (mode == generic::kLinear)
+    gather(std::integral_constant<int, generic::kLinear>{});
+  else
+    gather(std::integral_constant<int, generic::kInfer>{});
   return hipGetLastError();
 }
 

@@ -470,12 +470,7 @@ hipError_t launch_gt_wgrad(const void* x, long long x_rows, const void* dz, long
   // ~2048 workgroups (8 per CU over the 256 CUs), but at least minc chunks each: every workgroup ends
   // with k * 16 * 64 * NCO fp32 atomics, and the chip adds ~1.3 TB/s of atomic bytes, so at 4 chunks
   // per workgroup the k = 9 blocks of ModelSpec(30, 1) spent ~100 us of a ~106 us wgrad on them.
-  // APNEAUQ_GWG_MINC overrides (probes).
-  static const int minc_env = [] {
-    const char* e = getenv("APNEAUQ_GWG_MINC");
-    return e ? atoi(e) : 0;
-  }();
-  const long long minc = minc_env > 0 ? minc_env : (k <= 3 ? 4 : 2 * k);
+  const long long minc = k <= 3 ? 4 : 2 * k;
   const long long blocks = (long long)A.n_ci * A.n_co;
   long long rg = 2048 / blocks;
   if (rg < 1) rg = 1;

@@ -329,6 +329,17 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgArgs A) {
     }
 }
 
+// dispatch the runtime tap count (1 .. kWgKMax) to its wgrad_kernel<K> instantiation
+template <int K>
+bool launch_wgrad_k(int k, dim3 grid, const WgArgs& A, hipStream_t st) {
+  if (k == K) {
+    hipLaunchKernelGGL(wgrad_kernel<K>, grid, dim3(256), 0, st, A);
+    return true;
+  }
+  if constexpr (K < kWgKMax) return launch_wgrad_k<K + 1>(k, grid, A, st);
+  return false;
+}
+
 }  // namespace gf32
 
 hipError_t launch_gf32_conv(const float* x, const float* w, const float* bias, float* y, float* stats, int n, int L,
@@ -370,15 +381,7 @@ hipError_t launch_gf32_wgrad(const float* x, const float* dz, long long R, int c
   groups = (R + rpg - 1) / rpg;
   gf32::WgArgs A{x, dz, part, R, cin, cout, k, (int)rpg};
   const dim3 grid((unsigned)ci_t, (unsigned)co_g, (unsigned)groups);
-  switch (k) {
-#define APNEAUQ_GF32_WG(KK) \
-  case KK: hipLaunchKernelGGL(gf32::wgrad_kernel<KK>, grid, dim3(256), 0, st, A); break;
-    APNEAUQ_GF32_WG(1) APNEAUQ_GF32_WG(2) APNEAUQ_GF32_WG(3) APNEAUQ_GF32_WG(4) APNEAUQ_GF32_WG(5)
-    APNEAUQ_GF32_WG(6) APNEAUQ_GF32_WG(7) APNEAUQ_GF32_WG(8) APNEAUQ_GF32_WG(9) APNEAUQ_GF32_WG(10)
-    APNEAUQ_GF32_WG(11) APNEAUQ_GF32_WG(12) APNEAUQ_GF32_WG(13) APNEAUQ_GF32_WG(14) APNEAUQ_GF32_WG(15)
-#undef APNEAUQ_GF32_WG
-    default: return hipErrorInvalidValue;
-  }
+  if (!gf32::launch_wgrad_k<1>(k, grid, A, st)) return hipErrorInvalidValue;
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return launch_ordered_sum(part, (int)groups, wfl, gw, st);

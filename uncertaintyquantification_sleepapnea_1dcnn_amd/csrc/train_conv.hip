@@ -1145,48 +1145,17 @@ template <int l> struct WgCfg;
 // wgrad LDS tiles: the row stride is an odd multiple of 32 B (conflict-free tr_frag reads)
 __host__ __device__ constexpr int wg_rs(int width_bytes) { return (width_bytes / 32) % 2 ? width_bytes : width_bytes + 32; }
 // wgrad of blocks 4 and 6 prefetch the next row tile into registers during the MFMAs
-// (-DAPNEAUQ_WG_NOPF: stage each tile between the barriers, the round-3 loop)
-#ifdef APNEAUQ_WG_NOPF
-constexpr bool kWgPrefetch = false;
-#else
 constexpr bool kWgPrefetch = true;
-#endif
-// A/B builds may replace an entry (-DAPNEAUQ_WGCFG4='CIB = 32, COB = 128, ...'): every entry is a
-// complete, correct configuration, only the speed differs.
 // MINWG values: batch-1024 step measured with tools/probes/train_variants.sh (block 5 512 -> 768 took
 // the step 0.795 -> 0.786 ms, block 2 256 -> 512 0.766-0.775 -> 0.758-0.768 ms, three interleaved rounds;
 // round 4, with the straggler-free grouping: block 3 256 -> 512 batch 8192 4.20-4.22 -> 4.13-4.16 ms,
 // batch 1024 / 8 members unchanged; block 4 512 -> 1024 slower)
-#ifdef APNEAUQ_WGCFG0
-template <> struct WgCfg<0> { static constexpr int APNEAUQ_WGCFG0; };
-#else
 template <> struct WgCfg<0> { static constexpr int CIB = 32, COB = 128, WCO = 4, WCI = 1, RTILES = 2, MINWG = 512, U = 4, MINB = 2; };  // im2col kk=32
-#endif
-#ifdef APNEAUQ_WGCFG1
-template <> struct WgCfg<1> { static constexpr int APNEAUQ_WGCFG1; };
-#else
 template <> struct WgCfg<1> { static constexpr int CIB = 32, COB = 192, WCO = 2, WCI = 2, RTILES = 8, MINWG = 512, U = 8, MINB = 2; };
-#endif
-#ifdef APNEAUQ_WGCFG2
-template <> struct WgCfg<2> { static constexpr int APNEAUQ_WGCFG2; };
-#else
 template <> struct WgCfg<2> { static constexpr int CIB = 32, COB = 224, WCO = 2, WCI = 2, RTILES = 8, MINWG = 512, U = 8, MINB = 2; };
-#endif
-#ifdef APNEAUQ_WGCFG3
-template <> struct WgCfg<3> { static constexpr int APNEAUQ_WGCFG3; };
-#else
 template <> struct WgCfg<3> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = 512, U = 8, MINB = kWgPrefetch ? 2 : 3; };
-#endif
-#ifdef APNEAUQ_WGCFG4
-template <> struct WgCfg<4> { static constexpr int APNEAUQ_WGCFG4; };
-#else
 template <> struct WgCfg<4> { static constexpr int CIB = 16, COB = 128, WCO = 4, WCI = 1, RTILES = 16, MINWG = 768, U = 8, MINB = 3; };
-#endif
-#ifdef APNEAUQ_WGCFG5
-template <> struct WgCfg<5> { static constexpr int APNEAUQ_WGCFG5; };
-#else
 template <> struct WgCfg<5> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = 512, U = 4, MINB = 2; };
-#endif
 
 
 template <int l, bool MB>

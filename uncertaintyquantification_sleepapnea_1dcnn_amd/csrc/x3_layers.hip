@@ -816,7 +816,7 @@ hipError_t launch_layer(const LayerArgs& A, int grid, hipStream_t stream) {
 // 6 run 4 MFMA waves of 24 accumulator tiles (WM 2 x WN 2) rather than 8 of 12: each weight fragment
 // is re-read by 2 wave rows instead of 4 (their texture path was the busy one), -1.2 % MCD.
 // Measurements: profiles/x3_epilogue_ab_r3.md, profiles/x3_mask_side_r4.md.
-// A/B builds may substitute another table (-DAPNEAUQ_X3_TABLE='"path.h"', tools/probes/x3_tables/):
+// A/B builds may substitute another table (APNEAUQ_X3_TABLE=<path.h> in csrc/build.py, tools/probes/x3_tables/):
 // every entry is a complete, correct configuration, only the speed differs.
 #ifdef APNEAUQ_X3_TABLE
 #include APNEAUQ_X3_TABLE

@@ -185,6 +185,16 @@ class AlarconCNN1D:
                                       seed=self.seed if seed is None else seed, pass_offset=pass_offset,
                                       window_offset=window_offset, logits=logits)[0]
         if self.precision == "fp32" and self.uses_generic():
+            from ..ops import generic_train
+
+            if not generic_train.supports_fp32(self.spec):
+                import warnings
+
+                warnings.warn(f"precision='fp32': no fp32 HIP kernels for {self.spec} (kernel sizes > 15); "
+                              "inference runs on the bf16 layer-wise kernels", RuntimeWarning, stacklevel=2)
+                return self.hip_forward(x.to(torch.bfloat16).contiguous(), n_pass=n_pass, dropout=dropout,
+                                        seed=seed, pass_offset=pass_offset, window_offset=window_offset,
+                                        logits=logits)
             # any other architecture (MaxPool1D blocks, the 30 s single-channel window) at fp32: the
             # fp32-input MFMA layer-wise path (ops/generic_train.py:forward_running_f32)
             from ..ops import generic_train

@@ -125,7 +125,7 @@ class GenericTrainWorkspace:
             # the head's per-workgroup records
             wmax = max(self.ks[l] * self.ch[l] * self.ch[l + 1] for l in range(nl))
             if self.f32:  # gf_wgrad row groups: up to ~512 workgroups per layer (csrc/gf32_conv.hip)
-                want = [-(-512 // (-(-self.ch[l] // 16) * -(-self.ch[l + 1] // 64))) for l in range(nl)]
+                want = [-(-512 // (-(-self.ch[l] // 32) * -(-self.ch[l + 1] // 64))) for l in range(nl)]
                 nf = max(w * self.ks[l] * self.ch[l] * self.ch[l + 1] for l, w in enumerate(want))
                 self.wpart = torch.empty(min(nf, 1 << 24), device=dev)
             else:
@@ -419,6 +419,18 @@ def running_affine(model, ws: GenericTrainWorkspace) -> None:
         ws.bn[l].copy_(torch.cat([scale, v[f"batchnorm_{i}/beta"] - mm * scale, mm, rstd]))
 
 
+# fp32 inference workspace cap (activations of one window chunk, all layers): large Deep-Ensemble /
+# MC-Dropout sets are processed in window chunks that fit it, so the cached workspace stays bounded
+F32_INFER_WS_BYTES = 1 << 31
+
+
+def _f32_chunk_windows(model) -> int:
+    spec = model.spec
+    L, ch = spec.lengths(), spec.channels()
+    per = sum((L[l] + b.kernel_size) * ch[l] + L[l] * ch[l + 1] for l, b in enumerate(spec.blocks)) * 4
+    return max(1, F32_INFER_WS_BYTES // per)
+
+
 @torch.no_grad()
 def forward_running_f32(model, x: torch.Tensor, n_pass: int = 1, dropout: bool = False, seed: int = 0,
                         pass_offset: int = 0, window_offset: int = 0, logits: bool = False) -> torch.Tensor:
@@ -427,11 +439,53 @@ def forward_running_f32(model, x: torch.Tensor, n_pass: int = 1, dropout: bool =
     thesis' ``ensemble_cnn`` members (``evaluate_de_global.py:18-38``), the 30 s single-channel window --
     on the fp32-input MFMA conv (``csrc/gf32_conv.hip``) and the fp32 BN / pool / dropout kernels:
     (n_pass, N) probabilities (or logits).  The passes run one after the other (each its own dropout
-    stream, keyed by the global window id)."""
+    stream, keyed by the global window id); windows in chunks of at most ``F32_INFER_WS_BYTES`` of
+    activations (the dropout keys stay global: chunk s starts at window_offset + s)."""
     n = int(x.shape[0])
     out = torch.empty(n_pass, n, dtype=torch.float32, device=x.device)
     if n == 0:
         return out
+    step = _f32_chunk_windows(model)
+    for s in range(0, n, step):
+        e = min(n, s + step)
+        out[:, s:e] = _forward_running_f32_chunk(model, x[s:e], n_pass, dropout, seed, pass_offset,
+                                                 window_offset + s, logits)
+    return out
+
+
+def _forward_running_f32_chunk(model, x, n_pass, dropout, seed, pass_offset, window_offset, logits):
+    n = int(x.shape[0])
+    out = torch.empty(n_pass, n, dtype=torch.float32, device=x.device)
+    spec, o = model.spec, _ext.ops()
+    ws = _get_ws(model, n, with_backward=False, f32=True)
+    running_affine(model, ws)
+    ws.load_input(x)
+    v = model.store.views
+    wdense = v["output_layer/kernel"].reshape(-1)
+    nl = len(spec.blocks)
+    conv0 = True
+    for t in range(n_pass if dropout else 1):
+        for l, b in enumerate(spec.blocks):
+            i = l + 1
+            cin, cout, L = ws.ch[l], ws.ch[l + 1], ws.L[l]
+            if l > 0 or conv0:  # block 1 does not depend on the pass (no dropout before it)
+                o.gf_conv(ws.xin[l], v[f"conv1d_{i}/kernel"], v[f"conv1d_{i}/bias"], ws.z[l], ws.st[l], n, L, cin,
+                          cout, ws.ks[l], 1, ws.rs[l], 2 * ws.pads[l], True)
+            if l + 1 < nl:
+                dst, drs, doff = ws.xin[l + 1], ws.rs[l + 1], 2 * ws.pads[l + 1]
+            else:
+                dst, drs, doff = ws.hlast, ws.L[-1], 0
+            drop = bool(dropout and b.dropout > 0)
+            o.gt_apply(ws.z[l], ws.bn[l], dst, n, L, cout, bool(b.pool), drs, doff, drop,
+                       rng.dropout_threshold(b.dropout), _inv_keep(b.dropout),
+                       rng.stream_key(seed, l, pass_offset + t), int(window_offset), None)
+        conv0 = False
+        h = ws.hlast[: n * ws.L[-1]].view(n, ws.L[-1], ws.ch[-1])
+        lg = torch.addmv(v["output_layer/bias"], h.mean(dim=1), wdense)
+        out[t] = lg if logits else torch.sigmoid(lg)
+    if not dropout:
+        out[1:] = out[0]
+    return out
     spec, o = model.spec, _ext.ops()
     ws = _get_ws(model, n, with_backward=False, f32=True)
     running_affine(model, ws)

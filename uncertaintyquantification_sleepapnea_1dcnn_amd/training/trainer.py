@@ -161,6 +161,7 @@ def _fit_batched(models: List, x, y, per_cbs, **fit_kwargs) -> List[History]:
         except StopIteration as stop:
             hist[i] = stop.value
     steps = {}
+    step_stream = {}  # step key -> the stream of its last replay
     streams: List = []
     # every member's step, its next batch's gather and its metric updates run on its group's stream, so
     # the groups are never joined between steps; a member whose group (stream) changes -- regrouping
@@ -180,6 +181,10 @@ def _fit_batched(models: List, x, y, per_cbs, **fit_kwargs) -> List[History]:
             ng = min(n_groups, len(ids))
             want.update(tuple(ids[g::ng]) for g in range(ng))
         for key in [k for k in steps if k[0] not in want]:
+            # its last replay may still run on a group stream home never waited on, and its workspace /
+            # counters were allocated on home: join before the allocator may hand them out again
+            if key in step_stream:
+                home.wait_stream(step_stream.pop(key))
             del steps[key]
         for n, ids in by_n.items():
             ng = min(n_groups, len(ids))
@@ -191,13 +196,17 @@ def _fit_batched(models: List, x, y, per_cbs, **fit_kwargs) -> List[History]:
                 key = (tuple(sub), n)
                 st = steps.get(key)
                 if st is None or not st.valid_for(ms):
+                    if key in step_stream:
+                        home.wait_stream(step_stream.pop(key))
                     st = steps[key] = train_ops.GraphedEnsembleStep(ms, n)
+                    s_.wait_stream(home)  # built and initialised on home (zeros, counters)
                 for prev in {id(last[i]): last[i] for i in sub if last[i] is not s_}.values():
                     s_.wait_stream(prev)
                 for i in sub:
                     if last[i] is not s_:  # a batch allocated on another stream, read on this one
                         req[i][0].record_stream(s_)
                         req[i][1].record_stream(s_)
+                step_stream[key] = s_
                 with torch.cuda.stream(s_):
                     outs = st([req[i][0] for i in sub], [req[i][1] for i in sub])
                     for i, res in zip(sub, outs):
