@@ -72,6 +72,16 @@ hipError_t launch_gf32_conv(const float* x, const float* w, const float* bias, f
 hipError_t launch_gf32_wgrad(const float* x, const float* dz, long long R, int cin, int cout, int k, float* gw,
                              float* part, long long part_floats, hipStream_t st);
 int gt_pack_max_blocks();
+int gx3_max_blocks();
+hipError_t launch_gx3_pack(int nb, const float* const* w, void* const* fwd, void* const* dgr, float* const* wsc,
+                           const int* k, const int* cin, const int* cout, float* wpart, hipStream_t st);
+hipError_t launch_gx3_amax(const float* x, long long n, unsigned* out, hipStream_t st);
+hipError_t launch_gx3_conv(const float* x, long long x_rows, const void* wfrag, const float* wsc, const float* bias,
+                           float* y, float* stats, unsigned* amax_out, int n, int L, int cin, int cout, int ksize,
+                           int mode, int in_rs, int in_off, int det_slots, hipStream_t st);
+hipError_t launch_gx3_wgrad(const float* x, const float* dz, const unsigned* amax_x, const unsigned* amax_dz,
+                            long long R, int cin, int cout, int k, float* gw, float* part, long long part_floats,
+                            hipStream_t st);
 long long train_wgrad_part_floats(int B);
 int train_det_floats(int B);
 hipError_t launch_gt_pack(int nb, const float* const* w, void* const* fwd, void* const* dgr, const int* k,
@@ -801,6 +811,121 @@ void gt_pack(at::TensorList w, at::TensorList fwd, at::TensorList dgr, at::IntAr
         "gt_pack");
 }
 
+// ---- fp32-faithful (fp16x3) generic conv kernels (csrc/gx3_conv.hip): the precision="fp32" path ----
+// packed hi/lo fragments of nb blocks' kernels (forward; + dgrad where dgr[i] is non-empty), per-tensor
+// scales wsc[i] (one fp32 each), wpart: >= 16 nb floats of scratch
+void gx3_pack(at::TensorList w, at::TensorList fwd, at::TensorList dgr, at::TensorList wsc, at::IntArrayRef k,
+              at::IntArrayRef cin, at::IntArrayRef cout, at::Tensor& wpart) {
+  const int64_t nb = (int64_t)w.size();
+  TORCH_CHECK(nb >= 1 && nb <= apneauq::gx3_max_blocks() && (int64_t)fwd.size() == nb && (int64_t)dgr.size() == nb &&
+                  (int64_t)wsc.size() == nb && (int64_t)k.size() == nb && (int64_t)cin.size() == nb &&
+                  (int64_t)cout.size() == nb,
+              "gx3_pack: inconsistent block lists");
+  need_f32(wpart, 16 * nb, "gx3_pack wpart");
+  std::vector<const float*> wp(nb);
+  std::vector<void*> fp(nb), dp(nb);
+  std::vector<float*> sp(nb);
+  std::vector<int> kk(nb), ci(nb), co(nb);
+  for (int64_t i = 0; i < nb; ++i) {
+    kk[i] = (int)k[i];
+    ci[i] = (int)cin[i];
+    co[i] = (int)cout[i];
+    TORCH_CHECK(k[i] >= 1 && cin[i] >= 1 && cout[i] % 4 == 0, "gx3_pack: cout must be a multiple of 4");
+    TORCH_CHECK(w[i].is_cuda() && w[i].scalar_type() == at::kFloat && w[i].is_contiguous() &&
+                    w[i].numel() == k[i] * cin[i] * cout[i] && reinterpret_cast<uintptr_t>(w[i].data_ptr()) % 16 == 0,
+                "gx3_pack: w must be contiguous, 16-B aligned fp32 (k, cin, cout)");
+    const int64_t nf = 2 * ((k[i] * cin[i] + 31) / 32) * 512 * ((cout[i] + 15) / 16);
+    const int64_t nd = 2 * ((k[i] * cout[i] + 31) / 32) * 512 * ((cin[i] + 15) / 16);
+    TORCH_CHECK(fwd[i].scalar_type() == at::kHalf && fwd[i].is_contiguous() && fwd[i].numel() == nf,
+                "gx3_pack: forward fragment buffer must be fp16 of the packed size");
+    TORCH_CHECK(dgr[i].numel() == 0 || (dgr[i].scalar_type() == at::kHalf && dgr[i].is_contiguous() && dgr[i].numel() == nd),
+                "gx3_pack: dgrad fragment buffer must be fp16 of the packed size");
+    need_f32(wsc[i], 1, "gx3_pack wsc");
+    wp[i] = w[i].data_ptr<float>();
+    fp[i] = fwd[i].data_ptr();
+    dp[i] = dgr[i].numel() ? dgr[i].data_ptr() : nullptr;
+    sp[i] = const_cast<float*>(wsc[i].data_ptr<float>());
+  }
+  const at::DeviceGuard guard(w[0].device());
+  check(apneauq::launch_gx3_pack((int)nb, wp.data(), fp.data(), dp.data(), sp.data(), kk.data(), ci.data(), co.data(),
+                                 wpart.data_ptr<float>(), cur_stream()),
+        "gx3_pack");
+}
+
+// amax (int32, >= 1): atomicMax of max |x| (fp32 bits) over x's first n elements
+void gx3_amax(const at::Tensor& x, int64_t n, at::Tensor& amax) {
+  need_f32(x, n, "gx3_amax x");
+  TORCH_CHECK(amax.is_cuda() && amax.scalar_type() == at::kInt && amax.numel() >= 1, "gx3_amax: amax must be int32");
+  const at::DeviceGuard guard(x.device());
+  check(apneauq::launch_gx3_amax(x.data_ptr<float>(), n, reinterpret_cast<unsigned*>(amax.data_ptr<int32_t>()),
+                                 cur_stream()),
+        "gx3_amax");
+}
+
+// mode 1: y = relu(conv(x) + bias) + BN moment slots (det: one per (workgroup, wave row)); mode 2:
+// y = conv(x) with the flipped packed kernel (dgrad; cin = the forward Cout).  wfrag: gx3_pack output of
+// that orientation, wsc its scale.  The input's row layout must keep >= pad zero rows around every
+// sample's data (in_off >= pad, in_rs - L >= pad): taps never reach a neighbour's rows.
+// amax (int32, nullable): atomicMax of the input's max |x| (the tensor maximum, for gx3_wgrad).
+void gx3_conv(const at::Tensor& x, const at::Tensor& wfrag, const at::Tensor& wsc, const c10::optional<at::Tensor>& bias,
+              at::Tensor& y, const c10::optional<at::Tensor>& stats, const c10::optional<at::Tensor>& amax, int64_t n,
+              int64_t L, int64_t cin, int64_t cout, int64_t ksize, int64_t mode, int64_t in_rs, int64_t in_off, bool det) {
+  TORCH_CHECK(mode == 1 || mode == 2, "gx3_conv: mode must be 1 (train) or 2 (dgrad)");
+  TORCH_CHECK(ksize % 2 == 1 && cout % 4 == 0 && cin >= 1 && n >= 0 && L >= 1, "gx3_conv: bad shape");
+  const int64_t pad = (ksize - 1) / 2;
+  TORCH_CHECK(in_off >= pad && in_rs - L >= pad, "gx3_conv: input rows need >= pad zero rows around each sample");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && y.scalar_type() == at::kFloat, "gx3_conv: fp32 activations");
+  need_rows(x, n > 0 ? (n - 1) * in_rs + in_off + L + pad : 0, cin, "gx3_conv x");
+  need_rows(y, n * L, cout, "gx3_conv y");
+  TORCH_CHECK(wfrag.is_cuda() && wfrag.scalar_type() == at::kHalf && wfrag.is_contiguous() &&
+                  wfrag.numel() == 2 * ((ksize * cin + 31) / 32) * 512 * ((cout + 15) / 16),
+              "gx3_conv: wfrag must be the fp16 hi/lo fragments of this orientation");
+  need_f32(wsc, 1, "gx3_conv wsc");
+  TORCH_CHECK(n * L < (int64_t(1) << 31), "gx3_conv: too many rows");
+  const float* bp = nullptr;
+  float* sp = nullptr;
+  int det_slots = 0;
+  if (mode == 1) {
+    TORCH_CHECK(bias.has_value() && stats.has_value(), "gx3_conv: mode 1 needs bias and stats");
+    need_f32(*bias, cout, "gx3_conv bias");
+    need_f32(*stats, kGtSlots * 2 * cout, "gx3_conv stats");
+    bp = bias->data_ptr<float>();
+    sp = stats->data_ptr<float>();
+    if (det) det_slots = (int)(stats->numel() / (2 * cout));
+  }
+  unsigned* ap = nullptr;
+  if (amax.has_value()) {
+    TORCH_CHECK(amax->is_cuda() && amax->scalar_type() == at::kInt && amax->numel() >= 1, "gx3_conv: amax must be int32");
+    ap = reinterpret_cast<unsigned*>(amax->data_ptr<int32_t>());
+  }
+  const at::DeviceGuard guard(y.device());
+  check(apneauq::launch_gx3_conv(x.data_ptr<float>(), x.numel() / cin, wfrag.data_ptr(), wsc.data_ptr<float>(), bp,
+                                 y.data_ptr<float>(), sp, ap, (int)n, (int)L, (int)cin, (int)cout, (int)ksize, (int)mode,
+                                 (int)in_rs, (int)in_off, det_slots, cur_stream()),
+        "gx3_conv");
+}
+
+// gw (k, cin, cout) = sum_R x[R + tap] dz[R] on the fp16x3 MFMA, the operands prescaled by their tensor
+// maxima amax_x / amax_dz (int32 fp32 bits, >= the true maxima); row-group partials in part summed in a
+// fixed order (deterministic)
+void gx3_wgrad(const at::Tensor& x, const at::Tensor& dz, const at::Tensor& amax_x, const at::Tensor& amax_dz, int64_t R,
+               int64_t cin, int64_t cout, int64_t k, at::Tensor& gw, at::Tensor& part) {
+  TORCH_CHECK(x.scalar_type() == at::kFloat && dz.scalar_type() == at::kFloat, "gx3_wgrad: fp32 activations");
+  TORCH_CHECK(k >= 1 && k <= 15 && cin >= 1 && cout % 4 == 0, "gx3_wgrad: 1 <= k <= 15, cout % 4 == 0");
+  need_rows(x, R + k - 1, cin, "gx3_wgrad x");
+  need_rows(dz, R, cout, "gx3_wgrad dz");
+  need_f32(gw, k * cin * cout, "gx3_wgrad gw");
+  need_f32(part, k * cin * cout, "gx3_wgrad part");
+  TORCH_CHECK(amax_x.is_cuda() && amax_x.scalar_type() == at::kInt && amax_dz.is_cuda() && amax_dz.scalar_type() == at::kInt,
+              "gx3_wgrad: amax must be int32");
+  const at::DeviceGuard guard(x.device());
+  check(apneauq::launch_gx3_wgrad(x.data_ptr<float>(), dz.data_ptr<float>(),
+                                  reinterpret_cast<const unsigned*>(amax_x.data_ptr<int32_t>()),
+                                  reinterpret_cast<const unsigned*>(amax_dz.data_ptr<int32_t>()), R, (int)cin, (int)cout,
+                                  (int)k, gw.data_ptr<float>(), part.data_ptr<float>(), part.numel(), cur_stream()),
+        "gx3_wgrad");
+}
+
 at::Tensor generic_head(const at::Tensor& y, const at::Tensor& w, double b, bool out_logits) {
   TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kBFloat16 && y.is_contiguous() && y.dim() == 3, "generic_head: y must be (N, L, C) bf16");
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == y.size(2), "generic_head: w must be (C,) fp32");
@@ -917,6 +1042,13 @@ TORCH_LIBRARY(apneauq, m) {
   m.def("gf_conv(Tensor x, Tensor w, Tensor? bias, Tensor(a!) y, Tensor(b!)? stats, int n, int L, int cin, int cout, "
         "int ksize, int mode, int in_rs, int in_off, bool det=False) -> ()");
   m.def("gf_wgrad(Tensor x, Tensor dz, int R, int cin, int cout, int k, Tensor(a!) gw, Tensor(b!) part) -> ()");
+  m.def("gx3_pack(Tensor[] w, Tensor(a!)[] fwd, Tensor(b!)[] dgr, Tensor(c!)[] wsc, int[] k, int[] cin, int[] cout, "
+        "Tensor(d!) wpart) -> ()");
+  m.def("gx3_amax(Tensor x, int n, Tensor(a!) amax) -> ()");
+  m.def("gx3_conv(Tensor x, Tensor wfrag, Tensor wsc, Tensor? bias, Tensor(a!) y, Tensor(b!)? stats, Tensor(c!)? amax, "
+        "int n, int L, int cin, int cout, int ksize, int mode, int in_rs, int in_off, bool det=False) -> ()");
+  m.def("gx3_wgrad(Tensor x, Tensor dz, Tensor amax_x, Tensor amax_dz, int R, int cin, int cout, int k, Tensor(a!) gw, "
+        "Tensor(b!) part) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
@@ -944,6 +1076,10 @@ TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
   m.impl("gt_pack", &gt_pack);
   m.impl("gf_conv", &gf_conv);
   m.impl("gf_wgrad", &gf_wgrad);
+  m.impl("gx3_pack", &gx3_pack);
+  m.impl("gx3_amax", &gx3_amax);
+  m.impl("gx3_conv", &gx3_conv);
+  m.impl("gx3_wgrad", &gx3_wgrad);
   m.impl("prep_standardize", &prep_standardize);
   m.impl("prep_knn", &prep_knn);
 }

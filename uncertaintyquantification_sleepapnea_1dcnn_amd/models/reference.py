@@ -110,6 +110,7 @@ def forward(
     return_logits: bool = False,
     bn_stats_hook=None,
     dtype: Optional[torch.dtype] = None,
+    relu_masks=None,
 ) -> torch.Tensor:
     """Forward pass; returns probabilities (N, 1) (or logits).
 
@@ -120,7 +121,10 @@ def forward(
     the reference MC Dropout loop).  ``bn_stats_hook(h) -> (mean, var)`` replaces the
     local batch statistics (data-parallel SyncBN: global moments via a differentiable all-reduce).
     ``dtype`` (default fp32, the reference's precision) selects the compute dtype; tests use float64
-    (with float64 parameters) as the exact oracle the fp32 paths are measured against.
+    (with float64 parameters) as the exact oracle the fp32 paths are measured against.  ``relu_masks``
+    (one bool (N, L, C) tensor per block) replaces each ReLU's branch choice by the given pattern -- the
+    oracle then differentiates the same piecewise-linear branch as an fp32 run whose pre-activations
+    sat within rounding of zero (a flipped ReLU moves a gradient by a whole element, not by rounding).
     """
     use_drop = training if dropout is None else dropout
     use_batch = training if bn_batch_stats is None else bn_batch_stats
@@ -129,7 +133,8 @@ def forward(
         sample_ids = torch.arange(n, device=x.device)
     h = x.float() if dtype is None else x.to(dtype)
     for i, b in enumerate(spec.blocks, start=1):
-        h = torch.relu(conv1d_same(h, p[f"conv1d_{i}/kernel"], p[f"conv1d_{i}/bias"]))
+        h = conv1d_same(h, p[f"conv1d_{i}/kernel"], p[f"conv1d_{i}/bias"])
+        h = torch.relu(h) if relu_masks is None else h * relu_masks[i - 1].to(h.dtype)
         gamma, beta = p[f"batchnorm_{i}/gamma"], p[f"batchnorm_{i}/beta"]
         mm, mv = p[f"batchnorm_{i}/moving_mean"], p[f"batchnorm_{i}/moving_variance"]
         if use_batch:

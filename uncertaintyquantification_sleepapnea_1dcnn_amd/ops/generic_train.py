@@ -43,6 +43,10 @@ TRAIN_PASS_BASE = 1 << 30  # == training/step.py
 SLOTS = 16  # == kStatSlots (csrc/generic_conv.hip, csrc/generic_train.hip)
 DET_BWD_SLOTS = 256  # deterministic mode: workgroups (= partial slots) of each backward-sum launch
 DET_WGRAD_GROUPS = 16  # deterministic mode: row groups (= partial slices) of each wgrad launch
+# conv kernels of the fp32 precision path: "x3" = fp16x3 MFMA (csrc/gx3_conv.hip: 22-bit operand
+# splits, fp32 accumulation, ~fp32 GEMM rounding, 3 bf16-rate MFMAs per 32-deep k-step) or "exact" =
+# the fp32-input MFMA (csrc/gf32_conv.hip: exact fp32 products at 1/16 of the bf16 rate)
+FP32_ENGINE = "x3"
 
 
 def deterministic() -> bool:
@@ -85,8 +89,10 @@ class GenericTrainWorkspace:
         self.model = model
         self.B = int(batch)
         self.with_backward = with_backward
-        # f32: precision="fp32" -- fp32 activations / gradients and fp32-input MFMA convs (csrc/gf32_conv.hip)
+        # f32: precision="fp32" -- fp32 activations / gradients; the convs on the fp16x3 MFMA
+        # (csrc/gx3_conv.hip) or, with FP32_ENGINE "exact", the fp32-input MFMA (csrc/gf32_conv.hip)
         self.f32 = bool(f32)
+        self.x3 = self.f32 and FP32_ENGINE == "x3"
         # deterministic mode: every cross-workgroup sum -- BN moments, backward sums, bias,
         # weight and head gradients -- goes through per-workgroup partial slots written with plain
         # stores and added in a fixed order (csrc/generic_*.hip ``det``), instead of fp32 atomics.
@@ -106,8 +112,13 @@ class GenericTrainWorkspace:
         # forward moment slots: (slots, 2, C); deterministic: one per (conv workgroup of 128 rows, wave row)
         fslots = [max(SLOTS, 2 * -(-B * self.L[l] // 128)) if self.det else SLOTS for l in range(nl)]
         sizes = [fslots[l] * 2 * self.ch[l + 1] for l in range(nl)]
-        self.st_all = torch.zeros(sum(sizes), device=dev)
-        self.st = list(torch.split(self.st_all, sizes))
+        # + the fp16x3 operand maxima (fp32 bits as int32, atomicMax): [conv input of block l] * nl,
+        # [dZ of block l] * nl -- zeroed with the moment slots every forward
+        self.st_all = torch.zeros(sum(sizes) + 2 * nl, device=dev)
+        self.st = list(torch.split(self.st_all[: sum(sizes)], sizes))
+        amax = self.st_all[sum(sizes):].view(torch.int32)
+        self.amax_x = [amax[l:l + 1] for l in range(nl)]
+        self.amax_dz = [amax[nl + l:nl + l + 1] for l in range(nl)]
         self.bn = [torch.zeros(4 * self.ch[l + 1], device=dev) for l in range(nl)]
         if with_backward:
             # dz of block l, zero-padded rows (n, t) at n * rs + p + t; dh[l] = dL/d(input of block l)
@@ -151,14 +162,34 @@ class GenericTrainWorkspace:
         self.xin[0][p: p + n * self.rs[0]].view(n, self.rs[0], self.ch[0])[:, p: p + self.L[0]].copy_(x)
 
     def pack(self, backward: bool):
-        """bf16 MFMA fragments of every conv kernel (forward; + dgrad orientation when training), all
-        blocks in one HIP launch into buffers allocated once (the weights change every step).  The fp32
-        kernels read the Keras kernels in place: nothing to pack."""
+        """MFMA fragments of every conv kernel (forward; + dgrad orientation when training), all blocks
+        in one HIP launch into buffers allocated once (the weights change every step): bf16, or on the
+        fp32 path the fp16x3 hi/lo fragments with one power-of-two prescale per kernel (two launches,
+        ``gx3_pack``; the scales in ``self.wsc``).  The exact-fp32 kernels read the Keras kernels in place."""
         v = self.model.store.views
         nl = len(self.ks)
-        if self.f32:
-            w = [v[f"conv1d_{l + 1}/kernel"] for l in range(nl)]
+        w = [v[f"conv1d_{l + 1}/kernel"] for l in range(nl)]
+        if self.f32 and not self.x3:
             return w, w
+        if self.x3:
+            if getattr(self, "_xf", None) is None:
+                dev = self.model.store.device
+                self._xf, self._xd = [], []
+                for l in range(nl):
+                    k, cin, cout = self.ks[l], self.ch[l], self.ch[l + 1]
+                    self._xf.append(torch.empty(2 * ((k * cin + 31) // 32) * 512 * ((cout + 15) // 16),
+                                                dtype=torch.float16, device=dev))
+                    self._xd.append(torch.empty(2 * ((k * cout + 31) // 32) * 512 * ((cin + 15) // 16),
+                                                dtype=torch.float16, device=dev) if l > 0 else
+                                    torch.empty(0, dtype=torch.float16, device=dev))
+                self._xnone = torch.empty(0, dtype=torch.float16, device=dev)
+                self._wsc_all = torch.ones(4 * nl, device=dev)  # one 16-B aligned slot per block
+                self.wsc = [self._wsc_all[4 * l:4 * l + 1] for l in range(nl)]
+                self._wmaxpart = torch.empty(16 * nl, device=dev)
+            dgr = self._xd if backward else [self._xnone] * nl
+            _ext.ops().gx3_pack(w, self._xf, dgr, self.wsc, list(self.ks), list(self.ch[:-1]), list(self.ch[1:]),
+                                self._wmaxpart)
+            return self._xf, [d if d.numel() else None for d in dgr]
         if getattr(self, "_wf", None) is None:
             dev = self.model.store.device
             self._wf, self._wd = [], []
@@ -185,7 +216,8 @@ def _frag(w: torch.Tensor) -> torch.Tensor:
 def _get_ws(model, batch: int, with_backward: bool = True, f32: bool = False) -> GenericTrainWorkspace:
     attr = ("_gtrain_ws" if with_backward else "_gfwd_ws") + ("32" if f32 else "")
     ws = getattr(model, attr, None)
-    if ws is None or ws.B < batch or (not f32 and ws.det != deterministic()):
+    if (ws is None or ws.B < batch or (not f32 and ws.det != deterministic())
+            or (f32 and ws.x3 != (FP32_ENGINE == "x3"))):
         ws = GenericTrainWorkspace(model, batch, with_backward=with_backward, f32=f32)
         setattr(model, attr, ws)
     return ws
@@ -203,9 +235,13 @@ def _forward(ws: GenericTrainWorkspace, n: int, global_n: int, seed: int, pass_i
     for l, b in enumerate(spec.blocks):
         i = l + 1
         cin, cout, L = ws.ch[l], ws.ch[l + 1], ws.L[l]
-        conv = o.gf_conv if ws.f32 else o.gt_conv
-        conv(ws.xin[l], wf[l], v[f"conv1d_{i}/bias"], ws.z[l], ws.st[l], n, L, cin, cout, ws.ks[l], 1,
-             ws.rs[l], 2 * ws.pads[l], ws.det)
+        if ws.x3:
+            o.gx3_conv(ws.xin[l], wf[l], ws.wsc[l], v[f"conv1d_{i}/bias"], ws.z[l], ws.st[l], ws.amax_x[l], n, L, cin,
+                       cout, ws.ks[l], 1, ws.rs[l], 2 * ws.pads[l], ws.det)
+        else:
+            conv = o.gf_conv if ws.f32 else o.gt_conv
+            conv(ws.xin[l], wf[l], v[f"conv1d_{i}/bias"], ws.z[l], ws.st[l], n, L, cin, cout, ws.ks[l], 1,
+                 ws.rs[l], 2 * ws.pads[l], ws.det)
         if sync is not None:
             sync(ws.st[l])
         o.gt_bn_finalize(ws.st[l], cout, 1.0 / (global_n * L), v[f"batchnorm_{i}/gamma"], v[f"batchnorm_{i}/beta"],
@@ -267,6 +303,16 @@ def _grads(model, ws: GenericTrainWorkspace, y: torch.Tensor, n: int, gb: int, p
                  thr, ik, skey, int(window_offset), None, ws.coef[l], v[f"batchnorm_{i}/gamma"], ws.dzp[l], ws.rs[l], p,
                  ws.dbs[l], kd, ws.det)
         torch.sum(ws.dbs[l], 0, out=g[f"conv1d_{i}/bias"])
+        if ws.x3:
+            # dgrad publishes dZ's tensor maximum for the wgrad prescale (block 1: no dgrad, amax kernel)
+            if l > 0:
+                o.gx3_conv(ws.dzp[l], wd[l], ws.wsc[l], None, ws.dh[l], None, ws.amax_dz[l], n, L, cout, cin, k, 2,
+                           ws.rs[l], p)
+            else:
+                o.gx3_amax(ws.dzp[l], n * ws.rs[l] * cout, ws.amax_dz[l])
+            o.gx3_wgrad(ws.xin[l], ws.dzp[l], ws.amax_x[l], ws.amax_dz[l], n * ws.rs[l], cin, cout, k,
+                        g[f"conv1d_{i}/kernel"], ws.wpart)
+            continue
         if l > 0:
             (o.gf_conv if ws.f32 else o.gt_conv)(ws.dzp[l], wd[l], None, ws.dh[l], None, n, L, cout, cin, k, 2,
                                                  ws.rs[l], p)
@@ -378,7 +424,7 @@ def graph_train_step(model, x: torch.Tensor, y: torch.Tensor):
     n = int(x.shape[0])
     cur = g.get(n)
     if (cur is None or not train_ops._same_bound(cur.bound, train_ops.bound_key(model)) or cur.f32 != _f32(model)
-            or (not cur.f32 and cur.det != deterministic())):
+            or (not cur.f32 and cur.det != deterministic()) or (cur.f32 and cur.ws.x3 != (FP32_ENGINE == "x3"))):
         g[n] = cur = GraphedGenericStep(model, n)
     return cur(x, y)
 
@@ -437,7 +483,8 @@ def forward_running_f32(model, x: torch.Tensor, n_pass: int = 1, dropout: bool =
     """Inference with BN on the moving statistics (Deep-Ensemble ``predict`` / standard MC Dropout,
     ``uq_techniques.py:22-30``) at the reference's fp32 for ANY spec -- the MaxPool1D variant of the
     thesis' ``ensemble_cnn`` members (``evaluate_de_global.py:18-38``), the 30 s single-channel window --
-    on the fp32-input MFMA conv (``csrc/gf32_conv.hip``) and the fp32 BN / pool / dropout kernels:
+    on the fp16x3 conv (``csrc/gx3_conv.hip``; FP32_ENGINE "exact": ``csrc/gf32_conv.hip``) and the fp32
+    BN / pool / dropout kernels:
     (n_pass, N) probabilities (or logits).  The passes run one after the other (each its own dropout
     stream, keyed by the global window id); windows in chunks of at most ``F32_INFER_WS_BYTES`` of
     activations (the dropout keys stay global: chunk s starts at window_offset + s)."""
@@ -460,6 +507,7 @@ def _forward_running_f32_chunk(model, x, n_pass, dropout, seed, pass_offset, win
     ws = _get_ws(model, n, with_backward=False, f32=True)
     running_affine(model, ws)
     ws.load_input(x)
+    wf, _ = ws.pack(backward=False)
     v = model.store.views
     wdense = v["output_layer/kernel"].reshape(-1)
     nl = len(spec.blocks)
@@ -469,38 +517,12 @@ def _forward_running_f32_chunk(model, x, n_pass, dropout, seed, pass_offset, win
             i = l + 1
             cin, cout, L = ws.ch[l], ws.ch[l + 1], ws.L[l]
             if l > 0 or conv0:  # block 1 does not depend on the pass (no dropout before it)
-                o.gf_conv(ws.xin[l], v[f"conv1d_{i}/kernel"], v[f"conv1d_{i}/bias"], ws.z[l], ws.st[l], n, L, cin,
-                          cout, ws.ks[l], 1, ws.rs[l], 2 * ws.pads[l], True)
-            if l + 1 < nl:
-                dst, drs, doff = ws.xin[l + 1], ws.rs[l + 1], 2 * ws.pads[l + 1]
-            else:
-                dst, drs, doff = ws.hlast, ws.L[-1], 0
-            drop = bool(dropout and b.dropout > 0)
-            o.gt_apply(ws.z[l], ws.bn[l], dst, n, L, cout, bool(b.pool), drs, doff, drop,
-                       rng.dropout_threshold(b.dropout), _inv_keep(b.dropout),
-                       rng.stream_key(seed, l, pass_offset + t), int(window_offset), None)
-        conv0 = False
-        h = ws.hlast[: n * ws.L[-1]].view(n, ws.L[-1], ws.ch[-1])
-        lg = torch.addmv(v["output_layer/bias"], h.mean(dim=1), wdense)
-        out[t] = lg if logits else torch.sigmoid(lg)
-    if not dropout:
-        out[1:] = out[0]
-    return out
-    spec, o = model.spec, _ext.ops()
-    ws = _get_ws(model, n, with_backward=False, f32=True)
-    running_affine(model, ws)
-    ws.load_input(x)
-    v = model.store.views
-    wdense = v["output_layer/kernel"].reshape(-1)
-    nl = len(spec.blocks)
-    conv0 = True
-    for t in range(n_pass if dropout else 1):
-        for l, b in enumerate(spec.blocks):
-            i = l + 1
-            cin, cout, L = ws.ch[l], ws.ch[l + 1], ws.L[l]
-            if l > 0 or conv0:  # block 1 does not depend on the pass (no dropout before it)
-                o.gf_conv(ws.xin[l], v[f"conv1d_{i}/kernel"], v[f"conv1d_{i}/bias"], ws.z[l], ws.st[l], n, L, cin,
-                          cout, ws.ks[l], 1, ws.rs[l], 2 * ws.pads[l], True)
+                if ws.x3:
+                    o.gx3_conv(ws.xin[l], wf[l], ws.wsc[l], v[f"conv1d_{i}/bias"], ws.z[l], ws.st[l], None, n, L,
+                               cin, cout, ws.ks[l], 1, ws.rs[l], 2 * ws.pads[l], True)
+                else:
+                    o.gf_conv(ws.xin[l], wf[l], v[f"conv1d_{i}/bias"], ws.z[l], ws.st[l], n, L, cin, cout,
+                              ws.ks[l], 1, ws.rs[l], 2 * ws.pads[l], True)
             if l + 1 < nl:
                 dst, drs, doff = ws.xin[l + 1], ws.rs[l + 1], 2 * ws.pads[l + 1]
             else:
