@@ -583,6 +583,7 @@ void gt_bn_finalize(const at::Tensor& st, int64_t C, double inv_count, const at:
   need_f32(bn, 4 * C, "gt_bn_finalize bn");
   const at::DeviceGuard guard(bn.device());
   // every slot of the table is summed (in a fixed order): kGtSlots atomic copies or the deterministic slots
+  // (large tables in 64-slot ranges whose sums overwrite the ranges' first slots: st is consumed)
   check(apneauq::launch_gt_bn_finalize(st.data_ptr<float>(), (int)(st.numel() / (2 * C)), (int)C, (float)inv_count,
                                        gamma.data_ptr<float>(),
                                        beta.data_ptr<float>(), (float)eps, (float)momentum, mmean.data_ptr<float>(),

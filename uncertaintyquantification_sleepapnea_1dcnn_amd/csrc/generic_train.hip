@@ -55,14 +55,79 @@ __device__ __forceinline__ bool slot_pair_sums(const float* st, int nslots, int 
   return true;
 }
 
+// Large slot tables (deterministic mode: one slot per producing workgroup, ~15 k for a 16384-window
+// batch-statistics MC-Dropout pass) are summed in two launches: slot_partial_kernel adds every range of
+// kRange consecutive slots (fixed order, fp64) and parks the two sums in the range's first two slots
+// (their fp32 words hold the fp64 bits: the raw table is dead after the finalize), then the finalize
+// adds the ranges in order.  One 16-channel block per C / 16 with a serial pass over 15 k slots took
+// ~130 us per call.
+constexpr int kRange = 64;
+
+__global__ __launch_bounds__(256) void slot_partial_kernel(float* st, int nslots, int C) {
+  __shared__ double red[2][256];
+  const int chl = threadIdx.x & 15, lane = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + chl;
+  const int s0 = blockIdx.y * kRange, s1e = min(nslots, s0 + kRange);
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    for (int s = s0 + lane; s < s1e; s += 16) {
+      a += (double)st[(long long)s * 2 * C + c];
+      b += (double)st[(long long)s * 2 * C + C + c];
+    }
+  }
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = b;
+  __syncthreads();  // every read of this range is done before the range's first slots are overwritten
+  if (threadIdx.x >= 16 || c >= C) return;
+  double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    t1 += red[0][j * 16 + chl];
+    t2 += red[1][j * 16 + chl];
+  }
+  unsigned* w = reinterpret_cast<unsigned*>(st) + (long long)s0 * 2 * C;
+  const unsigned long long b1 = __double_as_longlong(t1), b2 = __double_as_longlong(t2);
+  w[c] = (unsigned)b1;
+  w[C + c] = (unsigned)(b1 >> 32);
+  w[2 * C + c] = (unsigned)b2;
+  w[3 * C + c] = (unsigned)(b2 >> 32);
+}
+
+__device__ __forceinline__ double packed_sum(const float* st, int C, int range, int word) {
+  const unsigned* w = reinterpret_cast<const unsigned*>(st) + (long long)range * kRange * 2 * C;
+  return __longlong_as_double((long long)(((unsigned long long)w[word + C] << 32) | w[word]));
+}
+
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* st, int nslots, int C, float inv_count,
                                                           const float* gamma, const float* beta, float eps,
                                                           float momentum, float* mmean, float* mvar, int update,
-                                                          float* bn) {
+                                                          float* bn, int packed) {
   __shared__ double red[2][256];
   double s1, s2;
   int c;
-  if (!slot_pair_sums(st, nslots, C, red, s1, s2, c)) return;
+  if (packed) {  // nslots = ranges of slot_partial_kernel: their fp64 sums, added in range order
+    const int chl = threadIdx.x & 15, lane = threadIdx.x >> 4;
+    c = blockIdx.x * 16 + chl;
+    double a = 0.0, b = 0.0;
+    if (c < C) {
+      for (int r = lane; r < nslots; r += 16) {
+        a += packed_sum(st, C, r, c);
+        b += packed_sum(st, C, r, 2 * C + c);
+      }
+    }
+    red[0][threadIdx.x] = a;
+    red[1][threadIdx.x] = b;
+    __syncthreads();
+    if (threadIdx.x >= 16 || c >= C) return;
+    s1 = s2 = 0.0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      s1 += red[0][j * 16 + chl];
+      s2 += red[1][j * 16 + chl];
+    }
+  } else if (!slot_pair_sums(st, nslots, C, red, s1, s2, c)) {
+    return;
+  }
   const double meand = s1 * inv_count;
   const float mean = (float)meand;
   const float var = (float)fmax(s2 * inv_count - meand * meand, 0.0);
@@ -305,8 +370,16 @@ inline int elem_grid(long long items, int per_block) {
 hipError_t launch_gt_bn_finalize(const float* st, int nslots, int C, float inv_count, const float* gamma,
                                  const float* beta, float eps, float momentum, float* mmean, float* mvar, int update,
                                  float* bn, hipStream_t stream) {
+  if (nslots >= 4 * gtrain::kRange) {
+    const int ranges = (nslots + gtrain::kRange - 1) / gtrain::kRange;
+    hipLaunchKernelGGL(gtrain::slot_partial_kernel, dim3((C + 15) / 16, ranges), dim3(256), 0, stream,
+                       const_cast<float*>(st), nslots, C);
+    hipLaunchKernelGGL(gtrain::bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, stream, st, ranges, C, inv_count,
+                       gamma, beta, eps, momentum, mmean, mvar, update, bn, 1);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(gtrain::bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, stream, st, nslots, C, inv_count,
-                     gamma, beta, eps, momentum, mmean, mvar, update, bn);
+                     gamma, beta, eps, momentum, mmean, mvar, update, bn, 0);
   return hipGetLastError();
 }
 

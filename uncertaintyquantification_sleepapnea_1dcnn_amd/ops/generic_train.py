@@ -172,6 +172,11 @@ class GenericTrainWorkspace:
         if self.f32 and not self.x3:
             return w, w
         if self.x3:
+            # inference packs once per parameter version (training repacks every step)
+            key = (id(self.model.store), self.model.store.version, bool(backward))
+            if not backward and getattr(self, "_xpack_key", None) == key:
+                return self._xf, [None] * nl
+            self._xpack_key = key
             if getattr(self, "_xf", None) is None:
                 dev = self.model.store.device
                 self._xf, self._xd = [], []
@@ -232,6 +237,7 @@ def _forward(ws: GenericTrainWorkspace, n: int, global_n: int, seed: int, pass_i
     spec, v = ws.model.spec, ws.model.store.views
     nl = len(spec.blocks)
     ws.st_all.zero_()
+    ws._running_key = None  # ws.bn gets the batch affine below (running_affine must rebuild it)
     for l, b in enumerate(spec.blocks):
         i = l + 1
         cin, cout, L = ws.ch[l], ws.ch[l + 1], ws.L[l]
@@ -455,8 +461,13 @@ def forward_batch_stats(model, x: torch.Tensor, n_pass: int, pass_base: int, see
 
 
 def running_affine(model, ws: GenericTrainWorkspace) -> None:
-    """BN on the moving statistics, as the (4, C) rows [scale, shift, mean, rstd] gt_apply reads."""
+    """BN on the moving statistics, as the (4, C) rows [scale, shift, mean, rstd] gt_apply reads
+    (recomputed only when the store's parameters changed since the last call on this workspace)."""
     spec, v = model.spec, model.store.views
+    key = (id(model.store), model.store.version)
+    if getattr(ws, "_running_key", None) == key:
+        return
+    ws._running_key = key
     for l in range(len(spec.blocks)):
         i = l + 1
         mm, mv = v[f"batchnorm_{i}/moving_mean"], v[f"batchnorm_{i}/moving_variance"]
