@@ -48,6 +48,7 @@ namespace x3 {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(1))) const f16x8 gf16x8;
 
 // Staging waves of a layer without loader waves: the HBM loads of the next chunk are issued by MFMA
@@ -293,16 +294,28 @@ __global__ __launch_bounds__((WM * WN + loaders(LW)) * 64, (waves_per_eu<WM * WN
         for (int i = 1; i < kSP; ++i) sp = (s >> 2) == i ? sa_pack[i] : sp;
         sa = __builtin_amdgcn_sbfe((int)sp, 8 * (s & 3), 8);
       }
-      f16x4 hi, lo;
+      float a[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float a = (valid && keep[i]) ? ldexpf(__builtin_fmaf(v[i], R.a[i], R.b[i]), sa) : 0.f;
-        hi[i] = (_Float16)a;
-        lo[i] = (_Float16)(a - (float)hi[i]);
+      for (int i = 0; i < 4; ++i) a[i] = (valid && keep[i]) ? ldexpf(__builtin_fmaf(v[i], R.a[i], R.b[i]), sa) : 0.f;
+      // hi = fp16(a) two at a time (v_cvt_pk_f16_f32); lo = fp16(a - hi) in one mixed-precision FMA
+      // per element, a - hi evaluated in fp32 from hi's f16 half (op_sel_hi on src0), written straight
+      // into the pair's lo/hi half: 6 VALU per 4 elements instead of 16, bit-identical to the plain
+      // convert/convert/subtract/convert (tools/probes/split/split_check.hip, 8.4 M pairs)
+      uint2 hi, lo;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const unsigned u = __builtin_bit_cast(unsigned, (f16x2){(_Float16)a[2 * p], (_Float16)a[2 * p + 1]});
+        unsigned l;
+        asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l) : "v"(u), "v"(a[2 * p]));
+        asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+                     : "+v"(l)
+                     : "v"(u), "v"(a[2 * p + 1]));
+        (p ? hi.y : hi.x) = u;
+        (p ? lo.y : lo.x) = l;
       }
       char* row = buf + (kHalo + s * kSR + t) * kRowB + 8 * q;
-      *reinterpret_cast<f16x4*>(row) = hi;
-      *reinterpret_cast<f16x4*>(row + 2 * kCK) = lo;
+      *reinterpret_cast<uint2*>(row) = hi;
+      *reinterpret_cast<uint2*>(row + 2 * kCK) = lo;
     }
   };
 
