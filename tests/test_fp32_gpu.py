@@ -17,7 +17,7 @@ import torch
 from uncertaintyquantification_sleepapnea_1dcnn_amd.models import reference as R
 from uncertaintyquantification_sleepapnea_1dcnn_amd.models.cnn import AlarconCNN1D
 from uncertaintyquantification_sleepapnea_1dcnn_amd.models.spec import DEFAULT_SPEC
-from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import _ext, generic_train
+from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import _ext, fused, generic_train
 from uncertaintyquantification_sleepapnea_1dcnn_amd.training import step as tstep
 
 from .test_generic_gpu import SPECS
@@ -266,3 +266,55 @@ def test_gx3_conv_and_wgrad_match_float64(cin, L, k, scale):
     ref = torch.stack([xp[t: t + n * rs].t() @ dzc for t in range(k)])
     err = (gw.cpu().double() - ref).abs().max().item()
     assert err <= 2e-6 * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize("name", ["pooled", "single30"])
+@pytest.mark.parametrize("scale", [1e-4, 1.0, 3e3])
+def test_fused_x3_matches_float64(name, scale):
+    """``csrc/fused_tiled_x3.hip`` (the fp32 default for the pooled / single-channel nets) against the
+    float64 reference forward with BN on the moving statistics, dropout off and on (standard MC Dropout,
+    the same counter-based masks) at input scales 1e-4 .. 3e3 (the per-sample power-of-two prescales
+    keep every fp16 half in range): logits within 1e-5 (1 + |logit|) of float64, plus 4x the error of
+    the fp32 PyTorch reference itself (at 3e3 the moving-statistics BN leaves the activations ~1e3
+    times their trained range and the GAP . Dense sum cancels: fp32 itself is off by ~1e-4 there)."""
+    from .test_fused_tiled_gpu import NETS
+
+    _ext.require()
+    fused.check_layout_x3()
+    spec = NETS[name]
+    p = R.synthetic_params(spec, 7)
+    m = AlarconCNN1D(spec=spec, seed=7, device="cuda", params=p)
+    n = 37
+    x = torch.randn(n, spec.input_length, spec.input_channels, generator=torch.Generator().manual_seed(8)) * scale
+    p64 = {k: v.double() for k, v in p.items()}
+    blob = m.fused_blob_x3()
+    for drop in (False, True):
+        got = fused.tiled_x3_forward(x.cuda(), blob, spec, n_pass=2, dropout=drop, seed=3, pass_offset=4,
+                                     window_offset=100, logits=True)[0].double().cpu()
+        for t in range(2):
+            ref = R.forward(spec, p64, x.double(), dropout=drop, bn_batch_stats=False, seed=3, pass_id=4 + t,
+                            sample_ids=torch.arange(100, 100 + n), return_logits=True, dtype=torch.float64).reshape(-1)
+            r32 = R.forward(spec, p, x, dropout=drop, bn_batch_stats=False, seed=3, pass_id=4 + t,
+                            sample_ids=torch.arange(100, 100 + n), return_logits=True).reshape(-1).double()
+            e32 = float((r32 - ref).abs().max())
+            err = (got[t] - ref).abs()
+            assert bool((err <= 1e-5 * (1.0 + ref.abs()) + 4 * e32).all()), (drop, t, float(err.max()), e32)
+
+
+def test_fused_x3_is_the_fp32_default_and_shard_invariant(monkeypatch):
+    """hip_infer at precision "fp32" on the pooled net runs the fused x3 kernel (the layer-wise path is
+    not called), and a sample's result does not depend on the samples sharing its workgroup: windows
+    split into shards with global window ids give bitwise the same MC-Dropout probabilities."""
+    _ext.require()
+    spec = SPECS["pooled"]
+    m = AlarconCNN1D(spec=spec, seed=5, device="cuda", params=R.synthetic_params(spec, 5))
+
+    def boom(*a, **k):
+        raise AssertionError("layer-wise fp32 path used")
+
+    monkeypatch.setattr(generic_train, "forward_running_f32", boom)
+    x = torch.randn(45, spec.input_length, spec.input_channels, generator=torch.Generator().manual_seed(6)).cuda()
+    x[7] *= 1e3  # a loud neighbour must not change the others' prescales
+    full = m.hip_infer(x, n_pass=3, dropout=True, seed=2)
+    parts = [m.hip_infer(x[a:b], n_pass=3, dropout=True, seed=2, window_offset=a) for a, b in ((0, 5), (5, 22), (22, 45))]
+    torch.testing.assert_close(torch.cat(parts, dim=1), full, atol=0, rtol=0)

@@ -170,3 +170,31 @@ def test_fused_pooled_dispatch_and_blob():
     a = generic.emulate(pooled, p, x, logits=True)
     b = generic.emulate(pooled, p, x, logits=True, last_fp32=True)
     assert torch.equal(a, b)
+
+
+def test_fused_x3_blob_packing():
+    """fp16x3 blob of the fp32 fused kernel (ops/fused.py:pack_blob_x3): the hi + lo fragments of each
+    layer reproduce W within 2^-21 of max |W| (one power-of-two prescale per layer), the epilogue scale
+    carries the inverse power of two, the layout matches the kernel's constants (fused_blob.h)."""
+    import dataclasses
+
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import fused
+
+    pooled = dataclasses.replace(DEFAULT_SPEC, blocks=tuple(dataclasses.replace(b, pool=(i < 5))
+                                                            for i, b in enumerate(DEFAULT_SPEC.blocks)))
+    p = R.synthetic_params(pooled, 3)
+    blob = fused.pack_blob_x3(pooled, p)
+    lay = fused.layout_x3()
+    assert blob.numel() == lay["bytes"]
+    ch, ks = fused.FUSED_CHANNELS, fused.FUSED_KSIZES
+    for l in range(6):
+        w = p[f"conv1d_{l + 1}/kernel"].float()
+        fr, sw = fused.pack_conv_fragments_x3(w)
+        nb = fr.numel() * 2
+        assert torch.equal(blob[lay["woff"][l]: lay["woff"][l] + nb].view(torch.float16).reshape(fr.shape), fr)
+        assert fused.pow2_exponent(float(w.abs().max() * 2.0 ** sw)) == 0  # max |W| 2^sw in [2^13, 2^14)
+        back = fused.unpack_conv_fragments_x3(fr, sw, ks[l], ch[l], ch[l + 1])
+        assert (back - w).abs().max() <= 2.0 ** -21 * w.abs().max()
+        epi = blob[lay["eoff"][l]: lay["eoff"][l] + 4 * 8 * ch[l + 1]].view(torch.float32).reshape(8, ch[l + 1])
+        scale, _ = fused.bn_affine(pooled, p, l + 1)
+        torch.testing.assert_close(epi[0], scale * 2.0 ** -sw, rtol=0, atol=0)

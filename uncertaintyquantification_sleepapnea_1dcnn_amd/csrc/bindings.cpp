@@ -23,6 +23,11 @@ hipError_t launch_fused_tiled(int net, const void* x, const uint8_t* blob, long 
                               hipStream_t stream);
 int fused_pooled_lds_bytes();
 void fused_layout(int* woffs, int* eoffs, int* dense_off);
+hipError_t launch_fused_tiled_x3(int net, const float* x, const uint8_t* blob, long long blob_stride, float* out,
+                                 int n_win, int n_pass, int n_member, unsigned window_offset, unsigned pass_offset,
+                                 unsigned long long seed, int dropout, int out_logits, const unsigned* thr,
+                                 hipStream_t stream);
+void fused_layout_x3(int* woffs, int* eoffs, int* dense_off, int* bytes, int* lds);
 hipError_t launch_uq_reduce(const float* probs, int t_count, int n, float* out, hipStream_t stream);
 hipError_t launch_bootstrap(const float* metrics, const int* y, const int* idx, unsigned seed, int n, int n_boot,
                             double* out, hipStream_t stream);
@@ -187,6 +192,40 @@ at::Tensor fused_single_forward(const at::Tensor& x, const at::Tensor& blob, int
                                 int64_t pass_offset, int64_t seed, bool dropout, bool out_logits, at::IntArrayRef thr,
                                 at::ArrayRef<double> dscale) {
   return fused_forward_impl(x, blob, n_pass, window_offset, pass_offset, seed, dropout, out_logits, thr, dscale, 0, 1);
+}
+
+// fp32-faithful fused inference of the pooled (net 0) / single-channel 30 s (net 1) CNN
+// (csrc/fused_tiled_x3.hip): fp32 x, fp16x3 blob (ops/fused.py:pack_blob_x3)
+at::Tensor fused_tiled_x3_forward(const at::Tensor& x, const at::Tensor& blob, int64_t net, int64_t n_pass,
+                                  int64_t window_offset, int64_t pass_offset, int64_t seed, bool dropout,
+                                  bool out_logits, at::IntArrayRef thr) {
+  TORCH_CHECK(net == 0 || net == 1, "fused_tiled_x3: net 0 (pooled) or 1 (single-channel)");
+  TORCH_CHECK(x.is_cuda() && blob.is_cuda(), "fused_tiled_x3: tensors must be on the GPU");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && x.is_contiguous(), "fused_tiled_x3: x must be contiguous fp32");
+  const int64_t want_l = net == 1 ? 30 : 60, want_c = net == 1 ? 1 : 4;
+  TORCH_CHECK(x.dim() == 3 && x.size(1) == want_l && x.size(2) == want_c, "fused_tiled_x3: x must be (N, ", want_l,
+              ", ", want_c, "), got ", x.sizes());
+  int w[6], e[6], d, nbytes, lds;
+  apneauq::fused_layout_x3(w, e, &d, &nbytes, &lds);
+  TORCH_CHECK(blob.scalar_type() == at::kByte && blob.dim() == 2 && blob.is_contiguous() && blob.size(1) == nbytes,
+              "fused_tiled_x3: blob must be contiguous uint8 (members, ", nbytes, ")");
+  TORCH_CHECK(thr.size() == 6, "fused_tiled_x3: need 6 dropout thresholds");
+  TORCH_CHECK(n_pass >= 1, "fused_tiled_x3: n_pass >= 1");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(blob.data_ptr()) % 16 == 0,
+              "fused_tiled_x3: 16-B alignment required");
+  const int64_t n_win = x.size(0), n_member = blob.size(0);
+  TORCH_CHECK(n_pass * n_win < (int64_t(1) << 31), "fused_tiled_x3: too many samples for one launch");
+  const at::DeviceGuard guard(x.device());
+  auto out = at::empty({n_member, n_pass, n_win}, x.options());
+  if (n_win == 0) return out;
+  unsigned t[6];
+  for (int i = 0; i < 6; ++i) t[i] = static_cast<unsigned>(thr[i]);
+  check(apneauq::launch_fused_tiled_x3((int)net, x.data_ptr<float>(), blob.data_ptr<uint8_t>(), blob.stride(0),
+                                       out.data_ptr<float>(), (int)n_win, (int)n_pass, (int)n_member,
+                                       (unsigned)window_offset, (unsigned)pass_offset, (unsigned long long)seed,
+                                       dropout ? 1 : 0, out_logits ? 1 : 0, t, cur_stream()),
+        "fused_tiled_x3");
+  return out;
 }
 
 at::Tensor uq_reduce(const at::Tensor& probs) {
@@ -994,6 +1033,19 @@ std::vector<int64_t> fused_layout() {
   return v;
 }
 
+// [woff x6, eoff x6, dense, bytes, lds(pooled), lds(single)] of the fp16x3 blob / kernel
+std::vector<int64_t> fused_layout_x3() {
+  int w[6], e[6], d, nbytes, lds[2];
+  apneauq::fused_layout_x3(w, e, &d, &nbytes, lds);
+  std::vector<int64_t> v(w, w + 6);
+  v.insert(v.end(), e, e + 6);
+  v.push_back(d);
+  v.push_back(nbytes);
+  v.push_back(lds[0]);
+  v.push_back(lds[1]);
+  return v;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(apneauq, m) {
@@ -1007,6 +1059,9 @@ TORCH_LIBRARY(apneauq, m) {
   m.def("bootstrap(Tensor metrics, Tensor y, Tensor? idx, int seed, int n_boot) -> Tensor");
   m.def("bootstrap_partial(Tensor metrics, Tensor y, Tensor? idx, int seed, int n_boot, int n_global, int lo) -> Tensor");
   m.def("fused_layout() -> int[]", &fused_layout);
+  m.def("fused_layout_x3() -> int[]", &fused_layout_x3);
+  m.def("fused_tiled_x3_forward(Tensor x, Tensor blob, int net, int n_pass, int window_offset, int pass_offset, "
+        "int seed, bool dropout, bool out_logits, int[] thr) -> Tensor");
   m.def("train_call(Tensor ctx, int op, int layer, int flag, int pass_base, int device) -> ()", &train_call);
   m.def("train_args_dev(Tensor[] ctxs, int device) -> Tensor", &train_args_dev);
   m.def("train_call_mb(Tensor args_dev, Tensor ctx0, int M, int op, int layer, int flag) -> ()", &train_call_mb);
@@ -1056,6 +1111,7 @@ TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
   m.impl("fused_forward", &fused_forward);
   m.impl("fused_pooled_forward", &fused_pooled_forward);
   m.impl("fused_single_forward", &fused_single_forward);
+  m.impl("fused_tiled_x3_forward", &fused_tiled_x3_forward);
   m.impl("uq_reduce", &uq_reduce);
   m.impl("bootstrap", &bootstrap);
   m.impl("bootstrap_partial", &bootstrap_partial);

@@ -19,5 +19,13 @@ __host__ __device__ constexpr int eoff(int l) { return l == 0 ? woff(6) : eoff(l
 constexpr int kDenseOff = eoff(6);
 constexpr int kBlobBytes = kDenseOff + ((C[6] + 1) * 4 + 15) / 16 * 16;
 
+// fp16x3 blob (fused_tiled_x3.hip, ops/fused.py:pack_blob_x3): per (k-step, channel tile) the hi and
+// the lo fragment of W 2^sw (2 KiB), then the same epilogue rows (scale x 2^-sw) and dense head
+__host__ __device__ constexpr int wbytes3(int l) { return 2 * wbytes(l); }
+__host__ __device__ constexpr int woff3(int l) { return l == 0 ? 0 : woff3(l - 1) + wbytes3(l - 1); }
+__host__ __device__ constexpr int eoff3(int l) { return l == 0 ? woff3(6) : eoff3(l - 1) + ebytes(l - 1); }
+constexpr int kDenseOff3 = eoff3(6);
+constexpr int kBlobBytes3 = kDenseOff3 + ((C[6] + 1) * 4 + 15) / 16 * 16;
+
 }  // namespace fused
 }  // namespace apneauq

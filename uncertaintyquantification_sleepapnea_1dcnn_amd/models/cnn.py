@@ -195,8 +195,15 @@ class AlarconCNN1D:
                 return self.hip_forward(x.to(torch.bfloat16).contiguous(), n_pass=n_pass, dropout=dropout,
                                         seed=seed, pass_offset=pass_offset, window_offset=window_offset,
                                         logits=logits)
-            # any other architecture (MaxPool1D blocks, the 30 s single-channel window) at fp32: the
-            # fp32-input MFMA layer-wise path (ops/generic_train.py:forward_running_f32)
+            _ext.require()
+            if fused.tiled_net(self.spec) is not None and os.environ.get("APNEAUQ_TILED_FUSED", "1") != "0":
+                # the pooled ensemble_cnn members / the 30 s single-channel window: the fp16x3 fused
+                # whole-network kernel (csrc/fused_tiled_x3.hip)
+                return fused.tiled_x3_forward(x, self.fused_blob_x3(), self.spec, n_pass=n_pass, dropout=dropout,
+                                              seed=self.seed if seed is None else seed, pass_offset=pass_offset,
+                                              window_offset=window_offset, logits=logits)[0]
+            # any other architecture at fp32: the fp16x3 layer-wise path
+            # (ops/generic_train.py:forward_running_f32)
             from ..ops import generic_train
 
             _ext.require()
@@ -236,6 +243,13 @@ class AlarconCNN1D:
 
         return generic.forward(self.generic_pack(), self.spec, x_bf16, n_pass=n_pass, dropout=dropout, seed=seed,
                                pass_offset=pass_offset, window_offset=window_offset, logits=logits)
+
+    def fused_blob_x3(self) -> torch.Tensor:
+        """Packed fp16x3 parameters for the fp32 fused kernel (cached per weight version)."""
+        if getattr(self, "_blob3", None) is None or self._blob3_version != self.store.version:
+            self._blob3 = fused.pack_blob_x3(self.spec, self.store.as_dict()).unsqueeze(0)
+            self._blob3_version = self.store.version
+        return self._blob3
 
     def fused_blob(self) -> torch.Tensor:
         """Packed parameters for the fused HIP kernel (cached per weight version)."""

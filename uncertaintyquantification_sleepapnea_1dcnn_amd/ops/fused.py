@@ -166,6 +166,122 @@ def pack_blob(spec: ModelSpec, p, bn_override: Optional[Sequence] = None) -> tor
     return blob
 
 
+# ------------------------------------------------------------------------------------------------
+# fp16x3 blob of the fp32-faithful fused kernel (csrc/fused_tiled_x3.hip): per (k-step, channel tile)
+# the hi and the lo fp16 fragment of W 2^sw (sw: one power of two per layer putting max |W| 2^sw in
+# [2^13, 2^14)), then the epilogue rows with the BN scale x 2^-sw, then the dense head.
+# ------------------------------------------------------------------------------------------------
+def layout_x3() -> Dict[str, object]:
+    ch, ks = FUSED_CHANNELS, FUSED_KSIZES
+    woff, eoff = [], []
+    off = 0
+    for l in range(6):
+        woff.append(off)
+        off += 2 * ((ch[l] * ks[l] + 31) // 32) * (ch[l + 1] // 16) * 1024
+    for l in range(6):
+        eoff.append(off)
+        off += _ceil(EPI_ROWS * ch[l + 1] * 4, 16)
+    dense = off
+    total = dense + _ceil((ch[6] + 1) * 4, 16)
+    return {"woff": woff, "eoff": eoff, "dense": dense, "bytes": total}
+
+
+def check_layout_x3() -> None:
+    lay = layout_x3()
+    v = list(_ext.ops().fused_layout_x3())
+    want = lay["woff"] + lay["eoff"] + [lay["dense"], lay["bytes"]]
+    if v[:14] != want:
+        raise RuntimeError(f"fused x3 blob layout mismatch host={want} kernel={v[:14]}")
+
+
+def pow2_exponent(maxabs: float) -> int:
+    """The power of two that puts a nonzero ``maxabs`` into [2^13, 2^14) (0 for zero / non-finite)."""
+    import math
+
+    if not (maxabs > 0.0 and math.isfinite(maxabs)):
+        return 0
+    return max(-100, min(100, 14 - math.frexp(maxabs)[1]))
+
+
+def pack_conv_fragments_x3(kernel: torch.Tensor):
+    """Keras conv kernel (k, Cin, Cout) -> (fragments (nstep, Cout/16, 2, 64, 8) fp16 [hi, lo] of
+    W 2^sw, sw)."""
+    k, cin, cout = kernel.shape
+    K = k * cin
+    nstep = (K + 31) // 32
+    w = kernel.detach().float()
+    sw = pow2_exponent(float(w.abs().max()))
+    wt = torch.ldexp(w.reshape(K, cout).t(), torch.tensor(float(sw), device=w.device))
+    wt = torch.nn.functional.pad(wt, (0, nstep * 32 - K))
+    fr = wt.reshape(cout // 16, 16, nstep, 4, 8).permute(2, 0, 3, 1, 4).reshape(nstep, cout // 16, 64, 8)
+    hi = fr.to(torch.float16)
+    lo = (fr - hi.float()).to(torch.float16)
+    return torch.stack([hi, lo], dim=2).contiguous(), sw
+
+
+def unpack_conv_fragments_x3(fr: torch.Tensor, sw: int, k: int, cin: int, cout: int) -> torch.Tensor:
+    """Inverse of :func:`pack_conv_fragments_x3` (fp32 (k, Cin, Cout), hi + lo scaled back)."""
+    nstep = fr.shape[0]
+    w = fr[:, :, 0].float() + fr[:, :, 1].float()
+    wt = w.reshape(nstep, cout // 16, 4, 16, 8).permute(1, 3, 0, 2, 4).reshape(cout, nstep * 32)
+    return torch.ldexp(wt[:, : k * cin].t(), torch.tensor(float(-sw))).reshape(k, cin, cout)
+
+
+def pack_blob_x3(spec: ModelSpec, p) -> torch.Tensor:
+    """Pack one model into the fp16x3 fused kernel's blob (uint8, on the params' device); BN on the
+    moving statistics."""
+    if tiled_net(spec) is None:
+        raise ValueError("the fp32 fused kernel supports the pooled (60, 4) and the single-channel (30, 1) CNN")
+    lay = layout_x3()
+    dev = p["conv1d_1/kernel"].device
+    blob = torch.zeros(lay["bytes"], dtype=torch.uint8, device=dev)
+    for l in range(6):
+        i = l + 1
+        fr, sw = pack_conv_fragments_x3(p[f"conv1d_{i}/kernel"].to(dev))
+        b = fr.view(torch.uint8).reshape(-1)
+        blob[lay["woff"][l]: lay["woff"][l] + b.numel()] = b
+        scale, shift = bn_affine(spec, p, i)
+        epi = epilogue_constants(p[f"conv1d_{i}/bias"].float().to(dev), scale.float().to(dev), shift.float().to(dev))
+        epi[0] = torch.ldexp(epi[0], torch.tensor(float(-sw), device=dev))  # undo the weight prescale
+        rate = spec.blocks[l].dropout
+        epi = torch.cat([epi, epi * (1.0 / (1.0 - rate) if rate < 1.0 else 0.0)])
+        e = epi.contiguous().view(torch.uint8).reshape(-1)
+        blob[lay["eoff"][l]: lay["eoff"][l] + e.numel()] = e
+    head = torch.cat([p["output_layer/kernel"].float().reshape(-1), p["output_layer/bias"].float().reshape(-1)]).to(dev)
+    h = head.contiguous().view(torch.uint8)
+    blob[lay["dense"]: lay["dense"] + h.numel()] = h
+    return blob
+
+
+def tiled_x3_forward(x: torch.Tensor, blobs: torch.Tensor, spec: ModelSpec, *, n_pass: int = 1,
+                     dropout: bool = False, seed: int = 0, window_offset: int = 0, pass_offset: int = 0,
+                     logits: bool = False) -> torch.Tensor:
+    """(members, n_pass, N) probabilities (or logits) of the pooled / single-channel CNN at fp32 on
+    ``csrc/fused_tiled_x3.hip`` (BN on the moving statistics).  Launches hold < 2^31 samples; masks
+    are keyed by the global (pass, window) ids, so splitting does not change the result."""
+    o = _ext.ops()
+    net = tiled_net(spec)
+    if blobs.dim() == 1:
+        blobs = blobs.unsqueeze(0)
+    thr, _ = dropout_tables(spec)
+    s63 = int(seed) & ((1 << 63) - 1)
+    x = x.to(torch.float32).contiguous()
+    n = x.shape[0]
+    if not dropout:  # deterministic: every pass is identical
+        y = o.fused_tiled_x3_forward(x, blobs, net, 1, int(window_offset), 0, s63, False, bool(logits), thr)
+        return y.expand(blobs.shape[0], n_pass, n).contiguous()
+    out = torch.empty(blobs.shape[0], n_pass, n, dtype=torch.float32, device=x.device)
+    wc = min(n, _MAX_SAMPLES // 2)
+    pc = max(1, (_MAX_SAMPLES // 2) // max(wc, 1))
+    for w0 in range(0, n, wc):
+        w1 = min(n, w0 + wc)
+        for p0 in range(0, n_pass, pc):
+            p1 = min(n_pass, p0 + pc)
+            out[:, p0:p1, w0:w1] = o.fused_tiled_x3_forward(x[w0:w1], blobs, net, p1 - p0, int(window_offset) + w0,
+                                                            int(pass_offset) + p0, s63, True, bool(logits), thr)
+    return out
+
+
 _MAX_SAMPLES = 1 << 31  # samples per fused launch (32-bit sample index); tests lower it
 
 
