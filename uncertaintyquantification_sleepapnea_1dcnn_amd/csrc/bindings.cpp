@@ -211,7 +211,9 @@ at::Tensor fused_tiled_x3_forward(const at::Tensor& x, const at::Tensor& blob, i
               "fused_tiled_x3: blob must be contiguous uint8 (members, ", nbytes, ")");
   TORCH_CHECK(thr.size() == 6, "fused_tiled_x3: need 6 dropout thresholds");
   TORCH_CHECK(n_pass >= 1, "fused_tiled_x3: n_pass >= 1");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(blob.data_ptr()) % 16 == 0,
+  // x: 16-B row loads except for the single-channel net (element loads into its im2col rows)
+  TORCH_CHECK((net == 1 || reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0) &&
+                  reinterpret_cast<uintptr_t>(blob.data_ptr()) % 16 == 0,
               "fused_tiled_x3: 16-B alignment required");
   const int64_t n_win = x.size(0), n_member = blob.size(0);
   TORCH_CHECK(n_pass * n_win < (int64_t(1) << 31), "fused_tiled_x3: too many samples for one launch");

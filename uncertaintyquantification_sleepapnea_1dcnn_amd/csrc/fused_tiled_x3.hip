@@ -547,7 +547,9 @@ __global__ __launch_bounds__(kThreads, 2) void fused_tiled_x3_kernel(Args A) {
   unsigned* keys = reinterpret_cast<unsigned*>(smem + Y::kActBytes + Y::kX0Bytes);
   float* red = reinterpret_cast<float*>(smem + Y::kActBytes + Y::kX0Bytes + Y::kKeyBytes);
   float* head = red + 4 * NS;
-  // zero rows every block may read as padding (leading rows, the discarded rows' tail), once
+  // zero rows every block may read as padding (leading rows, the discarded rows' tail), once.  The rest
+  // of the LDS is written before it is read by any stored row (a NaN-filled LDS gives bitwise the same
+  // results: tools/debug/ft3_ab.py)
   for (int i = threadIdx.x; i < Y::kHB / 16; i += kThreads) reinterpret_cast<f32x4*>(smem)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int i = threadIdx.x; i < Y::trail() / 16; i += kThreads)
     reinterpret_cast<f32x4*>(smem + Y::kHB + Y::max_act())[i] = f32x4{0.f, 0.f, 0.f, 0.f};
