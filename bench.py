@@ -277,6 +277,16 @@ def run(a):
         torch.cuda.empty_cache()
         train = train_extra.measure(dev, a.seed)
 
+    fp32_paths = None
+    if not cpu and not a.no_train:  # the reference-precision paths of the other architectures + fp32 training
+        from bench import fp32_micro
+
+        torch.cuda.empty_cache()
+        fp32_paths = fp32_micro.measure(reps=2, steps=20, precisions=("fp32",))
+        fp32_paths["note"] = ("pooled ensemble_cnn members (MaxPool1D after blocks 1-5) at precision fp32: DE / "
+                              "running-BN MCD on the fused fp16x3 kernel, batch-BN MCD layer-wise; fp32 training "
+                              "steps (train_precision='fp32') of the reference and pooled CNN; best of 2")
+
     macs = SPEC.forward_macs()
     devices = pdist.gather_device_ids()  # collective: every rank
     if rank == 0:
@@ -324,6 +334,7 @@ def run(a):
                 "fp32_deviation": deviation,
                 ("bf16" if head_prec == "fp32" else "fp32"): secondary,
                 "train": train,
+                "fp32_paths": fp32_paths,
             },
         }
         _emit(json.dumps(out))
