@@ -128,6 +128,88 @@ __global__ __launch_bounds__(256) void zero_kernel(ZeroArgs Z) {
 
 int zero_max_buffers() { return kZeroMax; }
 
+// Training-step tail (the graph's last node): bump every member's device counters [dropout step, Adam
+// iterations] and write probs = sigmoid(logits) of up to kTailMax members -- what a bump launch plus one
+// torch sigmoid per member did.
+constexpr int kTailMax = 32;
+struct TailArgs {
+  const float* logits[kTailMax];
+  float* probs[kTailMax];
+  int* counters;
+  int ncounters, n;
+};
+
+__global__ __launch_bounds__(256) void train_tail_kernel(TailArgs T) {
+  const int m = blockIdx.y;
+  if (m == 0 && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < T.ncounters; i += blockDim.x) T.counters[i] += 1;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < T.n; i += gridDim.x * blockDim.x)
+    T.probs[m][i] = 1.0f / (1.0f + __expf(-T.logits[m][i]));
+}
+
+int train_tail_max() { return kTailMax; }
+
+hipError_t launch_train_tail(int* counters, int ncounters, int members, const float* const* logits,
+                             float* const* probs, int n, hipStream_t stream) {
+  if (members < 1 || members > kTailMax || n < 0) return hipErrorInvalidValue;
+  TailArgs T = {};
+  for (int i = 0; i < members; ++i) {
+    T.logits[i] = logits[i];
+    T.probs[i] = probs[i];
+  }
+  T.counters = counters;
+  T.ncounters = ncounters;
+  T.n = n;
+  int gx = (n + 255) / 256;
+  gx = gx < 1 ? 1 : (gx > 64 ? 64 : gx);
+  hipLaunchKernelGGL(train_tail_kernel, dim3(gx, members), dim3(256), 0, stream, T);
+  return hipGetLastError();
+}
+
+// The step's inputs for up to kTailMax members in one launch: x (n, L, C) fp32 -> the workspace's
+// padded-row bf16 layout (row stride SR*C per sample), y (n) fp32 -> the label buffer.
+struct InputArgs {
+  const float* x[kTailMax];
+  __bf16* xd[kTailMax];
+  const float* y[kTailMax];
+  float* yd[kTailMax];
+  int n, L, C, SR;
+};
+
+__global__ __launch_bounds__(256) void train_inputs_kernel(InputArgs A) {
+  const int m = blockIdx.y;
+  const long long nx = (long long)A.n * A.L * A.C;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nx + A.n; i += stride) {
+    if (i < nx) {
+      const long long b = i / ((long long)A.L * A.C), r = i - b * A.L * A.C;
+      A.xd[m][b * A.SR * A.C + r] = (__bf16)A.x[m][i];
+    } else {
+      A.yd[m][i - nx] = A.y[m][i - nx];
+    }
+  }
+}
+
+hipError_t launch_train_inputs(int members, const float* const* x, void* const* xd, const float* const* y,
+                               float* const* yd, int n, int L, int C, int SR, hipStream_t stream) {
+  if (members < 1 || members > kTailMax || n < 0 || SR < L) return hipErrorInvalidValue;
+  InputArgs A = {};
+  for (int i = 0; i < members; ++i) {
+    A.x[i] = x[i];
+    A.xd[i] = reinterpret_cast<__bf16*>(xd[i]);
+    A.y[i] = y[i];
+    A.yd[i] = yd[i];
+  }
+  A.n = n;
+  A.L = L;
+  A.C = C;
+  A.SR = SR;
+  long long gx = ((long long)n * L * C + n + 255) / 256;
+  gx = gx < 1 ? 1 : (gx > 512 ? 512 : gx);
+  hipLaunchKernelGGL(train_inputs_kernel, dim3((unsigned)gx, members), dim3(256), 0, stream, A);
+  return hipGetLastError();
+}
+
 hipError_t launch_zero(int nb, void* const* ptrs, const long long* words, hipStream_t stream) {
   if (nb <= 0) return hipSuccess;
   if (nb > kZeroMax) return hipErrorInvalidValue;

@@ -90,7 +90,14 @@ hipError_t launch_gx3_wgrad(const float* x, const float* dz, const unsigned* ama
 long long train_wgrad_part_floats(int B);
 int train_det_floats(int B);
 hipError_t launch_gt_pack(int nb, const float* const* w, void* const* fwd, void* const* dgr, const int* k,
-                          const int* cin, const int* cout, hipStream_t st);
+                          const int* cin, const int* cout, hipStream_t st, int nz, void* const* zp,
+                          const long long* zw);
+int gt_pack_max_zero();
+int train_tail_max();
+hipError_t launch_train_tail(int* counters, int ncounters, int members, const float* const* logits,
+                             float* const* probs, int n, hipStream_t stream);
+hipError_t launch_train_inputs(int members, const float* const* x, void* const* xd, const float* const* y,
+                               float* const* yd, int n, int L, int C, int SR, hipStream_t stream);
 namespace train {
 struct Layer {
   const void* wf; const void* wd; const float* bias; const float* gamma; const float* beta;
@@ -112,7 +119,7 @@ hipError_t launch_knn(const double* X, int n, int D, long long* out, int k, hipS
 int knn_lds_bytes(int D, int K);
 int train_layer_size();
 hipError_t train_launch_fwd(const train::Args& A, int l, hipStream_t st);
-hipError_t train_launch_head(const train::Args& A, int backward, hipStream_t st);
+hipError_t train_launch_head(const train::Args& A, int backward, hipStream_t st, bool with_tab);
 hipError_t train_launch_dgrad(const train::Args& A, int l, hipStream_t st);
 hipError_t train_launch_wgrad(const train::Args& A, int l, hipStream_t st);
 hipError_t train_launch_finalize(const train::Args& A, int update_moving, int grads, hipStream_t st);
@@ -459,7 +466,7 @@ apneauq::train::Args args_from_ctx(const at::Tensor& ctx, int64_t pass_base) {
 }
 
 // op: 0 fwd(layer; flag=1: the pass-shared block 1 of batch-BN MC Dropout, over the n_win windows)
-//     | 1 head(flag=backward) | 2 dgrad(layer) | 3 wgrad(layer) | 4 finalize(layer=update_moving, flag=grads)
+//     | 1 head(flag bit 0 = backward, bit 1 = + the table's forward rows, replacing op 5) | 2 dgrad(layer) | 3 wgrad(layer) | 4 finalize(layer=update_moving, flag=grads)
 //     (2 / 3: flag 1 = Args::bwd_self, the backward BN rows from the slots instead of the table)
 //     | 5 parameter table (flag 0: forward rows of every block, 1: backward rows of block ``layer``)
 void train_call(const at::Tensor& ctx, int64_t op, int64_t layer, int64_t flag, int64_t pass_base, int64_t device) {
@@ -476,7 +483,7 @@ void train_call(const at::Tensor& ctx, int64_t op, int64_t layer, int64_t flag, 
       }
       check(apneauq::train_launch_fwd(A, (int)layer, s), "train fwd");
       break;
-    case 1: check(apneauq::train_launch_head(A, (int)flag, s), "train head"); break;
+    case 1: check(apneauq::train_launch_head(A, (int)(flag & 1), s, (flag & 2) != 0), "train head"); break;
     case 2:
       TORCH_CHECK(layer >= 1 && layer < 6);
       A.bwd_self = (int)(flag & 1);
@@ -820,9 +827,10 @@ void gf_wgrad(const at::Tensor& x, const at::Tensor& dz, int64_t R, int64_t cin,
         "gf_wgrad");
 }
 
-// All blocks' forward (+ dgrad) MFMA fragments in one launch (csrc/generic_wgrad.hip pack_kernel).
-void gt_pack(at::TensorList w, at::TensorList fwd, at::TensorList dgr, at::IntArrayRef k, at::IntArrayRef cin,
-             at::IntArrayRef cout) {
+// All blocks' forward (+ dgrad) MFMA fragments in one launch (csrc/generic_wgrad.hip pack_kernel), and
+// optionally (zero) a list of accumulators cleared by the same launch.
+void gt_pack_impl(at::TensorList w, at::TensorList fwd, at::TensorList dgr, at::IntArrayRef k, at::IntArrayRef cin,
+                  at::IntArrayRef cout, at::TensorList zero) {
   const int64_t nb = (int64_t)w.size();
   TORCH_CHECK(nb >= 1 && nb <= apneauq::gt_pack_max_blocks() && (int64_t)fwd.size() == nb && (int64_t)dgr.size() == nb &&
                   (int64_t)k.size() == nb && (int64_t)cin.size() == nb && (int64_t)cout.size() == nb,
@@ -848,9 +856,90 @@ void gt_pack(at::TensorList w, at::TensorList fwd, at::TensorList dgr, at::IntAr
     fp[i] = fwd[i].data_ptr();
     dp[i] = dgr[i].numel() ? dgr[i].data_ptr() : nullptr;
   }
+  const int nz = (int)zero.size();
+  TORCH_CHECK(nz <= apneauq::gt_pack_max_zero(), "gt_pack_zero: at most ", apneauq::gt_pack_max_zero(), " buffers");
+  std::vector<void*> zp(nz);
+  std::vector<long long> zw(nz);
+  for (int i = 0; i < nz; ++i) {
+    TORCH_CHECK(zero[i].is_cuda() && zero[i].is_contiguous() && zero[i].device() == w[0].device() &&
+                    (zero[i].numel() * zero[i].element_size()) % 4 == 0 &&
+                    reinterpret_cast<uintptr_t>(zero[i].data_ptr()) % 4 == 0,
+                "gt_pack_zero: contiguous GPU buffers of whole 4-byte words on the weights' device required");
+    zp[i] = zero[i].data_ptr();
+    zw[i] = (long long)(zero[i].numel() * zero[i].element_size() / 4);
+  }
   const at::DeviceGuard guard(w[0].device());
-  check(apneauq::launch_gt_pack((int)nb, wp.data(), fp.data(), dp.data(), kk.data(), ci.data(), co.data(), cur_stream()),
+  check(apneauq::launch_gt_pack((int)nb, wp.data(), fp.data(), dp.data(), kk.data(), ci.data(), co.data(), cur_stream(),
+                                nz, zp.data(), zw.data()),
         "gt_pack");
+}
+
+void gt_pack(at::TensorList w, at::TensorList fwd, at::TensorList dgr, at::IntArrayRef k, at::IntArrayRef cin,
+             at::IntArrayRef cout) {
+  gt_pack_impl(w, fwd, dgr, k, cin, cout, {});
+}
+
+void gt_pack_zero(at::TensorList w, at::TensorList fwd, at::TensorList dgr, at::IntArrayRef k, at::IntArrayRef cin,
+                  at::IntArrayRef cout, at::TensorList zero) {
+  gt_pack_impl(w, fwd, dgr, k, cin, cout, zero);
+}
+
+// The training step's tail: bump the device counters, probs = sigmoid(logits[:n]) of every member.
+void train_tail(at::Tensor& counters, at::TensorList logits, at::TensorList probs) {
+  const int M = (int)logits.size();
+  TORCH_CHECK(M >= 1 && M <= apneauq::train_tail_max() && (int)probs.size() == M, "train_tail: 1..",
+              apneauq::train_tail_max(), " members, one probs buffer each");
+  TORCH_CHECK(counters.is_cuda() && counters.scalar_type() == at::kInt && counters.is_contiguous(),
+              "train_tail: contiguous int32 GPU counters");
+  const int64_t n = logits[0].numel();
+  std::vector<const float*> lp(M);
+  std::vector<float*> pp(M);
+  for (int i = 0; i < M; ++i) {
+    TORCH_CHECK(logits[i].is_cuda() && logits[i].scalar_type() == at::kFloat && logits[i].is_contiguous() &&
+                    logits[i].numel() == n && probs[i].scalar_type() == at::kFloat && probs[i].is_contiguous() &&
+                    probs[i].numel() == n && probs[i].device() == counters.device() &&
+                    logits[i].device() == counters.device(),
+                "train_tail: contiguous fp32 logits / probs of one length on the counters' device");
+    lp[i] = logits[i].data_ptr<float>();
+    pp[i] = probs[i].data_ptr<float>();
+  }
+  const at::DeviceGuard guard(counters.device());
+  check(apneauq::launch_train_tail(counters.data_ptr<int>(), (int)counters.numel(), M, lp.data(), pp.data(), (int)n,
+                                   cur_stream()),
+        "train_tail");
+}
+
+// The step's inputs of every member in one launch: x (n, L, C) fp32 into the padded-row bf16 buffer
+// (rows of SR, the first n * SR * C elements of xd), y (n) fp32 into yd.
+void train_inputs(at::TensorList x, at::TensorList y, at::TensorList xd, at::TensorList yd, int64_t sr) {
+  const int M = (int)x.size();
+  TORCH_CHECK(M >= 1 && M <= apneauq::train_tail_max() && (int)y.size() == M && (int)xd.size() == M &&
+                  (int)yd.size() == M,
+              "train_inputs: 1..", apneauq::train_tail_max(), " members with x, y, xd, yd each");
+  const int64_t n = x[0].size(0), L = x[0].size(1), C = x[0].size(2);
+  std::vector<const float*> xp(M), yp(M);
+  std::vector<void*> xdp(M);
+  std::vector<float*> ydp(M);
+  for (int i = 0; i < M; ++i) {
+    TORCH_CHECK(x[i].is_cuda() && x[i].scalar_type() == at::kFloat && x[i].is_contiguous() && x[i].dim() == 3 &&
+                    x[i].size(0) == n && x[i].size(1) == L && x[i].size(2) == C,
+                "train_inputs: contiguous fp32 (n, L, C) inputs of one shape");
+    TORCH_CHECK(y[i].is_cuda() && y[i].scalar_type() == at::kFloat && y[i].is_contiguous() && y[i].numel() == n,
+                "train_inputs: contiguous fp32 labels (n)");
+    TORCH_CHECK(xd[i].scalar_type() == at::kBFloat16 && xd[i].is_contiguous() && xd[i].numel() >= n * sr * C &&
+                    yd[i].scalar_type() == at::kFloat && yd[i].is_contiguous() && yd[i].numel() >= n,
+                "train_inputs: destination buffers too small");
+    TORCH_CHECK(x[i].device() == xd[i].device() && y[i].device() == xd[i].device() && yd[i].device() == xd[i].device(),
+                "train_inputs: one device per member");
+    xp[i] = x[i].data_ptr<float>();
+    yp[i] = y[i].data_ptr<float>();
+    xdp[i] = xd[i].data_ptr();
+    ydp[i] = yd[i].data_ptr<float>();
+  }
+  const at::DeviceGuard guard(xd[0].device());
+  check(apneauq::launch_train_inputs(M, xp.data(), xdp.data(), yp.data(), ydp.data(), (int)n, (int)L, (int)C, (int)sr,
+                                     cur_stream()),
+        "train_inputs");
 }
 
 // ---- fp32-faithful (fp16x3) generic conv kernels (csrc/gx3_conv.hip): the precision="fp32" path ----
@@ -1097,6 +1186,10 @@ TORCH_LIBRARY(apneauq, m) {
   m.def("gt_head(Tensor h, Tensor w, Tensor b, Tensor y, Tensor(a!) prob, Tensor(b!) dlog, Tensor(c!) loss, "
         "Tensor(d!) gw, Tensor(e!) gb, int n, int L, int C, float inv_gb, Tensor(f!)? part=None) -> ()");
   m.def("gt_pack(Tensor[] w, Tensor(a!)[] fwd, Tensor(b!)[] dgr, int[] k, int[] cin, int[] cout) -> ()");
+  m.def("gt_pack_zero(Tensor[] w, Tensor(a!)[] fwd, Tensor(b!)[] dgr, int[] k, int[] cin, int[] cout, "
+        "Tensor(c!)[] zero) -> ()");
+  m.def("train_tail(Tensor(a!) counters, Tensor[] logits, Tensor(b!)[] probs) -> ()");
+  m.def("train_inputs(Tensor[] x, Tensor[] y, Tensor(a!)[] xd, Tensor(b!)[] yd, int sr) -> ()");
   m.def("gf_conv(Tensor x, Tensor w, Tensor? bias, Tensor(a!) y, Tensor(b!)? stats, int n, int L, int cin, int cout, "
         "int ksize, int mode, int in_rs, int in_off, bool det=False) -> ()");
   m.def("gf_wgrad(Tensor x, Tensor dz, int R, int cin, int cout, int k, Tensor(a!) gw, Tensor(b!) part) -> ()");
@@ -1133,6 +1226,9 @@ TORCH_LIBRARY_IMPL(apneauq, CUDA, m) {
   m.impl("gt_wgrad", &gt_wgrad);
   m.impl("gt_head", &gt_head);
   m.impl("gt_pack", &gt_pack);
+  m.impl("gt_pack_zero", &gt_pack_zero);
+  m.impl("train_tail", &train_tail);
+  m.impl("train_inputs", &train_inputs);
   m.impl("gf_conv", &gf_conv);
   m.impl("gf_wgrad", &gf_wgrad);
   m.impl("gx3_pack", &gx3_pack);

@@ -20,6 +20,7 @@
 //
 // Reference: models/train_deep_ensemble_cnns.py:30-71 (the pooled variants), cnn_baseline_train.py:
 // 100-102 (Adam, BCE) -- the Keras train step these kernels implement.
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.h"
@@ -368,12 +369,26 @@ struct PackBlock {
   int k, cin, cout;
   long long nf, nd;  // elements of each fragment array
 };
+// + up to kMaxZero buffers zeroed by the rows of blocks past the packs (the training step's
+// accumulators: the step's first two graph nodes, one launch)
+constexpr int kMaxZero = 48;
 struct PackArgs {
   PackBlock b[kMaxBlocks];
-  int nblocks;
+  uint32_t* zp[kMaxZero];
+  long long zw[kMaxZero];  // 4-byte words
+  int nblocks, nzero;
 };
 
 __global__ void pack_kernel(PackArgs P) {
+  if ((int)blockIdx.y >= P.nblocks) {  // zero rows (block-uniform)
+    uint32_t* p = P.zp[blockIdx.y - P.nblocks];
+    const long long n = P.zw[blockIdx.y - P.nblocks];
+    const long long stride = (long long)gridDim.x * blockDim.x, t0 = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    const long long n4 = (reinterpret_cast<uintptr_t>(p) & 15) == 0 ? n >> 2 : 0;
+    for (long long i = t0; i < n4; i += stride) reinterpret_cast<uint4*>(p)[i] = uint4{0u, 0u, 0u, 0u};
+    for (long long i = (n4 << 2) + t0; i < n; i += stride) p[i] = 0u;
+    return;
+  }
   const PackBlock B = P.b[blockIdx.y];
   const long long tot = B.nf + (B.dgr ? B.nd : 0);
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < tot; e += (long long)gridDim.x * blockDim.x) {
@@ -522,13 +537,21 @@ hipError_t launch_gt_head(const void* h, const float* w, const float* b, const f
 }
 
 int gt_pack_max_blocks() { return gwgrad::kMaxBlocks; }
+int gt_pack_max_zero() { return gwgrad::kMaxZero; }
 
-// blocks: nb descriptors (w, fwd, dgr-or-null, k, cin, cout)
+// blocks: nb descriptors (w, fwd, dgr-or-null, k, cin, cout); nz buffers (ptr, 4-byte words) zeroed in the
+// same launch
 hipError_t launch_gt_pack(int nb, const float* const* w, void* const* fwd, void* const* dgr, const int* k,
-                          const int* cin, const int* cout, hipStream_t st) {
-  if (nb < 1 || nb > gwgrad::kMaxBlocks) return hipErrorInvalidValue;
+                          const int* cin, const int* cout, hipStream_t st, int nz, void* const* zp,
+                          const long long* zw) {
+  if (nb < 1 || nb > gwgrad::kMaxBlocks || nz < 0 || nz > gwgrad::kMaxZero) return hipErrorInvalidValue;
   gwgrad::PackArgs P;
   P.nblocks = nb;
+  P.nzero = nz;
+  for (int i = 0; i < nz; ++i) {
+    P.zp[i] = reinterpret_cast<uint32_t*>(zp[i]);
+    P.zw[i] = zw[i];
+  }
   long long most = 0;
   for (int i = 0; i < nb; ++i) {
     auto& B = P.b[i];
@@ -543,9 +566,10 @@ hipError_t launch_gt_pack(int nb, const float* const* w, void* const* fwd, void*
     const long long t = B.nf + (B.dgr ? B.nd : 0);
     most = t > most ? t : most;
   }
+  for (int i = 0; i < nz; ++i) most = std::max(most, zw[i] / 4);
   long long gx = (most + 255) / 256;
   if (gx > 1024) gx = 1024;
-  hipLaunchKernelGGL(gwgrad::pack_kernel, dim3((unsigned)gx, nb), dim3(256), 0, st, P);
+  hipLaunchKernelGGL(gwgrad::pack_kernel, dim3((unsigned)gx, nb + nz), dim3(256), 0, st, P);
   return hipGetLastError();
 }
 

@@ -801,9 +801,16 @@ __global__ __launch_bounds__(256) void tab_kernel(Args A_, const Args* __restric
 // each lane owning channels (lane, lane + 64).
 // ------------------------------------------------------------------------------------------------
 template <bool MB>
-__global__ __launch_bounds__(kThreads) void head_kernel(Args A_, const Args* __restrict__ Am, int backward, int spw) {
+__global__ __launch_bounds__(kThreads) void head_kernel(Args A_, const Args* __restrict__ Am, int backward, int spw,
+                                                      int tabx) {
   const MbPos pos = mb_pos<MB>();
   const Args& A = member_args<MB>(A_, Am, pos);
+  // tabx > 0: the last tabx workgroups write the forward rows of the parameter table (what a tab_kernel
+  // launch did before the head), the head computes block 6's rows itself with the same arithmetic
+  if (tabx > 0 && pos.bx >= (int)gridDim.x - tabx) {
+    tab_write_fwd(A, pos.bx - ((int)gridDim.x - tabx));
+    return;
+  }
   // One sample at a time per wave, spw samples per wave (4 * spw per workgroup: fewer workgroups'
   // sums to merge at large batches).  Lane (cw, ph) = (lane % 12, lane / 12), lanes 0..59: channels
   // [8cw, 8cw+8) of rows ph, ph+5, ..., ph+55 — twelve 16-B loads per lane, all in flight at once
@@ -823,7 +830,7 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A_, const Args* __r
   const int g_last = min(nwg0 + 4 * spw - 1, A.B - 1) / A.n_win;
   for (int c = threadIdx.x; c < 3 * Cc + 2; c += kThreads) dw[c] = 0.f;
   auto params = [&](int g) {
-    if (A.tab != nullptr) {  // single-device training (one group): the forward rows of T[5]
+    if (A.tab != nullptr && tabx == 0) {  // single-device training (one group): the forward rows of T[5]
       for (int c = threadIdx.x; c < Cc; c += kThreads) {
         pmu[c] = tab_row(A, 5, kTabMean)[c];
         prs[c] = tab_row(A, 5, kTabRstd)[c];
@@ -836,11 +843,11 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A_, const Args* __r
     for (int c = threadIdx.x; c < Cc; c += kThreads) {
       float m1, var;
       bn_moments(A, 5, g, c, m1, var);
-      const float r = rsqrtf(var + A.eps);
+      const float r = rsqrtf(var + A.eps), sc = Ly.gamma[c] * r;  // as tab_write_fwd
       pmu[c] = m1;
       prs[c] = r;
-      psc[c] = Ly.gamma[c] * r;
-      psh[c] = Ly.beta[c] - m1 * Ly.gamma[c] * r;
+      psc[c] = sc;
+      psh[c] = Ly.beta[c] - m1 * sc;
       pw[c] = A.dense_w[c];
     }
   };
@@ -1558,10 +1565,11 @@ static int head_spw(int B, int M, int backward) {
   return spw;
 }
 
-hipError_t train_launch_head(const Args& A, int backward, hipStream_t st) {
+hipError_t train_launch_head(const Args& A, int backward, hipStream_t st, bool with_tab) {
   const int spw = head_spw(A.B, 1, backward);
-  hipLaunchKernelGGL(train::head_kernel<false>, dim3((A.B + 4 * spw - 1) / (4 * spw)), dim3(256), (8 * train::C[6] + 2) * 4, st,
-                     A, nullptr, backward, spw);
+  const int tabx = (with_tab && A.tab != nullptr) ? 6 : 0;  // + the table's forward rows, one workgroup per block
+  hipLaunchKernelGGL(train::head_kernel<false>, dim3((A.B + 4 * spw - 1) / (4 * spw) + tabx), dim3(256),
+                     (8 * train::C[6] + 2) * 4, st, A, nullptr, backward, spw, tabx);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess || !backward || A.det == nullptr) return e;
   constexpr int cc = train::C[6];  // per-sample records: loss, dlogit, dW, sum dY, sum dY xhat
@@ -1701,7 +1709,7 @@ hipError_t train_launch_mb(const Args& A0, const Args* Am, int M, int op, int la
     case 1: {
       const int spw = head_spw(A0.B, M, flag);
       hipLaunchKernelGGL(train::head_kernel<true>, dim3((A0.B + 4 * spw - 1) / (4 * spw), 1, M), dim3(256),
-                         (8 * train::C[6] + 2) * 4, st, A0, Am, flag, spw);
+                         (8 * train::C[6] + 2) * 4, st, A0, Am, flag, spw, 0);
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess || !det || !flag) return e;
       return det_reduce_mb(A0, Am, M, 1, 0, A0.B, train::kHeadRec, st);

@@ -189,10 +189,31 @@ class TrainWorkspace:
         _ext.ops().gt_pack([v[f"conv1d_{l + 1}/kernel"] for l in range(6)], self.wf,
                            [self._no_dgr] + self.wd[1:], self.ks, self.ch[:6], self.ch[1:])
 
+    def accumulators(self) -> List[torch.Tensor]:
+        """BN moment / backward sums, the flat gradient, the loss (and the head's slots)."""
+        return [self.st_all, self.bst_all, self.grad, self.loss] + ([self.hpart] if self.hpart is not None else [])
+
     def zero_accumulators(self) -> None:
-        """BN moment / backward sums, the flat gradient and the loss: one launch."""
-        bufs = [self.st_all, self.bst_all, self.grad, self.loss]
-        _ext.ops().zero_buffers(bufs + ([self.hpart] if self.hpart is not None else []))
+        """The accumulators: one launch."""
+        _ext.ops().zero_buffers(self.accumulators())
+
+    def pack_args(self):
+        v = self.model.store.views
+        if not hasattr(self, "_no_dgr"):
+            self._no_dgr = torch.empty(0, dtype=torch.bfloat16, device=self.wf[0].device)
+        return ([v[f"conv1d_{l + 1}/kernel"] for l in range(6)], list(self.wf), [self._no_dgr] + self.wd[1:],
+                list(self.ks), list(self.ch[:6]), list(self.ch[1:]))
+
+    def pack_zero(self) -> None:
+        """:meth:`pack` and :meth:`zero_accumulators` as ONE launch (the graphed step's first node)."""
+        _ext.ops().gt_pack_zero(*self.pack_args(), self.accumulators())
+
+
+def _inputs_direct(xs, ys, n: int) -> bool:
+    """The fused input copy applies: fp32 contiguous (n, 60, C) windows and (n,) labels."""
+    return all(x.dtype == torch.float32 and x.is_contiguous() and x.dim() == 3 and x.shape[0] == n and
+               x.shape[1] == 60 for x in xs) and \
+        all(y.dtype == torch.float32 and y.is_contiguous() and y.numel() == n for y in ys)
 
 
 def _call(ctx, op, layer=0, flag=0, pass_base=-1, device=0):
@@ -248,8 +269,7 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, syn
         _call(ctx, 0, l, 0, pb, dev)
         if sync is not None:
             sync(ws.st[l])
-    _call(ctx, 5, 0, 0, pb, dev)  # BN parameter table (forward rows; a no-op without a table)
-    _call(ctx, 1, 0, 1, pb, dev)
+    _call(ctx, 1, 0, 3, pb, dev)  # head + the BN parameter table's forward rows (no-op without a table)
     if sync is not None:
         sync(ws.bst[5])
     for l in range(5, 0, -1):
@@ -338,6 +358,7 @@ class GraphedTrainStep:
         # pad rows stay zero), outside the graph: no copy nodes inside it
         self.x_in = self.ws.x[HALO: HALO + SR * n].view(n, SR, self.ws.ch[0])[:, :60]
         self.y_in = self.ws.y[:n]
+        self.probs = torch.empty(n, dtype=torch.float32, device=dev)
         self.ctx = self.ws.build_ctx(n, n, 1, 0, model.seed, True, 1.0 / (n * 60), 1.0 / n, device_counters=True,
                                      table=True)
         model.optimizer._ensure(model.store.flat)
@@ -363,12 +384,10 @@ class GraphedTrainStep:
     def _body(self):
         ws, n, o = self.ws, self.batch, _ext.ops()
         dev = self.x_in.device.index or 0
-        ws.zero_accumulators()
-        ws.pack()
+        ws.pack_zero()
         for l in range(6):
             _call(self.ctx, 0, l, 0, TRAIN_PASS_BASE, dev)
-        _call(self.ctx, 5, 0, 0, TRAIN_PASS_BASE, dev)  # BN parameter table (forward rows)
-        _call(self.ctx, 1, 0, 1, TRAIN_PASS_BASE, dev)
+        _call(self.ctx, 1, 0, 3, TRAIN_PASS_BASE, dev)  # head + the BN parameter table's forward rows
         if self.overlap:
             # wgrad_l needs only dgrad_l's dZ_l (and forward state), and no dgrad reads a wgrad
             # output: the wgrad + reduce chain runs on its own stream, forked after each dgrad and
@@ -400,16 +419,20 @@ class GraphedTrainStep:
         opt = self.model.optimizer
         o.adam_step(self.model.store.flat, ws.grad, opt.m, opt.v, opt.beta_1, opt.beta_2, opt.learning_rate,
                     opt.epsilon, 1.0, ws.counters)
-        o.bump_counters(ws.counters)
+        o.train_tail(ws.counters, [ws.logits[:n]], [self.probs])  # counters + 1, probs: one node
         # the loss sum as a 0-d view of the kernels' fp32 accumulator (no cast / reduce nodes)
-        return ws.loss.view(()), torch.sigmoid(ws.logits[:n])
+        return ws.loss.view(()), self.probs
 
     def __call__(self, x: torch.Tensor, y: torch.Tensor):
         """One step; returns (loss_sum, probs) views of static buffers (valid until the next replay)."""
         if self._state() != self._dev_state:
             self._sync_counters()
-        self.x_in.copy_(x)
-        self.y_in.copy_(y.reshape(-1))
+        yf = y.reshape(-1)
+        if _inputs_direct([x], [yf], self.batch):  # both copies in one launch
+            _ext.ops().train_inputs([x], [yf], [self.ws.x[HALO:]], [self.ws.y], SR)
+        else:
+            self.x_in.copy_(x)
+            self.y_in.copy_(yf)
         self.graph.replay()
         self.model.optimizer.iterations += 1
         self._dev_state = (self._dev_state[0] + 1, self._dev_state[1] + 1)
@@ -463,6 +486,7 @@ class GraphedEnsembleStep:
             self.ctx.append(ws.build_ctx(n, n, 1, 0, m.seed, True, 1.0 / (n * 60), 1.0 / n, device_counters=True,
                                          table=True))
             m.optimizer._ensure(m.store.flat)
+        self.probs = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(M)]
         self.args = _ext.ops().train_args_dev(self.ctx, dev.index or 0)
         self.bound = [bound_key(m) for m in self.models]
         self._sync_counters()
@@ -481,26 +505,12 @@ class GraphedEnsembleStep:
 
     def _body(self):
         o, M, n = _ext.ops(), len(self.models), self.batch
-        bufs = []
-        for ws in self.ws:
-            bufs += [ws.st_all, ws.bst_all, ws.grad, ws.loss] + ([ws.hpart] if ws.det is None else [])
-        zmax = 60  # csrc/adam.hip kZeroMax = 64 buffers per launch
-        for b0 in range(0, len(bufs), zmax):
-            o.zero_buffers(bufs[b0:b0 + zmax])
-        # bf16 fragments of every member's six kernels: one launch (up to 8 members)
+        # bf16 fragments of every member's six kernels and the members' accumulators cleared: one
+        # launch per 8 members (csrc/generic_wgrad.hip pack_kernel: 48 blocks, 48 zero buffers)
         for g0 in range(0, M, 8):
-            grp = list(zip(self.models[g0:g0 + 8], self.ws[g0:g0 + 8]))
-            w, wf, wd, ks, ci, co = [], [], [], [], [], []
-            for m, ws in grp:
-                if not hasattr(ws, "_no_dgr"):
-                    ws._no_dgr = torch.empty(0, dtype=torch.bfloat16, device=ws.wf[0].device)
-                w += [m.store.views[f"conv1d_{l + 1}/kernel"] for l in range(6)]
-                wf += ws.wf
-                wd += [ws._no_dgr] + ws.wd[1:]
-                ks += ws.ks
-                ci += ws.ch[:6]
-                co += ws.ch[1:]
-            o.gt_pack(w, wf, wd, ks, ci, co)
+            packs = [ws.pack_args() for ws in self.ws[g0:g0 + 8]]
+            o.gt_pack_zero(*[sum((p[i] for p in packs), []) for i in range(6)],
+                           sum((ws.accumulators() for ws in self.ws[g0:g0 + 8]), []))
         a, c0 = self.args, self.ctx[0]
         for l in range(6):
             o.train_call_mb(a, c0, M, 0, l, 0)
@@ -524,10 +534,12 @@ class GraphedEnsembleStep:
                 opt = m.optimizer
                 o.adam_step(m.store.flat, ws.grad, opt.m, opt.v, opt.beta_1, opt.beta_2, opt.learning_rate,
                             opt.epsilon, 1.0, ws.counters)
+        # every member's counters + 1 and probs = sigmoid(logits): one launch per 32 members
         flat = self.counters.view(-1)
-        for c0 in range(0, flat.numel(), 64):  # <= 64 counters per launch
-            o.bump_counters(flat[c0:c0 + 64])
-        return [ws.loss.view(()) for ws in self.ws] + [torch.sigmoid(ws.logits[:n]) for ws in self.ws]
+        for g0 in range(0, M, 32):
+            o.train_tail(flat[2 * g0: 2 * min(M, g0 + 32)], [ws.logits[:n] for ws in self.ws[g0:g0 + 32]],
+                         self.probs[g0:g0 + 32])
+        return [ws.loss.view(()) for ws in self.ws] + list(self.probs)
 
     def valid_for(self, models) -> bool:
         return (len(models) == len(self.models) and all(a is b for a, b in zip(models, self.models)) and
@@ -539,9 +551,17 @@ class GraphedEnsembleStep:
         returns per-member (loss_sum, probs) views of static buffers (valid until the next replay)."""
         if self._state() != self._dev_state:
             self._sync_counters()
-        for i in range(len(self.models)):
-            self.x_in[i].copy_(xs[i])
-            self.y_in[i].copy_(ys[i].reshape(-1))
+        yfs = [y.reshape(-1) for y in ys]
+        M = len(self.models)
+        if _inputs_direct(xs, yfs, self.batch):  # every member's x and y in one launch per 32 members
+            for g0 in range(0, M, 32):
+                _ext.ops().train_inputs(list(xs[g0:g0 + 32]), yfs[g0:g0 + 32],
+                                        [ws.x[HALO:] for ws in self.ws[g0:g0 + 32]],
+                                        [ws.y for ws in self.ws[g0:g0 + 32]], SR)
+        else:
+            for i in range(M):
+                self.x_in[i].copy_(xs[i])
+                self.y_in[i].copy_(yfs[i])
         self.graph.replay()
         for m in self.models:
             m.optimizer.iterations += 1
