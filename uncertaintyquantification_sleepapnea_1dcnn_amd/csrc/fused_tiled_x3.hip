@@ -390,22 +390,23 @@ __device__ __forceinline__ SA<N::NS> block(const Ctx X, const SA<N::NS> sa_in) {
   }
   // the sample of row tile r of this lane; undo its input exponent (exact powers of two)
   auto smp_of = [&](int r) { return ROWHEAD ? m : (rt_of(r) * 16 + m) / OPSL; };
-  float mxs[NS];
+  // per row tile: the max |v| this lane stores (folded into per-sample maxima once, after the loop)
+  float mr[NRW];
+  int einr[NRW];
 #pragma unroll
-  for (int j = 0; j < NS; ++j) mxs[j] = 0.f;
-  auto upd = [&](int smp, bool st, float a) {
-#pragma unroll
-    for (int j = 0; j < NS; ++j) mxs[j] = (st && smp == j) ? fmaxf(mxs[j], a) : mxs[j];
-  };
+  for (int r = 0; r < NRW; ++r) {
+    mr[r] = 0.f;
+    einr[r] = -pick(sa_in, smp_of(r));
+  }
+  auto upd = [&](int r, bool st, float a) { mr[r] = st ? fmaxf(mr[r], a) : mr[r]; };
 #pragma unroll
   for (int c = 0; c < NFL_A; ++c) {
     if (!ct_ok(c)) break;  // wave-uniform
 #pragma unroll
     for (int r = 0; r < NRW; ++r) {
       if (r >= nrows(c)) break;
-      const int ein = -pick(sa_in, smp_of(r));
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[c][r][i] = ldexpf(acc[c][r][i], ein);
+      for (int i = 0; i < 4; ++i) acc[c][r][i] = ldexpf(acc[c][r][i], einr[r]);
     }
   }
 #pragma unroll
@@ -440,7 +441,7 @@ __device__ __forceinline__ SA<N::NS> block(const Ctx X, const SA<N::NS> sa_in) {
           x1v = (bits >> 16) >= X.thr ? x1v : 0.f;
         }
         const bool st = tp < N::LOUT[L] && smp < NS;
-        upd(smp, st, fmaxf(fabsf(x0v), fabsf(x1v)));
+        upd(r, st, fmaxf(fabsf(x0v), fabsf(x1v)));
         acc[c][r][0] = x0v;
         acc[c][r][1] = x1v;
       }
@@ -467,13 +468,24 @@ __device__ __forceinline__ SA<N::NS> block(const Ctx X, const SA<N::NS> sa_in) {
         } else {
           const bool st = t < N::LOUT[L] && smp < NS;
           const float a = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
-          upd(smp, st, a);
+          upd(r, st, a);
           acc[c][r] = v;
         }
       }
     }
   }
-  if constexpr (!G::HEAD) publish_max<NS>(mxs, red, wave, lane);
+  if constexpr (!G::HEAD) {
+    float mxs[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) mxs[j] = 0.f;
+#pragma unroll
+    for (int r = 0; r < NRW; ++r) {
+      const int smp = smp_of(r);
+#pragma unroll
+      for (int j = 0; j < NS; ++j) mxs[j] = smp == j ? fmaxf(mxs[j], mr[r]) : mxs[j];
+    }
+    publish_max<NS>(mxs, red, wave, lane);
+  }
   __syncthreads();  // input rows read by every wave; wave maxima visible
   SA<NS> sa_out;
 #pragma unroll
