@@ -162,6 +162,12 @@ class AlarconCNN1D:
 
         return self.device.type == "cuda" and self.precision == "fp32" and x3.supports(self.spec)
 
+    def uses_tiled_x3(self) -> bool:
+        """Running-BN inference on the fp32 fused whole-network kernel (``csrc/fused_tiled_x3.hip``: the
+        pooled ensemble_cnn members, the 30 s single-channel window; precision "fp32", GPU)."""
+        return (self.device.type == "cuda" and self.precision == "fp32" and not fused.supports(self.spec)
+                and fused.tiled_net(self.spec) is not None and os.environ.get("APNEAUQ_TILED_FUSED", "1") != "0")
+
     def x3_model(self):
         """The engine's packed view of this model (cached per weight version; the BN moving statistics
         are views of the store's tensors, so batch-statistics MC Dropout updates them in place)."""
@@ -196,7 +202,7 @@ class AlarconCNN1D:
                                         seed=seed, pass_offset=pass_offset, window_offset=window_offset,
                                         logits=logits)
             _ext.require()
-            if fused.tiled_net(self.spec) is not None and os.environ.get("APNEAUQ_TILED_FUSED", "1") != "0":
+            if self.uses_tiled_x3():
                 # the pooled ensemble_cnn members / the 30 s single-channel window: the fp16x3 fused
                 # whole-network kernel (csrc/fused_tiled_x3.hip)
                 return fused.tiled_x3_forward(x, self.fused_blob_x3(), self.spec, n_pass=n_pass, dropout=dropout,

@@ -120,6 +120,16 @@ def deep_ensembles_predict(ensemble_models: List, x_test_data, as_numpy: bool = 
         blobs = torch.cat([m.fused_blob().to(m0.device) for m in ensemble_models])
         out = fused.fused_forward(x, blobs, m0.spec)[:, 0].unsqueeze(-1)
         out = out.float().cpu().numpy() if as_numpy else out
+    elif (ensemble_models and all(getattr(m, "uses_tiled_x3", lambda: False)() for m in ensemble_models)
+          and all(m.spec == ensemble_models[0].spec for m in ensemble_models)):
+        # the pooled / single-channel members at fp32: every member in ONE fused fp16x3 launch
+        from ..ops import _ext, fused
+
+        _ext.require()
+        m0 = ensemble_models[0]
+        blobs = torch.cat([m.fused_blob_x3().to(m0.device) for m in ensemble_models])
+        out = fused.tiled_x3_forward(m0._as_input(x_test_data), blobs, m0.spec)[:, 0].unsqueeze(-1)
+        out = out.cpu().numpy() if as_numpy else out
     elif ensemble_models and all(getattr(m, "uses_hip", lambda: False)() for m in ensemble_models):
         m0 = ensemble_models[0]
         x = m0._as_input(x_test_data)
