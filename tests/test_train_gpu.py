@@ -325,3 +325,42 @@ def test_member_batched_step_many_members():
     out = st([x[i] for i in range(M)], [y[i] for i in range(M)])
     assert all(m.optimizer.iterations == 2 and m._train_step_counter == 2 for m in ms)
     assert all(np.isfinite(float(o[0])) for o in out)
+
+
+def test_step_node_kernels():
+    """The merged small nodes of the graphed step (round 5): ``train_inputs`` copies every member's x into
+    the padded-row bf16 layout exactly as ``copy_`` does (round to nearest even, pad rows untouched) and y
+    verbatim; ``train_tail`` bumps the counters once and writes sigmoid(logits) within 2 ulp of torch;
+    ``gt_pack_zero`` packs like ``gt_pack`` and clears the listed buffers."""
+    _ext.require()
+    o = _ext.ops()
+    g = torch.Generator().manual_seed(3)
+    n, SR = 37, train_ops.SR
+    xs = [torch.randn(n, 60, 4, generator=g).cuda() for _ in range(3)]
+    ys = [torch.rand(n, generator=g).cuda() for _ in range(3)]
+    xd = [torch.full((n * SR + 8, 4), 7.0, dtype=torch.bfloat16, device="cuda") for _ in range(3)]
+    yd = [torch.zeros(n + 5, device="cuda") for _ in range(3)]
+    o.train_inputs(xs, ys, xd, yd, SR)
+    for x, y, a, b in zip(xs, ys, xd, yd):
+        v = a[: n * SR].view(n, SR, 4)
+        assert torch.equal(v[:, :60], x.to(torch.bfloat16))
+        assert bool((v[:, 60:] == 7.0).all()) and bool((a[n * SR:] == 7.0).all())
+        assert torch.equal(b[:n], y) and bool((b[n:] == 0).all())
+    cnt = torch.tensor([[3, 5], [7, 11]], dtype=torch.int32, device="cuda")
+    lg = [torch.randn(n, generator=g).cuda() * 8 for _ in range(2)]
+    pr = [torch.empty(n, device="cuda") for _ in range(2)]
+    o.train_tail(cnt.view(-1), lg, pr)
+    assert cnt.cpu().tolist() == [[4, 6], [8, 12]]
+    for a, b in zip(lg, pr):
+        torch.testing.assert_close(b, torch.sigmoid(a), rtol=2.5e-7, atol=1e-7)
+    m = AlarconCNN1D(seed=4, device="cuda")
+    ws = train_ops.TrainWorkspace(m, 64)
+    for t in ws.accumulators():
+        t.fill_(1)
+    ws.pack()
+    ref = [w.clone() for w in ws.wf] + [w.clone() for w in ws.wd[1:]]
+    for w in ws.wf + ws.wd[1:]:
+        w.zero_()
+    ws.pack_zero()
+    assert all(torch.equal(a, b) for a, b in zip(ref, list(ws.wf) + list(ws.wd[1:])))
+    assert all(bool((t == 0).all()) for t in ws.accumulators())
