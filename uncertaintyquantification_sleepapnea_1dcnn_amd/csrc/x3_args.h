@@ -63,6 +63,7 @@ struct AffArgs {
   int repeat;            // moving updates per stats group (block 1 moments are shared by all passes)
   double inv_count;
   float eps, momentum, dsc;
+  int running;           // affine from the moving statistics; stats (if given) only bound the range (gscale)
 };
 
 struct HeadArgs {

@@ -154,8 +154,9 @@ void x3_l1(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b, at::Te
 void x3_aff(const c10::optional<at::Tensor>& stats, const at::Tensor& gamma, const at::Tensor& beta, at::Tensor& mmean,
             at::Tensor& mvar, at::Tensor& aff, int64_t C, int64_t groups, int64_t p_gstride, bool update,
             int64_t repeat, double inv_count, double eps, double momentum, double dsc,
-            const c10::optional<at::Tensor>& amax, const c10::optional<at::Tensor>& gscale) {
+            const c10::optional<at::Tensor>& amax, const c10::optional<at::Tensor>& gscale, bool running) {
   TORCH_CHECK(C >= 1 && C <= 4096 && groups >= 1, "x3_aff: bad sizes");
+  TORCH_CHECK(!(running && update), "x3_aff: running affine and the moving update are exclusive");
   TORCH_CHECK(p_gstride == 0 || p_gstride == C, "x3_aff: p_gstride must be 0 or C");
   const int64_t pg = p_gstride ? groups : 1;
   need(gamma, at::kFloat, pg * C, "x3_aff: gamma");
@@ -183,7 +184,8 @@ void x3_aff(const c10::optional<at::Tensor>& stats, const at::Tensor& gamma, con
   const at::DeviceGuard guard(gamma.device());
   apneauq::x3::AffArgs A{st, gamma.data_ptr<float>(), beta.data_ptr<float>(), mmean.data_ptr<float>(),
                          mvar.data_ptr<float>(), aff.data_ptr<float>(), amp, gsp, (int)C, (int)groups, (int)p_gstride,
-                         update ? 1 : 0, (int)repeat, inv_count, (float)eps, (float)momentum, (float)dsc};
+                         update ? 1 : 0, (int)repeat, inv_count, (float)eps, (float)momentum, (float)dsc,
+                         running ? 1 : 0};
   check(apneauq::x3_launch_aff(A, cur_stream()), "x3_aff");
 }
 
@@ -219,7 +221,7 @@ TORCH_LIBRARY_FRAGMENT(apneauq, m) {
         "Tensor(c!)? smax=None) -> ()");
   m.def("x3_aff(Tensor? stats, Tensor gamma, Tensor beta, Tensor(a!) mmean, Tensor(b!) mvar, Tensor(c!) aff, int C, "
         "int groups, int p_gstride, bool update, int repeat, float inv_count, float eps, float momentum, float dsc, "
-        "Tensor(d!)? amax=None, Tensor(e!)? gscale=None) -> ()");
+        "Tensor(d!)? amax=None, Tensor(e!)? gscale=None, bool running=False) -> ()");
   m.def("x3_head(Tensor sums, Tensor aff, int aff_gstride, Tensor dw, Tensor db, int p_gstride, Tensor(a!) out, "
         "int n_win, int groups, bool logits) -> ()");
   m.def("x3_lds(int layer) -> int", &x3_lds);

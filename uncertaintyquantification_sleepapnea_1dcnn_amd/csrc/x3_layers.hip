@@ -723,7 +723,7 @@ __global__ __launch_bounds__(256) void aff_kernel(const AffArgs A) {
     for (int c = tid; c < A.C; c += 256) {
       const long long po = (long long)g * A.p_gstride + c;
       float mean, var;
-      if (A.stats != nullptr) {
+      if (A.stats != nullptr && !A.running) {
         aff_moments(A, g, c, mean, var);
       } else {
         mean = A.mmean[po];
@@ -735,7 +735,8 @@ __global__ __launch_bounds__(256) void aff_kernel(const AffArgs A) {
       A.aff[((long long)g * 2 + 1) * A.C + c] = t_;
       if (A.gscale != nullptr) {
         // batch moments: R >= 0 gives max R_c <= sqrt(sum R_c^2) over the group's rows (of all ranks), so
-        // b = max_c |s_c| sqrt(sum R_c^2) + |t_c| bounds every staged |a| of the group
+        // b = max_c |s_c| sqrt(sum R_c^2) + |t_c| bounds every staged |a| of the group (with A.running the
+        // affine is the moving statistics' and the sums of squares serve only this bound)
         const double* p = A.stats + (long long)g * kStatSlots * 2 * A.C + A.C + c;
         double q = 0.0;
         for (int s = 0; s < kStatSlots; ++s) q += p[s * 2 * A.C];

@@ -385,6 +385,8 @@ def _forward_running(model: X3Model, x: torch.Tensor, n_pass: int, dropout: bool
     dsc = [_dsc(b.dropout) if dropout else 1.0 for b in spec.blocks]
     eps, mom = float(spec.bn_epsilon), float(spec.bn_momentum)
     seed = int(seed) & ((1 << 63) - 1)
+    if not dropout:
+        return _predict_members(model, ws, x, G, eps, mom, logits)
     sl = _sign_layers()
     # BN affine of the moving statistics, per member (shared by all passes with dropout)
     for l in range(6):
@@ -411,6 +413,36 @@ def _forward_running(model: X3Model, x: torch.Tensor, n_pass: int, dropout: bool
 # CPU emulation of the engine's arithmetic from the packed fragments (fp32 conv of hi + lo weights,
 # activations split the same way): validates the packing on the CPU tier.
 # ------------------------------------------------------------------------------------------------
+def _predict_members(model: X3Model, ws: "_Workspace", x: torch.Tensor, G: int, eps: float, mom: float,
+                     logits: bool) -> torch.Tensor:
+    """Deep-Ensemble predict (``uq_techniques.py:29``): BN on each member's moving statistics, every member
+    in one launch per layer.  The staged activations' range-safe prescale is one power of two per member
+    and block, bounded by the block output's sums of squares (max R_c <= sqrt(sum R_c^2): the moment
+    epilogue of the batch-statistics kernels, used here for the bound only) -- the layer kernels of the
+    MC-Dropout phase, no per-sample maximum tracking (2.5 % of the phase)."""
+    spec, o = model.spec, _ops()
+    n = x.shape[0]
+    per_member = G > 1
+    ps = CH[1:] if per_member else [0] * 6
+    o.zero_buffers([ws.stats[l][: G * STAT_SLOTS * 2 * CH[l + 1]] for l in range(5)])
+    g, b, mm, mv = model.bn[5]  # block 6 feeds the fp32 head: no prescale
+    o.x3_aff(None, g, b, mm, mv, ws.aff[5], CH[6], G, ps[5], False, 1, 1.0, eps, mom, 1.0, None)
+    o.x3_l1(x, model.w1, model.b1, ws.r1, ws.stats[0], n, G, None)
+    for l in range(1, 6):
+        g, b, mm, mv = model.bn[l - 1]
+        o.x3_aff(ws.stats[l - 1], g, b, mm, mv, ws.aff[l - 1], CH[l], G, ps[l - 1], False, 1, 1.0, eps, mom, 1.0,
+                 None, ws.gscale[l - 1], True)
+        src = ws.r1 if l == 1 else ws.buf[(l - 2) % 2]
+        dst = ws.sums if l == 5 else ws.buf[(l - 1) % 2]
+        wstride = model.wfrag[l].shape[1] // 8 if per_member else 0
+        o.x3_layer(l, src, dst, model.wfrag[l], wstride, model.bias[l], model.wscale[l], ps[l],
+                   ws.aff[l - 1], 2 * CH[l] if per_member else 0, ws.stats[l] if l < 5 else None, n, G, False, 0, 0,
+                   0, 0, 0, 0, None, None, None, ws.gscale[l - 1], False, False)
+    o.x3_head(ws.sums, ws.aff[5], 2 * CH[6] if per_member else 0, model.dw, model.db, CH[6] if per_member else 0,
+              ws.out, n, G, bool(logits))
+    return ws.out[: G * n].view(G, 1, n).clone()
+
+
 def split_f16(a: torch.Tensor):
     hi = a.half()
     lo = (a - hi.float()).half()
