@@ -1,5 +1,6 @@
-"""Short fp32-path loop for kernel traces: ``python -m bench.fp32_prof --mode de|mcd_batch|mcd_running``
-(pooled CNN, 16384 windows; Deep Ensemble of 8 members or MC Dropout T=50, precision="fp32")."""
+"""Short fp32-path loop for kernel traces: ``python -m bench.fp32_prof --mode de|mcd_batch|mcd_running|train``
+(pooled CNN, 16384 windows; Deep Ensemble of 8 members or MC Dropout T=50, precision="fp32"; ``train``:
+30 batch-1024 steps of the reference CNN at train_precision="fp32")."""
 import argparse
 import os
 import sys
@@ -21,6 +22,14 @@ def main():
     from uncertaintyquantification_sleepapnea_1dcnn_amd.uq import uq_techniques as U
 
     x = torch.randn(16384, 60, 4, generator=torch.Generator().manual_seed(0)).cuda()
+    if a.mode == "train":
+        y = (torch.rand(1024, generator=torch.Generator().manual_seed(1)) > 0.5).float().cuda()
+        m = AlarconCNN1D(seed=3, device="cuda", train_precision="fp32")
+        for _ in range(30):
+            m.train_step(x[:1024], y)
+        torch.cuda.synchronize()
+        print("done", a.mode)
+        return
     ms = [AlarconCNN1D(spec=POOLED, seed=10 + i, device="cuda", precision="fp32") for i in range(8)]
     for _ in range(a.reps):
         if a.mode == "de":

@@ -61,7 +61,8 @@ hipError_t launch_gt_bwd(int dz_mode, const void* z, const float* bn, const void
                          const float* gamma, void* dz, int dz_rs, int dz_off, float* gbias, hipStream_t stream,
                          const unsigned* skey_dev, int det_slots, int f32);
 hipError_t launch_gt_bwd_finalize(const float* bst, int nslots, int C, float inv_count, float* coef, float* ggamma,
-                                  float* gbeta, hipStream_t stream);
+                                  float* gbeta, const float* dbs, int bslots, int BC, float* gbias,
+                                  hipStream_t stream);
 hipError_t launch_metrics_update(const float* p, const float* y, long long n, const float* thr, int n_thr,
                                  unsigned long long* counts, hipStream_t stream);
 hipError_t launch_generic_head(const void* y, const float* w, float b, int n, int L, int C, int out_logits, float* out,
@@ -720,16 +721,38 @@ void gt_bwd(bool dz_mode, const at::Tensor& z, const at::Tensor& bn, const c10::
         "gt_bwd");
 }
 
+// BN-backward finalize of one block (C > 0; C == 0: none) plus, as extra workgroups of the same launch,
+// the bias gradient gbias (BC) = column sums of a (slots, BC) table (the block above's, done by now).
 void gt_bwd_finalize(const at::Tensor& bst, int64_t C, double inv_count, at::Tensor& coef, at::Tensor& ggamma,
-                     at::Tensor& gbeta) {
-  need_f32(bst, kGtSlots * 2 * C, "gt_bwd_finalize bst");
-  need_f32(coef, 2 * C, "gt_bwd_finalize coef");
-  TORCH_CHECK(ggamma.is_cuda() && ggamma.scalar_type() == at::kFloat && ggamma.numel() == C && gbeta.numel() == C,
-              "gt_bwd_finalize: grads must have C elements");
-  const at::DeviceGuard guard(coef.device());
-  check(apneauq::launch_gt_bwd_finalize(bst.data_ptr<float>(), (int)(bst.numel() / (2 * C)), (int)C, (float)inv_count,
-                                        coef.data_ptr<float>(),
-                                        ggamma.data_ptr<float>(), gbeta.data_ptr<float>(), cur_stream()),
+                     at::Tensor& gbeta, const c10::optional<at::Tensor>& dbs, const c10::optional<at::Tensor>& gbias) {
+  TORCH_CHECK(C >= 0, "gt_bwd_finalize: C >= 0");
+  if (C > 0) {
+    need_f32(bst, kGtSlots * 2 * C, "gt_bwd_finalize bst");
+    need_f32(coef, 2 * C, "gt_bwd_finalize coef");
+    TORCH_CHECK(ggamma.is_cuda() && ggamma.scalar_type() == at::kFloat && ggamma.numel() == C && gbeta.numel() == C,
+                "gt_bwd_finalize: grads must have C elements");
+  }
+  TORCH_CHECK(dbs.has_value() == gbias.has_value(), "gt_bwd_finalize: dbs and gbias go together");
+  int bslots = 0, BC = 0;
+  float* gbp = nullptr;
+  const float* dbp = nullptr;
+  if (gbias.has_value()) {
+    const at::Tensor& d = *dbs;
+    const at::Tensor& gbt = *gbias;
+    TORCH_CHECK(d.is_cuda() && d.scalar_type() == at::kFloat && d.is_contiguous() && d.dim() == 2,
+                "gt_bwd_finalize: dbs must be a contiguous (slots, C) fp32 GPU tensor");
+    TORCH_CHECK(gbt.is_cuda() && gbt.scalar_type() == at::kFloat && gbt.is_contiguous() && gbt.numel() == d.size(1),
+                "gt_bwd_finalize: gbias must have dbs.size(1) fp32 elements");
+    bslots = (int)d.size(0);
+    BC = (int)d.size(1);
+    dbp = d.data_ptr<float>();
+    gbp = gbt.data_ptr<float>();
+  }
+  const at::DeviceGuard guard(C > 0 ? coef.device() : gbias->device());
+  check(apneauq::launch_gt_bwd_finalize(C > 0 ? bst.data_ptr<float>() : nullptr, C > 0 ? (int)(bst.numel() / (2 * C)) : 0,
+                                        (int)C, (float)inv_count, C > 0 ? coef.data_ptr<float>() : nullptr,
+                                        C > 0 ? ggamma.data_ptr<float>() : nullptr,
+                                        C > 0 ? gbeta.data_ptr<float>() : nullptr, dbp, bslots, BC, gbp, cur_stream()),
         "gt_bwd_finalize");
 }
 
@@ -1181,7 +1204,7 @@ TORCH_LIBRARY(apneauq, m) {
         "int C, bool pool, bool dropout, int thr, float inv_keep, int skey, int window_offset, Tensor(a!)? bst, "
         "Tensor? coef, Tensor? gamma, Tensor(b!)? dz, int dz_rs, int dz_off, Tensor(c!)? gbias, Tensor? skey_dev=None, "
         "bool det=False) -> ()");
-  m.def("gt_bwd_finalize(Tensor bst, int C, float inv_count, Tensor(a!) coef, Tensor(b!) ggamma, Tensor(c!) gbeta) -> ()");
+  m.def("gt_bwd_finalize(Tensor bst, int C, float inv_count, Tensor(a!) coef, Tensor(b!) ggamma, Tensor(c!) gbeta, Tensor? dbs=None, Tensor(d!)? gbias=None) -> ()");
   m.def("gt_wgrad(Tensor x, Tensor dz, int R, int cin, int cout, int k, Tensor(a!) gw, Tensor(b!)? part=None) -> ()");
   m.def("gt_head(Tensor h, Tensor w, Tensor b, Tensor y, Tensor(a!) prob, Tensor(b!) dlog, Tensor(c!) loss, "
         "Tensor(d!) gw, Tensor(e!) gb, int n, int L, int C, float inv_gb, Tensor(f!)? part=None) -> ()");

@@ -348,9 +348,29 @@ __global__ __launch_bounds__(256) void bwd_kernel(BwdArgs<T> A) {
   }
 }
 
+// Blocks [0, ceil(C / 16)) finalize the BN backward of one block; blocks after that (side job, no
+// node of its own) add the bias-gradient slot table (bslots, BC) of the block above it in fixed order:
+// lane j sums slots j, j + 16, ... (fp64), then the 16 lane sums in order -> reproducible.
 __global__ __launch_bounds__(256) void bwd_finalize_kernel(const float* bst, int nslots, int C, float inv_count,
-                                                           float* coef, float* ggamma, float* gbeta) {
+                                                           float* coef, float* ggamma, float* gbeta, const float* dbs,
+                                                           int bslots, int BC, float* gbias) {
   __shared__ double red[2][256];
+  const int nfin = (C + 15) / 16;
+  if ((int)blockIdx.x >= nfin) {
+    const int chl = threadIdx.x & 15, lane = threadIdx.x >> 4;
+    const int c = ((int)blockIdx.x - nfin) * 16 + chl;
+    double a = 0.0;
+    if (c < BC)
+      for (int s = lane; s < bslots; s += 16) a += (double)dbs[(long long)s * BC + c];
+    red[0][threadIdx.x] = a;
+    __syncthreads();
+    if (threadIdx.x >= 16 || c >= BC) return;
+    double t = 0.0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t += red[0][j * 16 + chl];
+    gbias[c] = (float)t;
+    return;
+  }
   double s1, s2;
   int c;
   if (!slot_pair_sums(bst, nslots, C, red, s1, s2, c)) return;
@@ -476,9 +496,13 @@ hipError_t launch_gt_bwd(int dz_mode, const void* z, const float* bn, const void
 }
 
 hipError_t launch_gt_bwd_finalize(const float* bst, int nslots, int C, float inv_count, float* coef, float* ggamma,
-                                  float* gbeta, hipStream_t stream) {
-  hipLaunchKernelGGL(gtrain::bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, stream, bst, nslots, C,
-                     inv_count, coef, ggamma, gbeta);
+                                  float* gbeta, const float* dbs, int bslots, int BC, float* gbias,
+                                  hipStream_t stream) {
+  if (gbias == nullptr) BC = 0;
+  const int blocks = (C + 15) / 16 + (BC + 15) / 16;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(gtrain::bwd_finalize_kernel, dim3(blocks), dim3(256), 0, stream, bst, nslots, C, inv_count, coef,
+                     ggamma, gbeta, dbs, bslots, BC, gbias);
   return hipGetLastError();
 }
 

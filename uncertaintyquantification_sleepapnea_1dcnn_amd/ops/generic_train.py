@@ -229,14 +229,17 @@ def _get_ws(model, batch: int, with_backward: bool = True, f32: bool = False) ->
 
 
 def _forward(ws: GenericTrainWorkspace, n: int, global_n: int, seed: int, pass_id: int, window_offset: int,
-             dropout: bool, update_moving: bool, sync: Optional[Callable], wf, keys_dev=None) -> torch.Tensor:
+             dropout: bool, update_moving: bool, sync: Optional[Callable], wf, keys_dev=None,
+             zero_stats: bool = True) -> torch.Tensor:
     """Batch-statistics forward of ``n`` windows already loaded in ``ws.xin[0]``; returns the
     last block's output (n, L_out, C) bf16.  ``keys_dev`` (int32 (blocks,)) makes the kernels read
-    the dropout stream keys from device memory (HIP-graph replays)."""
+    the dropout stream keys from device memory (HIP-graph replays).  ``zero_stats=False``: the caller
+    has zeroed ``ws.st_all`` already (one launch with its other accumulators)."""
     o = _ext.ops()
     spec, v = ws.model.spec, ws.model.store.views
     nl = len(spec.blocks)
-    ws.st_all.zero_()
+    if zero_stats:
+        ws.st_all.zero_()
     ws._running_key = None  # ws.bn gets the batch affine below (running_affine must rebuild it)
     for l, b in enumerate(spec.blocks):
         i = l + 1
@@ -278,17 +281,15 @@ def _grads(model, ws: GenericTrainWorkspace, y: torch.Tensor, n: int, gb: int, p
     nl = len(spec.blocks)
     seed = model.seed
     wf, wd = ws.pack(backward=True)
-    h = _forward(ws, n, gb, seed, pass_id, window_offset, True, True, sync, wf, keys_dev)
+    # every accumulator of the step (forward / backward BN moments, bias slots, gradient, loss): one launch
+    o.zero_buffers([ws.st_all, ws.bst_all, ws.dbs_all, ws.grad, ws.head_loss])
+    h = _forward(ws, n, gb, seed, pass_id, window_offset, True, True, sync, wf, keys_dev, zero_stats=False)
     # head: GAP + Dense + BCE(logits) + dlogit + dense gradients (mean over the global batch), one launch
     wdense = v["output_layer/kernel"].reshape(-1)
-    ws.grad.zero_()
-    ws.head_loss.zero_()
     ws.y[:n].copy_(y.reshape(-1))
     o.gt_head(h, wdense, v["output_layer/bias"], ws.y, ws.prob, ws.dlog, ws.head_loss, g["output_layer/kernel"],
               g["output_layer/bias"], n, ws.L[-1], ws.ch[-1], 1.0 / gb, ws.hpart)
     dlog = ws.dlog
-    ws.bst_all.zero_()
-    ws.dbs_all.zero_()
     for l in range(nl - 1, -1, -1):
         i, b = l + 1, spec.blocks[l]
         cin, cout, L, p, k = ws.ch[l], ws.ch[l + 1], ws.L[l], ws.pads[l], ws.ks[l]
@@ -303,12 +304,16 @@ def _grads(model, ws: GenericTrainWorkspace, y: torch.Tensor, n: int, gb: int, p
                  thr, ik, skey, int(window_offset), ws.bst[l], None, None, None, 0, 0, None, kd, ws.det)
         if sync is not None:
             sync(ws.bst[l])
+        # + the bias gradient of block l + 1 (its slots are complete) as extra workgroups of the finalize
+        above = (ws.dbs[l + 1], g[f"conv1d_{i + 1}/bias"]) if l + 1 < nl else (None, None)
         o.gt_bwd_finalize(ws.bst[l], cout, 1.0 / (gb * L), ws.coef[l], g[f"batchnorm_{i}/gamma"],
-                          g[f"batchnorm_{i}/beta"])
+                          g[f"batchnorm_{i}/beta"], *above)
         o.gt_bwd(True, ws.z[l], ws.bn[l], up["dh"], up["dlog"], up["w"], up["invL"], n, L, cout, bool(b.pool), drop,
                  thr, ik, skey, int(window_offset), None, ws.coef[l], v[f"batchnorm_{i}/gamma"], ws.dzp[l], ws.rs[l], p,
                  ws.dbs[l], kd, ws.det)
-        torch.sum(ws.dbs[l], 0, out=g[f"conv1d_{i}/bias"])
+        if l == 0:  # block 1's bias gradient: a finalize launch with no BN part
+            o.gt_bwd_finalize(ws.bst[0], 0, 1.0, ws.coef[0], g["batchnorm_1/gamma"], g["batchnorm_1/beta"], ws.dbs[0],
+                              g["conv1d_1/bias"])
         if ws.x3:
             # dgrad publishes dZ's tensor maximum for the wgrad prescale (block 1: no dgrad, amax kernel)
             if l > 0:
