@@ -1,0 +1,7 @@
+// wgrad table probe w8d: the library table with block 5 as 8 waves over a 16 x 256 block (one co block).
+template <> struct WgCfg<0> { static constexpr int CIB = 32, COB = 128, WCO = 4, WCI = 1, RTILES = 2, MINWG = 512, U = 4, MINB = 2, WAVES = 4; static constexpr bool PF = false, PFA = false; };  // im2col kk=32
+template <> struct WgCfg<1> { static constexpr int CIB = 32, COB = 192, WCO = 4, WCI = 2, RTILES = 8, MINWG = 256, U = 8, MINB = 1, WAVES = 8; static constexpr bool PF = true, PFA = true; };
+template <> struct WgCfg<2> { static constexpr int CIB = 64, COB = 224, WCO = 2, WCI = 4, RTILES = 8, MINWG = 256, U = 8, MINB = 1, WAVES = 8; static constexpr bool PF = true, PFA = true; };
+template <> struct WgCfg<3> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = 512, U = 8, MINB = 2, WAVES = 4; static constexpr bool PF = true, PFA = true; };
+template <> struct WgCfg<4> { static constexpr int CIB = 16, COB = 256, WCO = 8, WCI = 1, RTILES = 16, MINWG = 256, U = 8, MINB = 1, WAVES = 8; static constexpr bool PF = true, PFA = true; };
+template <> struct WgCfg<5> { static constexpr int CIB = 64, COB = 96, WCO = 2, WCI = 4, RTILES = 16, MINWG = 256, U = 4, MINB = 1, WAVES = 8; static constexpr bool PF = true, PFA = true; };

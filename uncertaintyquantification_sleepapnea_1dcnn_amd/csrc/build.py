@@ -42,6 +42,9 @@ HOST_SAN = os.environ.get("APNEAUQ_HOST_SANITIZE", "")
 # a correct configuration, only the speed differs (tools/probes/x3_tables/)
 X3_TABLE = os.environ.get("APNEAUQ_X3_TABLE", "")
 EXTRA = [f'-DAPNEAUQ_X3_TABLE="{os.path.abspath(X3_TABLE)}"'] if X3_TABLE else []
+# ... and of the training wgrad kernels (csrc/train_conv.hip WgCfg)
+WG_TABLE = os.environ.get("APNEAUQ_WG_TABLE", "")
+EXTRA += [f'-DAPNEAUQ_WG_TABLE="{os.path.abspath(WG_TABLE)}"'] if WG_TABLE else []
 
 
 def _torch_paths():

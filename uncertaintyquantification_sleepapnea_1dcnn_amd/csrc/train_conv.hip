@@ -45,9 +45,9 @@ struct bf16x16 {
   bf16x8 a, b;
 };
 
-template <int N, int UMAX = kStageU, typename Load, typename Store>
+template <int N, int UMAX = kStageU, int NT = kThreads, typename Load, typename Store>
 __device__ __forceinline__ void staged_loop(Load load, Store store) {
-  constexpr int IT = (N + kThreads - 1) / kThreads;
+  constexpr int IT = (N + NT - 1) / NT;
   constexpr int U = IT < UMAX ? IT : UMAX;
   using P = decltype(load(0));
   // opaque thread index: inside a tile loop (wgrad) LICM would otherwise hoist every per-item
@@ -59,12 +59,12 @@ __device__ __forceinline__ void staged_loop(Load load, Store store) {
     P v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int i = tid + (b + u) * kThreads;
+      const int i = tid + (b + u) * NT;
       if (b + u < IT && i < N) v[u] = load(i);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int i = tid + (b + u) * kThreads;
+      const int i = tid + (b + u) * NT;
       if (b + u < IT && i < N) store(i, v[u]);
     }
   }
@@ -99,11 +99,11 @@ __device__ __forceinline__ void lds_row8(const float* tab, int c0, float scale, 
 // the second stats group (a tile straddling an MC-Dropout pass boundary, g1 = s/t + 256) is selected
 // per row only when it differs.  The dropout mask is R_l's sign bit (set by the producer), so the
 // transform is  a = sign ? 0 : |r| * s + t  on the packed bf16 pairs.
-template <int l, int NR, int NCW, int UMAX = kStageU>
+template <int l, int NR, int NCW, int UMAX = kStageU, int NT = kThreads>
 __device__ __forceinline__ void stage_act(const Args& A, char* lds, int ldsrs, int row0, int c0, const float* s,
                                           const float* t, int g0) {
   constexpr int Cc = C[l + 1];
-  constexpr int RP = kThreads / NCW;  // rows per pass over the workgroup
+  constexpr int RP = NT / NCW;  // rows per pass over the workgroup
   constexpr int NK = (NR + RP - 1) / RP;
   constexpr int U = NK < UMAX ? NK : UMAX;
   const Layer& Ly = A.L[l];
@@ -390,11 +390,11 @@ __device__ __forceinline__ void stage_dz(const Args& A, char* lds, int ldsrs, in
 }
 
 // dZ_l rows [row0, row0+NR) x channels [c0, c0+NCW*8) into LDS (wgrad; dgrad materialised them)
-template <int l, int NR, int NCW, int UMAX>
+template <int l, int NR, int NCW, int UMAX, int NT = kThreads>
 __device__ __forceinline__ void stage_dz_copy(const Args& A, char* lds, int ldsrs, int row0, int c0) {
   constexpr int Cc = C[l + 1];
   const Layer& Ly = A.L[l];
-  staged_loop<NR * NCW, UMAX>(
+  staged_loop<NR * NCW, UMAX, NT>(
       [&](int i) -> bf16x8 {
         const int rc = i / NCW, cw = i - rc * NCW;
         return gld<bf16x8>(Ly.dZ + (long long)(row0 + rc) * Cc + c0 + cw * 8);
@@ -1151,25 +1151,34 @@ template <int l> struct WgCfg;
 // workgroups per CU save 17 % on block 4 and spill on block 6)
 // wgrad LDS tiles: the row stride is an odd multiple of 32 B (conflict-free tr_frag reads)
 __host__ __device__ constexpr int wg_rs(int width_bytes) { return (width_bytes / 32) % 2 ? width_bytes : width_bytes + 32; }
-// wgrad of blocks 4 and 6 prefetch the next row tile into registers during the MFMAs
-constexpr bool kWgPrefetch = true;
 // MINWG values: batch-1024 step measured with tools/probes/train_variants.sh (block 5 512 -> 768 took
 // the step 0.795 -> 0.786 ms, block 2 256 -> 512 0.766-0.775 -> 0.758-0.768 ms, three interleaved rounds;
 // round 4, with the straggler-free grouping: block 3 256 -> 512 batch 8192 4.20-4.22 -> 4.13-4.16 ms,
 // batch 1024 / 8 members unchanged; block 4 512 -> 1024 slower)
-template <> struct WgCfg<0> { static constexpr int CIB = 32, COB = 128, WCO = 4, WCI = 1, RTILES = 2, MINWG = 512, U = 4, MINB = 2; };  // im2col kk=32
-template <> struct WgCfg<1> { static constexpr int CIB = 32, COB = 192, WCO = 2, WCI = 2, RTILES = 8, MINWG = 512, U = 8, MINB = 2; };
-template <> struct WgCfg<2> { static constexpr int CIB = 32, COB = 224, WCO = 2, WCI = 2, RTILES = 8, MINWG = 512, U = 8, MINB = 2; };
-template <> struct WgCfg<3> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = 512, U = 8, MINB = kWgPrefetch ? 2 : 3; };
-template <> struct WgCfg<4> { static constexpr int CIB = 16, COB = 128, WCO = 4, WCI = 1, RTILES = 16, MINWG = 768, U = 8, MINB = 3; };
-template <> struct WgCfg<5> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = 512, U = 4, MINB = 2; };
+#ifdef APNEAUQ_WG_TABLE  // A/B builds swap the complete table (tools/probes/wg_tables/)
+#include APNEAUQ_WG_TABLE
+#else
+// WAVES: 4 (two workgroups per CU) or 8 (one per CU: the output block over twice the waves, so each
+// wave holds half the accumulators and the next row tile's dZ / A rows fit in registers); PF / PFA: those
+// rows (dZ / A) are loaded into registers during this tile's MFMAs and written to LDS after them.
+// Blocks 2, 3, 5, 6 at 8 waves with both prefetches (tools/probes/wg_tables/w8a.h, profiles/train_step_r5.md):
+// batch 1024 0.725 -> 0.687 ms, batch 8192 4.12 -> 3.94 ms, 8 members 4.21 -> 4.07 ms (two rounds each);
+// block 4 keeps 4 waves (no 8-way split of its 224 x 96 block), block 1 its im2col.
+template <> struct WgCfg<0> { static constexpr int CIB = 32, COB = 128, WCO = 4, WCI = 1, RTILES = 2, MINWG = 512, U = 4, MINB = 2, WAVES = 4; static constexpr bool PF = false, PFA = false; };  // im2col kk=32
+template <> struct WgCfg<1> { static constexpr int CIB = 32, COB = 192, WCO = 4, WCI = 2, RTILES = 8, MINWG = 256, U = 8, MINB = 1, WAVES = 8; static constexpr bool PF = true, PFA = true; };
+template <> struct WgCfg<2> { static constexpr int CIB = 64, COB = 224, WCO = 2, WCI = 4, RTILES = 8, MINWG = 256, U = 8, MINB = 1, WAVES = 8; static constexpr bool PF = true, PFA = true; };
+template <> struct WgCfg<3> { static constexpr int CIB = 32, COB = 96, WCO = 2, WCI = 2, RTILES = 16, MINWG = 512, U = 8, MINB = 2, WAVES = 4; static constexpr bool PF = true, PFA = true; };
+template <> struct WgCfg<4> { static constexpr int CIB = 32, COB = 128, WCO = 4, WCI = 2, RTILES = 16, MINWG = 256, U = 8, MINB = 1, WAVES = 8; static constexpr bool PF = true, PFA = true; };
+template <> struct WgCfg<5> { static constexpr int CIB = 64, COB = 96, WCO = 2, WCI = 4, RTILES = 16, MINWG = 256, U = 4, MINB = 1, WAVES = 8; static constexpr bool PF = true, PFA = true; };
+#endif
 
 
 template <int l, bool MB>
-__global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A_, const Args* __restrict__ Am) {
+__global__ __launch_bounds__(WgCfg<l>::WAVES * 64, WgCfg<l>::MINB) void wgrad_kernel(Args A_, const Args* __restrict__ Am) {
   const MbPos pos = mb_pos<MB>();
   const Args& A = member_args<MB>(A_, Am, pos);
   using W = WgCfg<l>;
+  constexpr int NT = W::WAVES * 64;
   constexpr int CIN = C[l], COUT = C[l + 1], K = KS[l], PAD = (K - 1) / 2;
   constexpr bool FIRST = (l == 0);
   constexpr int NTAP = FIRST ? 1 : K;           // block 1: taps folded into the im2col columns
@@ -1177,7 +1186,7 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A_
   constexpr int NCI = W::CIB / 16 / W::WCI;     // ci tiles per wave
   constexpr int DZRS = wg_rs(W::COB * 2);       // LDS row strides (bytes): odd multiples of 32 B
   constexpr int ARS = wg_rs(FIRST ? 64 : W::CIB * 2);
-  static_assert(W::WCO * W::WCI == 4, "4 waves");
+  static_assert(W::WCO * W::WCI == W::WAVES && (W::WAVES == 4 || !(l == 0)), "one output sub-block per wave");
   static_assert((FIRST || CIN % W::CIB == 0) && COUT % W::COB == 0 && W::CIB % (16 * W::WCI) == 0 &&
                     W::COB % (16 * W::WCO) == 0,
                 "wgrad blocks must tile Cin x Cout exactly (e.g. CIB 64 on Cin 224 dropped channels)");
@@ -1284,11 +1293,11 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A_
   // blocks 4 and 6 (dZ only): blocks 2 and 3 have no registers left for it (spills), and block 5
   // loses more from 2 instead of 3 workgroups per CU than the prefetch gains (wgrad<4> 276 -> 333 us
   // at batch 8192; wgrad<3>: 278 -> 243 us; profiles/train_step_r4.md)
-  constexpr bool PF = kWgPrefetch && (l == 3 || l == 5);
-  constexpr bool PFA = PF && l == 3;  // block 6: dZ only (the A rows would spill)
-  constexpr int NCWD = W::COB / 8, ITD = PF ? kR * NCWD / kThreads : 1;
-  constexpr int NCWA = W::CIB / 8, RPA = kThreads / NCWA, ITA = PFA ? (kRows + RPA - 1) / RPA : 1;
-  static_assert(!PF || (kR * NCWD) % kThreads == 0, "dZ rows split evenly over the threads");
+  constexpr bool PF = W::PF;
+  constexpr bool PFA = W::PFA;  // block 6: dZ only (the A rows would spill)
+  constexpr int NCWD = W::COB / 8, ITD = PF ? kR * NCWD / NT : 1;
+  constexpr int NCWA = W::CIB / 8, RPA = NT / NCWA, ITA = PFA ? (kRows + RPA - 1) / RPA : 1;
+  static_assert(!PF || (kR * NCWD) % NT == 0, "dZ rows split evenly over the threads");
   bf16x8 pd[ITD];
   u32x4 pa[ITA];
   // the thread index is made opaque per call (see staged_loop): otherwise LICM keeps every item's
@@ -1304,7 +1313,7 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A_
     const __bf16* dz = A.L[l].dZ + (long long)(row0 + kHalo) * COUT + co0;
 #pragma unroll
     for (int i = 0; i < ITD; ++i) {
-      const int idx = ptid + i * kThreads, rc = idx / NCWD, cw = idx - rc * NCWD;
+      const int idx = ptid + i * NT, rc = idx / NCWD, cw = idx - rc * NCWD;
       pd[i] = gld<bf16x8>(dz + (long long)rc * COUT + cw * 8);
     }
     if constexpr (PFA) {
@@ -1320,7 +1329,7 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A_
     const int ptid = opaque_tid(), cwa = ptid % NCWA, rina = ptid / NCWA;
 #pragma unroll
     for (int i = 0; i < ITD; ++i) {
-      const int idx = ptid + i * kThreads, rc = idx / NCWD, cw = idx - rc * NCWD;
+      const int idx = ptid + i * NT, rc = idx / NCWD, cw = idx - rc * NCWD;
       *reinterpret_cast<bf16x8*>(dz_lds + lds_off(rc, cw * 16, DZRS)) = pd[i];
     }
     if constexpr (PFA) {
@@ -1348,7 +1357,7 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A_
     __syncthreads();
     if constexpr (PF) {
       pf_store();
-      if constexpr (!PFA) stage_act<l - 1, kRows, W::CIB / 8, 4>(A, a_lds, ARS, row0, ci0, sp, tp, 0);
+      if constexpr (!PFA) stage_act<l - 1, kRows, W::CIB / 8, 4, NT>(A, a_lds, ARS, row0, ci0, sp, tp, 0);
     } else if constexpr (FIRST) {  // no dgrad for block 1: dZ_1 is recomputed here (a single ci block)
       stage_dz<l, kR, W::COB / 8>(A, dz_lds, DZRS, row0 + kHalo, co0, gr, mean, rstd, mdy, mdyx);
       // im2col of the raw input: col kk = tap*4 + ci (kk < 28), rows = tile rows; one 8-B load per
@@ -1360,8 +1369,8 @@ __global__ __launch_bounds__(kThreads, WgCfg<l>::MINB) void wgrad_kernel(Args A_
         *reinterpret_cast<bf16x4*>(a_lds + lds_off(r, tap * 8, ARS)) = v;
       }
     } else {
-      stage_dz_copy<l, kR, W::COB / 8, W::U>(A, dz_lds, DZRS, row0 + kHalo, co0);
-      stage_act<l - 1, kRows, W::CIB / 8, 4>(A, a_lds, ARS, row0, ci0, sp, tp, 0);
+      stage_dz_copy<l, kR, W::COB / 8, W::U, NT>(A, dz_lds, DZRS, row0 + kHalo, co0);
+      stage_act<l - 1, kRows, W::CIB / 8, 4, NT>(A, a_lds, ARS, row0, ci0, sp, tp, 0);
     }
     __syncthreads();
     if constexpr (PF) {
@@ -1441,8 +1450,13 @@ constexpr int lds_wgrad() {
   return train::kR * train::wg_rs(train::WgCfg<l>::COB * 2) +
          train::kRows * train::wg_rs(l == 0 ? 64 : train::WgCfg<l>::CIB * 2) + 1792 * 4;
 }
-static_assert(2 * lds_wgrad<1>() <= 160 * 1024 && 2 * lds_wgrad<2>() <= 160 * 1024 && 2 * lds_wgrad<4>() <= 160 * 1024,
-              "wgrad tiles must fit two workgroups per CU");
+template <int l>
+constexpr bool wg_lds_fits() {
+  return train::WgCfg<l>::WAVES == 8 ? lds_wgrad<l>() <= 160 * 1024 : 2 * lds_wgrad<l>() <= 160 * 1024;
+}
+static_assert(wg_lds_fits<0>() && wg_lds_fits<1>() && wg_lds_fits<2>() && wg_lds_fits<3>() && wg_lds_fits<4>() &&
+                  wg_lds_fits<5>(),
+              "wgrad tiles must fit two 4-wave (or one 8-wave) workgroups per CU");
 
 int train_args_size() { return (int)sizeof(Args); }
 
@@ -1621,7 +1635,7 @@ static void wg_launch(const Args& A, const Args* Am, int M, hipStream_t st) {
   // deterministic mode: the single-model row grouping (M = 1), so a member-batched step sums every
   // gradient in the same order as the member's own step
   const int rgs = wg_rgs<l>(A.B, A.det != nullptr ? 1 : M);
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(train::wgrad_kernel<l, MB>), dim3(nci * nco * rgs, 1, M), dim3(256), lds_wgrad<l>(),
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(train::wgrad_kernel<l, MB>), dim3(nci * nco * rgs, 1, M), dim3(W::WAVES * 64), lds_wgrad<l>(),
                      st, A, Am);
   if (A.wpart != nullptr) {
     const int kcc = train::KS[l] * train::C[l] * train::C[l + 1];
