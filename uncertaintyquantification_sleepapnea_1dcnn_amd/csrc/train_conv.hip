@@ -990,6 +990,127 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A_, const Args* __r
 // ------------------------------------------------------------------------------------------------
 // dgrad: prefetch the epilogue's R_{l-1} loads ahead of the conv on blocks 2-5 (block 6: registers)
 template <int l> struct DgPre { static constexpr bool v = l >= 1 && l <= 4; };
+// Persistent dgrad: a workgroup runs row tiles tile, tile + grid, ...; the first DgPF<l>::v staging items
+// per thread of the NEXT tile (R_l and dY_l rows, 8 channels each) are loaded into registers before this
+// tile's conv, so their latency hides under the MFMAs (the rest load at staging time, as before).
+// Sized to the registers each block leaves (tools/kernel_resources.py: no spills).
+template <int l> struct DgPF { static constexpr int v = l == 1 ? 8 : l == 2 ? 2 : l == 4 ? 12 : l == 5 ? 7 : 0; };
+// workgroups of a single-model dgrad launch: two per CU (larger batches loop over their tiles)
+constexpr int kDgGrid = 512;
+
+// stage_dz for dgrad (all CIN channels of 136 rows, dZ_l also written to global for wgrad) split into
+// load() (the prefetched items, into registers) and store() (every item: the prefetched ones from
+// registers, the rest loaded in batches there), so the next tile's loads can overlap this tile's conv.
+template <int l, int NPF>
+struct DzStager {
+  static constexpr int Cc = C[l + 1], NCW = Cc / 8, RP = kThreads / NCW, NR = kRows;
+  static constexpr int NK = (NR + RP - 1) / RP;
+  static constexpr int NP = NPF < NK ? NPF : NK;
+  static constexpr int U = kStageU;
+  bf16x8 r[NP > 0 ? NP : 1];
+  bf16x8 d[(NP > 0 && l < 5) ? NP : 1];
+
+  __device__ __forceinline__ static int tid() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+  }
+  __device__ __forceinline__ static bool valid(const Args& A, int grow) {
+    const int n = row_sample(grow), tt = row_time(grow);
+    return !(grow < kHalo || n >= A.B || tt >= kL);
+  }
+  __device__ __forceinline__ void load(const Args& A, int row0) {
+    const int t = tid(), cw = t % NCW, rin = t / NCW;
+    const bool active = rin < RP;
+    const Layer& Ly = A.L[l];
+#pragma unroll
+    for (int u = 0; u < NP; ++u) {
+      const int rc = rin + u * RP, grow = row0 + rc;
+      const bool ok = active && rc < NR && valid(A, grow);
+      r[u] = ok ? gld<bf16x8>(Ly.R + (long long)grow * Cc + cw * 8) : zero8();
+      if constexpr (l < 5) d[u] = ok ? gld<bf16x8>(Ly.dY + (long long)grow * Cc + cw * 8) : zero8();
+    }
+  }
+  // dz = relu'(r) * (al * dy + be * r + ga) per element (see stage_dz); rows [kHalo, kHalo + kR) to dZ_l too
+  __device__ __forceinline__ void store(const Args& A, char* lds, int row0, const float* gam_rstd, const float* mean,
+                                        const float* rstd, const float* mdy, const float* mdyx) const {
+    const int t = tid(), cw = t % NCW, rin = t / NCW;
+    if (rin >= RP) return;
+    const Layer& Ly = A.L[l];
+    const int c = cw * 8;
+    const int smp0 = (row0 >> 7) * 2;
+    float al[8], be[8], ga[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float g = gam_rstd[c + j], q = rstd[c + j] * mdyx[c + j];
+      al[j] = g;
+      be[j] = -g * q;
+      ga[j] = g * (q * mean[c + j] - mdy[c + j]);
+    }
+    float dw[8] = {}, dl0 = 0.f, dl1 = 0.f;
+    if constexpr (l == 5) {
+      const float dsc = A.dropout ? Ly.dsc : 1.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dw[j] = A.dense_w[c + j] * dsc;
+      dl0 = A.dlogit[min(smp0, A.B - 1)] * (1.0f / kL);
+      dl1 = A.dlogit[min(smp0 + 1, A.B - 1)] * (1.0f / kL);
+    }
+    auto emit = [&](int rc, const bf16x8& rv, const bf16x8& dv) {
+      const int grow = row0 + rc;
+      bf16x8 o = zero8();
+      if (valid(A, grow)) {
+        float dy[8];
+        if constexpr (l == 5) {
+          const float dl = row_sample(grow) != smp0 ? dl1 : dl0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dy[j] = bf_dropped(rv[j]) ? 0.f : dl * dw[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dy[j] = (float)dv[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float rr = bf_abs(rv[j]);
+          const float dz = __builtin_fmaf(al[j], dy[j], __builtin_fmaf(be[j], rr, ga[j]));
+          o[j] = (__bf16)(rr > 0.f ? dz : 0.f);
+        }
+      }
+      *reinterpret_cast<bf16x8*>(lds + lds_off(rc, cw * 16, kRS)) = o;
+      if (rc >= kHalo && rc < kHalo + kR)
+        *reinterpret_cast<bf16x8*>(Ly.dZ + (long long)grow * Cc + c) = o;  // pad rows get their zeros too
+    };
+#pragma unroll
+    for (int u = 0; u < NP; ++u) {
+      const int rc = rin + u * RP;
+      if (rc >= NR) continue;
+      if constexpr (l < 5)
+        emit(rc, r[u], d[u]);
+      else
+        emit(rc, r[u], r[u]);  // block 6: dY recomputed, no payload
+    }
+#pragma unroll
+    for (int b = NP; b < NK; b += U) {
+      bf16x8 qr[U], qd[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int rc = rin + (b + u) * RP, grow = row0 + rc;
+        if (b + u >= NK) continue;
+        const bool ok = rc < NR && valid(A, grow);
+        qr[u] = ok ? gld<bf16x8>(Ly.R + (long long)grow * Cc + c) : zero8();
+        if constexpr (l < 5) qd[u] = ok ? gld<bf16x8>(Ly.dY + (long long)grow * Cc + c) : zero8();
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int rc = rin + (b + u) * RP;
+        if (b + u >= NK || rc >= NR) continue;
+        if constexpr (l < 5)
+          emit(rc, qr[u], qd[u]);
+        else
+          emit(rc, qr[u], qr[u]);
+      }
+    }
+  }
+};
 
 template <int l, bool MB>
 __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A_, const Args* __restrict__ Am) {
@@ -1009,10 +1130,8 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A_, const Args*
   float* mdyx = prm + 1024;
   float* mean_prev = prm + 1280;  // block l-1 mean / rstd for xhat
   float* rstd_prev = prm + 1536;
-  const int tile = pos.bx;
-  APNEAUQ_DASSERT(2 * tile < A.B + 1 && blockDim.x == kThreads);
-  const int row0 = kR * tile;
-  const int smp0 = 2 * tile;
+  const int ntiles = (A.B + 1) / 2;
+  APNEAUQ_DASSERT(blockDim.x == kThreads);
   if (A.tab != nullptr) {  // single-device training: T[l] (block 6: backward sums), T[l-1]
     const int c = threadIdx.x;
     if (c < CIN) {
@@ -1055,12 +1174,20 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A_, const Args*
     }
   }
   __syncthreads();
-  stage_dz<l, kRows, CIN / 8>(A, act, kRS, row0, 0, gr, mean, rstd, mdy, mdyx, A.L[l].dZ, kHalo, kHalo + kR);
-  __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave / T::WN, wn = wave % T::WN;
   const int m = lane & 15, h = lane >> 4;
   const Layer& Lp = A.L[l - 1];
+  DzStager<l, DgPF<l>::v> stager;
+  if (DgPF<l>::v > 0 && pos.bx < ntiles) stager.load(A, kR * pos.bx);
+  // blocks without a prefetch keep one tile per workgroup (a constant one-trip loop: the persistent form
+  // keeps more values live and spilled block 4's dgrad)
+  constexpr bool PERSIST = DgPF<l>::v > 0;
+  for (int tile = pos.bx, it = 0; PERSIST ? tile < ntiles : it < 1; tile += gridDim.x, ++it) {
+  const int row0 = kR * tile;
+  const int smp0 = 2 * tile;
+  stager.store(A, act, row0, gr, mean, rstd, mdy, mdyx);
+  __syncthreads();
   // R_{l-1} at this lane's epilogue elements (|R| for xhat, sign = block l-1's dropout mask), loaded
   // before the conv so the MFMAs cover their latency (DgPre: where the registers allow)
   constexpr bool PRE = DgPre<l>::v;
@@ -1076,6 +1203,9 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A_, const Args*
         rpre[c][r] = valid ? gld<bf16x4>(Lp.R + (long long)(row0 + kHalo + row) * COUT + co0)
                            : bf16x4{(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
       }
+  }
+  if constexpr (DgPF<l>::v > 0) {
+    if (tile + (int)gridDim.x < ntiles) stager.load(A, kR * (tile + gridDim.x));  // in flight during the conv
   }
   f32x4 acc[CV::CT][CV::RT];
   CV::template run<1, false>(A.L[l].wd, act, kRS, acc);  // (B ring at batch 8192: -0.6 %, batch 1024: +-0)
@@ -1122,7 +1252,7 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A_, const Args*
         }
       }
     } else {
-      double* bst = Lp.bst + (pos.bx % kStatSlots) * 2 * COUT;
+      double* bst = Lp.bst + (tile % kStatSlots) * 2 * COUT;
       atomic_channel_sums(bst, co0, b0, m == 0);
       atomic_channel_sums(bst + COUT, co0, b1, m == 0);
     }
@@ -1133,6 +1263,8 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A_, const Args*
     const int r = i / CW, cw = i - r * CW;
     *reinterpret_cast<bf16x8*>(Lp.dY + (long long)(row0 + kHalo + r) * COUT + cw * 8) =
         *reinterpret_cast<const bf16x8*>(act + r * kRS + cw * 16);
+  }
+  __syncthreads();  // the next tile's staging overwrites act
   }
 }
 
@@ -1538,7 +1670,13 @@ static hipError_t fwd_launch(const Args& A, const Args* Am, int M, int l, int gr
 
 template <bool MB>
 static hipError_t dgrad_launch(const Args& A, const Args* Am, int M, int l, hipStream_t st) {
-  const dim3 g((A.B + 1) / 2, 1, M);
+  // persistent blocks (DgPF > 0): at most kDgGrid workgroups over all members, each looping over its
+  // member's tiles; the others one workgroup per tile
+  const int tiles = (A.B + 1) / 2;
+  const bool persist = (l == 1 && train::DgPF<1>::v > 0) || (l == 2 && train::DgPF<2>::v > 0) ||
+                       (l == 3 && train::DgPF<3>::v > 0) || (l == 4 && train::DgPF<4>::v > 0) ||
+                       (l == 5 && train::DgPF<5>::v > 0);
+  const dim3 g(persist ? std::max(1, std::min(tiles, train::kDgGrid / std::max(1, M))) : tiles, 1, M);
   switch (l) {
     case 1: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::dgrad_kernel<1, MB>), g, dim3(256), lds_dgrad(), st, A, Am); break;
     case 2: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::dgrad_kernel<2, MB>), g, dim3(256), lds_dgrad(), st, A, Am); break;
