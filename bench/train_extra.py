@@ -11,7 +11,7 @@ synthetic (60, 4) windows:
 * ``single_b1024``: one model, the graphed step at the reference's batch size;
 * ``single_b8192``: one model at batch 8192 (the per-step work of 8 members);
 * ``members8_b1024``: 8 ensemble members, each at batch 1024, as member-batched graphs
-  (``GraphedEnsembleStep``, 4 groups of 2 on their own HIP streams: ``training/trainer.py:_fit_batched``);
+  (``GraphedEnsembleStep``, the trainer's groups (2 of 4) on their own HIP streams: ``training/trainer.py:_fit_batched``);
 * ``loss_parity``: the same 10 steps (same init, batches, dropout masks) on the HIP kernels and on the
   fp32 PyTorch autograd step (``training/step.py`` backend "torch"): per-step relative loss deviation.
 """
@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import os
 import time
+from typing import Optional
 
 
 def _timeit(torch, fn, steps: int, warmup: int) -> float:
@@ -32,7 +33,7 @@ def _timeit(torch, fn, steps: int, warmup: int) -> float:
     return (time.perf_counter() - t0) / steps
 
 
-def measure(dev, seed: int = 2025, steps: int = 50, warmup: int = 5, members: int = 8, groups: int = 4,
+def measure(dev, seed: int = 2025, steps: int = 50, warmup: int = 5, members: int = 8, groups: Optional[int] = None,
             batch: int = 1024, big_batch: int = 8192, parity_steps: int = 10) -> dict:
     import torch
 
@@ -59,6 +60,8 @@ def measure(dev, seed: int = 2025, steps: int = 50, warmup: int = 5, members: in
     out["single_b8192"] = {"batch": big_batch, "ms_per_step": round(t * 1e3, 4), "windows_per_s": round(big_batch / t, 1)}
 
     ms = [AlarconCNN1D(seed=seed + 10 + i, device=dev) for i in range(members)]
+    if groups is None:  # the trainer's member-batched grouping (training/trainer.py:ENSEMBLE_GROUPS)
+        from uncertaintyquantification_sleepapnea_1dcnn_amd.training.trainer import ENSEMBLE_GROUPS as groups
     ng = max(1, min(groups, members))
     parts = [list(range(members))[i::ng] for i in range(ng)]
     ens = [train_ops.GraphedEnsembleStep([ms[i] for i in p], batch) for p in parts]

@@ -137,13 +137,16 @@ def fit_concurrent(models: List, x, y, streams: Optional[List] = None, batched: 
     return hist
 
 
-ENSEMBLE_GROUPS = 4  # member groups per batch size, one batched graph + HIP stream each (profiles/x3_epilogue_ab_r3.md)
+# member groups per batch size, one batched graph + HIP stream each (profiles/x3_epilogue_ab_r3.md); 2 since
+# the persistent dgrad / 8-wave wgrad (8 members x batch 1024: 4 groups 3.90 ms, 2 groups 3.73-3.80, 1 group
+# 3.83, 8 groups 4.23; tools/probes/train_groups.sh, profiles/train_step_r5.md)
+ENSEMBLE_GROUPS = 2
 
 
 def _fit_batched(models: List, x, y, per_cbs, **fit_kwargs) -> List[History]:
     """fit_concurrent's member-batched mode: the members' fit_steps generators hand their batches out
     (``external_step``); each round the live members of one batch size are split into up to
-    ``APNEAUQ_ENSEMBLE_GROUPS`` (default 4) groups, each run as one GraphedEnsembleStep replayed on its
+    ``APNEAUQ_ENSEMBLE_GROUPS`` (default ENSEMBLE_GROUPS) groups, each run as one GraphedEnsembleStep replayed on its
     own HIP stream (the groups' latency-bound phases overlap: 8 members 1.67 M -> 1.80 M windows/s with
     4 groups of 2).  A group's steps, gathers and metric updates all run on its stream: no joins."""
     import os
