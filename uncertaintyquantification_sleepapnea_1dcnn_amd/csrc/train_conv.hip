@@ -988,13 +988,15 @@ __global__ __launch_bounds__(kThreads) void head_kernel(Args A_, const Args* __r
 // dgrad of block l (l >= 1): dA_{l-1} = conv^T(dZ_l, W_l);  epilogue -> dY_{l-1} = dA * mask_{l-1}
 // plus the backward sums of block l-1.
 // ------------------------------------------------------------------------------------------------
-// dgrad: prefetch the epilogue's R_{l-1} loads ahead of the conv on blocks 2-5 (block 6: registers)
-template <int l> struct DgPre { static constexpr bool v = l >= 1 && l <= 4; };
+// dgrad: prefetch the epilogue's R_{l-1} loads ahead of the conv (every block; block 6 has had the
+// registers for it since its staging became DzStager: dgrad<5> b8192 -0.6 %, 8 members -0.5..-1.9 %)
+template <int l> struct DgPre { static constexpr bool v = l >= 1 && l <= 5; };
 // Persistent dgrad: a workgroup runs row tiles tile, tile + grid, ...; the first DgPF<l>::v staging items
 // per thread of the NEXT tile (R_l and dY_l rows, 8 channels each) are loaded into registers before this
 // tile's conv, so their latency hides under the MFMAs (the rest load at staging time, as before).
-// Sized to the registers each block leaves (tools/kernel_resources.py: no spills).
-template <int l> struct DgPF { static constexpr int v = l == 1 ? 8 : l == 2 ? 2 : l == 4 ? 12 : l == 5 ? 7 : 0; };
+// Sized to the registers each block leaves with DgPre (tools/kernel_resources.py: no spills); trading
+// DgPre for a deeper staging prefetch measured slower (profiles/train_step_r5.md).
+template <int l> struct DgPF { static constexpr int v = l == 1 ? 8 : l == 2 ? 2 : l == 4 ? 12 : 0; };
 // workgroups of a single-model dgrad launch: two per CU (larger batches loop over their tiles)
 constexpr int kDgGrid = 512;
 
