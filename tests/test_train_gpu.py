@@ -38,7 +38,9 @@ def _rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
-@pytest.mark.parametrize("n", [64, 37])
+# 2563: 1282 row tiles, so the persistent dgrad workgroups (at most 512) run 2-3 tiles each with the
+# next tile's staging prefetched, and the 8-wave wgrad several row tiles per workgroup; odd: a half tile
+@pytest.mark.parametrize("n", [64, 37, 2563])
 def test_hip_train_step_matches_autograd(n):
     _ext.require()
     dev = torch.device("cuda")
@@ -249,26 +251,30 @@ def test_bf16_hip_training_matches_fp32_training(monkeypatch, deterministic):
 def _member_steps(x, y, batched: bool):
     ms = [AlarconCNN1D(seed=10 + i, device="cuda") for i in range(3)]
     ls = [[], [], []]
+    b = x.shape[2]
     if batched:
-        st = train_ops.GraphedEnsembleStep(ms, 64)
+        st = train_ops.GraphedEnsembleStep(ms, b)
         for s in range(4):
             out = st([x[i, s] for i in range(3)], [y[i, s] for i in range(3)])
             for i, (loss, p) in enumerate(out):
                 ls[i].append(float(loss))
-                assert p.shape == (64,) and bool(((p > 0) & (p < 1)).all())
+                assert p.shape == (b,) and bool(((p > 0) & (p < 1)).all())
     else:
         ls = [[float(m.train_step(x[i, s], y[i, s])) for s in range(4)] for i, m in enumerate(ms)]
     return ms, ls
 
 
-def test_member_batched_step_matches_single_graphs(deterministic):
+# batch 1100: 550 row tiles per member, so the member-batched persistent dgrad (512 / 3 workgroups per
+# member) and the single-model one (512) loop over different tile sets per workgroup
+@pytest.mark.parametrize("batch", [64, 1100])
+def test_member_batched_step_matches_single_graphs(deterministic, batch):
     """GraphedEnsembleStep (one member-batched launch per layer for 3 members) IS each member's own
     graphed step: in deterministic mode 4 steps on member-specific batches give bitwise-identical
     losses, weights and BN statistics, and the host / device counters advance alike.  Atomic mode:
     the first-step losses agree (later steps inherit the atomics' summation order)."""
     g = torch.Generator().manual_seed(8)
-    x = torch.randn(3, 4, 64, 60, 4, generator=g).cuda()
-    y = (torch.rand(3, 4, 64, generator=g) < 0.4).float().cuda()
+    x = torch.randn(3, 4, batch, 60, 4, generator=g).cuda()
+    y = (torch.rand(3, 4, batch, generator=g) < 0.4).float().cuda()
     single, ls = _member_steps(x, y, False)
     batched, lb = _member_steps(x, y, True)
     for i in range(3):
