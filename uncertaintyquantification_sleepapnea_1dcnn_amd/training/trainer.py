@@ -147,8 +147,9 @@ def _fit_batched(models: List, x, y, per_cbs, **fit_kwargs) -> List[History]:
     """fit_concurrent's member-batched mode: the members' fit_steps generators hand their batches out
     (``external_step``); each round the live members of one batch size are split into up to
     ``APNEAUQ_ENSEMBLE_GROUPS`` (default ENSEMBLE_GROUPS) groups, each run as one GraphedEnsembleStep replayed on its
-    own HIP stream (the groups' latency-bound phases overlap: 8 members 1.67 M -> 1.80 M windows/s with
-    4 groups of 2).  A group's steps, gathers and metric updates all run on its stream: no joins."""
+    own HIP stream (the groups' latency-bound phases overlap: round 3, 8 members 1.67 M -> 1.80 M windows/s
+    with 4 groups of 2; round 5, 2 groups of 4 2.17 M).  A group's steps, gathers and metric updates all run
+    on its stream: no joins."""
     import os
 
     from ..ops import train_ops
