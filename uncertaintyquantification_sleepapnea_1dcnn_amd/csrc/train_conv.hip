@@ -545,6 +545,13 @@ constexpr int kFwdPD = 1;
 // at once (ActStager): blocks 3 and 6 spilled 22 / 44 VGPRs with one batch; split, neither spills and
 // the batch-BN MC-Dropout chunk is ~2 % faster (profiles/batch_bn_fwd_r2.md, session 3).
 template <int l> struct FwdStageSplit { static constexpr bool v = l == 2 || l == 5; };
+// Large training launches (more row tiles than kFwdTrainGrid workgroups: batch >= 2048, or the
+// member-batched step) run the PF instantiation of the forward: kFwdTrainGrid persistent workgroups over
+// contiguous tile ranges, the first FwdPF<l>::v input-row loads per thread of the NEXT tile issued before
+// this tile's conv (registers each block leaves: 8 of 8 on block 2, 14 of 14 on block 4).  Batch 1024 (one
+// tile per workgroup anyway) keeps the plain instantiation: the PF one measured +1 % there.
+template <int l> struct FwdPF { static constexpr int v = l == 1 ? 8 : l == 3 ? 14 : 0; };
+constexpr int kFwdTrainGrid = 512;
 
 // wave tilings (WM, WN) per output-channel count
 template <int COUT> struct Tiling;
@@ -569,7 +576,7 @@ __device__ __forceinline__ void atomic_channel_sums(double* dst, int co0, const 
 // ------------------------------------------------------------------------------------------------
 // Forward of block l:  R_l = relu(conv(A_{l-1}) + b), fwd sums of R_l per stats group.
 // ------------------------------------------------------------------------------------------------
-template <int l, bool MB>
+template <int l, bool MB, bool PFT = false>
 __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A_, const Args* __restrict__ Am) {
   const MbPos pos = mb_pos<MB>();
   const Args& A = member_args<MB>(A_, Am, pos);
@@ -640,6 +647,11 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A_, const Args* _
   int gaff = -1;  // stats group whose BN affine (of block l-1) is in prm
   // input staging: loads of a tile's rows, then A = dropout(BN(R)) decoded into LDS
   ActStager<(l > 0 ? l - 1 : 0), l == 1> stg;
+  constexpr int NPF = !PFT || l == 0 || FwdStageSplit<l>::v ? 0
+                      : (FwdPF<l>::v < decltype(stg)::NK ? FwdPF<l>::v : decltype(stg)::NK);
+  if constexpr (NPF > 0) {
+    if (t_begin < t_end) stg.template load<0, NPF>(A, kR * t_begin, hash_in);
+  }
   for (int tile = t_begin; tile < t_end; ++tile) {
     APNEAUQ_DASSERT(2 * tile < A.B + 1 && blockDim.x == kThreads);
     const int row0 = kR * tile;                        // first staged row (global PL index)
@@ -663,12 +675,18 @@ __global__ __launch_bounds__(kThreads, 2) void fwd_kernel(Args A_, const Args* _
         stg.template store<0, H>(A, act, row0, prm, prm + 512, g0, hash_in);
         stg.template load<H, NK>(A, row0, hash_in);
         stg.template store<H, NK>(A, act, row0, prm, prm + 512, g0, hash_in);
+      } else if constexpr (NPF > 0) {  // items [0, NPF) were loaded during the previous tile's conv
+        stg.template load<NPF, decltype(stg)::NK>(A, row0, hash_in);
+        stg.store(A, act, row0, prm, prm + 512, g0, hash_in);
       } else {
         stg.load(A, row0, hash_in);
         stg.store(A, act, row0, prm, prm + 512, g0, hash_in);
       }
     }
     __syncthreads();
+    if constexpr (NPF > 0) {
+      if (tile + 1 < t_end) stg.template load<0, NPF>(A, kR * (tile + 1), hash_in);
+    }
     // epilogue of one 16 x 16 accumulator tile: bias + ReLU -> bf16 LDS tile (rows outside the batch /
     // pad rows: 0).  Only the row tiles holding t = 48..63 (pad rows on lanes m >= 12) and the batch's
     // last tile need the select.
@@ -1656,18 +1674,36 @@ int train_det_floats(int B) { return (int)(det_scratch_base(B) + 2LL * train::kD
 // Kernel launches shared by the single-model path (MB = false: by-value Args, Am = nullptr, M = 1)
 // and the member-batched path (MB = true: gridDim.z = M members, Args from the device array Am).
 template <bool MB>
-static hipError_t fwd_launch(const Args& A, const Args* Am, int M, int l, int grid, hipStream_t st) {
+static hipError_t fwd_launch(const Args& A, const Args* Am, int M, int l, int grid, hipStream_t st, bool pf = false) {
   const dim3 g(grid, 1, M);
   switch (l) {
     case 0: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::fwd_kernel<0, MB>), g, dim3(256), lds_fwd(), st, A, Am); break;
-    case 1: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::fwd_kernel<1, MB>), g, dim3(256), lds_fwd(), st, A, Am); break;
+    case 1:
+      if (pf)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(train::fwd_kernel<1, MB, true>), g, dim3(256), lds_fwd(), st, A, Am);
+      else
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(train::fwd_kernel<1, MB>), g, dim3(256), lds_fwd(), st, A, Am);
+      break;
     case 2: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::fwd_kernel<2, MB>), g, dim3(256), lds_fwd(), st, A, Am); break;
-    case 3: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::fwd_kernel<3, MB>), g, dim3(256), lds_fwd(), st, A, Am); break;
+    case 3:
+      if (pf)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(train::fwd_kernel<3, MB, true>), g, dim3(256), lds_fwd(), st, A, Am);
+      else
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(train::fwd_kernel<3, MB>), g, dim3(256), lds_fwd(), st, A, Am);
+      break;
     case 4: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::fwd_kernel<4, MB>), g, dim3(256), lds_fwd(), st, A, Am); break;
     case 5: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::fwd_kernel<5, MB>), g, dim3(256), lds_fwd(), st, A, Am); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+// the PF forward (FwdPF) for a training launch of M members x B samples: persistent workgroups, only
+// when the tiles outnumber kFwdTrainGrid (never in deterministic mode: its moment partials are per
+// workgroup of the fwd_grid layout, which the member-batched step must share with the single one)
+static bool fwd_pf(const Args& A, int M, int l) {
+  const bool has = (l == 1 && train::FwdPF<1>::v > 0) || (l == 3 && train::FwdPF<3>::v > 0);
+  return has && A.det == nullptr && A.groups == 1 && !A.shared0 && (long long)((A.B + 1) / 2) * M > train::kFwdTrainGrid;
 }
 
 template <bool MB>
@@ -1700,6 +1736,7 @@ hipError_t train_launch_fwd(const Args& A, int l, hipStream_t st) {
     return det_reduce(A, grid, 2 * cc, det_dst(A.L[l].st, 2 * cc, 1), st);
   }
   // persistent forward: each workgroup over a contiguous tile range
+  if (fwd_pf(A, 1, l)) return fwd_launch<false>(A, nullptr, 1, l, train::kFwdTrainGrid, st, true);
   return fwd_launch<false>(A, nullptr, 1, l, grid, st);
 }
 
@@ -1856,6 +1893,8 @@ hipError_t train_launch_mb(const Args& A0, const Args* Am, int M, int op, int la
   if (det && A0.tab != nullptr) return hipErrorInvalidValue;
   switch (op) {
     case 0: {
+      if (fwd_pf(A0, M, layer))
+        return fwd_launch<true>(A0, Am, M, layer, std::max(1, train::kFwdTrainGrid / M), st, true);
       const hipError_t e = fwd_launch<true>(A0, Am, M, layer, fwd_grid(A0.B), st);
       if (e != hipSuccess || !det) return e;
       return det_reduce_mb(A0, Am, M, 0, layer, fwd_grid(A0.B), 2 * train::C[layer + 1], st);
