@@ -370,3 +370,25 @@ def test_step_node_kernels():
     ws.pack_zero()
     assert all(torch.equal(a, b) for a, b in zip(ref, list(ws.wf) + list(ws.wd[1:])))
     assert all(bool((t == 0).all()) for t in ws.accumulators())
+
+
+def test_large_batch_prefetch_paths_match_deterministic(deterministic):
+    """Batch 3000 (1500 row tiles): the atomic-mode step runs the prefetching persistent forward (FwdPF,
+    512 workgroups over tile ranges), the deterministic one the plain one-tile-per-workgroup forward; both
+    run the persistent dgrad and the 8-wave wgrad.  Same weights, masks and inputs: the same loss and
+    gradients up to the summation order of the atomics."""
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(30)
+    x = torch.randn(3000, 60, 4, generator=g).to(dev)
+    y = (torch.rand(3000, generator=g) > 0.5).float().to(dev)
+    out = {}
+    for det in (True, False):
+        train_ops.set_deterministic(det)
+        m = AlarconCNN1D(seed=6, device=dev)
+        m.optimizer.learning_rate = 0.0
+        loss, _ = train_ops.train_step(m, x, y)
+        out[det] = (float(loss), m._train_ws.grad.clone())
+    (ld, gd), (la, ga) = out[True], out[False]
+    assert abs(la - ld) < 1e-4 * abs(ld), (la, ld)
+    assert _rel(ga, gd) < 1e-2, _rel(ga, gd)
+    assert torch.nn.functional.cosine_similarity(ga, gd, dim=0).item() > 0.9999
