@@ -126,11 +126,18 @@ def test_fp32_training_loss_history_matches_torch_backend(monkeypatch):
     Two fp32 implementations that differ only in summation order drift apart under Adam (a parameter
     whose gradient is near zero flips the sign of its lr-sized update), so the tolerance is calibrated
     in the same run: fp32 autograd with MIOpen's convolutions against fp32 autograd with PyTorch's own
-    (im2col + GEMM).  Every epoch, the HIP history's relative distance to the nearer of the two fp32
-    histories must be within 2x the largest fp32-vs-fp32 drift seen up to that epoch, floored at 1e-4
-    for epoch 1 and 1e-3 after (the drift wanders: measured 4e-5 .. 5e-3 over the 10 epochs; the HIP
-    run's atomics make it a third summation order, as close to either as they are to each other).
-    A reduced-precision path (bf16 products: ~1e-2 relative from the first steps) fails it."""
+    (im2col + GEMM).  The HIP run's atomics make it a third summation order.
+
+    * Epoch 1 (72 steps, before the trajectories fan out) is the precision check: the HIP loss within
+      2x the fp32-vs-fp32 distance, floored at 1e-4 relative.  A reduced-precision path (bf16 products:
+      ~1e-2 relative from the first steps) fails it by two orders of magnitude.
+    * Epochs 2-10 check that the fit loop stays on an fp32 trajectory: within 4x the largest
+      fp32-vs-fp32 drift seen so far, floored at 1.5e-3.  The drift is chaotic, not a rounding bound:
+      measured 4e-5 .. 5.3e-3 between the two PyTorch runs, and the HIP run's distance to the nearer one
+      3.9e-3 at epoch 6 of one driver run where the torch pair happened to sit at 1.8e-3 -- a 2x
+      envelope failed there (GPUTEST_r05), so a bound on one fp32-vs-fp32 sample of a chaotic
+      quantity needs this margin.  An rtol of 1e-3 with no floor is below what two fp32 PyTorch
+      backends achieve against each other, so it cannot be asked of a third."""
     _ext.require()
     # the torch side in true fp32 (no TF32-style reduced-precision convolutions / matmuls)
     monkeypatch.setattr(torch.backends.cudnn, "allow_tf32", False)
@@ -150,10 +157,11 @@ def test_fp32_training_loss_history_matches_torch_backend(monkeypatch):
                                     verbose=0).history["loss"])
     hip, ref, alt = hist["hip"], hist["torch"], hist["torch_gemm"]
     assert len(hip) == 10 and hip.min() >= 0.05, hip
-    floor = np.where(np.arange(10) == 0, 1e-4, 1e-3)
-    env = np.maximum.accumulate(np.maximum(np.abs(alt - ref) / ref, floor))
+    drift = np.abs(alt - ref) / ref
     near = np.minimum(np.abs(hip - ref), np.abs(hip - alt)) / ref
-    assert np.all(near <= 2.0 * env), (hip, ref, alt)
+    assert near[0] <= 2.0 * max(drift[0], 1e-4), (near, drift)
+    env = np.maximum.accumulate(np.maximum(drift, 1.5e-3))
+    assert np.all(near[1:] <= 4.0 * env[1:]), (near, drift, hip, ref, alt)
 
 
 @pytest.mark.parametrize("name", ["pooled", "single30"])
