@@ -279,13 +279,18 @@ def run(a):
 
     fp32_paths = None
     if not cpu and not a.no_train:  # the reference-precision paths of the other architectures + fp32 training
+        # single-device numbers: rank 0 alone, between barriers (the other ranks wait), distributed=False
         from bench import fp32_micro
 
-        torch.cuda.empty_cache()
-        fp32_paths = fp32_micro.measure(reps=2, steps=20, precisions=("fp32",))
-        fp32_paths["note"] = ("pooled ensemble_cnn members (MaxPool1D after blocks 1-5) at precision fp32: DE / "
-                              "running-BN MCD on the fused fp16x3 kernel, batch-BN MCD layer-wise; fp32 training "
-                              "steps (train_precision='fp32') of the reference and pooled CNN; best of 2")
+        pdist.barrier()
+        if rank == 0:
+            torch.cuda.empty_cache()
+            fp32_paths = fp32_micro.measure(reps=2, steps=20, precisions=("fp32",))
+            fp32_paths["note"] = ("pooled ensemble_cnn members (MaxPool1D after blocks 1-5) at precision fp32: DE / "
+                                  "running-BN MCD on the fused fp16x3 kernel, batch-BN MCD layer-wise; fp32 training "
+                                  "steps (train_precision='fp32') of the reference and pooled CNN; best of 2; "
+                                  "measured on rank 0 alone (single device, no collectives)")
+        pdist.barrier()
 
     macs = SPEC.forward_macs()
     devices = pdist.gather_device_ids()  # collective: every rank

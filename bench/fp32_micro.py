@@ -10,7 +10,9 @@
 * one training step (batch 1024, Keras semantics, HIP graph) of the reference CNN and of the pooled CNN,
   ``train_precision="fp32"`` (``ops/generic_train.py`` fp16x3 kernels) vs ``"bf16"``.
 
-Random-init weights, synthetic (60, 4) windows; best of ``reps`` timings after one warm-up call.
+Random-init weights, synthetic (60, 4) windows; best of ``reps`` timings after one warm-up call.  Always
+the single-device path (``distributed=False``): under ``torchrun`` ``bench.py`` calls it on rank 0 only,
+between barriers, so the numbers are the fused kernels' own and carry no collectives.
 """
 import argparse
 import dataclasses
@@ -48,11 +50,11 @@ def measure(windows: int = 16384, members: int = 8, passes: int = 50, reps: int 
     out = {"windows": windows, "members": members, "passes": passes, "pooled": {}, "train_b1024": {}}
     for prec in precisions:
         ms = [AlarconCNN1D(spec=POOLED, seed=10 + i, device="cuda", precision=prec) for i in range(members)]
-        r = {"de_ms": _best(lambda: U.deep_ensembles_predict(ms, xd, as_numpy=False), reps),
+        r = {"de_ms": _best(lambda: U.deep_ensembles_predict(ms, xd, as_numpy=False, distributed=False), reps),
              "mcd_batch_ms": _best(lambda: U.mc_dropout_predict(ms[0], xd, n_pred=passes, bn_mode="batch", seed=1,
-                                                               as_numpy=False), reps),
+                                                               as_numpy=False, distributed=False), reps),
              "mcd_running_ms": _best(lambda: U.mc_dropout_predict(ms[0], xd, n_pred=passes, bn_mode="running",
-                                                                 seed=1, as_numpy=False), reps)}
+                                                                 seed=1, as_numpy=False, distributed=False), reps)}
         out["pooled"][prec] = r
         del ms
     xb = torch.randn(1024, 60, 4, generator=g).cuda()

@@ -168,3 +168,20 @@ def test_graph_bound_key_tracks_optimizer_scalars():
     assert train_ops._same_bound(k1, train_ops.bound_key(m))
     m.optimizer.learning_rate = 5e-4
     assert not train_ops._same_bound(k1, train_ops.bound_key(m))
+
+
+def test_fused_input_copy_only_takes_matching_device_batches():
+    """the graphed step's fused input copy (ops/train_ops.py ``_inputs_direct``) reads the batch
+    in place, so it applies only to fp32 contiguous (n, 60, C_in) windows and (n,) labels on the
+    workspace's own device; a CPU batch, a wrong channel count or shape falls back to ``copy_``."""
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.ops.train_ops import _inputs_direct
+
+    dev = torch.device("cpu")
+    x, y = torch.zeros(8, 60, 4), torch.zeros(8)
+    assert not _inputs_direct([x], [y], 8, dev, 4)  # CPU tensors are never read by the kernel
+    meta = torch.device("meta")
+    xm, ym = torch.zeros(8, 60, 4, device=meta), torch.zeros(8, device=meta)
+    assert not _inputs_direct([xm], [ym], 8, dev, 4)  # not a GPU tensor
+    assert not _inputs_direct([x[:, :, :3].contiguous()], [y], 8, dev, 4)
+    assert not _inputs_direct([x], [y[:7]], 8, dev, 4)
+    assert not _inputs_direct([x.double()], [y], 8, dev, 4)

@@ -130,6 +130,31 @@ def test_mask_side_matches_reference(monkeypatch, sign, bn):
         assert (ph[t].cpu() - r).abs().max().item() <= BOUND
 
 
+def test_de_chunking_and_float64_large():
+    """the Deep-Ensemble path picks its fp16 prescale per member and block from the whole
+    launch's sums of squares (ops/x3.py _predict_members), so a window's last bits may depend on the
+    windows sharing its chunk.  At 4096 windows (bound overshoot ~2^9 of a window's own maximum) the
+    window-chunked result (8 chunks) stays within 1e-6 of the one-launch result, and both within the
+    usual bounds of the fp32 reference and the float64 oracle."""
+    _ext.require()
+    dev = torch.device("cuda")
+    n = 4096
+    ps = [_params(300 + m, dev) for m in range(2)]
+    model = x3.X3Model(SPEC, ps)
+    x = _x(n, 99)
+    one = x3.forward_running(model, x.to(dev))
+    chunked = x3.forward_running(model, x.to(dev), max_samples=2 * (n // 8))
+    assert one.shape == chunked.shape == (2, 1, n)
+    assert (one - chunked).abs().max().item() <= 1e-6
+    for m in range(2):
+        r32, _ = _ref(ps[m], x)
+        r64, _ = _ref(ps[m], x, dtype=torch.float64)
+        ref_err = (r32.double() - r64).abs().max().item()
+        for got in (one, chunked):
+            assert (got[m, 0].cpu() - r32).abs().max().item() <= BOUND
+            assert (got[m, 0].cpu().double() - r64).abs().max().item() <= max(4 * ref_err, 2e-6)
+
+
 def test_mcd_batch_chunked_equals_unchunked():
     _ext.require()
     dev = torch.device("cuda")

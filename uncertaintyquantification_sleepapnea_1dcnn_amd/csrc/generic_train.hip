@@ -60,14 +60,22 @@ __device__ __forceinline__ bool slot_pair_sums(const float* st, int nslots, int 
 // kRange consecutive slots (fixed order, fp64) and parks the two sums in the range's first two slots
 // (their fp32 words hold the fp64 bits: the raw table is dead after the finalize), then the finalize
 // adds the ranges in order.  One 16-channel block per C / 16 with a serial pass over 15 k slots took
-// ~130 us per call.
+// ~130 us per call.  The packed sums take four words per channel = two slots, so no range may hold a
+// single slot: a one-slot tail joins the range before it (the last range runs to nslots; see
+// partial_ranges).
 constexpr int kRange = 64;
+
+__host__ __device__ inline int partial_ranges(int nslots) {
+  const int r = (nslots + kRange - 1) / kRange;
+  return (nslots % kRange == 1 && r > 1) ? r - 1 : r;
+}
 
 __global__ __launch_bounds__(256) void slot_partial_kernel(float* st, int nslots, int C) {
   __shared__ double red[2][256];
   const int chl = threadIdx.x & 15, lane = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + chl;
-  const int s0 = blockIdx.y * kRange, s1e = min(nslots, s0 + kRange);
+  const int s0 = blockIdx.y * kRange, s1e = blockIdx.y + 1 == gridDim.y ? nslots : s0 + kRange;
+  APNEAUQ_DASSERT(s1e - s0 >= 2 && s1e <= nslots);
   double a = 0.0, b = 0.0;
   if (c < C) {
     for (int s = s0 + lane; s < s1e; s += 16) {
@@ -391,7 +399,7 @@ hipError_t launch_gt_bn_finalize(const float* st, int nslots, int C, float inv_c
                                  const float* beta, float eps, float momentum, float* mmean, float* mvar, int update,
                                  float* bn, hipStream_t stream) {
   if (nslots >= 4 * gtrain::kRange) {
-    const int ranges = (nslots + gtrain::kRange - 1) / gtrain::kRange;
+    const int ranges = gtrain::partial_ranges(nslots);
     hipLaunchKernelGGL(gtrain::slot_partial_kernel, dim3((C + 15) / 16, ranges), dim3(256), 0, stream,
                        const_cast<float*>(st), nslots, C);
     hipLaunchKernelGGL(gtrain::bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, stream, st, ranges, C, inv_count,

@@ -253,6 +253,9 @@ def _forward(ws: GenericTrainWorkspace, n: int, global_n: int, seed: int, pass_i
                  ws.rs[l], 2 * ws.pads[l], ws.det)
         if sync is not None:
             sync(ws.st[l])
+        # consumes ws.st[l]: a large slot table (deterministic mode) is summed in place, its first slots
+        # overwritten by packed fp64 range sums (csrc/generic_train.hip slot_partial_kernel), so nothing
+        # may read ws.st[l] after this call
         o.gt_bn_finalize(ws.st[l], cout, 1.0 / (global_n * L), v[f"batchnorm_{i}/gamma"], v[f"batchnorm_{i}/beta"],
                          spec.bn_epsilon, spec.bn_momentum, v[f"batchnorm_{i}/moving_mean"],
                          v[f"batchnorm_{i}/moving_variance"], bool(update_moving), ws.bn[l])

@@ -209,11 +209,14 @@ class TrainWorkspace:
         _ext.ops().gt_pack_zero(*self.pack_args(), self.accumulators())
 
 
-def _inputs_direct(xs, ys, n: int) -> bool:
-    """The fused input copy applies: fp32 contiguous (n, 60, C) windows and (n,) labels."""
+def _inputs_direct(xs, ys, n: int, dev: torch.device, cin: int) -> bool:
+    """The fused input copy applies: fp32 contiguous (n, 60, cin) windows and (n,) labels, already on the
+    workspace's device (the kernel reads them in place).  Anything else -- CPU batches, another device,
+    another channel count -- takes the ``copy_`` path, which moves or rejects it."""
     return all(x.dtype == torch.float32 and x.is_contiguous() and x.dim() == 3 and x.shape[0] == n and
-               x.shape[1] == 60 for x in xs) and \
-        all(y.dtype == torch.float32 and y.is_contiguous() and y.numel() == n for y in ys)
+               x.shape[1] == 60 and x.shape[2] == cin and x.is_cuda and x.device == dev for x in xs) and \
+        all(y.dtype == torch.float32 and y.is_contiguous() and y.numel() == n and y.is_cuda and y.device == dev
+            for y in ys)
 
 
 def _call(ctx, op, layer=0, flag=0, pass_base=-1, device=0):
@@ -428,7 +431,7 @@ class GraphedTrainStep:
         if self._state() != self._dev_state:
             self._sync_counters()
         yf = y.reshape(-1)
-        if _inputs_direct([x], [yf], self.batch):  # both copies in one launch
+        if _inputs_direct([x], [yf], self.batch, self.ws.x.device, self.ws.ch[0]):  # both copies in one launch
             _ext.ops().train_inputs([x], [yf], [self.ws.x[HALO:]], [self.ws.y], SR)
         else:
             self.x_in.copy_(x)
@@ -553,7 +556,7 @@ class GraphedEnsembleStep:
             self._sync_counters()
         yfs = [y.reshape(-1) for y in ys]
         M = len(self.models)
-        if _inputs_direct(xs, yfs, self.batch):  # every member's x and y in one launch per 32 members
+        if _inputs_direct(xs, yfs, self.batch, self.ws[0].x.device, self.ws[0].ch[0]):  # one launch per 32 members
             for g0 in range(0, M, 32):
                 _ext.ops().train_inputs(list(xs[g0:g0 + 32]), yfs[g0:g0 + 32],
                                         [ws.x[HALO:] for ws in self.ws[g0:g0 + 32]],

@@ -356,7 +356,12 @@ def forward_running(model: X3Model, x: torch.Tensor, n_pass: int = 1, dropout: b
     G > 1 members run as one launch per layer (Deep Ensemble predict, ``uq_techniques.py:29``);
     ``dropout=True`` is standard MC Dropout with n_pass passes (one model).  Windows are independent
     here, so sets larger than the activation budget (``max_samples`` window x group rows) run in window
-    chunks (masks are keyed by the global window id: the result does not depend on the chunking)."""
+    chunks.  With ``dropout=True`` the result does not depend on the chunking, bitwise (masks are keyed
+    by the global window id and the range-safe prescale is per sample).  The Deep-Ensemble path
+    (``dropout=False``, :func:`_predict_members`) picks its prescale per member and block from the whole
+    launch's sums of squares, so a window's fp16 split -- and with it the last bits of its result -- can
+    depend on the other windows of its chunk: results of different chunkings agree to ~1e-7 in
+    probability, not bitwise (``tests/test_x3_gpu.py::test_de_chunking_and_float64_large``)."""
     x = x.to(device=model.device, dtype=torch.float32).contiguous()
     n = x.shape[0]
     groups = (n_pass if dropout else model.G) if n > 0 else 1
@@ -419,7 +424,16 @@ def _predict_members(model: X3Model, ws: "_Workspace", x: torch.Tensor, G: int, 
     in one launch per layer.  The staged activations' range-safe prescale is one power of two per member
     and block, bounded by the block output's sums of squares (max R_c <= sqrt(sum R_c^2): the moment
     epilogue of the batch-statistics kernels, used here for the bound only) -- the layer kernels of the
-    MC-Dropout phase, no per-sample maximum tracking (2.5 % of the phase)."""
+    MC-Dropout phase, no per-sample maximum tracking (2.5 % of the phase).
+
+    Tolerance, not invariance: the bound is taken over every row of the launch, so it can overshoot a
+    window's own maximum by up to sqrt(rows) (~2^10 at 16384 windows).  An exact power of two commutes
+    with fp16 rounding while both halves stay normal; what the overshoot changes is that the lo halves of
+    a window's smallest activations (below ~2^-14 of the chunk's bound) become fp16 subnormals and lose
+    their last bits.  Those activations are < 2^-10 of the largest term of their dot products, so the
+    effect on a probability is ~1e-7 (measured: chunked vs one launch, and against float64 at 4096
+    windows, ``tests/test_x3_gpu.py::test_de_chunking_and_float64_large``); the per-sample prescale of the
+    dropout path is bitwise chunk-invariant instead."""
     spec, o = model.spec, _ops()
     n = x.shape[0]
     per_member = G > 1
