@@ -1817,9 +1817,11 @@ static void wg_launch(const Args& A, const Args* Am, int M, hipStream_t st) {
   if (A.wpart != nullptr) {
     const int kcc = train::KS[l] * train::C[l] * train::C[l + 1];
     const int s4 = (kcc + train::C[l + 1]) / 4;
-    // threads per column: enough columns x row-group splits to fill ~1024 workgroups' worth of lanes
+    // threads per column: enough columns x row-group splits to fill ~1024 workgroups' worth of lanes, at
+    // least 8 row groups per thread (one batch of 8 loads in flight).  Block 1 (928 float4 columns, 512
+    // row groups at batch 1024): J 16 -> 64, 58 -> 232 workgroups, one load batch per thread instead of 4
     int J = 1;
-    while (J < 16 && rgs >= 16 * J && (long long)s4 * J < 256LL * 1024) J *= 2;
+    while (J < 64 && rgs >= 8 * (2 * J) && (long long)s4 * J < 256LL * 1024) J *= 2;
     const int blocks = std::min(2048, (s4 * J + 255) / 256);
     // side job: block l-1's backward rows of the parameter table (bst[l-1] is complete after dgrad<l>,
     // which ran before this wgrad) for dgrad<l-1> / wgrad<l-1>
