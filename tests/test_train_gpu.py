@@ -187,6 +187,53 @@ def test_graphed_step_overlap_matches_single_stream(monkeypatch):
         assert rel < 5e-3, (name, rel)
 
 
+@pytest.mark.parametrize("graph,batch", [("1", 512), ("0", 384), ("1", 4100)])
+def test_fused_reductions_match_separate_launches(monkeypatch, graph, batch):
+    """The fused step (train_ops.FUSED_REDUCE: wgrad_l's partials reduced inside dgrad_{l-1}, those of
+    wgrad_1 / wgrad_0 next to the BN finalize, the table's backward rows written by wgrad's workgroup 0)
+    computes the separate launches' step: same loss and every gradient tensor within the atomics' order
+    noise (a skipped or misplaced reduction leaves a tensor stale or zero: O(1) error).  Step 2 runs
+    from identical states (the fused model gets the other's weights, statistics and Adam moments) so a
+    table row left stale from step 1 would show.  (Without the copy, Adam's ~lr first moves of
+    near-zero gradient elements whose sign the order noise flips move block 1's step-2 gradient by up to
+    7 %.)  Batch 4100 runs the large-batch row grouping and a partial last row tile."""
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.data.synthetic import synthetic_windows
+
+    x, y, _ = synthetic_windows(batch, seed=11)
+    x = torch.as_tensor(x, dtype=torch.float32).cuda()
+    y = torch.as_tensor(y, dtype=torch.float32).cuda()
+    monkeypatch.setenv("APNEAUQ_TRAIN_GRAPH", graph)
+    monkeypatch.setattr(train_ops, "FUSED_MAX_BATCH", 1 << 20)
+    train_ops.set_deterministic(False)
+    models, losses, grads = {}, {}, {}
+
+    def step(fused):
+        monkeypatch.setattr(train_ops, "FUSED_REDUCE", fused)
+        m = models[fused]
+        losses.setdefault(fused, []).append(float(m.train_step(x, y)))
+        ws = m._train_graphs[batch].ws if graph == "1" else m._train_ws
+        assert train_ops._fused(ws, batch) == fused
+        grads.setdefault(fused, []).append({k: v.clone() for k, v in ws.gviews.items()})
+
+    for fused in (False, True):
+        models[fused] = AlarconCNN1D(seed=6, device="cuda")
+        step(fused)
+    a, b = models[False], models[True]
+    b.store.flat.copy_(a.store.flat)
+    b.store.stats.copy_(a.store.stats)
+    b.optimizer.m.copy_(a.optimizer.m)
+    b.optimizer.v.copy_(a.optimizer.v)
+    for fused in (False, True):
+        step(fused)
+    for i in range(2):
+        assert abs(losses[True][i] - losses[False][i]) <= 1e-5 * abs(losses[False][i]), (i, losses)
+        for name, g0 in grads[False][i].items():
+            g1 = grads[True][i][name]
+            assert torch.isfinite(g1).all(), name
+            rel = ((g1 - g0).norm() / g0.norm().clamp_min(1e-30)).item()
+            assert rel < 5e-3, (i, name, rel)
+
+
 def test_fit_concurrent_on_streams_matches_sequential(deterministic):
     """Three members trained concurrently (training/trainer.py:fit_concurrent), on HIP streams and as
     member-batched launches, ARE back-to-back fits in deterministic mode (bitwise-identical loss

@@ -121,9 +121,9 @@ int knn_lds_bytes(int D, int K);
 int train_layer_size();
 hipError_t train_launch_fwd(const train::Args& A, int l, hipStream_t st);
 hipError_t train_launch_head(const train::Args& A, int backward, hipStream_t st, bool with_tab);
-hipError_t train_launch_dgrad(const train::Args& A, int l, hipStream_t st);
-hipError_t train_launch_wgrad(const train::Args& A, int l, hipStream_t st);
-hipError_t train_launch_finalize(const train::Args& A, int update_moving, int grads, hipStream_t st);
+hipError_t train_launch_dgrad(const train::Args& A, int l, hipStream_t st, bool fused);
+hipError_t train_launch_wgrad(const train::Args& A, int l, hipStream_t st, bool fused);
+hipError_t train_launch_finalize(const train::Args& A, int update_moving, int grads, hipStream_t st, bool fused);
 hipError_t train_launch_tab(const apneauq::train::Args& A, int mode, int l, hipStream_t st);
 hipError_t train_launch_mb(const train::Args& A0, const train::Args* Am, int M, int op, int layer, int flag,
                            hipStream_t st);
@@ -468,7 +468,9 @@ apneauq::train::Args args_from_ctx(const at::Tensor& ctx, int64_t pass_base) {
 
 // op: 0 fwd(layer; flag=1: the pass-shared block 1 of batch-BN MC Dropout, over the n_win windows)
 //     | 1 head(flag bit 0 = backward, bit 1 = + the table's forward rows, replacing op 5) | 2 dgrad(layer) | 3 wgrad(layer) | 4 finalize(layer=update_moving, flag=grads)
-//     (2 / 3: flag 1 = Args::bwd_self, the backward BN rows from the slots instead of the table)
+//     (2 / 3: flag bit 0 = Args::bwd_self, the backward BN rows from the slots instead of the table; bit 1 =
+//     the fused single-device step: wgrad launches no reduce, dgrad<l> reduces wgrad<l+1>'s partials, and
+//     finalize (flag bit 1, bit 0 = grads) those of wgrad<1> / wgrad<0>)
 //     | 5 parameter table (flag 0: forward rows of every block, 1: backward rows of block ``layer``)
 void train_call(const at::Tensor& ctx, int64_t op, int64_t layer, int64_t flag, int64_t pass_base, int64_t device) {
   const at::DeviceGuard guard(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(device)));
@@ -488,14 +490,14 @@ void train_call(const at::Tensor& ctx, int64_t op, int64_t layer, int64_t flag, 
     case 2:
       TORCH_CHECK(layer >= 1 && layer < 6);
       A.bwd_self = (int)(flag & 1);
-      check(apneauq::train_launch_dgrad(A, (int)layer, s), "train dgrad");
+      check(apneauq::train_launch_dgrad(A, (int)layer, s, (flag & 2) != 0), "train dgrad");
       break;
     case 3:
       TORCH_CHECK(layer >= 0 && layer < 6);
       A.bwd_self = (int)(flag & 1);
-      check(apneauq::train_launch_wgrad(A, (int)layer, s), "train wgrad");
+      check(apneauq::train_launch_wgrad(A, (int)layer, s, (flag & 2) != 0), "train wgrad");
       break;
-    case 4: check(apneauq::train_launch_finalize(A, (int)layer, (int)flag, s), "train finalize"); break;
+    case 4: check(apneauq::train_launch_finalize(A, (int)layer, (int)(flag & 1), s, (flag & 2) != 0), "train finalize"); break;
     case 5: check(apneauq::train_launch_tab(A, (int)flag, (int)layer, s), "train param table"); break;
     default: TORCH_CHECK(false, "train_call: unknown op ", op);
   }

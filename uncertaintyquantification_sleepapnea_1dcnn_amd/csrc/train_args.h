@@ -267,6 +267,74 @@ struct TabBwd {  // backward rows of one block's parameter table entry (wgrad_re
   int cc;
   float inv_count;
 };
+// One layer's wgrad partial reduction, run as a side job of another launch (single-device steps:
+// dgrad<l-1> reduces wgrad<l>'s partials for l = 2..5, step_reduce_kernel those of wgrad<1> and wgrad<0>
+// next to the BN finalize) -- the same column split and summation order as wgrad_reduce_kernel's, so the gradient
+// is bitwise the one the separate reduce launch computes.  part == nullptr: no job.
+struct RedJob {
+  const float* part;  // [rgs][kcc + cout]
+  float* gw;
+  float* gb;
+  int rgs, kcc, cout, J, blocks;  // J threads per float4 column; blocks = the reduce launch's grid
+};
+// dW, db = sum over the row groups of the wgrad partials in a fixed order: deterministic, and cheaper
+// than the ~K*Cin*Cout fp32 atomics per row group it replaces (25-35 us of a 70-80 us wgrad at batch
+// 1024, profiles/train_step_r2.md).  Workgroup bx of nbx (256 threads) covers 256/J float4 columns at a
+// time with J threads per column: thread j sums row groups j, j + J, ... (8 loads in flight), then the
+// J partials are added in j order through LDS (red: 256 f32x4).  J > 1 when the row groups outnumber
+// the columns' parallelism (block 1: 512 row groups of 928 float4 columns took 26 us with one thread
+// per column).  The result depends on J only, not on which launch or workgroup runs a column.
+__device__ __forceinline__ void wgrad_reduce_cols(const RedJob& jb, int bx, int nbx, f32x4* red) {
+  const int S4 = (jb.kcc + jb.cout) >> 2;  // Cout is a multiple of 4
+  const int J = jb.J, rgs = jb.rgs, kcc = jb.kcc;
+  const int ncol = 256 / J;
+  const int cl = threadIdx.x % ncol, j = threadIdx.x / ncol;
+  const f32x4* p4 = reinterpret_cast<const f32x4*>(jb.part);
+  for (int base = bx * ncol; base < S4; base += nbx * ncol) {  // workgroup-uniform
+    const int e4 = base + cl;
+    // 8 loads in flight per batch, the last (partial) batch predicated instead of a serial remainder
+    // loop whose loads each waited for the previous add (21 row groups per thread at J = 4: 2 batches +
+    // 5 dependent loads).  (16 per batch measured slower: 48.6 -> 54.7 us of reduce per step at batch 1024.)
+    f32x4 acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (e4 < S4) {
+      int r = j;
+      for (; r + 7 * J < rgs; r += 8 * J) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] += p4[(long long)(r + q * J) * S4 + e4];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (r + q * J < rgs) acc[q] += p4[(long long)(r + q * J) * S4 + e4];
+    }
+    red[threadIdx.x] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    __syncthreads();
+    if (j == 0 && e4 < S4) {
+      f32x4 s = red[cl];
+      for (int q = 1; q < J; ++q) s += red[q * ncol + cl];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = 4 * e4 + i;
+        if (e < kcc)
+          jb.gw[e] = s[i];
+        else
+          jb.gb[e - kcc] = s[i];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// The table's backward rows (mean dY, mean dY*xhat) of one block from its fp64 slots.
+__device__ __forceinline__ void tab_bwd_rows(const TabBwd& tb) {
+  const int c = threadIdx.x;
+  if (c < tb.cc) {
+    tb.mdy[c] = (float)(slot_sumd(tb.bst + c, 2 * tb.cc) * (double)tb.inv_count);
+    tb.mdyx[c] = (float)(slot_sumd(tb.bst + tb.cc + c, 2 * tb.cc) * (double)tb.inv_count);
+  }
+}
+
 struct DetSeg {
   void* ptr;
   int cols;
@@ -287,6 +355,8 @@ __global__ void det_pass1_mb_kernel(const Args* __restrict__ Am, int n, int w, l
 __global__ void det_pass2_mb_kernel(const Args* __restrict__ Am, int op, int l, int w, long long sbase);
 template <bool MB>
 __global__ void bn_finalize_kernel(Args A_, const Args* __restrict__ Am, int update_moving, int grads);
+// single-device fused step tail: BN finalize (blocks 0-5), then the partial reductions of blocks 2 and 1
+__global__ void step_reduce_kernel(Args A, RedJob j1, RedJob j0, int update_moving, int grads);
 
 }  // namespace train
 }  // namespace apneauq

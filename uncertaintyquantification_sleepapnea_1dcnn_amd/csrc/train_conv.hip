@@ -1133,7 +1133,7 @@ struct DzStager {
 };
 
 template <int l, bool MB>
-__global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A_, const Args* __restrict__ Am) {
+__global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A_, const Args* __restrict__ Am, RedJob rj) {
   const MbPos pos = mb_pos<MB>();
   const Args& A = member_args<MB>(A_, Am, pos);
   constexpr int CIN = C[l + 1], COUT = C[l];  // conv^T: input = dZ_l channels, output = block l-1 channels
@@ -1286,6 +1286,9 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A_, const Args*
   }
   __syncthreads();  // the next tile's staging overwrites act
   }
+  // fused step (single device): wgrad<l+1>'s partials, which ran just before this launch, reduced by the
+  // workgroups as they finish their tiles -- the separate reduce launch's ramp and drain are gone
+  if (rj.part != nullptr) wgrad_reduce_cols(rj, pos.bx, gridDim.x, reinterpret_cast<f32x4*>(smem));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1294,6 +1297,12 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A_, const Args*
 // with ds_read_b64_tr_b16 from row-major LDS tiles.  Block 1 stages an im2col (kk = tap*4+ci).
 // ------------------------------------------------------------------------------------------------
 template <int l> struct WgCfg;
+// launch extras of a single-device fused step: the partial region's offset (wgrad<0> writes behind the
+// region wgrad<1> leaves for step_reduce_kernel) and the table job (tb.bst == nullptr: none)
+struct WgExt {
+  long long part_off;
+  TabBwd tb;
+};
 // CI_BLK CO_BLK WCO WCI, RTILES = 128-row tiles summed in registers per workgroup (sized so a
 // batch of 1024 gives >= 256 workgroups without multiplying the output atomics needlessly)
 // MINWG: the launcher lowers the row tiles per workgroup until at least this many workgroups
@@ -1326,9 +1335,13 @@ template <> struct WgCfg<5> { static constexpr int CIB = 64, COB = 96, WCO = 2, 
 
 
 template <int l, bool MB>
-__global__ __launch_bounds__(WgCfg<l>::WAVES * 64, WgCfg<l>::MINB) void wgrad_kernel(Args A_, const Args* __restrict__ Am) {
+__global__ __launch_bounds__(WgCfg<l>::WAVES * 64, WgCfg<l>::MINB) void wgrad_kernel(Args A_, const Args* __restrict__ Am,
+                                                                                     WgExt ext) {
   const MbPos pos = mb_pos<MB>();
   const Args& A = member_args<MB>(A_, Am, pos);
+  // fused step: the table's backward rows of block l-1 (bst[l-1] is complete: dgrad<l> ran before) for
+  // dgrad<l-1> / wgrad<l-1>, the job of the separate reduce launch's extra workgroup
+  if (ext.tb.bst != nullptr && blockIdx.x == 0) tab_bwd_rows(ext.tb);
   using W = WgCfg<l>;
   constexpr int NT = W::WAVES * 64;
   constexpr int CIN = C[l], COUT = C[l + 1], K = KS[l], PAD = (K - 1) / 2;
@@ -1552,7 +1565,7 @@ __global__ __launch_bounds__(WgCfg<l>::WAVES * 64, WgCfg<l>::MINB) void wgrad_ke
   // lane (m, h) holds D[ci = 4h + i][co = m] of each tile: 16 consecutive co per row -> 64-B runs
   const int m = lane & 15, h = lane >> 4;
   const Layer& Ly = A.L[l];
-  float* part = A.wpart != nullptr ? A.wpart + (long long)rg * (K * CIN * COUT + COUT) : nullptr;
+  float* part = A.wpart != nullptr ? A.wpart + ext.part_off + (long long)rg * (K * CIN * COUT + COUT) : nullptr;
 #pragma unroll
   for (int k = 0; k < NTAP; ++k)
 #pragma unroll
@@ -1707,7 +1720,8 @@ static bool fwd_pf(const Args& A, int M, int l) {
 }
 
 template <bool MB>
-static hipError_t dgrad_launch(const Args& A, const Args* Am, int M, int l, hipStream_t st) {
+static hipError_t dgrad_launch(const Args& A, const Args* Am, int M, int l, hipStream_t st,
+                               const train::RedJob& rj = train::RedJob{}) {
   // persistent blocks (DgPF > 0): at most kDgGrid workgroups over all members, each looping over its
   // member's tiles; the others one workgroup per tile
   const int tiles = (A.B + 1) / 2;
@@ -1716,11 +1730,11 @@ static hipError_t dgrad_launch(const Args& A, const Args* Am, int M, int l, hipS
                        (l == 5 && train::DgPF<5>::v > 0);
   const dim3 g(persist ? std::max(1, std::min(tiles, train::kDgGrid / std::max(1, M))) : tiles, 1, M);
   switch (l) {
-    case 1: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::dgrad_kernel<1, MB>), g, dim3(256), lds_dgrad(), st, A, Am); break;
-    case 2: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::dgrad_kernel<2, MB>), g, dim3(256), lds_dgrad(), st, A, Am); break;
-    case 3: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::dgrad_kernel<3, MB>), g, dim3(256), lds_dgrad(), st, A, Am); break;
-    case 4: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::dgrad_kernel<4, MB>), g, dim3(256), lds_dgrad(), st, A, Am); break;
-    case 5: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::dgrad_kernel<5, MB>), g, dim3(256), lds_dgrad(), st, A, Am); break;
+    case 1: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::dgrad_kernel<1, MB>), g, dim3(256), lds_dgrad(), st, A, Am, rj); break;
+    case 2: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::dgrad_kernel<2, MB>), g, dim3(256), lds_dgrad(), st, A, Am, rj); break;
+    case 3: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::dgrad_kernel<3, MB>), g, dim3(256), lds_dgrad(), st, A, Am, rj); break;
+    case 4: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::dgrad_kernel<4, MB>), g, dim3(256), lds_dgrad(), st, A, Am, rj); break;
+    case 5: hipLaunchKernelGGL(HIP_KERNEL_NAME(train::dgrad_kernel<5, MB>), g, dim3(256), lds_dgrad(), st, A, Am, rj); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -1768,8 +1782,13 @@ hipError_t train_launch_head(const Args& A, int backward, hipStream_t st, bool w
                     det_dst(A.loss_sum, 1, 0, A.g_dense_b, 1, A.g_dense_w, cc, A.L[5].bst, 2 * cc, 1), st);
 }
 
-hipError_t train_launch_dgrad(const Args& A, int l, hipStream_t st) {
-  const hipError_t e = dgrad_launch<false>(A, nullptr, 1, l, st);
+static bool fused_ok(const Args& A);
+static train::RedJob red_job_rt(const Args& A, int l, const float* part);
+// fused (l <= 4): the launch also reduces wgrad<l+1>'s partials, which the previous launch wrote
+hipError_t train_launch_dgrad(const Args& A, int l, hipStream_t st, bool fused) {
+  if (fused && (!fused_ok(A) || l > 4)) return hipErrorInvalidValue;
+  const hipError_t e =
+      dgrad_launch<false>(A, nullptr, 1, l, st, fused ? red_job_rt(A, l + 1, A.wpart) : train::RedJob{});
   if (e != hipSuccess || A.det == nullptr) return e;
   const int tiles = (A.B + 1) / 2;
   static constexpr int wm[6] = {0, train::Tiling<train::C[1]>::WM, train::Tiling<train::C[2]>::WM,
@@ -1804,74 +1823,128 @@ static long long wg_part_floats(int B) {
   return (long long)wg_rgs<l>(B) * (train::KS[l] * train::C[l] * train::C[l + 1] + train::C[l + 1]);
 }
 
+// The reduction of wgrad<l>'s partials (row grouping of an M-member launch) at part.
+template <int l>
+static train::RedJob red_job(const Args& A, int M, const float* part) {
+  const int rgs = wg_rgs<l>(A.B, M);
+  const int kcc = train::KS[l] * train::C[l] * train::C[l + 1];
+  const int s4 = (kcc + train::C[l + 1]) / 4;
+  // threads per column: enough columns x row-group splits to fill ~1024 workgroups' worth of lanes, at
+  // least 8 row groups per thread (one batch of 8 loads in flight).  Block 1 (928 float4 columns, 512
+  // row groups at batch 1024): J 16 -> 64, 58 -> 232 workgroups, one load batch per thread instead of 4
+  int J = 1;
+  while (J < 64 && rgs >= 8 * (2 * J) && (long long)s4 * J < 256LL * 1024) J *= 2;
+  const int blocks = std::min(2048, (s4 * J + 255) / 256);
+  return {part, A.L[l].gw, A.L[l].gb, rgs, kcc, train::C[l + 1], J, blocks};
+}
+static train::RedJob red_job_rt(const Args& A, int l, const float* part) {
+  switch (l) {
+    case 0: return red_job<0>(A, 1, part);
+    case 1: return red_job<1>(A, 1, part);
+    case 2: return red_job<2>(A, 1, part);
+    case 3: return red_job<3>(A, 1, part);
+    case 4: return red_job<4>(A, 1, part);
+    default: return red_job<5>(A, 1, part);
+  }
+}
+// floats of the partial region wgrad<1..5> share, and of wgrad<0>'s own region behind it (fused step)
+static long long wg_main_floats(int B) {
+  return std::max({wg_part_floats<1>(B), wg_part_floats<2>(B), wg_part_floats<3>(B), wg_part_floats<4>(B),
+                   wg_part_floats<5>(B)});
+}
+
+// fused: the single-device step whose reductions run inside other launches (train_launch_dgrad /
+// train_launch_finalize with fused set): no reduce launch here; the table job in workgroup 0; wgrad<0>'s
+// partials behind the shared region
 template <int l, bool MB>
-static void wg_launch(const Args& A, const Args* Am, int M, hipStream_t st) {
+static void wg_launch(const Args& A, const Args* Am, int M, hipStream_t st, bool fused = false) {
   using W = train::WgCfg<l>;
   const int nci = (l == 0) ? 1 : train::C[l] / W::CIB;
   const int nco = train::C[l + 1] / W::COB;
   // deterministic mode: the single-model row grouping (M = 1), so a member-batched step sums every
   // gradient in the same order as the member's own step
   const int rgs = wg_rgs<l>(A.B, A.det != nullptr ? 1 : M);
+  // the table's backward rows of block l-1 (bst[l-1] is complete after dgrad<l>, which ran before this
+  // wgrad) for dgrad<l-1> / wgrad<l-1>: the reduce launch's extra workgroup, or (fused) wgrad's workgroup 0
+  const bool side = A.tab != nullptr && l >= 1 && !A.bwd_self;
+  train::TabBwd tb = {};
+  if constexpr (l >= 1) {
+    if (side) {
+      tb.bst = A.L[l - 1].bst;
+      tb.cc = train::C[l];
+      tb.mdy = A.tab + ((l - 1) * train::kTabRows + train::kTabMdy) * 256;
+      tb.mdyx = A.tab + ((l - 1) * train::kTabRows + train::kTabMdyx) * 256;
+      tb.inv_count = A.inv_count;
+    }
+  }
+  train::WgExt ext = {};
+  if (fused) {
+    ext.part_off = (l == 0) ? wg_main_floats(A.B) : 0;
+    ext.tb = tb;
+  }
   hipLaunchKernelGGL(HIP_KERNEL_NAME(train::wgrad_kernel<l, MB>), dim3(nci * nco * rgs, 1, M), dim3(W::WAVES * 64), lds_wgrad<l>(),
-                     st, A, Am);
-  if (A.wpart != nullptr) {
-    const int kcc = train::KS[l] * train::C[l] * train::C[l + 1];
-    const int s4 = (kcc + train::C[l + 1]) / 4;
-    // threads per column: enough columns x row-group splits to fill ~1024 workgroups' worth of lanes, at
-    // least 8 row groups per thread (one batch of 8 loads in flight).  Block 1 (928 float4 columns, 512
-    // row groups at batch 1024): J 16 -> 64, 58 -> 232 workgroups, one load batch per thread instead of 4
-    int J = 1;
-    while (J < 64 && rgs >= 8 * (2 * J) && (long long)s4 * J < 256LL * 1024) J *= 2;
-    const int blocks = std::min(2048, (s4 * J + 255) / 256);
-    // side job: block l-1's backward rows of the parameter table (bst[l-1] is complete after dgrad<l>,
-    // which ran before this wgrad) for dgrad<l-1> / wgrad<l-1>
-    const bool side = A.tab != nullptr && l >= 1 && !A.bwd_self;
+                     st, A, Am, ext);
+  if (A.wpart != nullptr && !fused) {
+    const train::RedJob rj = red_job<l>(A, A.det != nullptr ? 1 : M, A.wpart);
+    const int J = rj.J, blocks = rj.blocks, kcc = rj.kcc;
     if constexpr (MB) {
       hipLaunchKernelGGL(train::wgrad_reduce_mb_kernel, dim3(blocks + (side ? 1 : 0), 1, M), dim3(256), 0, st, Am, l,
                          rgs, kcc, train::C[l + 1], J, side ? 1 : 0);
     } else {
-      train::TabBwd tb = {};
-      if constexpr (l >= 1) {
-        if (side) {
-          tb.bst = A.L[l - 1].bst;
-          tb.cc = train::C[l];
-          tb.mdy = A.tab + ((l - 1) * train::kTabRows + train::kTabMdy) * 256;
-          tb.mdyx = A.tab + ((l - 1) * train::kTabRows + train::kTabMdyx) * 256;
-          tb.inv_count = A.inv_count;
-        }
-      }
       hipLaunchKernelGGL(train::wgrad_reduce_kernel, dim3(blocks, side ? 2 : 1), dim3(256), 0, st, A.wpart, rgs, kcc,
                          train::C[l + 1], A.L[l].gw, A.L[l].gb, J, tb);
     }
   }
 }
 
+// Partial floats a workspace of batch capacity B needs: the shared region plus wgrad<0>'s region of the
+// fused step, for EVERY batch n <= B (a partial last batch runs the row grouping of its own size, which
+// is not monotone in n: the row-tile cap changes at 2048 samples)
 long long train_wgrad_part_floats(int B) {
-  return std::max({wg_part_floats<0>(B), wg_part_floats<1>(B), wg_part_floats<2>(B), wg_part_floats<3>(B),
-                   wg_part_floats<4>(B), wg_part_floats<5>(B)});
+  long long mx = 0;
+  for (int n = 2; n < B + 2; n += 2) {  // the grouping depends on the tile count (n + 1) / 2 only
+    const int b = std::min(n, B);
+    mx = std::max(mx, wg_main_floats(b) + wg_part_floats<0>(b));
+  }
+  return mx;
 }
 
 template <bool MB>
-static hipError_t wgrad_launch(const Args& A, const Args* Am, int M, int l, hipStream_t st) {
+static hipError_t wgrad_launch(const Args& A, const Args* Am, int M, int l, hipStream_t st, bool fused = false) {
   switch (l) {
-    case 0: wg_launch<0, MB>(A, Am, M, st); break;
-    case 1: wg_launch<1, MB>(A, Am, M, st); break;
-    case 2: wg_launch<2, MB>(A, Am, M, st); break;
-    case 3: wg_launch<3, MB>(A, Am, M, st); break;
-    case 4: wg_launch<4, MB>(A, Am, M, st); break;
-    case 5: wg_launch<5, MB>(A, Am, M, st); break;
+    case 0: wg_launch<0, MB>(A, Am, M, st, fused); break;
+    case 1: wg_launch<1, MB>(A, Am, M, st, fused); break;
+    case 2: wg_launch<2, MB>(A, Am, M, st, fused); break;
+    case 3: wg_launch<3, MB>(A, Am, M, st, fused); break;
+    case 4: wg_launch<4, MB>(A, Am, M, st, fused); break;
+    case 5: wg_launch<5, MB>(A, Am, M, st, fused); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
-hipError_t train_launch_wgrad(const Args& A, int l, hipStream_t st) {
-  if (A.groups != 1) return hipErrorInvalidValue;  // training: one stats group (the staging's single affine)
-  return wgrad_launch<false>(A, nullptr, 1, l, st);
+// The fused single-device step (Python: train_ops.FUSED_REDUCE): atomic mode with the parameter table and
+// wgrad partials, backward BN rows from the table.
+static bool fused_ok(const Args& A) {
+  return A.tab != nullptr && A.det == nullptr && A.wpart != nullptr && A.groups == 1 && !A.bwd_self;
 }
 
-hipError_t train_launch_finalize(const Args& A, int update_moving, int grads, hipStream_t st) {
-  hipLaunchKernelGGL(train::bn_finalize_kernel<false>, dim3(6), dim3(256), 0, st, A, nullptr, update_moving, grads);
+hipError_t train_launch_wgrad(const Args& A, int l, hipStream_t st, bool fused) {
+  if (A.groups != 1) return hipErrorInvalidValue;  // training: one stats group (the staging's single affine)
+  if (fused && !fused_ok(A)) return hipErrorInvalidValue;
+  return wgrad_launch<false>(A, nullptr, 1, l, st, fused);
+}
+
+// fused: BN finalize and the reductions of wgrad<1> / wgrad<0>'s partials in one launch
+hipError_t train_launch_finalize(const Args& A, int update_moving, int grads, hipStream_t st, bool fused) {
+  if (!fused) {
+    hipLaunchKernelGGL(train::bn_finalize_kernel<false>, dim3(6), dim3(256), 0, st, A, nullptr, update_moving, grads);
+    return hipGetLastError();
+  }
+  if (!fused_ok(A)) return hipErrorInvalidValue;
+  const train::RedJob j1 = red_job<1>(A, 1, A.wpart), j0 = red_job<0>(A, 1, A.wpart + wg_main_floats(A.B));
+  hipLaunchKernelGGL(train::step_reduce_kernel, dim3(6 + j1.blocks + j0.blocks), dim3(256), 0, st, A, j1, j0,
+                     update_moving, grads);
   return hipGetLastError();
 }
 

@@ -7,58 +7,18 @@
 namespace apneauq {
 namespace train {
 
-// dW, db = sum over the row groups of the wgrad partials in a fixed order: deterministic, and cheaper
-// than the ~K*Cin*Cout fp32 atomics per row group it replaces (25-35 us of a 70-80 us wgrad at batch
-// 1024, profiles/train_step_r2.md).  A workgroup covers 256/J float4 columns with J threads per column:
-// thread j sums row groups j, j + J, ... (8 loads in flight), then the J partials are added in j order
-// through LDS.  J > 1 when the row groups outnumber the columns' parallelism (block 1: 512 row groups
-// of 928 float4 columns took 26 us with one thread per column).
+// The separate reduce launch (wgrad_reduce_cols, train_args.h) with its optional side job: the table's
+// backward rows of the block the NEXT dgrad / wgrad read.
 __device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ part, int rgs, int kcc, int cout,
                                                   float* __restrict__ gw, float* __restrict__ gb, int J,
                                                   const TabBwd& tb, int bx, int nbx, bool side_block) {
   __shared__ f32x4 red[256];
-  if (side_block) {  // the table's backward rows of the block the NEXT dgrad / wgrad read
-    const int c = threadIdx.x;
-    if (c < tb.cc) {
-      tb.mdy[c] = (float)(slot_sumd(tb.bst + c, 2 * tb.cc) * (double)tb.inv_count);
-      tb.mdyx[c] = (float)(slot_sumd(tb.bst + tb.cc + c, 2 * tb.cc) * (double)tb.inv_count);
-    }
+  if (side_block) {
+    tab_bwd_rows(tb);
     return;
   }
-  const int S = kcc + cout;  // a multiple of 4 (Cout is)
-  const int S4 = S >> 2;
-  const int ncol = 256 / J;
-  const int cl = threadIdx.x % ncol, j = threadIdx.x / ncol;
-  const f32x4* p4 = reinterpret_cast<const f32x4*>(part);
-  for (int base = bx * ncol; base < S4; base += nbx * ncol) {  // workgroup-uniform
-    const int e4 = base + cl;
-    f32x4 acc[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (e4 < S4) {
-      int r = j;
-      for (; r + 7 * J < rgs; r += 8 * J) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) acc[q] += p4[(long long)(r + q * J) * S4 + e4];
-      }
-      for (int q = 0; r < rgs; r += J, ++q) acc[q] += p4[(long long)r * S4 + e4];
-    }
-    red[threadIdx.x] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-    __syncthreads();
-    if (j == 0 && e4 < S4) {
-      f32x4 s = red[cl];
-      for (int q = 1; q < J; ++q) s += red[q * ncol + cl];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int e = 4 * e4 + i;
-        if (e < kcc)
-          gw[e] = s[i];
-        else
-          gb[e - kcc] = s[i];
-      }
-    }
-    __syncthreads();
-  }
+  const RedJob jb = {part, gw, gb, rgs, kcc, cout, J, nbx};
+  wgrad_reduce_cols(jb, bx, nbx, red);
 }
 
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int rgs, int kcc, int cout,
@@ -169,11 +129,7 @@ __global__ __launch_bounds__(256) void det_pass2_mb_kernel(const Args* __restric
   det_pass2(reinterpret_cast<const double*>(A.det + sbase), w, d, c);
 }
 
-template <bool MB>
-__global__ void bn_finalize_kernel(Args A_, const Args* __restrict__ Am, int update_moving, int grads) {
-  const MbPos pos = mb_pos<MB>();
-  const Args& A = member_args<MB>(A_, Am, pos);
-  const int l = pos.bx;
+__device__ __forceinline__ void bn_finalize_body(const Args& A, int l, int update_moving, int grads) {
   const Layer& Ly = A.L[l];
   const int Cc = (l == 0) ? C[1] : (l == 1) ? C[2] : (l == 2) ? C[3] : (l == 3) ? C[4] : (l == 4) ? C[5] : C[6];
   for (int c = threadIdx.x; c < Cc; c += blockDim.x) {
@@ -201,6 +157,27 @@ __global__ void bn_finalize_kernel(Args A_, const Args* __restrict__ Am, int upd
       else
         *A.g_dense_b = v;
     }
+  }
+}
+
+template <bool MB>
+__global__ void bn_finalize_kernel(Args A_, const Args* __restrict__ Am, int update_moving, int grads) {
+  const MbPos pos = mb_pos<MB>();
+  bn_finalize_body(member_args<MB>(A_, Am, pos), pos.bx, update_moving, grads);
+}
+
+// Single-device step tail (one launch instead of the reduces of blocks 2 and 1 plus the finalize): the
+// finalize of block b in workgroup b < 6, then the wgrad partial reductions of block 2 (j1, the shared
+// partial region) and block 1 (j0, its own region: wgrad_0 runs after wgrad_1 without a dgrad between).
+__global__ __launch_bounds__(256) void step_reduce_kernel(Args A, RedJob j1, RedJob j0, int update_moving, int grads) {
+  __shared__ f32x4 red[256];
+  const int b = blockIdx.x;
+  if (b < 6) {
+    bn_finalize_body(A, b, update_moving, grads);
+  } else if (b < 6 + j1.blocks) {
+    wgrad_reduce_cols(j1, b - 6, j1.blocks, red);
+  } else {
+    wgrad_reduce_cols(j0, b - 6 - j1.blocks, j0.blocks, red);
   }
 }
 

@@ -232,6 +232,16 @@ DETERMINISTIC = os.environ.get("APNEAUQ_DETERMINISTIC", "0") not in ("", "0")
 # kernel already holds every CU, so both slow ~2x and the step got slower (0.76 -> 0.82 ms at batch
 # 1024, 4.37 -> 4.51 ms at 8192; profiles/train_step_r4.md)
 OVERLAP = os.environ.get("APNEAUQ_TRAIN_OVERLAP", "0") not in ("", "0")
+# Fused reductions (single-device atomic-mode steps): wgrad_l's partial sums are reduced by the workgroups
+# of dgrad_{l-1} as they finish their tiles, those of wgrad_1 / wgrad_0 by one launch with the BN finalize
+# -- 7 reduce / finalize launches become 1 (csrc/train_conv.hip train_launch_dgrad / _finalize; the same
+# column split and summation order, so the gradients equal the separate reduces' bitwise).  Up to
+# FUSED_MAX_BATCH samples: dgrad's 8 waves per CU run the reduction latency-bound, ~2x the reduce
+# launch's time, which only the launch overhead saved at small batches pays for (batch 1024: -13 us of
+# kernel time per step; batch 8192: +16 us; profiles/train_fused_reduce_r6.md).
+# APNEAUQ_TRAIN_FUSED_REDUCE=0 restores the separate launches.
+FUSED_REDUCE = os.environ.get("APNEAUQ_TRAIN_FUSED_REDUCE", "1") not in ("", "0")
+FUSED_MAX_BATCH = int(os.environ.get("APNEAUQ_TRAIN_FUSED_MAX_BATCH", "2048"))
 
 
 def set_deterministic(flag: bool = True) -> None:
@@ -275,13 +285,14 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, syn
     _call(ctx, 1, 0, 3, pb, dev)  # head + the BN parameter table's forward rows (no-op without a table)
     if sync is not None:
         sync(ws.bst[5])
-    for l in range(5, 0, -1):
-        _call(ctx, 2, l, 0, pb, dev)
-        if sync is not None:
+        for l in range(5, 0, -1):
+            _call(ctx, 2, l, 0, pb, dev)
             sync(ws.bst[l - 1])
-        _call(ctx, 3, l, 0, pb, dev)
-    _call(ctx, 3, 0, 0, pb, dev)
-    _call(ctx, 4, 1, 1, pb, dev)
+            _call(ctx, 3, l, 0, pb, dev)
+        _call(ctx, 3, 0, 0, pb, dev)
+        _call(ctx, 4, 1, 1, pb, dev)
+    else:
+        _backward_calls(ctx, pb, dev, _fused(ws, n))
     if sync is not None and sync_world > 1:
         for i in range(1, 7):
             ws.gviews[f"batchnorm_{i}/gamma"].div_(sync_world)
@@ -292,6 +303,24 @@ def train_step(model, x: torch.Tensor, y: torch.Tensor, grad_allreduce=None, syn
     # device-side bias correction, as the captured step computes it (eager == graph bitwise)
     model.optimizer.step(model.store.flat, ws.grad, grad_scale=scale, counters=ws.counters)
     return ws.loss.double().sum(), torch.sigmoid(ws.logits[:n])
+
+
+def _fused(ws, n: int) -> bool:
+    """A step of n samples runs the fused reductions: atomic mode with the parameter table (single
+    device), at most FUSED_MAX_BATCH samples."""
+    return FUSED_REDUCE and n <= FUSED_MAX_BATCH and ws.tab is not None and ws.det is None and ws.wpart is not None
+
+
+def _backward_calls(ctx, pb, dev, fused: bool) -> None:
+    """dgrad_l, wgrad_l for l = 5..1, wgrad_0, finalize -- the eager step and the captured graph issue
+    the same launches.  fused: no reduce launches; dgrad_l (l <= 4) reduces wgrad_{l+1}'s partials and the
+    finalize launch those of wgrad_1 and wgrad_0."""
+    f = 2 if fused else 0
+    for l in range(5, 0, -1):
+        _call(ctx, 2, l, f if l < 5 else 0, pb, dev)
+        _call(ctx, 3, l, f, pb, dev)
+    _call(ctx, 3, 0, f, pb, dev)
+    _call(ctx, 4, 1, 1 | f, pb, dev)
 
 
 def capture_graph(body, dev):
@@ -413,12 +442,9 @@ class GraphedTrainStep:
             self._evs.append(ev)
             ev.record(aux)
             main.wait_event(ev)
+            _call(self.ctx, 4, 1, 1, TRAIN_PASS_BASE, dev)
         else:
-            for l in range(5, 0, -1):
-                _call(self.ctx, 2, l, 0, TRAIN_PASS_BASE, dev)
-                _call(self.ctx, 3, l, 0, TRAIN_PASS_BASE, dev)
-            _call(self.ctx, 3, 0, 0, TRAIN_PASS_BASE, dev)
-        _call(self.ctx, 4, 1, 1, TRAIN_PASS_BASE, dev)
+            _backward_calls(self.ctx, TRAIN_PASS_BASE, dev, _fused(ws, n))
         opt = self.model.optimizer
         o.adam_step(self.model.store.flat, ws.grad, opt.m, opt.v, opt.beta_1, opt.beta_2, opt.learning_rate,
                     opt.epsilon, 1.0, ws.counters)
