@@ -1017,6 +1017,9 @@ template <int l> struct DgPre { static constexpr bool v = l >= 1 && l <= 5; };
 template <int l> struct DgPF { static constexpr int v = l == 1 ? 8 : l == 2 ? 2 : l == 4 ? 12 : 0; };
 // workgroups of a single-model dgrad launch: two per CU (larger batches loop over their tiles)
 constexpr int kDgGrid = 512;
+// Weight-fragment prefetch depth of the dgrad conv (k-steps in flight): 2 where it fits the 256-VGPR budget
+// without spilling (blocks 3 / 6 spill at 2: 56 / 12 B of scratch)
+template <int l> struct DgPD { static constexpr int v = (l == 1 || l == 2 || l == 4) ? 2 : 1; };
 
 // stage_dz for dgrad (all CIN channels of 136 rows, dZ_l also written to global for wgrad) split into
 // load() (the prefetched items, into registers) and store() (every item: the prefetched ones from
@@ -1228,7 +1231,7 @@ __global__ __launch_bounds__(kThreads, 2) void dgrad_kernel(Args A_, const Args*
     if (tile + (int)gridDim.x < ntiles) stager.load(A, kR * (tile + gridDim.x));  // in flight during the conv
   }
   f32x4 acc[CV::CT][CV::RT];
-  CV::template run<1, false>(A.L[l].wd, act, kRS, acc);  // (B ring at batch 8192: -0.6 %, batch 1024: +-0)
+  CV::template run<DgPD<l>::v, false>(A.L[l].wd, act, kRS, acc);  // (B ring at batch 8192: -0.6 %, batch 1024: +-0)
   __syncthreads();
   const float dscp = A.dropout ? Lp.dsc : 1.f;
 #pragma unroll
