@@ -196,7 +196,8 @@ def test_fused_reductions_match_separate_launches(monkeypatch, graph, batch):
     from identical states (the fused model gets the other's weights, statistics and Adam moments) so a
     table row left stale from step 1 would show.  (Without the copy, Adam's ~lr first moves of
     near-zero gradient elements whose sign the order noise flips move block 1's step-2 gradient by up to
-    7 %.)  Batch 4100 runs the large-batch row grouping and a partial last row tile."""
+    7 %.)  Batch 4100 runs the large-batch row grouping and a partial last row tile; the eager case adds a
+    100-sample step on the 384-sample workspace."""
     from uncertaintyquantification_sleepapnea_1dcnn_amd.data.synthetic import synthetic_windows
 
     x, y, _ = synthetic_windows(batch, seed=11)
@@ -212,7 +213,7 @@ def test_fused_reductions_match_separate_launches(monkeypatch, graph, batch):
         m = models[fused]
         losses.setdefault(fused, []).append(float(m.train_step(x, y)))
         ws = m._train_graphs[batch].ws if graph == "1" else m._train_ws
-        assert train_ops._fused(ws, batch) == fused
+        assert train_ops._fused(ws, x.shape[0]) == fused
         grads.setdefault(fused, []).append({k: v.clone() for k, v in ws.gviews.items()})
 
     for fused in (False, True):
@@ -225,7 +226,17 @@ def test_fused_reductions_match_separate_launches(monkeypatch, graph, batch):
     b.optimizer.v.copy_(a.optimizer.v)
     for fused in (False, True):
         step(fused)
-    for i in range(2):
+    nsteps = 2
+    if graph == "0":  # eager: a partial batch on the same workspace (n < capacity: its own row grouping)
+        b.store.flat.copy_(a.store.flat)
+        b.store.stats.copy_(a.store.stats)
+        b.optimizer.m.copy_(a.optimizer.m)
+        b.optimizer.v.copy_(a.optimizer.v)
+        x, y = x[:100], y[:100]
+        for fused in (False, True):
+            step(fused)
+        nsteps = 3
+    for i in range(nsteps):
         assert abs(losses[True][i] - losses[False][i]) <= 1e-5 * abs(losses[False][i]), (i, losses)
         for name, g0 in grads[False][i].items():
             g1 = grads[True][i][name]
