@@ -185,3 +185,18 @@ def test_fused_input_copy_only_takes_matching_device_batches():
     assert not _inputs_direct([x[:, :, :3].contiguous()], [y], 8, dev, 4)
     assert not _inputs_direct([x], [y[:7]], 8, dev, 4)
     assert not _inputs_direct([x.double()], [y], 8, dev, 4)
+
+
+def test_wgrad_partial_buffer_covers_every_smaller_batch():
+    """csrc/train_conv.hip train_wgrad_part_floats: a workspace of capacity B serves every batch n <= B
+    (a partial last batch runs its own row grouping, which is not monotone in n: the row-tile cap changes
+    at 2048 samples), so the size is the running maximum -- non-decreasing in B -- and holds the fused
+    step's wgrad<0> region behind the shared one.  Host-only op: runs wherever the extension loads."""
+    from uncertaintyquantification_sleepapnea_1dcnn_amd.ops import _ext
+
+    if not _ext.load():
+        pytest.skip("HIP extension not built")
+    o = _ext.ops()
+    sizes = [o.train_wgrad_part_size(b) for b in list(range(1, 80)) + list(range(2000, 2100)) + [4096, 8192]]
+    assert all(b >= a for a, b in zip(sizes, sizes[1:]))
+    assert o.train_wgrad_part_size(2050) >= o.train_wgrad_part_size(2048) > 0
