@@ -30,7 +30,7 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from ..ops import _ext, fused, rng
+from ..ops import _ext, fused
 from . import reference as R
 from .params import ParamStore
 from .spec import ModelSpec

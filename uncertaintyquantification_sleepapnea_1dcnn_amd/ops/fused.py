@@ -10,7 +10,7 @@ and cross-checked against the kernel's own ``fused_layout()``.
 """
 from __future__ import annotations
 
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, Optional, Sequence
 
 import numpy as np
 import torch

@@ -32,7 +32,7 @@ sums.
 """
 from __future__ import annotations
 
-from typing import Callable, List, Optional
+from typing import Callable, Optional
 
 import torch
 

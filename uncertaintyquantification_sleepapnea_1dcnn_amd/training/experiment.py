@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import argparse
 import os
-from typing import Dict, Optional
+from typing import Dict
 
 import numpy as np
 import torch
